@@ -1,0 +1,33 @@
+# Builds the in-tree engine library trivy_amd/libtrivy_secret_gpu.so for gfx950.
+# (hipcc cross-compiles without a GPU; the .so travels to the GPU box.)
+HIPCC   ?= /opt/rocm/bin/hipcc
+ARCH    ?= gfx950
+CXXFLAGS = -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Iinclude -Itrivy_amd/csrc
+HIPFLAGS = $(CXXFLAGS) -x hip --offload-arch=$(ARCH) -munsafe-fp-atomics
+SRC_DIR  = trivy_amd/csrc
+BUILD    = build
+LIB      = trivy_amd/libtrivy_secret_gpu.so
+
+HOST_SRCS = $(SRC_DIR)/gre.cpp $(SRC_DIR)/ruleset.cpp $(SRC_DIR)/findings.cpp
+HIP_SRCS  = $(SRC_DIR)/engine.hip
+HDRS      = $(wildcard $(SRC_DIR)/*.h) include/trivy_secret_gpu.h
+
+OBJS = $(patsubst $(SRC_DIR)/%.cpp,$(BUILD)/%.o,$(HOST_SRCS)) $(patsubst $(SRC_DIR)/%.hip,$(BUILD)/%.o,$(HIP_SRCS))
+
+all: $(LIB)
+
+$(BUILD)/%.o: $(SRC_DIR)/%.cpp $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/%.o: $(SRC_DIR)/%.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJS) -lamdhip64
+
+clean:
+	rm -rf $(BUILD) $(LIB)
+
+.PHONY: all clean

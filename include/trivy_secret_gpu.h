@@ -1,0 +1,162 @@
+/*
+ * trivy_secret_gpu.h — C ABI of the MI355X secret-scanning engine.
+ *
+ * Drop-in backend for Trivy's secret scanner hot path:
+ *   pkg/fanal/secret/scanner.go:315  func NewScanner(config *Config) Scanner
+ *   pkg/fanal/secret/scanner.go:371  func (s *Scanner) Scan(args ScanArgs) types.Secret
+ *   pkg/fanal/analyzer/secret/secret.go:79  (*SecretAnalyzer).Analyze  (batched caller)
+ *
+ * Plain C types only (no torch / HIP types in signatures) so that a cgo shim
+ *  can bind it directly.  Conventions:
+ *   - every entry point returns an int status (TSG_OK = 0) and never aborts;
+ *     tsg_last_error() returns a thread-local message for the last failure;
+ *   - caller memory is never retained after a call returns;
+ *   - a compiled tsg_ruleset is immutable and may be shared across threads;
+ *     a tsg_engine serialises calls made on it (one HIP stream per engine).
+ */
+#ifndef TRIVY_SECRET_GPU_H
+#define TRIVY_SECRET_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TSG_OK 0
+#define TSG_ERR_INVALID_ARG 1
+#define TSG_ERR_REGEX 2       /* "regexp compile error" (scanner.go:77) */
+#define TSG_ERR_DEVICE 3      /* HIP runtime failure */
+#define TSG_ERR_NO_DEVICE 4   /* no MI355X visible: the product path does not fall back to CPU */
+#define TSG_ERR_UNSUPPORTED 5 /* rule feature outside this engine's coverage (e.g. \p{..}) */
+#define TSG_ERR_INTERNAL 6
+#define TSG_ERR_PANIC 7       /* input on which the Go reference panics (secret group did not participate) */
+
+/* AllowRule — pkg/fanal/secret/scanner.go:191-196 (Description stays host-side). */
+typedef struct tsg_allow_rule {
+  const char* id;
+  const char* regex; /* Go RE2 syntax applied to the whole match text, or NULL */
+  const char* path;  /* Go RE2 syntax applied to the file path, or NULL */
+} tsg_allow_rule;
+
+/* Rule — pkg/fanal/secret/scanner.go:84-95.  Category/Title/Severity are
+ * report metadata the host keeps; the engine needs only these fields. */
+typedef struct tsg_rule {
+  const char* id;
+  const char* regex; /* NULL => FindLocations returns nothing (scanner.go:98-100) */
+  const char* const* keywords;
+  size_t n_keywords;
+  const char* path;              /* NULL => every path (scanner.go:165-167) */
+  const char* secret_group_name; /* NULL or "" => whole match (scanner.go:102-104) */
+  const tsg_allow_rule* allow_rules;
+  size_t n_allow_rules;
+  const char* const* exclude_regexes; /* Rule.ExcludeBlock.Regexes */
+  size_t n_exclude_regexes;
+} tsg_rule;
+
+typedef struct tsg_ruleset tsg_ruleset;
+typedef struct tsg_engine tsg_engine;
+typedef struct tsg_result tsg_result;
+
+/* ScanArgs — scanner.go:361-364 (Content already CR-stripped by the caller,
+ * as analyzer/secret/secret.go:91 does). */
+typedef struct tsg_file {
+  const uint8_t* data;
+  uint64_t len;
+  const char* path;
+} tsg_file;
+
+/* One kept Location (scanner.go:223-226) after allow + exclude filtering. */
+typedef struct tsg_loc {
+  uint32_t file;       /* index into the batch */
+  uint32_t rule;       /* index into the ruleset's rules (config order) */
+  uint64_t start, end; /* byte offsets into the file content */
+  uint32_t start_line; /* findLocation (scanner.go:481-537), 1-based */
+  uint32_t end_line;
+} tsg_loc;
+
+/* One types.Line (pkg/fanal/types/misconf.go:53-62); Highlighted == Content. */
+typedef struct tsg_line {
+  uint32_t number;
+  const char* content;
+  size_t content_len;
+  uint8_t is_cause, first_cause, last_cause;
+} tsg_line;
+
+/* One types.SecretFinding (pkg/fanal/types/secret.go:10-20) minus the rule
+ * metadata the host owns (look it up by `rule`). */
+typedef struct tsg_finding {
+  uint32_t file;
+  uint32_t rule;
+  uint32_t start_line, end_line;
+  const char* match; /* censored line window */
+  size_t match_len;
+  const tsg_line* lines;
+  size_t n_lines;
+  uint64_t start, end;
+} tsg_finding;
+
+/* Per-file flags in a result. */
+#define TSG_FILE_PATH_ALLOWED 1u /* Global.AllowPath matched: Secret{FilePath} without findings (scanner.go:375-379) */
+#define TSG_FILE_SPECIAL 2u      /* content holds U+0130/U+017F/U+212A: scanned on the exact full-scan path */
+
+const char* tsg_version(void);
+const char* tsg_last_error(void);
+
+/* NewScanner: compile rules (builtin ∪ custom, already filtered by the caller
+ * exactly as scanner.go:315-359 does), global allow rules and the global
+ * exclude block. */
+int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_rule* allow_rules,
+                        size_t n_allow_rules, const char* const* exclude_regexes,
+                        size_t n_exclude_regexes, tsg_ruleset** out, char* err, size_t errlen);
+void tsg_ruleset_free(tsg_ruleset* rs);
+size_t tsg_ruleset_rule_count(const tsg_ruleset* rs);
+/* Anchor diagnostics for rule i: mode 0 = never matches, 1 = anchored, 2 = full scan. */
+int tsg_ruleset_rule_info(const tsg_ruleset* rs, size_t i, int* mode, uint32_t* anchor_min,
+                          uint32_t* anchor_max, size_t* n_literals);
+
+/* Engine bound to one GPU (one process per GPU; `device` is the HIP ordinal). */
+int tsg_engine_create(int device, tsg_engine** out);
+void tsg_engine_free(tsg_engine* e);
+
+/* Scan a batch of host files: pack -> H2D -> kernels -> D2H -> findings. */
+int tsg_scan(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, size_t n_files,
+             tsg_result** out);
+
+/* Scan a batch already resident in HBM (device pointers): n_files files,
+ * file i = d_data[d_offsets[i] .. d_offsets[i+1]), path i = d_paths[d_path_offsets[i] ..
+ * d_path_offsets[i+1]).  Produces locs (with line numbers); findings need
+ * host content and are not built (tsg_result_findings returns 0). */
+int tsg_scan_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
+                    const uint64_t* d_offsets, const uint8_t* d_paths,
+                    const uint64_t* d_path_offsets, size_t n_files, tsg_result** out);
+
+size_t tsg_result_loc_count(const tsg_result* r);
+const tsg_loc* tsg_result_locs(const tsg_result* r);
+size_t tsg_result_file_count(const tsg_result* r);
+const uint8_t* tsg_result_file_flags(const tsg_result* r);
+/* Findings of file i in Scan order (sorted by RuleID, then Match). */
+size_t tsg_result_findings(const tsg_result* r, size_t file, const tsg_finding** out);
+/* Per-stage device timings of the last scan, milliseconds. */
+int tsg_result_timings(const tsg_result* r, double* ms, size_t n, size_t* n_out);
+void tsg_result_free(tsg_result* r);
+
+/* Prefilter-only pass (BASELINE config 2): per-file rule gate bitmasks
+ * (rule i passes iff bit i set), exactly MatchKeywords (scanner.go:169-181). */
+int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
+                    const uint64_t* d_offsets, size_t n_files, uint32_t* h_gates_out,
+                    size_t gate_words_per_file);
+
+/* Host-side path regex evaluation (per-file, not per-byte): Go MatchString. */
+int tsg_regex_match(const char* pattern, const uint8_t* text, size_t len, int* matched);
+/* Host-side FindAllIndex for diagnostics/tests of the compiler + VM: writes
+ * up to cap (start,end) pairs. */
+int tsg_regex_find_all(const char* pattern, const uint8_t* text, size_t len, int64_t* pairs,
+                       size_t cap, size_t* n_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TRIVY_SECRET_GPU_H */

@@ -72,6 +72,7 @@ class _Translator:
         self.p = pat
         self.i = 0
         self.names: List[str] = [""]  # group 0
+        self.pending = ""
 
     def peek(self, k=0):
         j = self.i + k
@@ -84,6 +85,9 @@ class _Translator:
         return out
 
     def alt(self, flags):
+        # Go's parser keeps flags as parser state restored only at the group's
+        # closing paren: a (?i) in one branch also covers later branches.
+        flags = dict(flags)
         parts = [self.concat(flags)]
         while self.peek() == "|":
             self.i += 1
@@ -91,14 +95,16 @@ class _Translator:
         return "|".join(parts)
 
     def concat(self, flags):
-        flags = dict(flags)  # (?i) inside a group scopes to the group's end
         out = []
         while self.i < len(self.p) and self.peek() not in "|)":
             if self.p.startswith("(?", self.i) and self._try_flags(flags):
                 continue
+            self.pending = ""
             atom = self.atom(flags)
             if atom is None:
                 continue
+            if self.pending:
+                out.append(self.pending)
             out.append(self.repeat(atom, flags))
         return "".join(out)
 
@@ -158,7 +164,11 @@ class _Translator:
                 raise GoSyntaxError("invalid nested repetition operator")
 
     def wrap(self, s, flags):
-        return "(?i:%s)" % s if flags["i"] else s
+        if not flags["i"]:
+            return s
+        # Go's simple folding keeps U+0130/U+0131 out of the i/I orbit;
+        # python's (?i) folds them in, so exclude them explicitly.
+        return "(?:(?![\\u0130\\u0131])(?i:%s))" % s
 
     def atom(self, flags):
         c = self.peek()
@@ -241,7 +251,12 @@ class _Translator:
                 end = self.p.find("\\E", self.i)
                 lit = self.p[self.i:] if end < 0 else self.p[self.i:end]
                 self.i = len(self.p) if end < 0 else end + 2
-                return "".join(self.wrap(_esc_char(ch), flags) for ch in lit)
+                # Go pushes \Q..\E as single-rune literals: a following
+                # repetition binds to the last rune only.
+                if not lit:
+                    return None
+                self.pending = "".join(self.wrap(_esc_char(ch), flags) for ch in lit[:-1])
+                return self.wrap(_esc_char(lit[-1]), flags)
         if c in "pP":
             if self.peek() == "{":
                 end = self.p.index("}", self.i)

@@ -1,0 +1,144 @@
+"""ctypes binding of the C ABI in include/trivy_secret_gpu.h.
+
+The product path has exactly one implementation: libtrivy_secret_gpu.so (HIP
+kernels for gfx950 + host C++).  If the library is missing this module raises
+on import; if no GPU is visible, engine creation raises — there is no CPU
+fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtrivy_secret_gpu.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build it with `make` (or __graft_entry__.build()); "
+        "the secret engine has no CPU fallback")
+
+lib = ctypes.CDLL(LIB_PATH)
+
+TSG_OK = 0
+TSG_ERR_INVALID_ARG = 1
+TSG_ERR_REGEX = 2
+TSG_ERR_DEVICE = 3
+TSG_ERR_NO_DEVICE = 4
+TSG_ERR_UNSUPPORTED = 5
+TSG_ERR_INTERNAL = 6
+TSG_ERR_PANIC = 7
+
+TSG_FILE_PATH_ALLOWED = 1
+TSG_FILE_SPECIAL = 2
+
+c_char_pp = ctypes.POINTER(ctypes.c_char_p)
+
+
+class AllowRuleC(ctypes.Structure):
+    _fields_ = [("id", ctypes.c_char_p), ("regex", ctypes.c_char_p), ("path", ctypes.c_char_p)]
+
+
+class RuleC(ctypes.Structure):
+    _fields_ = [
+        ("id", ctypes.c_char_p),
+        ("regex", ctypes.c_char_p),
+        ("keywords", c_char_pp),
+        ("n_keywords", ctypes.c_size_t),
+        ("path", ctypes.c_char_p),
+        ("secret_group_name", ctypes.c_char_p),
+        ("allow_rules", ctypes.POINTER(AllowRuleC)),
+        ("n_allow_rules", ctypes.c_size_t),
+        ("exclude_regexes", c_char_pp),
+        ("n_exclude_regexes", ctypes.c_size_t),
+    ]
+
+
+class FileC(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_uint64), ("path", ctypes.c_char_p)]
+
+
+class LocC(ctypes.Structure):
+    _fields_ = [("file", ctypes.c_uint32), ("rule", ctypes.c_uint32), ("start", ctypes.c_uint64),
+                ("end", ctypes.c_uint64), ("start_line", ctypes.c_uint32), ("end_line", ctypes.c_uint32)]
+
+
+class LineC(ctypes.Structure):
+    _fields_ = [("number", ctypes.c_uint32), ("content", ctypes.c_void_p), ("content_len", ctypes.c_size_t),
+                ("is_cause", ctypes.c_uint8), ("first_cause", ctypes.c_uint8), ("last_cause", ctypes.c_uint8)]
+
+
+class FindingC(ctypes.Structure):
+    _fields_ = [("file", ctypes.c_uint32), ("rule", ctypes.c_uint32), ("start_line", ctypes.c_uint32),
+                ("end_line", ctypes.c_uint32), ("match", ctypes.c_void_p), ("match_len", ctypes.c_size_t),
+                ("lines", ctypes.POINTER(LineC)), ("n_lines", ctypes.c_size_t),
+                ("start", ctypes.c_uint64), ("end", ctypes.c_uint64)]
+
+
+_SIGS = {
+    "tsg_version": (ctypes.c_char_p, []),
+    "tsg_last_error": (ctypes.c_char_p, []),
+    "tsg_ruleset_compile": (ctypes.c_int, [ctypes.POINTER(RuleC), ctypes.c_size_t, ctypes.POINTER(AllowRuleC),
+                                           ctypes.c_size_t, c_char_pp, ctypes.c_size_t,
+                                           ctypes.POINTER(ctypes.c_void_p), ctypes.c_char_p, ctypes.c_size_t]),
+    "tsg_ruleset_free": (None, [ctypes.c_void_p]),
+    "tsg_ruleset_rule_count": (ctypes.c_size_t, [ctypes.c_void_p]),
+    "tsg_ruleset_rule_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int),
+                                             ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                                             ctypes.POINTER(ctypes.c_size_t)]),
+    "tsg_engine_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "tsg_engine_free": (None, [ctypes.c_void_p]),
+    "tsg_scan": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(FileC), ctypes.c_size_t,
+                                ctypes.POINTER(ctypes.c_void_p)]),
+    "tsg_scan_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                       ctypes.POINTER(ctypes.c_void_p)]),
+    "tsg_result_loc_count": (ctypes.c_size_t, [ctypes.c_void_p]),
+    "tsg_result_locs": (ctypes.POINTER(LocC), [ctypes.c_void_p]),
+    "tsg_result_file_count": (ctypes.c_size_t, [ctypes.c_void_p]),
+    "tsg_result_file_flags": (ctypes.POINTER(ctypes.c_uint8), [ctypes.c_void_p]),
+    "tsg_result_findings": (ctypes.c_size_t, [ctypes.c_void_p, ctypes.c_size_t,
+                                              ctypes.POINTER(ctypes.POINTER(FindingC))]),
+    "tsg_result_timings": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_size_t,
+                                          ctypes.POINTER(ctypes.c_size_t)]),
+    "tsg_result_free": (None, [ctypes.c_void_p]),
+    "tsg_gate_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t]),
+    "tsg_regex_match": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t,
+                                       ctypes.POINTER(ctypes.c_int)]),
+    "tsg_regex_find_all": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t,
+                                          ctypes.POINTER(ctypes.c_int64), ctypes.c_size_t,
+                                          ctypes.POINTER(ctypes.c_size_t)]),
+}
+
+for _name, (_res, _args) in _SIGS.items():
+    _fn = getattr(lib, _name)  # AttributeError here = symbol missing from the .so
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+EXPORTED = sorted(_SIGS)
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[tsg {code}] {msg}")
+        self.code = code
+
+
+def check(rc):
+    if rc != TSG_OK:
+        raise EngineError(rc, lib.tsg_last_error().decode("utf-8", "replace"))
+
+
+def regex_find_all(pattern: str, text: bytes, cap: int = 1 << 16):
+    """Host compiler + VM diagnostics (FindAllIndex); not used by the scan path."""
+    arr = (ctypes.c_int64 * (2 * cap))()
+    n = ctypes.c_size_t()
+    check(lib.tsg_regex_find_all(pattern.encode(), text, len(text), arr, cap, ctypes.byref(n)))
+    return [[arr[2 * i], arr[2 * i + 1]] for i in range(min(n.value, cap))]
+
+
+def regex_match(pattern: str, text: bytes) -> bool:
+    m = ctypes.c_int()
+    check(lib.tsg_regex_match(pattern.encode(), text, len(text), ctypes.byref(m)))
+    return bool(m.value)

@@ -1,0 +1,146 @@
+// Internal structures of the MI355X secret engine (not part of the C ABI).
+#pragma once
+#include <cstdint>
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "gre.h"
+#include "trivy_secret_gpu.h"
+
+namespace tsg {
+
+constexpr int kAcMaxLit = 16;  // trie depth; longer keywords are confirmed on hit
+constexpr uint32_t kNoKw = 0xFFFFFFFFu;
+
+enum RuleMode : uint8_t { MODE_NEVER = 0, MODE_ANCHORED = 1, MODE_FULL = 2 };
+
+// ---- device-visible POD records ------------------------------------------
+struct RuleDev {
+  uint32_t prog;        // program index
+  uint32_t kw_off, kw_n;  // keyword ids (kw_n == 0 => no gate)
+  uint32_t gate_always;   // empty keyword present => gate passes
+  uint32_t mode;
+  uint32_t off_min, off_max;  // anchor offset range
+  uint64_t alpha[4];          // anchor prefix alphabet
+  uint32_t group_off, group_n;  // capture slots of groups named SecretGroupName
+  uint32_t allow_off, allow_n;  // per-rule allow regex progs
+  uint32_t use_groups;          // SecretGroupName != ""
+  uint32_t pad;
+};
+
+struct PatDev {
+  uint32_t len;        // full (lowercased) length
+  uint32_t kw;         // keyword id or kNoKw
+  uint32_t bytes_off;  // full lowercased bytes
+  uint32_t req_off;    // required-case bytes (0 = either case), valid if confirm
+  uint32_t rule_off, rule_n;  // rules anchored on this pattern
+  uint8_t special;
+  uint8_t confirm;  // anchor roles need a case check
+  uint8_t trunc;    // len > kAcMaxLit
+  uint8_t pad;
+};
+
+struct AcDev {
+  const uint16_t* delta;  // [nstates * nclasses], bit15 = output state
+  const uint8_t* cls;     // [256]
+  const uint32_t* out_off;  // [nstates + 1]
+  const uint16_t* out_pat;  // pattern ids
+  const PatDev* pats;
+  const uint8_t* pat_bytes;
+  const uint32_t* pat_rules;
+  uint32_t nstates, nclasses;
+};
+
+struct RuleSetDev {
+  const gre::ProgView* progs;
+  const RuleDev* rules;
+  const uint32_t* kw_ids;
+  const uint32_t* group_slots;
+  const uint32_t* allow_progs;   // per-rule allow lists
+  const uint32_t* global_allow;  // global allow regex progs
+  uint32_t n_global_allow;
+  uint32_t n_rules;
+  uint32_t kw_words;       // uint32 words of keyword bits per file
+  uint32_t max_ninst;      // for VM scratch sizing
+  uint32_t max_ncap;
+  AcDev ac;
+};
+
+// ---- host-side compiled ruleset -------------------------------------------
+struct RegexHost {
+  std::string src;
+  gre::Compiled c;
+};
+
+struct RuleHost {
+  std::string id;
+  int regex = -1;  // index into regexes, -1 => never matches
+  std::vector<std::string> keywords;
+  int path = -1;
+  std::string group_name;
+  std::vector<int> allow_regex;  // rule allow rules: regex
+  std::vector<int> allow_path;   // rule allow rules: path
+  std::vector<int> exclude;
+  RuleMode mode = MODE_NEVER;
+};
+
+struct AcHost {
+  std::vector<uint16_t> delta;
+  uint8_t cls[256];
+  std::vector<uint32_t> out_off;
+  std::vector<uint16_t> out_pat;
+  uint32_t nstates = 0, nclasses = 0;
+};
+
+struct PatternHost {
+  std::string lower;   // full lowercased pattern
+  std::string req;     // confirm spec (same length), '\0' = any case
+  int kw = -1;
+  bool special = false;
+  bool confirm = false;
+  bool any_anchor = false;
+  std::vector<uint32_t> rules;
+};
+
+}  // namespace tsg
+
+struct tsg_ruleset {
+  std::vector<tsg::RegexHost> regexes;
+  std::vector<tsg::RuleHost> rules;
+  std::vector<int> global_allow_regex;  // AllowRules with Regex
+  std::vector<int> global_allow_path;   // AllowRules with Path
+  std::vector<int> global_exclude;
+  std::vector<std::string> keywords;     // unique lowercased keywords
+  std::vector<tsg::PatternHost> patterns;
+  tsg::AcHost ac;
+  bool any_path_rules = false;  // some rule has Path or per-rule allow paths
+  bool any_exclude = false;
+  uint64_t id = 0;  // unique id for device-image caching
+};
+
+namespace tsg {
+bool build_ac(tsg_ruleset* rs, std::string* err);
+}
+
+namespace tsg {
+constexpr uint32_t kMaxCap = 64;  // capture slots of a SecretGroupName rule's regex
+
+struct ResultImpl {
+  std::vector<tsg_loc> locs;
+  std::vector<uint8_t> file_flags;
+  std::vector<std::vector<tsg_finding>> findings;  // per file, Scan order
+  std::deque<std::vector<tsg_line>> lines;          // stable backing store for findings
+  std::deque<std::string> strs;                     // stable backing store for strings
+  std::vector<double> timings;
+  bool have_findings = false;
+};
+
+// censorLocation + toFinding + findLocation + sort (scanner.go:425-537) on the
+// caller's host content.
+bool build_findings(ResultImpl* r, const tsg_ruleset* rs, const tsg_file* files, size_t n_files);
+}  // namespace tsg
+
+struct tsg_result {
+  tsg::ResultImpl impl;
+};

@@ -1,0 +1,1453 @@
+// engine.hip — MI355X (gfx950) secret-scanning pipeline + C ABI.
+//
+// Replaces the per-file loop of Scanner.Scan (pkg/fanal/secret/scanner.go:371-452)
+// with a batched device pipeline over a packed multi-file buffer in HBM:
+//
+//   k_path_gate   Global.AllowPath / Rule.MatchPath / Rule.AllowPath per file     (scanner.go:375,391,397)
+//   k_scan        one HBM pass: Aho-Corasick over ASCII-lowercased bytes of every
+//                 keyword (MatchKeywords gate bits, scanner.go:169-181), every rule's
+//                 anchor literal (hit records) and the fold-special sequences
+//   k_expand      anchor hits -> (rule, position) candidates for gated files
+//   k_full_jobs   rules without an anchor / files with special bytes -> full-scan jobs
+//   radix sort    candidates by (rule, position)
+//   k_verify      one lane per (file, rule) job: Go leftmost-first Pike VM restricted to
+//                 the anchor windows, FindAll iteration, allow rules, secret groups
+//                 (FindLocations / FindSubmatchLocations / AllowLocation, scanner.go:97-163)
+//   k_exclude     exclude-block FindAll for files with kept locations (scanner.go:232-270)
+//   k_lines       StartLine / EndLine of every kept location (findLocation, scanner.go:481-503)
+//
+// Host code (findings.cpp) then censors and cuts Match/Code from the caller's
+// content exactly like censorLocation/toFinding (scanner.go:425-537).
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+#include "pikevm.h"
+
+namespace tsg {
+void set_last_error(const std::string& m);
+}  // namespace tsg
+
+using namespace tsg;
+
+#define HIP_TRY(expr)                                                                 \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess) {                                                           \
+      set_last_error(std::string(#expr " failed: ") + hipGetErrorString(_e));         \
+      return TSG_ERR_DEVICE;                                                          \
+    }                                                                                 \
+  } while (0)
+
+namespace {
+
+constexpr uint32_t kFileAllowed = 1u;
+constexpr uint32_t kFileSpecial = 2u;
+constexpr uint32_t kFullFlag = 0x80000000u;
+constexpr int kPosBits = 44;
+constexpr uint64_t kPosMask = (1ull << kPosBits) - 1;
+
+// k_scan geometry: 256 threads = 4 waves; each lane owns a 128-byte chunk,
+// stored in LDS as a 144-byte row (16-byte halo of the previous chunk first).
+constexpr int kScanThreads = 256;
+constexpr int kChunk = 128;
+constexpr int kRow = kChunk + 16;
+constexpr int kBlockBytes = kScanThreads * kChunk;        // 32 KiB per block step
+constexpr int kSegsPerLane = kBlockBytes / 16 / kScanThreads;  // 8 x 16-byte loads
+constexpr int kTileLds = kScanThreads * kRow;              // 36 KiB
+constexpr int kLdsTableMax = 96 * 1024;
+
+struct Ctrl {
+  unsigned long long hits;
+  unsigned long long cands;
+  unsigned long long locs;
+  unsigned long long excl;
+  unsigned int err;
+  unsigned int pad;
+};
+
+struct DevLoc {
+  uint32_t file;
+  uint32_t rule;
+  uint64_t start, end;
+  uint32_t start_line, end_line;
+  uint32_t flags;  // 1 = secret group did not participate (reference panics)
+  uint32_t pad;
+};
+
+struct ScanParams {
+  const uint8_t* data;
+  const uint64_t* off;  // n_files + 1
+  uint64_t nbytes;
+  uint32_t n_files;
+  RuleSetDev rs;
+  uint32_t* file_kw;     // n_files * kw_words
+  uint32_t* file_flags;  // n_files
+  uint64_t* hits;
+  uint64_t hit_cap;
+  Ctrl* ctrl;
+};
+
+__device__ inline uint32_t find_file(const uint64_t* off, uint32_t lo, uint32_t hi, uint64_t pos) {
+  // largest f in [lo, hi) with off[f] <= pos
+  while (hi - lo > 1) {
+    uint32_t m = (lo + hi) >> 1;
+    if (off[m] <= pos) lo = m; else hi = m;
+  }
+  return lo;
+}
+
+__device__ inline uint8_t lower_ascii(uint8_t b) { return (b >= 'A' && b <= 'Z') ? b + 32 : b; }
+
+// Report every pattern ending at global position p (state has outputs).
+__device__ __noinline__ void report(const ScanParams& P, uint32_t st, uint64_t p, uint32_t fi,
+                                    uint64_t fstart, uint64_t fend, uint32_t* last_kw) {
+  const AcDev& ac = P.rs.ac;
+  uint32_t o0 = ac.out_off[st], o1 = ac.out_off[st + 1];
+  for (uint32_t o = o0; o < o1; ++o) {
+    uint32_t pid = ac.out_pat[o];
+    PatDev pd = ac.pats[pid];
+    uint32_t tl = pd.len < (uint32_t)kAcMaxLit ? pd.len : (uint32_t)kAcMaxLit;
+    uint64_t start = p + 1 - tl;
+    if (pd.trunc) {
+      if (start + pd.len > fend) continue;
+      bool ok = true;
+      const uint8_t* pb = ac.pat_bytes + pd.bytes_off;
+      for (uint32_t k = kAcMaxLit; k < pd.len && ok; ++k) ok = lower_ascii(P.data[start + k]) == pb[k];
+      if (!ok) continue;
+    }
+    if (pd.special) atomicOr(&P.file_flags[fi], kFileSpecial);
+    if (pd.kw != kNoKw) {
+      uint32_t key = (fi << 8) ^ pd.kw;  // cheap per-lane dedupe of repeated keywords
+      if (*last_kw != key) {
+        *last_kw = key;
+        atomicOr(&P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)], 1u << (pd.kw & 31));
+      }
+    }
+    if (pd.rule_n) {
+      if (pd.confirm) {
+        const uint8_t* rq = ac.pat_bytes + pd.req_off;
+        bool ok = true;
+        for (uint32_t k = 0; k < pd.len && ok; ++k) ok = rq[k] == 0 || P.data[start + k] == rq[k];
+        if (!ok) continue;
+      }
+      unsigned long long idx = atomicAdd(&P.ctrl->hits, 1ull);
+      if (idx < P.hit_cap) P.hits[idx] = (start << 16) | pid;
+    }
+  }
+}
+
+template <bool kLdsTable>
+__global__ __launch_bounds__(kScanThreads) void k_scan(ScanParams P) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  uint8_t* cls = smem;                  // 256
+  uint8_t* tile = smem + 256;           // kTileLds
+  uint16_t* dl = (uint16_t*)(smem + 256 + kTileLds);
+  const AcDev& ac = P.rs.ac;
+  const uint32_t K = ac.nclasses;
+  for (int i = threadIdx.x; i < 256; i += kScanThreads) cls[i] = ac.cls[i];
+  if (kLdsTable) {
+    const uint32_t n = ac.nstates * K;
+    for (uint32_t i = threadIdx.x; i < n; i += kScanThreads) dl[i] = ac.delta[i];
+  }
+  const uint16_t* delta = kLdsTable ? dl : ac.delta;
+  __shared__ uint32_t s_flo, s_fhi;
+  const uint32_t tid = threadIdx.x;
+  const uint64_t nsteps = (P.nbytes + kBlockBytes - 1) / kBlockBytes;
+  uint32_t last_kw = 0xFFFFFFFFu;
+
+  for (uint64_t step = blockIdx.x; step < nsteps; step += gridDim.x) {
+    const uint64_t base = step * kBlockBytes;
+    __syncthreads();
+    // ---- stage the 32 KiB block (+16 B halo) into padded LDS rows
+#pragma unroll
+    for (int k = 0; k < kSegsPerLane; ++k) {
+      const uint32_t seg = k * kScanThreads + tid;
+      const uint64_t g = base + (uint64_t)seg * 16;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (g + 16 <= P.nbytes) {
+        v = *(const uint4*)(P.data + g);
+      } else if (g < P.nbytes) {
+        uint8_t tmp[16] = {0};
+        for (uint64_t q = g; q < P.nbytes; ++q) tmp[q - g] = P.data[q];
+        memcpy(&v, tmp, 16);
+      }
+      const uint32_t row = seg >> 3, col = seg & 7;
+      *(uint4*)(tile + row * kRow + 16 + col * 16) = v;
+      if (col == 7 && row + 1 < (uint32_t)kScanThreads) *(uint4*)(tile + (row + 1) * kRow) = v;
+    }
+    if (tid == 0) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (base >= 16) v = *(const uint4*)(P.data + base - 16);
+      *(uint4*)(tile) = v;
+      uint64_t last = base + kBlockBytes - 1;
+      if (last >= P.nbytes) last = P.nbytes - 1;
+      s_flo = find_file(P.off, 0, P.n_files, base);
+      s_fhi = find_file(P.off, 0, P.n_files, last) + 1;
+    }
+    __syncthreads();
+    const uint64_t p0 = base + (uint64_t)tid * kChunk;
+    if (p0 >= P.nbytes) continue;
+    const uint64_t pend = p0 + kChunk < P.nbytes ? p0 + kChunk : P.nbytes;
+    uint32_t fi = find_file(P.off, s_flo, s_fhi, p0);
+    uint64_t fstart = P.off[fi], fend = P.off[fi + 1];
+    while (fend <= p0) {  // skip empty files at p0
+      ++fi;
+      fstart = fend;
+      fend = P.off[fi + 1];
+    }
+    const uint8_t* row = tile + tid * kRow + 16;
+    uint32_t st = 0;
+    // warm-up: the automaton started 15 bytes earlier (never across a file start)
+    const uint64_t w0 = (p0 - fstart) >= (uint64_t)(kAcMaxLit - 1) ? p0 - (kAcMaxLit - 1) : fstart;
+    for (uint64_t p = w0; p < p0; ++p) {
+      const uint8_t b = row[(int64_t)p - (int64_t)p0];
+      st = delta[st * K + cls[b]] & 0x7FFFu;
+    }
+    for (uint64_t p = p0; p < pend; ++p) {
+      while (p == fend) {
+        ++fi;
+        fstart = fend;
+        fend = P.off[fi + 1];
+        st = 0;
+      }
+      const uint8_t b = row[p - p0];
+      const uint32_t nx = delta[st * K + cls[b]];
+      st = nx & 0x7FFFu;
+      if (nx & 0x8000u) report(P, st, p, fi, fstart, fend, &last_kw);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- gating --
+struct GateParams {
+  const uint64_t* off;
+  const uint8_t* paths;
+  const uint64_t* path_off;
+  uint32_t n_files;
+  RuleSetDev rs;
+  const uint32_t* gpath;  // global allow path progs
+  uint32_t n_gpath;
+  const int32_t* rule_path;       // per rule: path prog or -1
+  const uint32_t* rule_apath_off;  // per rule: offset into rule_apath (n_rules+1)
+  const uint32_t* rule_apath;
+  uint32_t any_rule_paths;
+  uint32_t* file_flags;
+  uint32_t* path_mask;  // n_files * rule_words: bit set => rule skipped by path
+  uint32_t rule_words;
+  uint8_t* scratch;
+  uint64_t scratch_stride;
+};
+
+__device__ inline gre::VmScratch make_scratch(uint8_t* base, uint32_t P, uint32_t ncap) {
+  gre::VmScratch sc;
+  uint8_t* q = base;
+  auto take = [&](size_t bytes) {
+    uint8_t* r = q;
+    q += (bytes + 15) & ~(size_t)15;
+    return r;
+  };
+  sc.sparse[0] = (uint16_t*)take(2ull * P);
+  sc.sparse[1] = (uint16_t*)take(2ull * P);
+  sc.dense[0] = (uint16_t*)take(2ull * P);
+  sc.dense[1] = (uint16_t*)take(2ull * P);
+  sc.start[0] = (uint32_t*)take(4ull * P);
+  sc.start[1] = (uint32_t*)take(4ull * P);
+  sc.stack = (uint16_t*)take(2ull * (P + 1));
+  sc.cur = (int32_t*)take(4ull * ncap);
+  sc.capstack = (int32_t*)take(8ull * (P + 1));
+  sc.caps[0] = (int32_t*)take(4ull * P * ncap);
+  sc.caps[1] = (int32_t*)take(4ull * P * ncap);
+  return sc;
+}
+
+__host__ inline uint64_t scratch_bytes(uint32_t P, uint32_t ncap) {
+  auto r = [](uint64_t b) { return (b + 15) & ~15ull; };
+  return r(2ull * P) * 4 + r(4ull * P) * 2 + r(2ull * (P + 1)) + r(4ull * ncap) + r(8ull * (P + 1)) +
+         r(4ull * P * ncap) * 2 + 256;
+}
+
+__device__ inline bool match_string(const gre::ProgView& pv, const uint8_t* s, uint32_t n,
+                                    gre::VmScratch& sc) {
+  uint32_t ms, me;
+  return gre::vm_search(pv, s, n, 0, n, true, sc, &ms, &me);
+}
+
+__global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
+  const uint32_t nthreads = gridDim.x * blockDim.x;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  gre::VmScratch sc = make_scratch(G.scratch + (uint64_t)t * G.scratch_stride, G.rs.max_ninst, G.rs.max_ncap);
+  for (uint32_t f = t; f < G.n_files; f += nthreads) {
+    const uint8_t* path = G.paths + G.path_off[f];
+    const uint32_t plen = (uint32_t)(G.path_off[f + 1] - G.path_off[f]);
+    bool allowed = false;
+    for (uint32_t k = 0; k < G.n_gpath && !allowed; ++k)
+      allowed = match_string(G.rs.progs[G.gpath[k]], path, plen, sc);
+    if (allowed) {
+      G.file_flags[f] |= kFileAllowed;
+      continue;
+    }
+    if (!G.any_rule_paths) continue;
+    for (uint32_t r = 0; r < G.rs.n_rules; ++r) {
+      bool skip = false;
+      if (G.rule_path[r] >= 0) skip = !match_string(G.rs.progs[G.rule_path[r]], path, plen, sc);
+      for (uint32_t k = G.rule_apath_off[r]; k < G.rule_apath_off[r + 1] && !skip; ++k)
+        skip = match_string(G.rs.progs[G.rule_apath[k]], path, plen, sc);
+      if (skip) G.path_mask[(size_t)f * G.rule_words + (r >> 5)] |= 1u << (r & 31);
+    }
+  }
+}
+
+struct ExpandParams {
+  const uint64_t* off;
+  uint32_t n_files;
+  RuleSetDev rs;
+  const uint32_t* file_kw;
+  const uint32_t* file_flags;
+  const uint32_t* path_mask;  // may be null
+  uint32_t rule_words;
+  const uint64_t* hits;
+  uint64_t n_hits;
+  uint64_t* keys;
+  uint32_t* vals;
+  uint64_t cand_cap;
+  Ctrl* ctrl;
+  const uint32_t* full_rules;  // rules in MODE_FULL
+  uint32_t n_full_rules;
+};
+
+__device__ inline bool rule_gate(const RuleSetDev& rs, const RuleDev& r, const uint32_t* kw) {
+  if (r.kw_n == 0 || r.gate_always) return true;
+  for (uint32_t k = 0; k < r.kw_n; ++k) {
+    const uint32_t id = rs.kw_ids[r.kw_off + k];
+    if ((kw[id >> 5] >> (id & 31)) & 1) return true;
+  }
+  return false;
+}
+
+__device__ inline void emit_cand(const ExpandParams& E, uint32_t rule, uint64_t gpos, uint32_t val) {
+  unsigned long long idx = atomicAdd(&E.ctrl->cands, 1ull);
+  if (idx < E.cand_cap) {
+    E.keys[idx] = ((uint64_t)rule << kPosBits) | gpos;
+    E.vals[idx] = val;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_expand(ExpandParams E) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E.n_hits) return;
+  const uint64_t h = E.hits[i];
+  const uint64_t gpos = h >> 16;
+  const uint32_t pid = (uint32_t)(h & 0xFFFF);
+  const uint32_t fi = find_file(E.off, 0, E.n_files, gpos);
+  const uint32_t fl = E.file_flags[fi];
+  if (fl & (kFileAllowed | kFileSpecial)) return;
+  const PatDev pd = E.rs.ac.pats[pid];
+  const uint32_t* kw = E.file_kw + (size_t)fi * E.rs.kw_words;
+  for (uint32_t k = 0; k < pd.rule_n; ++k) {
+    const uint32_t r = E.rs.ac.pat_rules[pd.rule_off + k];
+    if (E.path_mask && ((E.path_mask[(size_t)fi * E.rule_words + (r >> 5)] >> (r & 31)) & 1)) continue;
+    if (!rule_gate(E.rs, E.rs.rules[r], kw)) continue;
+    emit_cand(E, r, gpos, fi);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_full_jobs(ExpandParams E) {
+  const uint32_t fi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (fi >= E.n_files) return;
+  const uint32_t fl = E.file_flags[fi];
+  if (fl & kFileAllowed) return;
+  const uint32_t* kw = E.file_kw + (size_t)fi * E.rs.kw_words;
+  const uint64_t fstart = E.off[fi];
+  if (fl & kFileSpecial) {
+    for (uint32_t r = 0; r < E.rs.n_rules; ++r) {
+      const RuleDev& rd = E.rs.rules[r];
+      if (rd.mode == MODE_NEVER) continue;
+      if (E.path_mask && ((E.path_mask[(size_t)fi * E.rule_words + (r >> 5)] >> (r & 31)) & 1)) continue;
+      if (!rule_gate(E.rs, rd, kw)) continue;
+      emit_cand(E, r, fstart, fi | kFullFlag);
+    }
+    return;
+  }
+  for (uint32_t k = 0; k < E.n_full_rules; ++k) {
+    const uint32_t r = E.full_rules[k];
+    if (E.path_mask && ((E.path_mask[(size_t)fi * E.rule_words + (r >> 5)] >> (r & 31)) & 1)) continue;
+    if (!rule_gate(E.rs, E.rs.rules[r], kw)) continue;
+    emit_cand(E, r, fstart, fi | kFullFlag);
+  }
+}
+
+__global__ void k_mark_jobs(const uint64_t* keys, const uint32_t* vals, uint64_t n, uint8_t* flags) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t f = 1;
+  if (i > 0) {
+    f = ((keys[i] >> kPosBits) != (keys[i - 1] >> kPosBits)) ||
+        ((vals[i] & ~kFullFlag) != (vals[i - 1] & ~kFullFlag));
+  }
+  flags[i] = f;
+}
+
+// ----------------------------------------------------------------- verify --
+struct VerifyParams {
+  const uint8_t* data;
+  const uint64_t* off;
+  RuleSetDev rs;
+  const uint64_t* keys;
+  const uint32_t* vals;
+  uint64_t n_cands;
+  const uint32_t* job_start;
+  uint32_t n_jobs;
+  DevLoc* locs;
+  uint64_t loc_cap;
+  Ctrl* ctrl;
+  uint8_t* scratch;
+  uint64_t scratch_stride;
+};
+
+// Candidate start windows of one (file, rule) job, in increasing order
+// (DESIGN.md "anchor windows").
+struct IvIter {
+  const uint64_t* keys;
+  uint64_t ci, c1;
+  uint64_t fstart;
+  const uint8_t* text;
+  uint32_t n;
+  uint32_t a, b;
+  const uint64_t* alpha;
+  uint32_t h_prev, p_prev;
+  bool have_prev;
+  // current merged view
+  bool have;
+  uint32_t cs, ce;
+
+  __device__ bool in_alpha(uint8_t c) const { return (alpha[c >> 6] >> (c & 63)) & 1; }
+
+  __device__ bool next_raw(uint32_t* ws, uint32_t* we) {
+    while (ci < c1) {
+      const uint32_t h = (uint32_t)((keys[ci++] & kPosMask) - fstart);
+      if (h < a) continue;
+      const uint32_t lo = (b == gre::kInf || h < b) ? 0u : h - b;
+      uint32_t p;
+      if (have_prev && h_prev <= h) {
+        uint32_t q = h;
+        while (q > h_prev && in_alpha(text[q - 1])) --q;
+        p = (q == h_prev) ? (p_prev > lo ? p_prev : lo) : q;
+      } else {
+        uint32_t q = h;
+        while (q > lo && in_alpha(text[q - 1])) --q;
+        p = q;
+      }
+      if (p < lo) p = lo;
+      have_prev = true;
+      h_prev = h;
+      p_prev = p;
+      const uint32_t wend = h - a;
+      while (p <= wend && !gre::is_rune_start(text, n, p)) ++p;
+      if (p > wend) continue;
+      *ws = p;
+      *we = wend;
+      return true;
+    }
+    return false;
+  }
+  __device__ void advance() { have = next_raw(&cs, &ce); }
+  // Start-permission protocol used by vm_search_starts.
+  __device__ bool skip_to(uint32_t pos, uint32_t* np) {
+    while (have && ce < pos) advance();
+    if (!have) return false;
+    *np = pos < cs ? cs : pos;
+    return true;
+  }
+  __device__ bool allowed(uint32_t pos) {
+    while (have && ce < pos) advance();
+    return have && cs <= pos && pos <= ce;
+  }
+};
+
+struct LimitStarts {
+  uint32_t limit;
+  __device__ bool skip_to(uint32_t pos, uint32_t* np) {
+    if (pos > limit) return false;
+    *np = pos;
+    return true;
+  }
+  __device__ bool allowed(uint32_t pos) { return pos <= limit; }
+};
+
+// vm_search with a start-position oracle (anchor windows or a plain limit);
+// when no thread is alive the VM jumps to the next permitted start.
+template <class Starts>
+__device__ bool vm_search_starts(const gre::ProgView& p, const uint8_t* text, uint32_t n, uint32_t pos0,
+                                 Starts& S, gre::VmScratch& sc, uint32_t* ms, uint32_t* me) {
+  gre::Queue q[2] = {{sc.sparse[0], sc.dense[0], sc.start[0], nullptr, 0},
+                     {sc.sparse[1], sc.dense[1], sc.start[1], nullptr, 0}};
+  int cur = 0;
+  bool matched = false;
+  uint32_t pos = pos0;
+  uint32_t w = 0, w1 = 0;
+  int r = gre::decode_rune(text, n, pos, &w);
+  int r1 = r >= 0 ? gre::decode_rune(text, n, pos + w, &w1) : -1;
+  uint8_t ctx = gre::empty_ctx(gre::prev_ctx_rune(text, pos), r);
+  for (;;) {
+    gre::Queue& runq = q[cur];
+    gre::Queue& nextq = q[cur ^ 1];
+    if (runq.n == 0) {
+      if (matched) break;
+      uint32_t np;
+      if (!S.skip_to(pos, &np)) break;
+      if (np != pos) {
+        pos = np;
+        r = gre::decode_rune(text, n, pos, &w);
+        r1 = r >= 0 ? gre::decode_rune(text, n, pos + w, &w1) : -1;
+        ctx = gre::empty_ctx(gre::prev_ctx_rune(text, pos), r);
+      }
+    }
+    if (!matched && S.allowed(pos)) gre::vm_add(p, runq, sc.stack, p.start, pos, ctx);
+    const uint8_t nctx = gre::empty_ctx(r, r1);
+    nextq.n = 0;
+    for (uint32_t j = 0; j < runq.n; ++j) {
+      const gre::Inst in = p.inst[runq.dense[j]];
+      if (in.op == gre::I_MATCH) {
+        *ms = runq.start[j];
+        *me = pos;
+        matched = true;
+        break;
+      }
+      if (gre::inst_consumes(in, p, r)) gre::vm_add(p, nextq, sc.stack, in.out, runq.start[j], nctx);
+    }
+    runq.n = 0;
+    if (w == 0) break;
+    pos += w;
+    r = r1;
+    w = w1;
+    r1 = r >= 0 ? gre::decode_rune(text, n, pos + w, &w1) : -1;
+    ctx = nctx;
+    cur ^= 1;
+  }
+  return matched;
+}
+
+__device__ void emit_match(const VerifyParams& V, const RuleDev& rd, uint32_t rule, uint32_t fi,
+                           const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me,
+                           gre::VmScratch& sc) {
+  // AllowLocation (scanner.go:145-148): global then rule allow regexes on the whole match
+  for (uint32_t k = 0; k < V.rs.n_global_allow; ++k)
+    if (match_string(V.rs.progs[V.rs.global_allow[k]], text + ms, me - ms, sc)) return;
+  for (uint32_t k = 0; k < rd.allow_n; ++k)
+    if (match_string(V.rs.progs[V.rs.allow_progs[rd.allow_off + k]], text + ms, me - ms, sc)) return;
+  if (!rd.use_groups) {
+    unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
+    if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, ms, me, 0, 0, 0, 0};
+    return;
+  }
+  const gre::ProgView& pv = V.rs.progs[rd.prog];
+  int32_t out[kMaxCap];  // ncap <= kMaxCap is enforced by the rule compiler
+  bool ok = gre::vm_captures(pv, text, n, ms, sc, out);
+  if (!ok || (uint32_t)out[1] != me) atomicOr(&V.ctrl->err, 1u);
+  for (uint32_t g = 0; g < rd.group_n; ++g) {
+    const uint32_t slot = V.rs.group_slots[rd.group_off + g];
+    const int32_t s = out[2 * slot], e = out[2 * slot + 1];
+    unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
+    if (idx < V.loc_cap) {
+      if (s < 0 || e < 0) V.locs[idx] = DevLoc{fi, rule, 0, 0, 0, 0, 1, 0};
+      else V.locs[idx] = DevLoc{fi, rule, (uint64_t)s, (uint64_t)e, 0, 0, 0, 0};
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_verify(VerifyParams V) {
+  const uint32_t nthreads = gridDim.x * blockDim.x;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  gre::VmScratch sc = make_scratch(V.scratch + (uint64_t)t * V.scratch_stride, V.rs.max_ninst, V.rs.max_ncap);
+  for (uint32_t j = t; j < V.n_jobs; j += nthreads) {
+    const uint64_t c0 = V.job_start[j];
+    const uint64_t c1 = (j + 1 < V.n_jobs) ? V.job_start[j + 1] : V.n_cands;
+    const uint32_t rule = (uint32_t)(V.keys[c0] >> kPosBits);
+    const uint32_t fi = V.vals[c0] & ~kFullFlag;
+    bool full = false;
+    for (uint64_t c = c0; c < c1 && !full; ++c) full = (V.vals[c] & kFullFlag) != 0;
+    const RuleDev rd = V.rs.rules[rule];
+    const gre::ProgView& pv = V.rs.progs[rd.prog];
+    const uint64_t fstart = V.off[fi];
+    const uint8_t* text = V.data + fstart;
+    const uint32_t n = (uint32_t)(V.off[fi + 1] - fstart);
+    uint32_t ms, me;
+    if (full) {
+      // regexp.go allMatches over the whole file
+      uint32_t pos = 0;
+      int64_t prev_end = -1;
+      while (pos <= n) {
+        LimitStarts ls{n};
+        if (!vm_search_starts(pv, text, n, pos, ls, sc, &ms, &me)) break;
+        bool accept = true;
+        if (me == pos) {
+          if ((int64_t)ms == prev_end) accept = false;
+          uint32_t w;
+          gre::decode_rune(text, n, pos, &w);
+          pos = w > 0 ? pos + w : n + 1;
+        } else {
+          pos = me;
+        }
+        prev_end = me;
+        if (accept) emit_match(V, rd, rule, fi, text, n, ms, me, sc);
+      }
+    } else {
+      IvIter it;
+      it.keys = V.keys;
+      it.ci = c0;
+      it.c1 = c1;
+      it.fstart = fstart;
+      it.text = text;
+      it.n = n;
+      it.a = rd.off_min;
+      it.b = rd.off_max;
+      it.alpha = V.rs.rules[rule].alpha;
+      it.have_prev = false;
+      it.h_prev = it.p_prev = 0;
+      it.advance();
+      uint32_t pos = 0;
+      while (it.have) {
+        if (!vm_search_starts(pv, text, n, pos, it, sc, &ms, &me)) break;
+        emit_match(V, rd, rule, fi, text, n, ms, me, sc);
+        if (me == ms) break;  // cannot happen for anchored rules (non-empty literal)
+        pos = me;
+      }
+    }
+  }
+}
+
+// --------------------------------------------------------------- exclude --
+struct ExclJob {
+  uint32_t file;
+  uint32_t prog;
+  uint32_t tag;  // index of the (file, scope) group the ranges belong to
+  uint32_t pad;
+};
+struct ExclRange {
+  uint32_t tag;
+  uint32_t pad;
+  uint64_t s, e;
+};
+
+__global__ __launch_bounds__(256) void k_exclude(const uint8_t* data, const uint64_t* off, RuleSetDev rs,
+                                                 const ExclJob* jobs, uint32_t n_jobs, ExclRange* out,
+                                                 uint64_t cap, Ctrl* ctrl, uint8_t* scratch,
+                                                 uint64_t stride) {
+  const uint32_t nthreads = gridDim.x * blockDim.x;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  gre::VmScratch sc = make_scratch(scratch + (uint64_t)t * stride, rs.max_ninst, rs.max_ncap);
+  for (uint32_t j = t; j < n_jobs; j += nthreads) {
+    const ExclJob jb = jobs[j];
+    const uint8_t* text = data + off[jb.file];
+    const uint32_t n = (uint32_t)(off[jb.file + 1] - off[jb.file]);
+    const gre::ProgView& pv = rs.progs[jb.prog];
+    uint32_t pos = 0, ms, me;
+    int64_t prev_end = -1;
+    while (pos <= n) {
+      LimitStarts ls{n};
+      if (!vm_search_starts(pv, text, n, pos, ls, sc, &ms, &me)) break;
+      bool accept = true;
+      if (me == pos) {
+        if ((int64_t)ms == prev_end) accept = false;
+        uint32_t w;
+        gre::decode_rune(text, n, pos, &w);
+        pos = w > 0 ? pos + w : n + 1;
+      } else {
+        pos = me;
+      }
+      prev_end = me;
+      if (accept) {
+        unsigned long long idx = atomicAdd(&ctrl->excl, 1ull);
+        if (idx < cap) out[idx] = ExclRange{jb.tag, 0, ms, me};
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------- lines --
+// One wave per location: StartLine = 1 + count('\n' in [0,start)),
+// EndLine = StartLine + count('\n' in [start,end)) (scanner.go:482,503).
+__global__ __launch_bounds__(256) void k_lines(const uint8_t* data, const uint64_t* off, DevLoc* locs,
+                                               uint64_t n_locs) {
+  const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  if (w >= n_locs) return;
+  DevLoc L = locs[w];
+  if (L.flags) return;
+  const uint8_t* text = data + off[L.file];
+  uint32_t c1 = 0, c2 = 0;
+  for (uint64_t i = lane; i < L.end; i += 64) {
+    const uint32_t nl = text[i] == '\n';
+    if (i < L.start) c1 += nl; else c2 += nl;
+  }
+  for (int d = 32; d > 0; d >>= 1) {
+    c1 += __shfl_down(c1, d);
+    c2 += __shfl_down(c2, d);
+  }
+  if (lane == 0) {
+    locs[w].start_line = c1 + 1;
+    locs[w].end_line = c1 + 1 + c2;
+  }
+}
+
+}  // namespace
+
+// =========================================================== host side ======
+
+
+namespace {
+
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t want) {
+    if (want <= n) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    size_t cap = want + want / 4 + 64;
+    hipError_t e = hipMalloc(&p, cap * sizeof(T));
+    if (e == hipSuccess) n = cap;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+struct DevImage {
+  uint64_t rs_id = 0;
+  DBuf<gre::Inst> inst;
+  DBuf<gre::ClassDesc> classes;
+  DBuf<uint32_t> ranges;
+  DBuf<gre::ProgView> progs;
+  DBuf<RuleDev> rules;
+  DBuf<uint32_t> u32;  // kw_ids | group_slots | allow_progs | global_allow | gpath | rule_apath_off | rule_apath | full_rules
+  DBuf<int32_t> rule_path;
+  DBuf<uint16_t> delta;
+  DBuf<uint8_t> cls;
+  DBuf<uint32_t> out_off;
+  DBuf<uint16_t> out_pat;
+  DBuf<PatDev> pats;
+  DBuf<uint8_t> pat_bytes;
+  DBuf<uint32_t> pat_rules;
+  RuleSetDev view{};
+  // offsets into u32
+  uint32_t o_gpath = 0, n_gpath = 0, o_apoff = 0, o_ap = 0, o_full = 0, n_full = 0;
+  void release() {
+    inst.release(); classes.release(); ranges.release(); progs.release(); rules.release();
+    u32.release(); rule_path.release(); delta.release(); cls.release(); out_off.release();
+    out_pat.release(); pats.release(); pat_bytes.release(); pat_rules.release();
+  }
+};
+
+}  // namespace
+
+struct tsg_engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  DevImage img;
+  DBuf<uint8_t> data;
+  DBuf<uint64_t> off;
+  DBuf<uint8_t> paths;
+  DBuf<uint64_t> path_off;
+  DBuf<uint32_t> file_kw, file_flags, path_mask;
+  DBuf<uint64_t> hits;
+  DBuf<uint64_t> keys, keys2;
+  DBuf<uint32_t> vals, vals2;
+  DBuf<uint8_t> flags8;
+  DBuf<uint32_t> job_start;
+  DBuf<uint32_t> nsel;
+  DBuf<uint8_t> cub_tmp;
+  DBuf<DevLoc> locs;
+  DBuf<uint8_t> scratch;
+  DBuf<Ctrl> ctrl;
+  DBuf<ExclJob> excl_jobs;
+  DBuf<ExclRange> excl_out;
+  uint32_t vm_threads = 0;
+  uint64_t scratch_stride = 0;
+  hipEvent_t ev[12];
+  bool events = false;
+};
+
+namespace {
+
+int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
+  DevImage& im = e->img;
+  if (im.rs_id == rs->id) return TSG_OK;
+  // ---- programs
+  std::vector<gre::Inst> inst;
+  std::vector<gre::ClassDesc> classes;
+  std::vector<uint32_t> ranges;
+  struct Off { size_t i, c, r; };
+  std::vector<Off> offs;
+  uint32_t max_ninst = 1, max_ncap = 2;
+  for (auto& rx : rs->regexes) {
+    const gre::Prog& p = rx.c.prog;
+    offs.push_back({inst.size(), classes.size(), ranges.size()});
+    inst.insert(inst.end(), p.inst.begin(), p.inst.end());
+    for (auto cd : p.classes) {
+      cd.range_off += (uint32_t)ranges.size();
+      classes.push_back(cd);
+    }
+    ranges.insert(ranges.end(), p.ranges.begin(), p.ranges.end());
+    max_ninst = std::max<uint32_t>(max_ninst, (uint32_t)p.inst.size());
+  }
+  for (auto& r : rs->rules)
+    if (!r.group_name.empty() && r.regex >= 0)
+      max_ncap = std::max<uint32_t>(max_ncap, (uint32_t)rs->regexes[r.regex].c.prog.ncap);
+  HIP_TRY(im.inst.ensure(inst.size() + 1));
+  HIP_TRY(im.classes.ensure(classes.size() + 1));
+  HIP_TRY(im.ranges.ensure(ranges.size() + 1));
+  HIP_TRY(hipMemcpy(im.inst.p, inst.data(), inst.size() * sizeof(gre::Inst), hipMemcpyHostToDevice));
+  if (!classes.empty())
+    HIP_TRY(hipMemcpy(im.classes.p, classes.data(), classes.size() * sizeof(gre::ClassDesc), hipMemcpyHostToDevice));
+  if (!ranges.empty())
+    HIP_TRY(hipMemcpy(im.ranges.p, ranges.data(), ranges.size() * 4, hipMemcpyHostToDevice));
+  std::vector<gre::ProgView> views;
+  for (size_t k = 0; k < rs->regexes.size(); ++k) {
+    const gre::Prog& p = rs->regexes[k].c.prog;
+    views.push_back(gre::ProgView{im.inst.p + offs[k].i, im.classes.p + offs[k].c, im.ranges.p,
+                                  (uint32_t)p.inst.size(), p.start, (uint32_t)p.ncap});
+  }
+  HIP_TRY(im.progs.ensure(views.size() + 1));
+  if (!views.empty())
+    HIP_TRY(hipMemcpy(im.progs.p, views.data(), views.size() * sizeof(gre::ProgView), hipMemcpyHostToDevice));
+  // ---- rules + u32 side tables
+  std::vector<uint32_t> u32;
+  std::vector<RuleDev> rules;
+  std::vector<int32_t> rule_path;
+  std::map<std::string, uint32_t> kwid;
+  for (size_t k = 0; k < rs->keywords.size(); ++k) kwid[rs->keywords[k]] = (uint32_t)k;
+  std::vector<uint32_t> kw_ids, group_slots, allow_progs, apath_off, apath, full_rules;
+  for (size_t ri = 0; ri < rs->rules.size(); ++ri) {
+    const RuleHost& r = rs->rules[ri];
+    RuleDev d{};
+    d.prog = r.regex >= 0 ? (uint32_t)r.regex : 0;
+    d.mode = r.mode;
+    d.kw_off = (uint32_t)kw_ids.size();
+    for (auto& kw : r.keywords) {
+      if (kw.empty()) d.gate_always = 1;
+      else kw_ids.push_back(kwid[kw]);
+    }
+    d.kw_n = (uint32_t)kw_ids.size() - d.kw_off;
+    if (r.keywords.empty()) d.kw_n = 0;
+    if (r.regex >= 0) {
+      const gre::Compiled& c = rs->regexes[r.regex].c;
+      if (c.anchor.valid) {
+        d.off_min = c.anchor.off_min;
+        d.off_max = c.anchor.off_max;
+        for (int q = 0; q < 4; ++q) d.alpha[q] = c.anchor.alpha.w[q];
+      }
+      d.use_groups = !r.group_name.empty();
+      d.group_off = (uint32_t)group_slots.size();
+      if (d.use_groups)
+        for (size_t g = 0; g < c.prog.cap_names.size(); ++g)
+          if (c.prog.cap_names[g] == r.group_name) group_slots.push_back((uint32_t)g);
+      d.group_n = (uint32_t)group_slots.size() - d.group_off;
+    }
+    d.allow_off = (uint32_t)allow_progs.size();
+    for (int x : r.allow_regex) allow_progs.push_back((uint32_t)x);
+    d.allow_n = (uint32_t)allow_progs.size() - d.allow_off;
+    rules.push_back(d);
+    rule_path.push_back(r.path);
+    apath_off.push_back((uint32_t)apath.size());
+    for (int x : r.allow_path) apath.push_back((uint32_t)x);
+    if (r.mode == MODE_FULL) full_rules.push_back((uint32_t)ri);
+  }
+  apath_off.push_back((uint32_t)apath.size());
+  auto append = [&](const std::vector<uint32_t>& v) {
+    uint32_t o = (uint32_t)u32.size();
+    u32.insert(u32.end(), v.begin(), v.end());
+    return o;
+  };
+  uint32_t o_kw = append(kw_ids), o_gs = append(group_slots), o_ap = append(allow_progs);
+  std::vector<uint32_t> gallow(rs->global_allow_regex.begin(), rs->global_allow_regex.end());
+  std::vector<uint32_t> gpath(rs->global_allow_path.begin(), rs->global_allow_path.end());
+  uint32_t o_ga = append(gallow);
+  im.o_gpath = append(gpath);
+  im.n_gpath = (uint32_t)gpath.size();
+  im.o_apoff = append(apath_off);
+  im.o_ap = append(apath);
+  im.o_full = append(full_rules);
+  im.n_full = (uint32_t)full_rules.size();
+  HIP_TRY(im.u32.ensure(u32.size() + 1));
+  if (!u32.empty()) HIP_TRY(hipMemcpy(im.u32.p, u32.data(), u32.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(im.rules.ensure(rules.size() + 1));
+  if (!rules.empty())
+    HIP_TRY(hipMemcpy(im.rules.p, rules.data(), rules.size() * sizeof(RuleDev), hipMemcpyHostToDevice));
+  HIP_TRY(im.rule_path.ensure(rule_path.size() + 1));
+  if (!rule_path.empty())
+    HIP_TRY(hipMemcpy(im.rule_path.p, rule_path.data(), rule_path.size() * 4, hipMemcpyHostToDevice));
+  // ---- automaton
+  const AcHost& ac = rs->ac;
+  HIP_TRY(im.delta.ensure(ac.delta.size()));
+  HIP_TRY(hipMemcpy(im.delta.p, ac.delta.data(), ac.delta.size() * 2, hipMemcpyHostToDevice));
+  HIP_TRY(im.cls.ensure(256));
+  HIP_TRY(hipMemcpy(im.cls.p, ac.cls, 256, hipMemcpyHostToDevice));
+  HIP_TRY(im.out_off.ensure(ac.out_off.size()));
+  HIP_TRY(hipMemcpy(im.out_off.p, ac.out_off.data(), ac.out_off.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(im.out_pat.ensure(ac.out_pat.size() + 1));
+  if (!ac.out_pat.empty())
+    HIP_TRY(hipMemcpy(im.out_pat.p, ac.out_pat.data(), ac.out_pat.size() * 2, hipMemcpyHostToDevice));
+  std::vector<PatDev> pats;
+  std::vector<uint8_t> pbytes;
+  std::vector<uint32_t> prules;
+  for (auto& p : rs->patterns) {
+    PatDev d{};
+    d.len = (uint32_t)p.lower.size();
+    d.kw = p.kw >= 0 ? (uint32_t)p.kw : kNoKw;
+    d.bytes_off = (uint32_t)pbytes.size();
+    pbytes.insert(pbytes.end(), p.lower.begin(), p.lower.end());
+    d.req_off = (uint32_t)pbytes.size();
+    pbytes.insert(pbytes.end(), p.req.begin(), p.req.end());
+    d.rule_off = (uint32_t)prules.size();
+    prules.insert(prules.end(), p.rules.begin(), p.rules.end());
+    d.rule_n = (uint32_t)p.rules.size();
+    d.special = p.special;
+    d.confirm = p.confirm;
+    d.trunc = p.lower.size() > (size_t)kAcMaxLit;
+    pats.push_back(d);
+  }
+  HIP_TRY(im.pats.ensure(pats.size() + 1));
+  HIP_TRY(hipMemcpy(im.pats.p, pats.data(), pats.size() * sizeof(PatDev), hipMemcpyHostToDevice));
+  HIP_TRY(im.pat_bytes.ensure(pbytes.size() + 1));
+  if (!pbytes.empty()) HIP_TRY(hipMemcpy(im.pat_bytes.p, pbytes.data(), pbytes.size(), hipMemcpyHostToDevice));
+  HIP_TRY(im.pat_rules.ensure(prules.size() + 1));
+  if (!prules.empty())
+    HIP_TRY(hipMemcpy(im.pat_rules.p, prules.data(), prules.size() * 4, hipMemcpyHostToDevice));
+  // ---- view
+  RuleSetDev& v = im.view;
+  v.progs = im.progs.p;
+  v.rules = im.rules.p;
+  v.kw_ids = im.u32.p + o_kw;
+  v.group_slots = im.u32.p + o_gs;
+  v.allow_progs = im.u32.p + o_ap;
+  v.global_allow = im.u32.p + o_ga;
+  v.n_global_allow = (uint32_t)gallow.size();
+  v.n_rules = (uint32_t)rs->rules.size();
+  v.kw_words = std::max<uint32_t>(1, ((uint32_t)rs->keywords.size() + 31) / 32);
+  v.max_ninst = max_ninst;
+  v.max_ncap = max_ncap;
+  v.ac = AcDev{im.delta.p, im.cls.p, im.out_off.p, im.out_pat.p, im.pats.p, im.pat_bytes.p, im.pat_rules.p,
+               ac.nstates, ac.nclasses};
+  im.rs_id = rs->id;
+  // VM scratch
+  e->scratch_stride = (scratch_bytes(max_ninst, max_ncap) + 255) & ~255ull;
+  return TSG_OK;
+}
+
+int read_ctrl(tsg_engine* e, Ctrl* h) {
+  HIP_TRY(hipMemcpyAsync(h, e->ctrl.p, sizeof(Ctrl), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return TSG_OK;
+}
+
+// Run the device pipeline on a batch already in HBM.  Fills r->impl.locs and flags.
+int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, const uint64_t* d_off,
+                 const uint8_t* d_paths, const uint64_t* d_path_off, size_t n_files, uint64_t nbytes,
+                 tsg_result* res) {
+  int rc = upload_ruleset(e, rs);
+  if (rc) return rc;
+  const DevImage& im = e->img;
+  const RuleSetDev& RS = im.view;
+  hipStream_t s = e->stream;
+  const uint32_t nf = (uint32_t)n_files;
+  const uint32_t rule_words = std::max<uint32_t>(1, (RS.n_rules + 31) / 32);
+  HIP_TRY(e->ctrl.ensure(1));
+  HIP_TRY(e->file_kw.ensure((size_t)nf * RS.kw_words + 1));
+  HIP_TRY(e->file_flags.ensure(nf + 1));
+  if (rs->any_path_rules) HIP_TRY(e->path_mask.ensure((size_t)nf * rule_words + 1));
+  HIP_TRY(hipMemsetAsync(e->ctrl.p, 0, sizeof(Ctrl), s));
+  HIP_TRY(hipMemsetAsync(e->file_kw.p, 0, ((size_t)nf * RS.kw_words + 1) * 4, s));
+  HIP_TRY(hipMemsetAsync(e->file_flags.p, 0, (nf + 1) * 4, s));
+  if (rs->any_path_rules) HIP_TRY(hipMemsetAsync(e->path_mask.p, 0, ((size_t)nf * rule_words + 1) * 4, s));
+  // VM thread pool for path gate / verify / exclude
+  if (!e->vm_threads) {
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, e->device));
+    e->vm_threads = (uint32_t)prop.multiProcessorCount * 128;  // 2 waves per CU
+  }
+  HIP_TRY(e->scratch.ensure((size_t)e->vm_threads * e->scratch_stride));
+  std::vector<double>& tm = res->impl.timings;
+  tm.assign(8, 0.0);
+  if (!e->events) {
+    for (auto& ev : e->ev) HIP_TRY(hipEventCreate(&ev));
+    e->events = true;
+  }
+  HIP_TRY(hipEventRecord(e->ev[0], s));
+  // ---- 1. path gates
+  if (nf && (im.n_gpath || rs->any_path_rules)) {
+    GateParams G{};
+    G.off = d_off;
+    G.paths = d_paths;
+    G.path_off = d_path_off;
+    G.n_files = nf;
+    G.rs = RS;
+    G.gpath = im.u32.p + im.o_gpath;
+    G.n_gpath = im.n_gpath;
+    G.rule_path = im.rule_path.p;
+    G.rule_apath_off = im.u32.p + im.o_apoff;
+    G.rule_apath = im.u32.p + im.o_ap;
+    G.any_rule_paths = rs->any_path_rules;
+    G.file_flags = e->file_flags.p;
+    G.path_mask = e->path_mask.p;
+    G.rule_words = rule_words;
+    G.scratch = e->scratch.p;
+    G.scratch_stride = e->scratch_stride;
+    uint32_t blocks = std::min<uint32_t>((nf + 255) / 256, e->vm_threads / 256);
+    hipLaunchKernelGGL(k_path_gate, dim3(std::max(1u, blocks)), dim3(256), 0, s, G);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipEventRecord(e->ev[1], s));
+  // ---- 2. keyword/anchor scan
+  uint64_t hit_cap = std::max<uint64_t>(1 << 20, nbytes / 256);
+  HIP_TRY(e->hits.ensure(hit_cap));
+  hit_cap = e->hits.n;
+  ScanParams P{};
+  P.data = d_data;
+  P.off = d_off;
+  P.nbytes = nbytes;
+  P.n_files = nf;
+  P.rs = RS;
+  P.file_kw = e->file_kw.p;
+  P.file_flags = e->file_flags.p;
+  P.hits = e->hits.p;
+  P.hit_cap = hit_cap;
+  P.ctrl = e->ctrl.p;
+  const size_t table_bytes = (size_t)RS.ac.nstates * RS.ac.nclasses * 2;
+  const bool lds_table = table_bytes <= (size_t)kLdsTableMax;
+  const size_t lds = 256 + kTileLds + (lds_table ? table_bytes : 0);
+  const uint64_t nsteps = (nbytes + kBlockBytes - 1) / kBlockBytes;
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, e->device));
+  const uint32_t scan_blocks = (uint32_t)std::min<uint64_t>(nsteps, (uint64_t)prop.multiProcessorCount * 8);
+  for (int attempt = 0; attempt < 2 && nbytes; ++attempt) {
+    if (lds_table) {
+      HIP_TRY(hipFuncSetAttribute((const void*)k_scan<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(k_scan<true>, dim3(std::max(1u, scan_blocks)), dim3(kScanThreads), lds, s, P);
+    } else {
+      HIP_TRY(hipFuncSetAttribute((const void*)k_scan<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(k_scan<false>, dim3(std::max(1u, scan_blocks)), dim3(kScanThreads), lds, s, P);
+    }
+    HIP_TRY(hipGetLastError());
+    Ctrl c;
+    if ((rc = read_ctrl(e, &c))) return rc;
+    if (c.hits <= hit_cap) break;
+    // overflow: grow and rescan (keyword bits are idempotent)
+    HIP_TRY(e->hits.ensure(c.hits));
+    hit_cap = P.hit_cap = e->hits.n;
+    P.hits = e->hits.p;
+    HIP_TRY(hipMemsetAsync(e->ctrl.p, 0, sizeof(Ctrl), s));
+  }
+  HIP_TRY(hipEventRecord(e->ev[2], s));
+  Ctrl c;
+  if ((rc = read_ctrl(e, &c))) return rc;
+  const uint64_t n_hits = c.hits;
+  // ---- 3. candidates
+  uint64_t cand_cap = std::max<uint64_t>(1 << 16, n_hits * 2 + nf / 4);
+  ExpandParams E{};
+  E.off = d_off;
+  E.n_files = nf;
+  E.rs = RS;
+  E.file_kw = e->file_kw.p;
+  E.file_flags = e->file_flags.p;
+  E.path_mask = rs->any_path_rules ? e->path_mask.p : nullptr;
+  E.rule_words = rule_words;
+  E.hits = e->hits.p;
+  E.n_hits = n_hits;
+  E.ctrl = e->ctrl.p;
+  E.full_rules = im.u32.p + im.o_full;
+  E.n_full_rules = im.n_full;
+  uint64_t n_cands = 0;
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    HIP_TRY(e->keys.ensure(cand_cap));
+    HIP_TRY(e->vals.ensure(cand_cap));
+    E.keys = e->keys.p;
+    E.vals = e->vals.p;
+    E.cand_cap = e->keys.n;
+    HIP_TRY(hipMemsetAsync(&e->ctrl.p->cands, 0, 8, s));
+    if (n_hits)
+      hipLaunchKernelGGL(k_expand, dim3((uint32_t)((n_hits + 255) / 256)), dim3(256), 0, s, E);
+    if (nf) hipLaunchKernelGGL(k_full_jobs, dim3((nf + 255) / 256), dim3(256), 0, s, E);
+    HIP_TRY(hipGetLastError());
+    if ((rc = read_ctrl(e, &c))) return rc;
+    n_cands = c.cands;
+    if (n_cands <= E.cand_cap) break;
+    cand_cap = n_cands;
+  }
+  HIP_TRY(hipEventRecord(e->ev[3], s));
+  // ---- 4. sort by (rule, position) and segment into jobs
+  uint32_t n_jobs = 0;
+  if (n_cands) {
+    HIP_TRY(e->keys2.ensure(n_cands));
+    HIP_TRY(e->vals2.ensure(n_cands));
+    int end_bit = kPosBits;
+    while ((1ull << (end_bit - kPosBits)) < RS.n_rules + 1ull) ++end_bit;
+    size_t tmp = 0;
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
+                                               (int)n_cands, 0, end_bit, s));
+    HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp, e->keys.p, e->keys2.p, e->vals.p,
+                                               e->vals2.p, (int)n_cands, 0, end_bit, s));
+    HIP_TRY(e->flags8.ensure(n_cands));
+    HIP_TRY(e->job_start.ensure(n_cands));
+    HIP_TRY(e->nsel.ensure(1));
+    hipLaunchKernelGGL(k_mark_jobs, dim3((uint32_t)((n_cands + 255) / 256)), dim3(256), 0, s, e->keys2.p,
+                       e->vals2.p, n_cands, e->flags8.p);
+    hipcub::CountingInputIterator<uint32_t> cnt(0);
+    size_t tmp2 = 0;
+    HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tmp2, cnt, e->flags8.p, e->job_start.p, e->nsel.p,
+                                          (int)n_cands, s));
+    HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
+    HIP_TRY(hipcub::DeviceSelect::Flagged(e->cub_tmp.p, tmp2, cnt, e->flags8.p, e->job_start.p, e->nsel.p,
+                                          (int)n_cands, s));
+    HIP_TRY(hipMemcpyAsync(&n_jobs, e->nsel.p, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  HIP_TRY(hipEventRecord(e->ev[4], s));
+  // ---- 5. verify
+  uint64_t loc_cap = std::max<uint64_t>(1 << 16, n_jobs);
+  uint64_t n_locs = 0;
+  for (int attempt = 0; attempt < 3 && n_jobs; ++attempt) {
+    HIP_TRY(e->locs.ensure(loc_cap));
+    HIP_TRY(hipMemsetAsync(&e->ctrl.p->locs, 0, 8, s));
+    VerifyParams V{};
+    V.data = d_data;
+    V.off = d_off;
+    V.rs = RS;
+    V.keys = e->keys2.p;
+    V.vals = e->vals2.p;
+    V.n_cands = n_cands;
+    V.job_start = e->job_start.p;
+    V.n_jobs = n_jobs;
+    V.locs = e->locs.p;
+    V.loc_cap = e->locs.n;
+    V.ctrl = e->ctrl.p;
+    V.scratch = e->scratch.p;
+    V.scratch_stride = e->scratch_stride;
+    uint32_t blocks = std::min<uint32_t>((n_jobs + 255) / 256, e->vm_threads / 256);
+    hipLaunchKernelGGL(k_verify, dim3(std::max(1u, blocks)), dim3(256), 0, s, V);
+    HIP_TRY(hipGetLastError());
+    if ((rc = read_ctrl(e, &c))) return rc;
+    n_locs = c.locs;
+    if (n_locs <= e->locs.n) break;
+    loc_cap = n_locs;
+  }
+  if (c.err) {
+    set_last_error("internal: capture re-run disagreed with the whole-match run");
+    return TSG_ERR_INTERNAL;
+  }
+  HIP_TRY(hipEventRecord(e->ev[5], s));
+  // ---- 6. exclude blocks (only when the config has any)
+  std::vector<DevLoc> hl(n_locs);
+  if (n_locs && rs->any_exclude) {
+    HIP_TRY(hipMemcpyAsync(hl.data(), e->locs.p, n_locs * sizeof(DevLoc), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    // tags: (file, 0) = global block, (file, rule+1) = that rule's block
+    std::map<std::pair<uint32_t, uint32_t>, uint32_t> tag_of;
+    std::vector<ExclJob> jobs;
+    for (auto& L : hl) {
+      auto add_scope = [&](uint32_t scope, const std::vector<int>& progs) {
+        auto key = std::make_pair(L.file, scope);
+        if (progs.empty() || tag_of.count(key)) return;
+        uint32_t tag = (uint32_t)tag_of.size();
+        tag_of[key] = tag;
+        for (int p : progs) jobs.push_back(ExclJob{L.file, (uint32_t)p, tag, 0});
+      };
+      add_scope(0, rs->global_exclude);
+      add_scope(L.rule + 1, rs->rules[L.rule].exclude);
+    }
+    std::vector<ExclRange> ranges;
+    if (!jobs.empty()) {
+      HIP_TRY(e->excl_jobs.ensure(jobs.size()));
+      HIP_TRY(hipMemcpyAsync(e->excl_jobs.p, jobs.data(), jobs.size() * sizeof(ExclJob), hipMemcpyHostToDevice, s));
+      uint64_t cap = 1 << 16;
+      for (int attempt = 0; attempt < 3; ++attempt) {
+        HIP_TRY(e->excl_out.ensure(cap));
+        HIP_TRY(hipMemsetAsync(&e->ctrl.p->excl, 0, 8, s));
+        uint32_t blocks = std::min<uint32_t>(((uint32_t)jobs.size() + 255) / 256, e->vm_threads / 256);
+        hipLaunchKernelGGL(k_exclude, dim3(std::max(1u, blocks)), dim3(256), 0, s, d_data, d_off, RS,
+                           e->excl_jobs.p, (uint32_t)jobs.size(), e->excl_out.p, (uint64_t)e->excl_out.n,
+                           e->ctrl.p, e->scratch.p, e->scratch_stride);
+        HIP_TRY(hipGetLastError());
+        if ((rc = read_ctrl(e, &c))) return rc;
+        if (c.excl <= e->excl_out.n) break;
+        cap = c.excl;
+      }
+      ranges.resize(c.excl);
+      if (c.excl)
+        HIP_TRY(hipMemcpy(ranges.data(), e->excl_out.p, c.excl * sizeof(ExclRange), hipMemcpyDeviceToHost));
+    }
+    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> by_tag(tag_of.size());
+    for (auto& rg : ranges) by_tag[rg.tag].push_back({rg.s, rg.e});
+    std::vector<DevLoc> kept;
+    for (auto& L : hl) {
+      bool excluded = false;
+      for (uint32_t scope : {0u, L.rule + 1}) {
+        auto it = tag_of.find({L.file, scope});
+        if (it == tag_of.end()) continue;
+        for (auto& pr : by_tag[it->second])
+          if (pr.first <= L.start && L.end <= pr.second) excluded = true;
+      }
+      // a non-participating group never reaches censoring in Go if excluded
+      if (!excluded) kept.push_back(L);
+    }
+    hl.swap(kept);
+    n_locs = hl.size();
+    if (n_locs)
+      HIP_TRY(hipMemcpyAsync(e->locs.p, hl.data(), n_locs * sizeof(DevLoc), hipMemcpyHostToDevice, s));
+  }
+  HIP_TRY(hipEventRecord(e->ev[6], s));
+  // ---- 7. line numbers
+  if (n_locs) {
+    hipLaunchKernelGGL(k_lines, dim3((uint32_t)((n_locs * 64 + 255) / 256)), dim3(256), 0, s, d_data, d_off,
+                       e->locs.p, n_locs);
+    HIP_TRY(hipGetLastError());
+    hl.resize(n_locs);
+    HIP_TRY(hipMemcpyAsync(hl.data(), e->locs.p, n_locs * sizeof(DevLoc), hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(hipEventRecord(e->ev[7], s));
+  std::vector<uint32_t> flags(nf);
+  if (nf) HIP_TRY(hipMemcpyAsync(flags.data(), e->file_flags.p, nf * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (int k = 0; k < 7; ++k) {
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, e->ev[k], e->ev[k + 1]));
+    tm[k] = ms;
+  }
+  auto& R = res->impl;
+  R.file_flags.resize(nf);
+  for (uint32_t f = 0; f < nf; ++f) R.file_flags[f] = (uint8_t)flags[f];
+  R.locs.clear();
+  for (auto& L : hl) {
+    if (L.flags & 1) {
+      set_last_error("secret group did not participate in the match (the Go reference panics here)");
+      return TSG_ERR_PANIC;
+    }
+    R.locs.push_back(tsg_loc{L.file, L.rule, L.start, L.end, L.start_line, L.end_line});
+  }
+  return TSG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* tsg_version(void) { return "trivy-secret-mi355x 0.1 (gfx950)"; }
+
+int tsg_engine_create(int device, tsg_engine** out) {
+  if (!out) return TSG_ERR_INVALID_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) {
+    set_last_error("no HIP device available: the MI355X engine has no CPU fallback");
+    return TSG_ERR_NO_DEVICE;
+  }
+  auto* e = new tsg_engine();
+  e->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    set_last_error("hipSetDevice/hipStreamCreate failed");
+    delete e;
+    return TSG_ERR_DEVICE;
+  }
+  *out = e;
+  return TSG_OK;
+}
+
+void tsg_engine_free(tsg_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  (void)hipStreamSynchronize(e->stream);
+  e->img.release();
+  e->data.release(); e->off.release(); e->paths.release(); e->path_off.release();
+  e->file_kw.release(); e->file_flags.release(); e->path_mask.release(); e->hits.release();
+  e->keys.release(); e->keys2.release(); e->vals.release(); e->vals2.release(); e->flags8.release();
+  e->job_start.release(); e->nsel.release(); e->cub_tmp.release(); e->locs.release();
+  e->scratch.release(); e->ctrl.release(); e->excl_jobs.release(); e->excl_out.release();
+  if (e->events)
+    for (auto& ev : e->ev) (void)hipEventDestroy(ev);
+  (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+int tsg_scan(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, size_t n_files, tsg_result** out) {
+  if (!e || !rs || !out || (n_files && !files)) return TSG_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(e->mu);
+  *out = nullptr;
+  HIP_TRY(hipSetDevice(e->device));
+  // pack contents and paths (pinned staging -> HBM)
+  std::vector<uint64_t> off(n_files + 1, 0), poff(n_files + 1, 0);
+  for (size_t i = 0; i < n_files; ++i) {
+    if (files[i].len >= (1ull << 32)) {
+      set_last_error("files of 4 GiB or more are outside this engine's coverage");
+      return TSG_ERR_UNSUPPORTED;
+    }
+    off[i + 1] = off[i] + files[i].len;
+    poff[i + 1] = poff[i] + (files[i].path ? strlen(files[i].path) : 0);
+  }
+  const uint64_t nbytes = off[n_files], pbytes = poff[n_files];
+  uint8_t* h = nullptr;
+  const size_t stage = nbytes + pbytes + 16;
+  HIP_TRY(hipHostMalloc((void**)&h, stage, hipHostMallocDefault));
+  for (size_t i = 0; i < n_files; ++i) {
+    if (files[i].len) memcpy(h + off[i], files[i].data, files[i].len);
+    if (files[i].path) memcpy(h + nbytes + poff[i], files[i].path, poff[i + 1] - poff[i]);
+  }
+  auto cleanup = [&]() { (void)hipHostFree(h); };
+  if (e->data.ensure(nbytes + 16) != hipSuccess || e->off.ensure(n_files + 1) != hipSuccess ||
+      e->paths.ensure(pbytes + 16) != hipSuccess || e->path_off.ensure(n_files + 1) != hipSuccess) {
+    cleanup();
+    set_last_error("hipMalloc failed");
+    return TSG_ERR_DEVICE;
+  }
+  hipStream_t s = e->stream;
+  bool ok = hipMemcpyAsync(e->data.p, h, nbytes, hipMemcpyHostToDevice, s) == hipSuccess &&
+            hipMemcpyAsync(e->paths.p, h + nbytes, pbytes, hipMemcpyHostToDevice, s) == hipSuccess &&
+            hipMemcpyAsync(e->off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
+            hipMemcpyAsync(e->path_off.p, poff.data(), poff.size() * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
+            hipStreamSynchronize(s) == hipSuccess;
+  cleanup();
+  if (!ok) {
+    set_last_error("host-to-device copy failed");
+    return TSG_ERR_DEVICE;
+  }
+  auto* res = new tsg_result();
+  int rc = run_pipeline(e, rs, e->data.p, e->off.p, e->paths.p, e->path_off.p, n_files, nbytes, res);
+  if (rc) {
+    delete res;
+    return rc;
+  }
+  if (!build_findings(&res->impl, rs, files, n_files)) {
+    delete res;
+    return TSG_ERR_PANIC;
+  }
+  *out = res;
+  return TSG_OK;
+}
+
+int tsg_scan_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, const uint64_t* d_offsets,
+                    const uint8_t* d_paths, const uint64_t* d_path_offsets, size_t n_files, tsg_result** out) {
+  if (!e || !rs || !out || !d_offsets || !d_path_offsets) return TSG_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(e->mu);
+  *out = nullptr;
+  HIP_TRY(hipSetDevice(e->device));
+  uint64_t nbytes = 0;
+  HIP_TRY(hipMemcpy(&nbytes, d_offsets + n_files, 8, hipMemcpyDeviceToHost));
+  auto* res = new tsg_result();
+  int rc = run_pipeline(e, rs, d_data, d_offsets, d_paths, d_path_offsets, n_files, nbytes, res);
+  if (rc) {
+    delete res;
+    return rc;
+  }
+  *out = res;
+  return TSG_OK;
+}
+
+int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, const uint64_t* d_offsets,
+                    size_t n_files, uint32_t* h_gates_out, size_t gate_words_per_file) {
+  if (!e || !rs || !d_offsets) return TSG_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->device));
+  int rc = upload_ruleset(e, rs);
+  if (rc) return rc;
+  const RuleSetDev& RS = e->img.view;
+  const uint32_t nf = (uint32_t)n_files;
+  uint64_t nbytes = 0;
+  HIP_TRY(hipMemcpy(&nbytes, d_offsets + n_files, 8, hipMemcpyDeviceToHost));
+  hipStream_t s = e->stream;
+  HIP_TRY(e->ctrl.ensure(1));
+  HIP_TRY(e->file_kw.ensure((size_t)nf * RS.kw_words + 1));
+  HIP_TRY(e->file_flags.ensure(nf + 1));
+  HIP_TRY(hipMemsetAsync(e->ctrl.p, 0, sizeof(Ctrl), s));
+  HIP_TRY(hipMemsetAsync(e->file_kw.p, 0, ((size_t)nf * RS.kw_words + 1) * 4, s));
+  HIP_TRY(hipMemsetAsync(e->file_flags.p, 0, (nf + 1) * 4, s));
+  HIP_TRY(e->hits.ensure(1));
+  ScanParams P{};
+  P.data = d_data;
+  P.off = d_offsets;
+  P.nbytes = nbytes;
+  P.n_files = nf;
+  P.rs = RS;
+  P.file_kw = e->file_kw.p;
+  P.file_flags = e->file_flags.p;
+  P.hits = e->hits.p;
+  P.hit_cap = 0;  // prefilter only: hits are counted, not stored
+  P.ctrl = e->ctrl.p;
+  const size_t table_bytes = (size_t)RS.ac.nstates * RS.ac.nclasses * 2;
+  const bool lds_table = table_bytes <= (size_t)kLdsTableMax;
+  const size_t lds = 256 + kTileLds + (lds_table ? table_bytes : 0);
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, e->device));
+  const uint64_t nsteps = (nbytes + kBlockBytes - 1) / kBlockBytes;
+  const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nsteps, (uint64_t)prop.multiProcessorCount * 8));
+  if (nbytes) {
+    if (lds_table) {
+      HIP_TRY(hipFuncSetAttribute((const void*)k_scan<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(k_scan<true>, dim3(blocks), dim3(kScanThreads), lds, s, P);
+    } else {
+      HIP_TRY(hipFuncSetAttribute((const void*)k_scan<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(k_scan<false>, dim3(blocks), dim3(kScanThreads), lds, s, P);
+    }
+    HIP_TRY(hipGetLastError());
+  }
+  std::vector<uint32_t> kw((size_t)nf * RS.kw_words);
+  if (nf) HIP_TRY(hipMemcpyAsync(kw.data(), e->file_kw.p, kw.size() * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (h_gates_out) {
+    // rule gate bits from keyword bits (host: per file x rule, not per byte)
+    for (uint32_t f = 0; f < nf; ++f) {
+      uint32_t* g = h_gates_out + (size_t)f * gate_words_per_file;
+      memset(g, 0, gate_words_per_file * 4);
+      for (size_t r = 0; r < rs->rules.size() && r / 32 < gate_words_per_file; ++r) {
+        const RuleHost& rh = rs->rules[r];
+        bool pass = rh.keywords.empty();
+        for (auto& k : rh.keywords) {
+          if (k.empty()) { pass = true; break; }
+          size_t id = std::find(rs->keywords.begin(), rs->keywords.end(), k) - rs->keywords.begin();
+          if ((kw[(size_t)f * RS.kw_words + id / 32] >> (id % 32)) & 1) { pass = true; break; }
+        }
+        if (pass) g[r / 32] |= 1u << (r % 32);
+      }
+    }
+  }
+  return TSG_OK;
+}
+
+size_t tsg_result_loc_count(const tsg_result* r) { return r ? r->impl.locs.size() : 0; }
+const tsg_loc* tsg_result_locs(const tsg_result* r) { return r ? r->impl.locs.data() : nullptr; }
+size_t tsg_result_file_count(const tsg_result* r) { return r ? r->impl.file_flags.size() : 0; }
+const uint8_t* tsg_result_file_flags(const tsg_result* r) { return r ? r->impl.file_flags.data() : nullptr; }
+size_t tsg_result_findings(const tsg_result* r, size_t file, const tsg_finding** out) {
+  if (!r || !out || !r->impl.have_findings || file >= r->impl.findings.size()) {
+    if (out) *out = nullptr;
+    return 0;
+  }
+  *out = r->impl.findings[file].data();
+  return r->impl.findings[file].size();
+}
+int tsg_result_timings(const tsg_result* r, double* ms, size_t n, size_t* n_out) {
+  if (!r) return TSG_ERR_INVALID_ARG;
+  size_t k = std::min(n, r->impl.timings.size());
+  for (size_t i = 0; i < k; ++i) ms[i] = r->impl.timings[i];
+  if (n_out) *n_out = r->impl.timings.size();
+  return TSG_OK;
+}
+void tsg_result_free(tsg_result* r) { delete r; }
+
+}  // extern "C"

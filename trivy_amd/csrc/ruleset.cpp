@@ -1,0 +1,401 @@
+// Host rule compiler: turns the Rule / AllowRule / ExcludeBlock model of
+// pkg/fanal/secret/scanner.go:84-95,191-221 into the engine's compiled form:
+// Go-RE2 programs (gre.cpp), anchor literals, and one Aho-Corasick automaton
+// over every keyword (MatchKeywords, scanner.go:169-181) and anchor literal.
+#include <atomic>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <mutex>
+
+#include "engine.h"
+#include "pikevm.h"
+
+namespace {
+thread_local std::string g_last_error;
+std::atomic<uint64_t> g_ruleset_ids{1};
+
+void set_err(char* err, size_t errlen, const std::string& msg) {
+  g_last_error = msg;
+  if (err && errlen) {
+    size_t n = std::min(errlen - 1, msg.size());
+    memcpy(err, msg.data(), n);
+    err[n] = '\0';
+  }
+}
+
+std::string ascii_lower(const std::string& s) {
+  std::string o = s;
+  for (auto& c : o)
+    if (c >= 'A' && c <= 'Z') c = (char)(c + 32);
+  return o;
+}
+
+bool is_ascii(const std::string& s) {
+  for (unsigned char c : s)
+    if (c >= 0x80) return false;
+  return true;
+}
+}  // namespace
+
+namespace tsg {
+void set_last_error(const std::string& m) { g_last_error = m; }
+
+// Aho-Corasick over the lowercased patterns (truncated to kAcMaxLit bytes).
+bool build_ac(tsg_ruleset* rs, std::string* err) {
+  AcHost& ac = rs->ac;
+  // byte classes: every byte that appears in a (lowercased) pattern gets a
+  // class; 'A'-'Z' share the class of their lowercase letter.
+  int cmap[256];
+  for (int b = 0; b < 256; ++b) cmap[b] = 0;
+  int ncls = 1;
+  for (auto& p : rs->patterns) {
+    size_t L = std::min<size_t>(p.lower.size(), kAcMaxLit);
+    for (size_t k = 0; k < L; ++k) {
+      unsigned char c = p.lower[k];
+      if (!cmap[c]) cmap[c] = ncls++;
+    }
+  }
+  for (int b = 'A'; b <= 'Z'; ++b) cmap[b] = cmap[b + 32];
+  for (int b = 0; b < 256; ++b) ac.cls[b] = (uint8_t)cmap[b];
+  if (ncls > 255) {
+    *err = "too many byte classes";
+    return false;
+  }
+  // trie
+  std::vector<std::vector<int>> go;  // [state][class] -> state or -1
+  std::vector<std::vector<uint16_t>> term;
+  go.push_back(std::vector<int>(ncls, -1));
+  term.emplace_back();
+  for (size_t pi = 0; pi < rs->patterns.size(); ++pi) {
+    auto& p = rs->patterns[pi];
+    size_t L = std::min<size_t>(p.lower.size(), kAcMaxLit);
+    int s = 0;
+    for (size_t k = 0; k < L; ++k) {
+      int c = cmap[(unsigned char)p.lower[k]];
+      if (go[s][c] < 0) {
+        go[s][c] = (int)go.size();
+        go.push_back(std::vector<int>(ncls, -1));
+        term.emplace_back();
+      }
+      s = go[s][c];
+    }
+    term[s].push_back((uint16_t)pi);
+  }
+  int S = (int)go.size();
+  if (S >= 32768) {
+    *err = "keyword automaton too large";
+    return false;
+  }
+  std::vector<int> fail(S, 0);
+  std::vector<std::vector<uint16_t>> outs(S);
+  std::deque<int> q;
+  for (int c = 0; c < ncls; ++c) {
+    if (go[0][c] < 0) {
+      go[0][c] = 0;
+    } else {
+      fail[go[0][c]] = 0;
+      q.push_back(go[0][c]);
+    }
+  }
+  outs[0] = term[0];
+  std::vector<int> order;
+  while (!q.empty()) {
+    int s = q.front();
+    q.pop_front();
+    order.push_back(s);
+    outs[s] = term[s];
+    for (auto x : outs[fail[s]]) outs[s].push_back(x);
+    for (int c = 0; c < ncls; ++c) {
+      int t = go[s][c];
+      if (t >= 0) {
+        fail[t] = go[fail[s]][c];
+        q.push_back(t);
+      } else {
+        go[s][c] = go[fail[s]][c];
+      }
+    }
+  }
+  ac.nstates = (uint32_t)S;
+  ac.nclasses = (uint32_t)ncls;
+  ac.delta.assign((size_t)S * ncls, 0);
+  for (int s = 0; s < S; ++s)
+    for (int c = 0; c < ncls; ++c) {
+      int t = go[s][c];
+      uint16_t v = (uint16_t)t;
+      if (!outs[t].empty()) v |= 0x8000;
+      ac.delta[(size_t)s * ncls + c] = v;
+    }
+  ac.out_off.assign(S + 1, 0);
+  ac.out_pat.clear();
+  for (int s = 0; s < S; ++s) {
+    ac.out_off[s] = (uint32_t)ac.out_pat.size();
+    for (auto x : outs[s]) ac.out_pat.push_back(x);
+  }
+  ac.out_off[S] = (uint32_t)ac.out_pat.size();
+  return true;
+}
+}  // namespace tsg
+
+using namespace tsg;
+
+static int add_regex(tsg_ruleset* rs, const char* src, std::string* err) {
+  RegexHost r;
+  r.src = src;
+  if (!gre::compile(r.src, &r.c, err)) {
+    *err = "regexp compile error: " + *err;
+    return -1;
+  }
+  rs->regexes.push_back(std::move(r));
+  return (int)rs->regexes.size() - 1;
+}
+
+static int add_pattern(tsg_ruleset* rs, const std::string& lower) {
+  for (size_t i = 0; i < rs->patterns.size(); ++i)
+    if (rs->patterns[i].lower == lower) return (int)i;
+  PatternHost p;
+  p.lower = lower;
+  p.req.assign(lower.size(), '\0');
+  rs->patterns.push_back(p);
+  return (int)rs->patterns.size() - 1;
+}
+
+extern "C" {
+
+const char* tsg_last_error(void) { return g_last_error.c_str(); }
+
+int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_rule* allow_rules,
+                        size_t n_allow_rules, const char* const* exclude_regexes,
+                        size_t n_exclude_regexes, tsg_ruleset** out, char* err, size_t errlen) {
+  if (!out || (n_rules && !rules)) {
+    set_err(err, errlen, "invalid argument");
+    return TSG_ERR_INVALID_ARG;
+  }
+  *out = nullptr;
+  auto* rs = new tsg_ruleset();
+  rs->id = g_ruleset_ids.fetch_add(1);
+  std::string e;
+  auto fail = [&](int code) {
+    set_err(err, errlen, e);
+    delete rs;
+    return code;
+  };
+  for (size_t i = 0; i < n_allow_rules; ++i) {
+    if (allow_rules[i].regex) {
+      int r = add_regex(rs, allow_rules[i].regex, &e);
+      if (r < 0) return fail(TSG_ERR_REGEX);
+      rs->global_allow_regex.push_back(r);
+    }
+    if (allow_rules[i].path) {
+      int r = add_regex(rs, allow_rules[i].path, &e);
+      if (r < 0) return fail(TSG_ERR_REGEX);
+      rs->global_allow_path.push_back(r);
+    }
+  }
+  for (size_t i = 0; i < n_exclude_regexes; ++i) {
+    int r = add_regex(rs, exclude_regexes[i], &e);
+    if (r < 0) return fail(TSG_ERR_REGEX);
+    rs->global_exclude.push_back(r);
+    rs->any_exclude = true;
+  }
+  std::map<std::string, int> kwid;
+  for (size_t i = 0; i < n_rules; ++i) {
+    const tsg_rule& in = rules[i];
+    RuleHost r;
+    r.id = in.id ? in.id : "";
+    r.group_name = in.secret_group_name ? in.secret_group_name : "";
+    if (in.regex) {
+      r.regex = add_regex(rs, in.regex, &e);
+      if (r.regex < 0) return fail(TSG_ERR_REGEX);
+    }
+    for (size_t k = 0; k < in.n_keywords; ++k) {
+      std::string kw = in.keywords[k] ? in.keywords[k] : "";
+      if (!is_ascii(kw)) {
+        e = "rule " + r.id + ": non-ASCII keyword is outside this engine's coverage";
+        return fail(TSG_ERR_UNSUPPORTED);
+      }
+      r.keywords.push_back(ascii_lower(kw));
+    }
+    if (in.path) {
+      r.path = add_regex(rs, in.path, &e);
+      if (r.path < 0) return fail(TSG_ERR_REGEX);
+      rs->any_path_rules = true;
+    }
+    for (size_t k = 0; k < in.n_allow_rules; ++k) {
+      if (in.allow_rules[k].regex) {
+        int x = add_regex(rs, in.allow_rules[k].regex, &e);
+        if (x < 0) return fail(TSG_ERR_REGEX);
+        r.allow_regex.push_back(x);
+      }
+      if (in.allow_rules[k].path) {
+        int x = add_regex(rs, in.allow_rules[k].path, &e);
+        if (x < 0) return fail(TSG_ERR_REGEX);
+        r.allow_path.push_back(x);
+        rs->any_path_rules = true;
+      }
+    }
+    for (size_t k = 0; k < in.n_exclude_regexes; ++k) {
+      int x = add_regex(rs, in.exclude_regexes[k], &e);
+      if (x < 0) return fail(TSG_ERR_REGEX);
+      r.exclude.push_back(x);
+      rs->any_exclude = true;
+    }
+    if (r.regex < 0) {
+      r.mode = MODE_NEVER;
+    } else {
+      const gre::Compiled& c = rs->regexes[r.regex].c;
+      bool has_group = true;
+      if (!r.group_name.empty()) {
+        has_group = false;
+        for (auto& nm : c.prog.cap_names) has_group |= (nm == r.group_name);
+      }
+      if (has_group && !r.group_name.empty() && (uint32_t)c.prog.ncap > kMaxCap) {
+        e = "rule " + r.id + ": too many capture groups for the secret-group extractor";
+        return fail(TSG_ERR_UNSUPPORTED);
+      }
+      // no group of that name => getMatchSubgroupsLocations yields nothing
+      if (!has_group) r.mode = MODE_NEVER;
+      else r.mode = c.anchor.valid ? MODE_ANCHORED : MODE_FULL;
+    }
+    for (auto& kw : r.keywords) {
+      if (!kwid.count(kw) && !kw.empty()) {
+        int id = (int)rs->keywords.size();
+        kwid[kw] = id;
+        rs->keywords.push_back(kw);
+      }
+    }
+    rs->rules.push_back(std::move(r));
+  }
+  // patterns: keywords, anchor literals, fold-special sequences
+  for (size_t k = 0; k < rs->keywords.size(); ++k) {
+    int p = add_pattern(rs, rs->keywords[k]);
+    rs->patterns[p].kw = (int)k;
+  }
+  static const char* kSpecial[] = {"\xC4\xB0", "\xC5\xBF", "\xE2\x84\xAA"};
+  for (auto* s : kSpecial) {
+    int p = add_pattern(rs, s);
+    rs->patterns[p].special = true;
+  }
+  for (size_t ri = 0; ri < rs->rules.size(); ++ri) {
+    RuleHost& r = rs->rules[ri];
+    if (r.mode != MODE_ANCHORED) continue;
+    const gre::Anchor& a = rs->regexes[r.regex].c.anchor;
+    for (auto& lit : a.lits) {
+      int p = add_pattern(rs, lit.lower);
+      PatternHost& ph = rs->patterns[p];
+      bool has_req = false;
+      for (char c : lit.req) has_req |= c != '\0';
+      if (!ph.any_anchor) {
+        ph.req = lit.req;
+        ph.confirm = has_req;
+      } else if (ph.confirm && (!has_req || ph.req != lit.req)) {
+        ph.confirm = false;  // differing case requirements: record every hit
+      }
+      ph.any_anchor = true;
+      if (std::find(ph.rules.begin(), ph.rules.end(), (uint32_t)ri) == ph.rules.end())
+        ph.rules.push_back((uint32_t)ri);
+    }
+  }
+  if (rs->patterns.size() >= 65535) {
+    e = "too many keyword/anchor literals";
+    return fail(TSG_ERR_UNSUPPORTED);
+  }
+  if (!build_ac(rs, &e)) return fail(TSG_ERR_UNSUPPORTED);
+  *out = rs;
+  return TSG_OK;
+}
+
+void tsg_ruleset_free(tsg_ruleset* rs) { delete rs; }
+
+size_t tsg_ruleset_rule_count(const tsg_ruleset* rs) { return rs ? rs->rules.size() : 0; }
+
+int tsg_ruleset_rule_info(const tsg_ruleset* rs, size_t i, int* mode, uint32_t* amin,
+                          uint32_t* amax, size_t* nlits) {
+  if (!rs || i >= rs->rules.size()) return TSG_ERR_INVALID_ARG;
+  const RuleHost& r = rs->rules[i];
+  if (mode) *mode = r.mode;
+  const gre::Anchor* a = r.regex >= 0 ? &rs->regexes[r.regex].c.anchor : nullptr;
+  if (amin) *amin = a && a->valid ? a->off_min : 0;
+  if (amax) *amax = a && a->valid ? a->off_max : 0;
+  if (nlits) *nlits = a && a->valid ? a->lits.size() : 0;
+  return TSG_OK;
+}
+
+// ---- host regex diagnostics (compiler + VM on the CPU) ---------------------
+struct HostVm {
+  std::vector<uint16_t> sp0, sp1, d0, d1, stk;
+  std::vector<uint32_t> s0, s1;
+  gre::VmScratch sc;
+  explicit HostVm(size_t n) : sp0(n), sp1(n), d0(n), d1(n), stk(n + 1), s0(n), s1(n) {
+    sc.sparse[0] = sp0.data();
+    sc.sparse[1] = sp1.data();
+    sc.dense[0] = d0.data();
+    sc.dense[1] = d1.data();
+    sc.start[0] = s0.data();
+    sc.start[1] = s1.data();
+    sc.stack = stk.data();
+  }
+};
+
+static gre::ProgView view_of(const gre::Prog& p) {
+  return gre::ProgView{p.inst.data(), p.classes.data(), p.ranges.data(), (uint32_t)p.inst.size(),
+                       p.start, (uint32_t)p.ncap};
+}
+
+int tsg_regex_match(const char* pattern, const uint8_t* text, size_t len, int* matched) {
+  if (!pattern || !matched) return TSG_ERR_INVALID_ARG;
+  gre::Compiled c;
+  std::string e;
+  if (!gre::compile(pattern, &c, &e)) {
+    g_last_error = e;
+    return TSG_ERR_REGEX;
+  }
+  HostVm vm(c.prog.inst.size());
+  uint32_t ms, me;
+  *matched = gre::vm_search(view_of(c.prog), text, (uint32_t)len, 0, (uint32_t)len, true, vm.sc, &ms,
+                            &me);
+  return TSG_OK;
+}
+
+int tsg_regex_find_all(const char* pattern, const uint8_t* text, size_t len, int64_t* pairs,
+                       size_t cap, size_t* n_out) {
+  if (!pattern || !n_out) return TSG_ERR_INVALID_ARG;
+  gre::Compiled c;
+  std::string e;
+  if (!gre::compile(pattern, &c, &e)) {
+    g_last_error = e;
+    return TSG_ERR_REGEX;
+  }
+  HostVm vm(c.prog.inst.size());
+  gre::ProgView pv = view_of(c.prog);
+  size_t n = 0;
+  int64_t prev_end = -1;
+  uint32_t pos = 0;
+  uint32_t L = (uint32_t)len;
+  // Go regexp.go allMatches
+  while (pos <= L) {
+    uint32_t ms, me;
+    if (!gre::vm_search(pv, text, L, pos, L, false, vm.sc, &ms, &me)) break;
+    bool accept = true;
+    if (me == pos) {
+      if ((int64_t)ms == prev_end) accept = false;
+      uint32_t w;
+      gre::decode_rune(text, L, pos, &w);
+      pos = w > 0 ? pos + w : L + 1;
+    } else {
+      pos = me;
+    }
+    prev_end = me;
+    if (accept) {
+      if (n < cap) {
+        pairs[2 * n] = ms;
+        pairs[2 * n + 1] = me;
+      }
+      ++n;
+    }
+  }
+  *n_out = n;
+  return TSG_OK;
+}
+
+}  // extern "C"

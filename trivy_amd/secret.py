@@ -1,0 +1,307 @@
+"""Host-side mirror of Trivy's secret engine API, backed by the MI355X engine.
+
+Mirrors pkg/fanal/secret/scanner.go:
+  * Config / Rule / AllowRule / ExcludeBlock ............ scanner.go:28-95,191-221
+  * parse_config (ParseConfig) / convert_severity ........ scanner.go:272-313
+  * new_scanner (NewScanner) ............................. scanner.go:315-359
+  * Scanner.scan (Scan) / ScanArgs ....................... scanner.go:361-452
+plus Scanner.scan_batch, the batched entry the GPU needs (many files per
+launch).  Every byte of content is scanned by the HIP
+kernels in csrc/engine.hip; this module only marshals rules and results.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+import json
+import os
+import threading
+from typing import List, Optional, Sequence
+
+import yaml
+
+from . import _native as N
+from .types import Code, Line, Secret, SecretFinding
+
+_DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "builtin_rules.json")
+
+
+class ConfigError(ValueError):
+    pass
+
+
+@dataclasses.dataclass
+class AllowRule:
+    id: str = ""
+    description: str = ""
+    regex: Optional[str] = None
+    path: Optional[str] = None
+
+
+@dataclasses.dataclass
+class ExcludeBlock:
+    description: str = ""
+    regexes: List[str] = dataclasses.field(default_factory=list)
+
+
+@dataclasses.dataclass
+class Rule:
+    id: str = ""
+    category: str = ""
+    title: str = ""
+    severity: str = ""
+    regex: Optional[str] = None
+    keywords: List[str] = dataclasses.field(default_factory=list)
+    path: Optional[str] = None
+    allow_rules: List[AllowRule] = dataclasses.field(default_factory=list)
+    exclude_block: ExcludeBlock = dataclasses.field(default_factory=ExcludeBlock)
+    secret_group_name: str = ""
+
+
+@dataclasses.dataclass
+class Config:
+    enable_builtin_rule_ids: List[str] = dataclasses.field(default_factory=list)
+    disable_rule_ids: List[str] = dataclasses.field(default_factory=list)
+    disable_allow_rule_ids: List[str] = dataclasses.field(default_factory=list)
+    custom_rules: List[Rule] = dataclasses.field(default_factory=list)
+    custom_allow_rules: List[AllowRule] = dataclasses.field(default_factory=list)
+    exclude_block: ExcludeBlock = dataclasses.field(default_factory=ExcludeBlock)
+
+
+@dataclasses.dataclass
+class ScanArgs:
+    file_path: str
+    content: bytes
+
+
+# ---------------------------------------------------------------- builtin --
+
+def _load_builtin():
+    with open(_DATA) as fh:
+        d = json.load(fh)
+    rules = [Rule(id=r["id"], category=r["category"], title=r["title"], severity=r["severity"],
+                  regex=r["regex"], keywords=list(r["keywords"]), secret_group_name=r["secret_group_name"])
+             for r in d["rules"]]
+    allows = [AllowRule(id=a["id"], description=a["description"], regex=a["regex"], path=a["path"])
+              for a in d["allow_rules"]]
+    return rules, allows
+
+
+BUILTIN_RULES, BUILTIN_ALLOW_RULES = _load_builtin()
+
+
+# ----------------------------------------------------------------- config --
+
+def _validate_regex(src, what):
+    """regexp.Compile at YAML decode time (scanner.go:70-82)."""
+    if src is None:
+        return None
+    src = str(src)
+    m = ctypes.c_int()
+    rc = N.lib.tsg_regex_match(src.encode(), b"", 0, ctypes.byref(m))
+    if rc == N.TSG_ERR_REGEX:
+        raise ConfigError(f"secrets config decode error: regexp compile error: {N.lib.tsg_last_error().decode()}")
+    if rc == N.TSG_ERR_UNSUPPORTED:
+        raise ConfigError(N.lib.tsg_last_error().decode())
+    return src
+
+
+def convert_severity(severity) -> str:
+    """scanner.go:305-313."""
+    s = "" if severity is None else str(severity)
+    if s.lower() in ("low", "medium", "high", "critical", "unknown"):
+        return s.upper()
+    return "UNKNOWN"
+
+
+def _allow_rules(lst):
+    out = []
+    for a in lst or []:
+        out.append(AllowRule(id=str(a.get("id") or ""), description=str(a.get("description") or ""),
+                             regex=_validate_regex(a.get("regex"), "allow regex"),
+                             path=_validate_regex(a.get("path"), "allow path")))
+    return out
+
+
+def _exclude_block(d):
+    d = d or {}
+    return ExcludeBlock(description=str(d.get("description") or ""),
+                        regexes=[_validate_regex(x, "exclude") for x in (d.get("regexes") or [])])
+
+
+def parse_config(config_path: str) -> Optional[Config]:
+    """ParseConfig (scanner.go:272-302): None for "" or a missing file."""
+    if not config_path:
+        return None
+    if not os.path.exists(config_path):
+        return None
+    with open(config_path) as fh:
+        try:
+            raw = yaml.safe_load(fh) or {}
+        except yaml.YAMLError as e:
+            raise ConfigError(f"secrets config decode error: {e}") from e
+    cfg = Config(
+        enable_builtin_rule_ids=[str(x) for x in raw.get("enable-builtin-rules") or []],
+        disable_rule_ids=[str(x) for x in raw.get("disable-rules") or []],
+        disable_allow_rule_ids=[str(x) for x in raw.get("disable-allow-rules") or []],
+        custom_allow_rules=_allow_rules(raw.get("allow-rules")),
+        exclude_block=_exclude_block(raw.get("exclude-block")),
+    )
+    for r in raw.get("rules") or []:
+        cfg.custom_rules.append(Rule(
+            id=str(r.get("id") or ""), category=str(r.get("category") or ""), title=str(r.get("title") or ""),
+            severity=convert_severity(r.get("severity")), regex=_validate_regex(r.get("regex"), "regex"),
+            keywords=[str(k) for k in r.get("keywords") or []], path=_validate_regex(r.get("path"), "path"),
+            allow_rules=_allow_rules(r.get("allow-rules")), exclude_block=_exclude_block(r.get("exclude-block")),
+            secret_group_name=str(r.get("secret-group-name") or "")))
+    return cfg
+
+
+# ----------------------------------------------------------------- engine --
+
+_ENGINES = {}
+_ENGINE_LOCK = threading.Lock()
+
+
+def default_device() -> int:
+    return int(os.environ.get("TSG_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+
+
+def get_engine(device: Optional[int] = None):
+    """One tsg_engine (HIP stream + device buffers) per GPU per process."""
+    dev = default_device() if device is None else device
+    with _ENGINE_LOCK:
+        if dev not in _ENGINES:
+            h = ctypes.c_void_p()
+            N.check(N.lib.tsg_engine_create(dev, ctypes.byref(h)))
+            _ENGINES[dev] = h
+        return _ENGINES[dev]
+
+
+class _CompiledRuleSet:
+    def __init__(self, rules: Sequence[Rule], allow_rules: Sequence[AllowRule], exclude: ExcludeBlock):
+        keep = []
+        enc = lambda s: None if s is None else s.encode("utf-8", "surrogateescape")
+        crules = (N.RuleC * max(1, len(rules)))()
+        for i, r in enumerate(rules):
+            kws = (ctypes.c_char_p * max(1, len(r.keywords)))(*[enc(k) for k in r.keywords])
+            ars = (N.AllowRuleC * max(1, len(r.allow_rules)))()
+            for j, a in enumerate(r.allow_rules):
+                ars[j].id, ars[j].regex, ars[j].path = enc(a.id), enc(a.regex), enc(a.path)
+            exs = (ctypes.c_char_p * max(1, len(r.exclude_block.regexes)))(
+                *[enc(x) for x in r.exclude_block.regexes])
+            keep += [kws, ars, exs]
+            c = crules[i]
+            c.id, c.regex, c.path = enc(r.id), enc(r.regex), enc(r.path)
+            c.keywords, c.n_keywords = kws, len(r.keywords)
+            c.secret_group_name = enc(r.secret_group_name)
+            c.allow_rules, c.n_allow_rules = ars, len(r.allow_rules)
+            c.exclude_regexes, c.n_exclude_regexes = exs, len(r.exclude_block.regexes)
+        gar = (N.AllowRuleC * max(1, len(allow_rules)))()
+        for j, a in enumerate(allow_rules):
+            gar[j].id, gar[j].regex, gar[j].path = enc(a.id), enc(a.regex), enc(a.path)
+        gex = (ctypes.c_char_p * max(1, len(exclude.regexes)))(*[enc(x) for x in exclude.regexes])
+        h = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(1024)
+        rc = N.lib.tsg_ruleset_compile(crules, len(rules), gar, len(allow_rules), gex, len(exclude.regexes),
+                                       ctypes.byref(h), err, 1024)
+        if rc != N.TSG_OK:
+            raise N.EngineError(rc, err.value.decode("utf-8", "replace"))
+        self.handle = h
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            N.lib.tsg_ruleset_free(h)
+            self.handle = None
+
+
+def _s(ptr, n) -> str:
+    return ctypes.string_at(ptr, n).decode("utf-8", "surrogateescape") if n else ""
+
+
+class Scanner:
+    """NewScanner result; Scan/scan_batch run on the MI355X."""
+
+    def __init__(self, rules: List[Rule], allow_rules: List[AllowRule], exclude_block: ExcludeBlock,
+                 device: Optional[int] = None):
+        self.rules = rules
+        self.allow_rules = allow_rules
+        self.exclude_block = exclude_block
+        self.device = device
+        self._rs = _CompiledRuleSet(rules, allow_rules, exclude_block)
+        self.last_timings_ms: List[float] = []
+
+    # Global.AllowPath (scanner.go:55-58, 200-207): per-file host check.
+    def allow_path(self, path: str) -> bool:
+        p = path.encode("utf-8", "surrogateescape")
+        return any(a.path is not None and N.regex_match(a.path, p) for a in self.allow_rules)
+
+    def scan(self, args: ScanArgs) -> Secret:
+        return self.scan_batch([args])[0]
+
+    def scan_batch(self, batch: Sequence[ScanArgs]) -> List[Secret]:
+        eng = get_engine(self.device)
+        n = len(batch)
+        files = (N.FileC * max(1, n))()
+        keep = []
+        for i, a in enumerate(batch):
+            buf = ctypes.create_string_buffer(bytes(a.content), len(a.content)) if a.content else None
+            keep.append(buf)
+            files[i].data = ctypes.cast(buf, ctypes.c_void_p) if buf is not None else None
+            files[i].len = len(a.content)
+            files[i].path = a.file_path.encode("utf-8", "surrogateescape")
+        res = ctypes.c_void_p()
+        N.check(N.lib.tsg_scan(eng, self._rs.handle, files, n, ctypes.byref(res)))
+        try:
+            return self._convert(res, batch)
+        finally:
+            N.lib.tsg_result_free(res)
+
+    def _convert(self, res, batch) -> List[Secret]:
+        tm = (ctypes.c_double * 16)()
+        nt = ctypes.c_size_t()
+        N.lib.tsg_result_timings(res, tm, 16, ctypes.byref(nt))
+        self.last_timings_ms = [tm[i] for i in range(min(16, nt.value))]
+        flags = N.lib.tsg_result_file_flags(res)
+        out = []
+        for i, a in enumerate(batch):
+            if flags[i] & N.TSG_FILE_PATH_ALLOWED:
+                out.append(Secret(FilePath=a.file_path))
+                continue
+            fp = ctypes.POINTER(N.FindingC)()
+            k = N.lib.tsg_result_findings(res, i, ctypes.byref(fp))
+            if k == 0:
+                out.append(Secret())
+                continue
+            findings = []
+            for j in range(k):
+                f = fp[j]
+                rule = self.rules[f.rule]
+                lines = []
+                for q in range(f.n_lines):
+                    ln = f.lines[q]
+                    txt = _s(ln.content, ln.content_len)
+                    lines.append(Line(Number=ln.number, Content=txt, IsCause=bool(ln.is_cause),
+                                      Highlighted=txt, FirstCause=bool(ln.first_cause),
+                                      LastCause=bool(ln.last_cause)))
+                findings.append(SecretFinding(
+                    RuleID=rule.id, Category=rule.category, Severity=rule.severity or "UNKNOWN",
+                    Title=rule.title, StartLine=f.start_line, EndLine=f.end_line,
+                    Code=Code(Lines=lines), Match=_s(f.match, f.match_len)))
+            out.append(Secret(FilePath=a.file_path, Findings=findings))
+        return out
+
+
+def new_scanner(config: Optional[Config] = None, device: Optional[int] = None) -> Scanner:
+    """NewScanner (scanner.go:315-359)."""
+    if config is None:
+        return Scanner(list(BUILTIN_RULES), list(BUILTIN_ALLOW_RULES), ExcludeBlock(), device)
+    enabled = list(BUILTIN_RULES)
+    if config.enable_builtin_rule_ids:
+        enabled = [r for r in BUILTIN_RULES if r.id in config.enable_builtin_rule_ids]
+    enabled += list(config.custom_rules)
+    rules = [r for r in enabled if r.id not in config.disable_rule_ids]
+    allows = list(BUILTIN_ALLOW_RULES) + list(config.custom_allow_rules)
+    allows = [a for a in allows if a.id not in config.disable_allow_rule_ids]
+    return Scanner(rules, allows, config.exclude_block, device)
