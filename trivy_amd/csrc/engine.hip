@@ -676,8 +676,8 @@ __global__ __launch_bounds__(256) void k_exclude(const uint8_t* data, const uint
 }
 
 // ----------------------------------------------------------------- lines --
-// One wave per location: StartLine = 1 + count('\n' in [0,start)),
-// EndLine = StartLine + count('\n' in [start,end)) (scanner.go:482,503).
+// One wave per location: P(start) = count('\n' in [0,start)) and P(end) on the
+// uncensored content; censored_lines() turns them into findLocation's numbers.
 __global__ __launch_bounds__(256) void k_lines(const uint8_t* data, const uint64_t* off, DevLoc* locs,
                                                uint64_t n_locs) {
   const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -695,9 +695,9 @@ __global__ __launch_bounds__(256) void k_lines(const uint8_t* data, const uint64
     c1 += __shfl_down(c1, d);
     c2 += __shfl_down(c2, d);
   }
-  if (lane == 0) {
-    locs[w].start_line = c1 + 1;
-    locs[w].end_line = c1 + 1 + c2;
+  if (lane == 0) {  // raw prefix counts P(start), P(end); see censored_lines()
+    locs[w].start_line = c1;
+    locs[w].end_line = c1 + c2;
   }
 }
 
@@ -950,6 +950,52 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   // VM scratch
   e->scratch_stride = (scratch_bytes(max_ninst, max_ncap) + 255) & ~255ull;
   return TSG_OK;
+}
+
+// findLocation (scanner.go:481-503) counts '\n' in the FINAL censored buffer
+// (scanner.go:433-435): newlines inside any kept location have become '*'.
+// So StartLine = 1 + P(start) - (newlines censored before start), and
+// EndLine == StartLine because [start,end) itself is censored.  P(x) are the
+// raw prefix counts k_lines produced at every location boundary.
+void censored_lines(std::vector<DevLoc>& locs) {
+  std::vector<size_t> idx(locs.size());
+  for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+  std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {
+    const DevLoc &x = locs[a], &y = locs[b];
+    if (x.file != y.file) return x.file < y.file;
+    if (x.start != y.start) return x.start < y.start;
+    return x.end < y.end;
+  });
+  size_t i = 0;
+  while (i < idx.size()) {
+    size_t j = i;
+    while (j < idx.size() && locs[idx[j]].file == locs[idx[i]].file) ++j;
+    // merged censored intervals of this file: (a, b, P(a), P(b))
+    struct Iv { uint64_t a, b; uint32_t pa, pb; };
+    std::vector<Iv> iv;
+    for (size_t k = i; k < j; ++k) {
+      const DevLoc& L = locs[idx[k]];
+      if (L.flags) continue;
+      if (!iv.empty() && L.start <= iv.back().b) {
+        if (L.end > iv.back().b) { iv.back().b = L.end; iv.back().pb = L.end_line; }
+      } else {
+        iv.push_back(Iv{L.start, L.end, L.start_line, L.end_line});
+      }
+    }
+    size_t m = 0;
+    uint32_t before = 0;  // newlines censored in intervals entirely before the current one
+    for (size_t k = i; k < j; ++k) {
+      DevLoc& L = locs[idx[k]];
+      if (L.flags) continue;
+      while (m < iv.size() && iv[m].b <= L.start) { before += iv[m].pb - iv[m].pa; ++m; }
+      uint32_t hidden = before;
+      if (m < iv.size() && iv[m].a < L.start) hidden += L.start_line - iv[m].pa;
+      const uint32_t line = L.start_line - hidden + 1;
+      L.start_line = line;
+      L.end_line = line;
+    }
+    i = j;
+  }
 }
 
 int read_ctrl(tsg_engine* e, Ctrl* h) {
@@ -1234,6 +1280,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   auto& R = res->impl;
   R.file_flags.resize(nf);
   for (uint32_t f = 0; f < nf; ++f) R.file_flags[f] = (uint8_t)flags[f];
+  censored_lines(hl);
   R.locs.clear();
   for (auto& L : hl) {
     if (L.flags & 1) {
@@ -1286,7 +1333,34 @@ void tsg_engine_free(tsg_engine* e) {
   delete e;
 }
 
+static int scan_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, size_t n_files,
+                     tsg_result** out);
+static int scan_device_impl(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
+                            const uint64_t* d_offsets, const uint8_t* d_paths,
+                            const uint64_t* d_path_offsets, size_t n_files, tsg_result** out);
+
+// The C ABI never lets a C++ exception escape (never abort).
 int tsg_scan(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, size_t n_files, tsg_result** out) {
+  try {
+    return scan_impl(e, rs, files, n_files, out);
+  } catch (const std::exception& ex) {
+    set_last_error(std::string("internal error: ") + ex.what());
+    return TSG_ERR_INTERNAL;
+  }
+}
+
+int tsg_scan_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, const uint64_t* d_offsets,
+                    const uint8_t* d_paths, const uint64_t* d_path_offsets, size_t n_files, tsg_result** out) {
+  try {
+    return scan_device_impl(e, rs, d_data, d_offsets, d_paths, d_path_offsets, n_files, out);
+  } catch (const std::exception& ex) {
+    set_last_error(std::string("internal error: ") + ex.what());
+    return TSG_ERR_INTERNAL;
+  }
+}
+
+static int scan_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, size_t n_files,
+                     tsg_result** out) {
   if (!e || !rs || !out || (n_files && !files)) return TSG_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(e->mu);
   *out = nullptr;
@@ -1341,8 +1415,9 @@ int tsg_scan(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, size_t
   return TSG_OK;
 }
 
-int tsg_scan_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, const uint64_t* d_offsets,
-                    const uint8_t* d_paths, const uint64_t* d_path_offsets, size_t n_files, tsg_result** out) {
+static int scan_device_impl(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
+                            const uint64_t* d_offsets, const uint8_t* d_paths,
+                            const uint64_t* d_path_offsets, size_t n_files, tsg_result** out) {
   if (!e || !rs || !out || !d_offsets || !d_path_offsets) return TSG_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lk(e->mu);
   *out = nullptr;

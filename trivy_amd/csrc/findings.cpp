@@ -22,7 +22,7 @@ size_t line_start_back(const uint8_t* c, size_t pos, uint32_t cur, uint32_t targ
   size_t p = pos;
   // go to the start of line `cur`
   while (p > 0 && c[p - 1] != '\n') --p;
-  while (cur > target) {
+  while (cur > target && p > 0) {
     // p is the start of line cur; previous line ends at p-1 ('\n')
     --p;  // now at the '\n' terminating line cur-1
     while (p > 0 && c[p - 1] != '\n') --p;
@@ -80,7 +80,7 @@ bool build_findings(ResultImpl* R, const tsg_ruleset* rs, const tsg_file* files,
       auto& lines = R->lines.back();
       size_t p = line_start_back(c, start, sl, cs);
       bool found_first = false;
-      for (uint32_t ln = cs; ln < ce; ++ln) {
+      for (uint32_t ln = cs; ln < ce && p <= n; ++ln) {
         size_t q = p;
         while (q < n && c[q] != '\n') ++q;
         R->strs.emplace_back(censored.substr(p, q - p));
