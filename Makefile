@@ -9,7 +9,7 @@ BUILD    = build
 LIB      = trivy_amd/libtrivy_secret_gpu.so
 
 HOST_SRCS = $(SRC_DIR)/gre.cpp $(SRC_DIR)/ruleset.cpp $(SRC_DIR)/findings.cpp
-HIP_SRCS  = $(SRC_DIR)/engine.hip
+HIP_SRCS  = $(SRC_DIR)/engine.hip $(SRC_DIR)/corpus.hip
 HDRS      = $(wildcard $(SRC_DIR)/*.h) include/trivy_secret_gpu.h
 
 OBJS = $(patsubst $(SRC_DIR)/%.cpp,$(BUILD)/%.o,$(HOST_SRCS)) $(patsubst $(SRC_DIR)/%.hip,$(BUILD)/%.o,$(HIP_SRCS))

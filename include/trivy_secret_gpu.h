@@ -155,6 +155,17 @@ int tsg_regex_match(const char* pattern, const uint8_t* text, size_t len, int* m
 int tsg_regex_find_all(const char* pattern, const uint8_t* text, size_t len, int64_t* pairs,
                        size_t cap, size_t* n_out);
 
+/* ---- synthetic corpus (bench / test utility, not the scan path) ----------
+ * SURVEY.md §8(d) text model with planted builtin-rule secrets.  The device
+ * generator and the host twin produce identical bytes for a (seed, file). */
+int tsg_gen_corpus_device(uint8_t* d_data, const uint64_t* d_offsets, const uint64_t* d_chunk_ids,
+                          uint64_t n_chunks, uint8_t* d_paths, uint64_t* d_path_offsets, uint64_t n_files,
+                          uint64_t seed, double density, void* d_plants, uint64_t plant_cap,
+                          unsigned long long* d_nplants);
+int tsg_gen_file(uint64_t seed, uint32_t file, uint64_t len, double density, uint8_t* out);
+size_t tsg_gen_plant_record_size(void);
+uint32_t tsg_gen_chunk_bytes(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -62,8 +62,9 @@ struct RuleSetDev {
   uint32_t n_global_allow;
   uint32_t n_rules;
   uint32_t kw_words;       // uint32 words of keyword bits per file
-  uint32_t max_ninst;      // for VM scratch sizing
-  uint32_t max_ncap;
+  uint32_t max_ninst;      // for VM scratch sizing (all programs)
+  uint32_t max_ncap;       // capture VM: slots of the largest SecretGroupName regex
+  uint32_t max_ninst_cap;  // capture VM: instructions of the largest SecretGroupName regex
   AcDev ac;
 };
 

@@ -249,7 +249,8 @@ struct GateParams {
   uint64_t scratch_stride;
 };
 
-__device__ inline gre::VmScratch make_scratch(uint8_t* base, uint32_t P, uint32_t ncap) {
+__device__ inline gre::VmScratch make_scratch(uint8_t* base, const RuleSetDev& rs) {
+  const uint32_t P = rs.max_ninst, ncap = rs.max_ncap, PC = rs.max_ninst_cap;
   gre::VmScratch sc;
   uint8_t* q = base;
   auto take = [&](size_t bytes) {
@@ -266,15 +267,15 @@ __device__ inline gre::VmScratch make_scratch(uint8_t* base, uint32_t P, uint32_
   sc.stack = (uint16_t*)take(2ull * (P + 1));
   sc.cur = (int32_t*)take(4ull * ncap);
   sc.capstack = (int32_t*)take(8ull * (P + 1));
-  sc.caps[0] = (int32_t*)take(4ull * P * ncap);
-  sc.caps[1] = (int32_t*)take(4ull * P * ncap);
+  sc.caps[0] = (int32_t*)take(4ull * PC * ncap);  // capture VM runs only group rules
+  sc.caps[1] = (int32_t*)take(4ull * PC * ncap);
   return sc;
 }
 
-__host__ inline uint64_t scratch_bytes(uint32_t P, uint32_t ncap) {
+__host__ inline uint64_t scratch_bytes(uint32_t P, uint32_t ncap, uint32_t PC) {
   auto r = [](uint64_t b) { return (b + 15) & ~15ull; };
   return r(2ull * P) * 4 + r(4ull * P) * 2 + r(2ull * (P + 1)) + r(4ull * ncap) + r(8ull * (P + 1)) +
-         r(4ull * P * ncap) * 2 + 256;
+         r(4ull * PC * ncap) * 2 + 256;
 }
 
 __device__ inline bool match_string(const gre::ProgView& pv, const uint8_t* s, uint32_t n,
@@ -286,7 +287,7 @@ __device__ inline bool match_string(const gre::ProgView& pv, const uint8_t* s, u
 __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
   const uint32_t nthreads = gridDim.x * blockDim.x;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  gre::VmScratch sc = make_scratch(G.scratch + (uint64_t)t * G.scratch_stride, G.rs.max_ninst, G.rs.max_ncap);
+  gre::VmScratch sc = make_scratch(G.scratch + (uint64_t)t * G.scratch_stride, G.rs);
   for (uint32_t f = t; f < G.n_files; f += nthreads) {
     const uint8_t* path = G.paths + G.path_off[f];
     const uint32_t plen = (uint32_t)(G.path_off[f + 1] - G.path_off[f]);
@@ -569,7 +570,7 @@ __device__ void emit_match(const VerifyParams& V, const RuleDev& rd, uint32_t ru
 __global__ __launch_bounds__(256) void k_verify(VerifyParams V) {
   const uint32_t nthreads = gridDim.x * blockDim.x;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  gre::VmScratch sc = make_scratch(V.scratch + (uint64_t)t * V.scratch_stride, V.rs.max_ninst, V.rs.max_ncap);
+  gre::VmScratch sc = make_scratch(V.scratch + (uint64_t)t * V.scratch_stride, V.rs);
   for (uint32_t j = t; j < V.n_jobs; j += nthreads) {
     const uint64_t c0 = V.job_start[j];
     const uint64_t c1 = (j + 1 < V.n_jobs) ? V.job_start[j + 1] : V.n_cands;
@@ -646,7 +647,7 @@ __global__ __launch_bounds__(256) void k_exclude(const uint8_t* data, const uint
                                                  uint64_t stride) {
   const uint32_t nthreads = gridDim.x * blockDim.x;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  gre::VmScratch sc = make_scratch(scratch + (uint64_t)t * stride, rs.max_ninst, rs.max_ncap);
+  gre::VmScratch sc = make_scratch(scratch + (uint64_t)t * stride, rs);
   for (uint32_t j = t; j < n_jobs; j += nthreads) {
     const ExclJob jb = jobs[j];
     const uint8_t* text = data + off[jb.file];
@@ -796,7 +797,7 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   std::vector<uint32_t> ranges;
   struct Off { size_t i, c, r; };
   std::vector<Off> offs;
-  uint32_t max_ninst = 1, max_ncap = 2;
+  uint32_t max_ninst = 1, max_ncap = 2, max_ninst_cap = 1;
   for (auto& rx : rs->regexes) {
     const gre::Prog& p = rx.c.prog;
     offs.push_back({inst.size(), classes.size(), ranges.size()});
@@ -810,7 +811,10 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   }
   for (auto& r : rs->rules)
     if (!r.group_name.empty() && r.regex >= 0)
+    {
       max_ncap = std::max<uint32_t>(max_ncap, (uint32_t)rs->regexes[r.regex].c.prog.ncap);
+      max_ninst_cap = std::max<uint32_t>(max_ninst_cap, (uint32_t)rs->regexes[r.regex].c.prog.inst.size());
+    }
   HIP_TRY(im.inst.ensure(inst.size() + 1));
   HIP_TRY(im.classes.ensure(classes.size() + 1));
   HIP_TRY(im.ranges.ensure(ranges.size() + 1));
@@ -944,11 +948,12 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   v.kw_words = std::max<uint32_t>(1, ((uint32_t)rs->keywords.size() + 31) / 32);
   v.max_ninst = max_ninst;
   v.max_ncap = max_ncap;
+  v.max_ninst_cap = max_ninst_cap;
   v.ac = AcDev{im.delta.p, im.cls.p, im.out_off.p, im.out_pat.p, im.pats.p, im.pat_bytes.p, im.pat_rules.p,
                ac.nstates, ac.nclasses};
   im.rs_id = rs->id;
   // VM scratch
-  e->scratch_stride = (scratch_bytes(max_ninst, max_ncap) + 255) & ~255ull;
+  e->scratch_stride = (scratch_bytes(max_ninst, max_ncap, max_ninst_cap) + 255) & ~255ull;
   return TSG_OK;
 }
 
@@ -1084,6 +1089,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   HIP_TRY(hipGetDeviceProperties(&prop, e->device));
   const uint32_t scan_blocks = (uint32_t)std::min<uint64_t>(nsteps, (uint64_t)prop.multiProcessorCount * 8);
   for (int attempt = 0; attempt < 2 && nbytes; ++attempt) {
+    HIP_TRY(hipEventRecord(e->ev[8], s));
     if (lds_table) {
       HIP_TRY(hipFuncSetAttribute((const void*)k_scan<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       hipLaunchKernelGGL(k_scan<true>, dim3(std::max(1u, scan_blocks)), dim3(kScanThreads), lds, s, P);
@@ -1092,6 +1098,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
       hipLaunchKernelGGL(k_scan<false>, dim3(std::max(1u, scan_blocks)), dim3(kScanThreads), lds, s, P);
     }
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(e->ev[9], s));
     Ctrl c;
     if ((rc = read_ctrl(e, &c))) return rc;
     if (c.hits <= hit_cap) break;
@@ -1276,6 +1283,11 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, e->ev[k], e->ev[k + 1]));
     tm[k] = ms;
+  }
+  if (nbytes) {  // k_scan alone (the dominant, HBM-bound kernel)
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, e->ev[8], e->ev[9]));
+    tm[7] = ms;
   }
   auto& R = res->impl;
   R.file_flags.resize(nf);
