@@ -53,9 +53,11 @@ def file_sizes(seed, target_bytes):
 def build_corpus(N, torch, seed, gb, density, device):
     sizes = file_sizes(seed, int(gb * 1e9))
     n_files = len(sizes)
+    # device layout (include/trivy_secret_gpu.h): each file followed by one NUL separator
     off = np.zeros(n_files + 1, dtype=np.uint64)
-    off[1:] = np.cumsum(sizes).astype(np.uint64)
+    off[1:] = np.cumsum(sizes + 1).astype(np.uint64)
     total = int(off[-1])
+    content = int(sizes.sum())
     chunk = N.lib.tsg_gen_chunk_bytes()
     nchunks = (sizes + chunk - 1) // chunk
     file_of = np.repeat(np.arange(n_files, dtype=np.uint64), nchunks)
@@ -63,7 +65,7 @@ def build_corpus(N, torch, seed, gb, density, device):
     cidx = np.arange(len(file_of), dtype=np.uint64) - first.astype(np.uint64)
     chunk_ids = (file_of << np.uint64(24)) | cidx
     dev = torch.device("cuda", device)
-    d_data = torch.empty(total + 4096, dtype=torch.uint8, device=dev)
+    d_data = torch.zeros(total + 4096, dtype=torch.uint8, device=dev)
     d_off = torch.from_numpy(off.view(np.int64)).to(dev)
     d_chunks = torch.from_numpy(chunk_ids.view(np.int64)).to(dev)
     d_paths = torch.empty(n_files * 31 + 64, dtype=torch.uint8, device=dev)
@@ -80,7 +82,7 @@ def build_corpus(N, torch, seed, gb, density, device):
     nplants = min(int(d_np.item()), plant_cap)
     plants = np.frombuffer(d_plants[: nplants * rec].cpu().numpy().tobytes(), dtype=PLANT_DTYPE)
     del d_chunks
-    return dict(n_files=n_files, total=total, off=off, d_data=d_data, d_off=d_off, d_paths=d_paths,
+    return dict(n_files=n_files, total=content, packed=total, off=off, d_data=d_data, d_off=d_off, d_paths=d_paths,
                 d_poff=d_poff, plants=plants, sizes=sizes)
 
 

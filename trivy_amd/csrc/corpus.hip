@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void k_gen(uint8_t* data, const uint64_t* off,
   if (i >= n_chunks) return;
   const uint32_t f = (uint32_t)(chunk_id[i] >> 24);
   const uint32_t c = (uint32_t)(chunk_id[i] & 0xFFFFFF);
-  const uint64_t fstart = off[f], flen = off[f + 1] - off[f];
+  const uint64_t fstart = off[f], flen = off[f + 1] - off[f] - 1;  // NUL separator after each file
   const uint64_t cstart = (uint64_t)c * kGenChunk;
   const uint32_t n = (uint32_t)((flen - cstart) < kGenChunk ? (flen - cstart) : kGenChunk);
   Plant local[kMaxPlantsPerChunk];

@@ -10,7 +10,10 @@
 
 namespace tsg {
 
-constexpr int kAcMaxLit = 16;  // trie depth; longer keywords are confirmed on hit
+constexpr int kAcMaxLit = 8;   // trie depth; longer patterns are confirmed on hit
+constexpr uint32_t kNlBlock = 8192;  // newline-count granularity (bytes)
+constexpr uint32_t kFastClasses = 64;  // fast automaton rows are padded to 64 classes
+constexpr uint32_t kFastMaxStates = 511;  // 16-bit row byte offsets
 constexpr uint32_t kNoKw = 0xFFFFFFFFu;
 
 enum RuleMode : uint8_t { MODE_NEVER = 0, MODE_ANCHORED = 1, MODE_FULL = 2 };
@@ -26,7 +29,7 @@ struct RuleDev {
   uint32_t group_off, group_n;  // capture slots of groups named SecretGroupName
   uint32_t allow_off, allow_n;  // per-rule allow regex progs
   uint32_t use_groups;          // SecretGroupName != ""
-  uint32_t pad;
+  uint32_t max_len;             // longest possible match in bytes (gre::kInf if unbounded)
 };
 
 struct PatDev {
@@ -50,10 +53,16 @@ struct AcDev {
   const uint8_t* pat_bytes;
   const uint32_t* pat_rules;
   uint32_t nstates, nclasses;
+  const uint8_t* fast_lds;  // LDS image for k_scan_fast: u16 rows [nstates][64] then cls2[256]; null if too big
+  uint32_t fast_cls_off;    // byte offset of cls2 inside the image
 };
+
+constexpr uint32_t kLitRec = 36;  // prefilter literal record: len, lower[16], req[16], pad
 
 struct RuleSetDev {
   const gre::ProgView* progs;
+  const uint32_t* prog_lit_off;  // per program: range of prefilter literals (n_progs + 1)
+  const uint8_t* prog_lits;      // kLitRec-byte records
   const RuleDev* rules;
   const uint32_t* kw_ids;
   const uint32_t* group_slots;
@@ -87,7 +96,9 @@ struct RuleHost {
 };
 
 struct AcHost {
-  std::vector<uint16_t> delta;
+  std::vector<uint16_t> delta;  // generic: next state | 0x8000 output bit
+  std::vector<uint8_t> fast;    // fast image (see AcDev::fast_lds), empty if not representable
+  uint32_t fast_cls_off = 0;
   uint8_t cls[256];
   std::vector<uint32_t> out_off;
   std::vector<uint16_t> out_pat;

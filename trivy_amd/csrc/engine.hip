@@ -96,6 +96,9 @@ struct ScanParams {
   uint64_t* hits;
   uint64_t hit_cap;
   Ctrl* ctrl;
+  uint32_t* nl_blocks;  // newline count per kNlBlock bytes of the batch
+  const uint8_t* tail;  // virtual base of a zero-padded copy of data[tail_base-8, nbytes)
+  uint64_t tail_base;   // first byte of the final partial fast region
 };
 
 __device__ inline uint32_t find_file(const uint64_t* off, uint32_t lo, uint32_t hi, uint64_t pos) {
@@ -109,10 +112,12 @@ __device__ inline uint32_t find_file(const uint64_t* off, uint32_t lo, uint32_t 
 
 __device__ inline uint8_t lower_ascii(uint8_t b) { return (b >= 'A' && b <= 'Z') ? b + 32 : b; }
 
-// Report every pattern ending at global position p (state has outputs).
-__device__ __noinline__ void report(const ScanParams& P, uint32_t st, uint64_t p, uint32_t fi,
-                                    uint64_t fstart, uint64_t fend, uint32_t* last_kw) {
+// Report every pattern ending at global position p (AC state st has outputs).
+// Files are NUL-separated, so the pattern lies inside file fi.
+__device__ __noinline__ void report(const ScanParams& P, uint32_t st, uint64_t p, uint64_t* last_kw) {
   const AcDev& ac = P.rs.ac;
+  const uint32_t fi = find_file(P.off, 0, P.n_files, p);
+  const uint64_t fend = P.off[fi + 1] - 1;  // content end (separator excluded)
   uint32_t o0 = ac.out_off[st], o1 = ac.out_off[st + 1];
   for (uint32_t o = o0; o < o1; ++o) {
     uint32_t pid = ac.out_pat[o];
@@ -128,7 +133,7 @@ __device__ __noinline__ void report(const ScanParams& P, uint32_t st, uint64_t p
     }
     if (pd.special) atomicOr(&P.file_flags[fi], kFileSpecial);
     if (pd.kw != kNoKw) {
-      uint32_t key = (fi << 8) ^ pd.kw;  // cheap per-lane dedupe of repeated keywords
+      const uint64_t key = ((uint64_t)fi << 32) | pd.kw;  // per-lane dedupe of repeated keywords
       if (*last_kw != key) {
         *last_kw = key;
         atomicOr(&P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)], 1u << (pd.kw & 31));
@@ -147,11 +152,14 @@ __device__ __noinline__ void report(const ScanParams& P, uint32_t st, uint64_t p
   }
 }
 
+// Generic scan (any automaton size): one 128-byte chunk per lane, byte
+// loads from a padded LDS tile, transitions from LDS (or global when the
+// table exceeds the LDS budget).  Used for large custom rule sets.
 template <bool kLdsTable>
-__global__ __launch_bounds__(kScanThreads) void k_scan(ScanParams P) {
+__global__ __launch_bounds__(kScanThreads) void k_scan_generic(ScanParams P) {
   extern __shared__ __align__(16) uint8_t smem[];
-  uint8_t* cls = smem;                  // 256
-  uint8_t* tile = smem + 256;           // kTileLds
+  uint8_t* cls = smem;         // 256
+  uint8_t* tile = smem + 256;  // kTileLds
   uint16_t* dl = (uint16_t*)(smem + 256 + kTileLds);
   const AcDev& ac = P.rs.ac;
   const uint32_t K = ac.nclasses;
@@ -161,15 +169,12 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanParams P) {
     for (uint32_t i = threadIdx.x; i < n; i += kScanThreads) dl[i] = ac.delta[i];
   }
   const uint16_t* delta = kLdsTable ? dl : ac.delta;
-  __shared__ uint32_t s_flo, s_fhi;
   const uint32_t tid = threadIdx.x;
   const uint64_t nsteps = (P.nbytes + kBlockBytes - 1) / kBlockBytes;
-  uint32_t last_kw = 0xFFFFFFFFu;
-
+  uint64_t last_kw = ~0ull;
   for (uint64_t step = blockIdx.x; step < nsteps; step += gridDim.x) {
     const uint64_t base = step * kBlockBytes;
     __syncthreads();
-    // ---- stage the 32 KiB block (+16 B halo) into padded LDS rows
 #pragma unroll
     for (int k = 0; k < kSegsPerLane; ++k) {
       const uint32_t seg = k * kScanThreads + tid;
@@ -190,41 +195,217 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanParams P) {
       uint4 v = make_uint4(0, 0, 0, 0);
       if (base >= 16) v = *(const uint4*)(P.data + base - 16);
       *(uint4*)(tile) = v;
-      uint64_t last = base + kBlockBytes - 1;
-      if (last >= P.nbytes) last = P.nbytes - 1;
-      s_flo = find_file(P.off, 0, P.n_files, base);
-      s_fhi = find_file(P.off, 0, P.n_files, last) + 1;
     }
     __syncthreads();
     const uint64_t p0 = base + (uint64_t)tid * kChunk;
     if (p0 >= P.nbytes) continue;
     const uint64_t pend = p0 + kChunk < P.nbytes ? p0 + kChunk : P.nbytes;
-    uint32_t fi = find_file(P.off, s_flo, s_fhi, p0);
-    uint64_t fstart = P.off[fi], fend = P.off[fi + 1];
-    while (fend <= p0) {  // skip empty files at p0
-      ++fi;
-      fstart = fend;
-      fend = P.off[fi + 1];
-    }
     const uint8_t* row = tile + tid * kRow + 16;
     uint32_t st = 0;
-    // warm-up: the automaton started 15 bytes earlier (never across a file start)
-    const uint64_t w0 = (p0 - fstart) >= (uint64_t)(kAcMaxLit - 1) ? p0 - (kAcMaxLit - 1) : fstart;
-    for (uint64_t p = w0; p < p0; ++p) {
-      const uint8_t b = row[(int64_t)p - (int64_t)p0];
-      st = delta[st * K + cls[b]] & 0x7FFFu;
-    }
+    // warm-up: the automaton restarted kAcMaxLit-1 bytes earlier (a NUL
+    // separator inside the window resets it, so files never leak)
+    const uint64_t w0 = p0 >= (uint64_t)(kAcMaxLit - 1) ? p0 - (kAcMaxLit - 1) : 0;
+    for (uint64_t p = w0; p < p0; ++p) st = delta[st * K + cls[row[(int64_t)p - (int64_t)p0]]] & 0x7FFFu;
+    uint32_t nl = 0;
     for (uint64_t p = p0; p < pend; ++p) {
-      while (p == fend) {
-        ++fi;
-        fstart = fend;
-        fend = P.off[fi + 1];
-        st = 0;
-      }
       const uint8_t b = row[p - p0];
+      nl += b == '\n';
       const uint32_t nx = delta[st * K + cls[b]];
       st = nx & 0x7FFFu;
-      if (nx & 0x8000u) report(P, st, p, fi, fstart, fend, &last_kw);
+      if (nx & 0x8000u) report(P, st, p, &last_kw);
+    }
+    atomicAdd(&P.nl_blocks[p0 / kNlBlock], nl);
+  }
+}
+
+// Fast scan: gfx950-tuned AC pass over the whole batch (the HBM-bound hot loop).
+//  * 1024-thread blocks, one LDS copy of the automaton per CU: transition rows
+//    padded to 64 classes (128 B), entry = next-row byte offset | output bit,
+//    class table after it holding 2*class, so one step is
+//      e = T[(e & ~1) | cls2[b]]   (v_and_or_b32 + 2 ds_reads)
+//  * each lane owns two independent 128-byte chunks (two dependency chains
+//    per lane hide the LDS latency), loaded straight into VGPRs with 16-byte
+//    loads; 7 bytes of warm-up from the previous chunk
+//  * outputs are OR-ed per 8-byte group; the (rare) flagged groups are
+//    replayed byte by byte with reporting afterwards, so the hot loop has no
+//    divergent branch
+//  * per 8 KiB block newline counts (SWAR) for StartLine/EndLine.
+constexpr int kFastThreads = 1024;
+constexpr int kFastChunk = 128;                          // bytes per lane
+constexpr int kFastRegion = 64 * kFastChunk;             // 8 KiB per wave iteration
+static_assert(kFastRegion == (int)kNlBlock, "newline blocks follow the wave layout");
+
+__device__ inline uint32_t nl_count_dword(uint32_t w) {
+  const uint32_t t = w ^ 0x0A0A0A0Au;
+  const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
+  return __builtin_popcount(z);
+}
+
+__device__ inline uint32_t byte_of(uint32_t w, int j) { return (w >> (8 * j)) & 0xFFu; }
+
+__device__ __noinline__ void replay_group(const ScanParams& P, const uint8_t* lds, uint32_t e, uint64_t p,
+                                          uint64_t* last_kw) {
+  const uint16_t* T = (const uint16_t*)lds;
+  const uint8_t* cls2 = lds + P.rs.ac.fast_cls_off;
+  for (int k = 0; k < 8; ++k) {
+    if (p + k >= P.nbytes) break;
+    const uint32_t b = P.data[p + k];
+    e = T[((e & ~1u) | cls2[b]) >> 1];
+    if (e & 1u) report(P, e >> 7, p + k, last_kw);
+  }
+}
+
+// Flagged-group bookkeeping for one chain.
+struct Flags2 {
+  int g1, g2, glast;
+  uint32_t s1, s2;
+};
+
+__device__ inline void note_group(Flags2& f, int g, uint32_t acc, uint32_t gs) {
+  if (acc & 1u) {
+    if (f.g1 < 0) { f.g1 = g; f.s1 = gs; }
+    else if (f.g2 < 0) { f.g2 = g; f.s2 = gs; }
+    f.glast = g;
+  }
+}
+
+__device__ inline uint32_t ac_step(const uint16_t* T, const uint8_t* cls2, uint32_t e, uint32_t b) {
+  return T[((e & ~1u) | cls2[b]) >> 1];
+}
+
+// `src` is P.data, or for the final partial region a zero-padded copy of it
+// addressed with the same offsets (ScanParams::tail), so loads need no bounds.
+__device__ inline void fast_region(const ScanParams& P, const uint8_t* smem, const uint8_t* src, uint64_t base,
+                                   uint32_t lane, uint64_t* last_kw) {
+  const uint16_t* T = (const uint16_t*)smem;
+  const uint8_t* cls2 = smem + P.rs.ac.fast_cls_off;
+  const uint64_t p0 = base + (uint64_t)lane * kFastChunk;
+  // warm-up: the 7 bytes before the chunk
+  const uint2 h0 = p0 >= 8 ? *(const uint2*)(src + p0 - 8) : make_uint2(0, 0);
+  uint32_t e = 0;
+#pragma unroll
+  for (int j = 1; j < 8; ++j) e = ac_step(T, cls2, e, byte_of(j < 4 ? h0.x : h0.y, j & 3));
+  uint32_t nl = 0;
+  Flags2 f{-1, -1, -1, 0, 0};
+#pragma unroll
+  for (int k = 0; k < kFastChunk / 16; ++k) {
+    const uint4 v = *(const uint4*)(src + p0 + 16 * k);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // two 8-byte groups per 16-byte vector
+      const uint32_t gs = e;
+      uint32_t acc = 0;
+#pragma unroll
+      for (int dw = 0; dw < 2; ++dw) {
+        const uint32_t a = w[2 * h + dw];
+        nl += nl_count_dword(a);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          e = ac_step(T, cls2, e, byte_of(a, j));
+          acc |= e;
+        }
+      }
+      note_group(f, 2 * k + h, acc, gs);
+    }
+  }
+  // newline count of this wave's 8 KiB block
+  for (int o = 32; o > 0; o >>= 1) nl += __shfl_xor(nl, o);
+  if (lane == 0 && base < P.nbytes) P.nl_blocks[base / kNlBlock] = nl;
+  // rare path: replay flagged groups with reporting
+  if (f.g1 >= 0) {
+    replay_group(P, smem, f.s1, p0 + 8 * f.g1, last_kw);
+    if (f.g2 >= 0) {
+      uint32_t es = f.s2;
+      for (int g = f.g2; g <= f.glast; ++g) {
+        replay_group(P, smem, es, p0 + 8 * g, last_kw);
+        for (int k = 0; k < 8; ++k) {
+          const uint64_t a = p0 + 8 * g + k;
+          es = ac_step(T, cls2, es, a < P.nbytes ? P.data[a] : 0u);
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  const AcDev& ac = P.rs.ac;
+  {
+    const uint32_t words = (ac.fast_cls_off + 256) / 4;
+    const uint32_t* src = (const uint32_t*)ac.fast_lds;
+    for (uint32_t i = threadIdx.x; i < words; i += kFastThreads) ((uint32_t*)smem)[i] = src[i];
+  }
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = (blockIdx.x * (kFastThreads / 64)) + (threadIdx.x >> 6);
+  const uint32_t nwaves = gridDim.x * (kFastThreads / 64);
+  const uint64_t nregions = (P.nbytes + kFastRegion - 1) / kFastRegion;
+  uint64_t last_kw = ~0ull;
+  for (uint64_t rg = wave; rg < nregions; rg += nwaves) {
+    const uint64_t base = rg * kFastRegion;
+    fast_region(P, smem, base >= P.tail_base ? P.tail : P.data, base, lane, &last_kw);
+  }
+}
+
+// Exact MatchKeywords for files holding U+0130 (C4 B0) or U+212A (E2 84 AA):
+// bytes.ToLower maps them to 'i' / 'k' (scanner.go:175), the only non-ASCII
+// runes whose lowercase is ASCII; every other byte >= 0x80 can never be part
+// of an (ASCII) keyword.  One wave per flagged file, one segment per lane,
+// 32 raw bytes of warm-up (>= 7 lowered runes) snapped to a rune start.
+// Keyword bits are idempotent, so overlapping segments are harmless.
+__global__ __launch_bounds__(256) void k_special_gate(ScanParams P) {
+  const AcDev& ac = P.rs.ac;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  for (uint64_t f = wave0; f < P.n_files; f += nwaves) {
+    if (!(P.file_flags[f] & kFileSpecial)) continue;
+    const uint64_t fs = P.off[f], fe = P.off[f + 1] - 1;
+    const uint64_t len = fe - fs;
+    const uint64_t seg = (len + 63) / 64;
+    uint64_t a = fs + lane * seg, b = a + seg < fe ? a + seg : fe;
+    if (a >= b) continue;
+    uint64_t p = a >= fs + 32 ? a - 32 : fs;
+    while (p > fs && (P.data[p] & 0xC0) == 0x80) --p;  // snap to a rune start
+    uint32_t st = 0;
+    while (p < b) {
+      uint32_t c = P.data[p];
+      uint32_t w = 1;
+      if (c == 0xC4 && p + 1 < fe && P.data[p + 1] == 0xB0) {
+        c = 'i';
+        w = 2;
+      } else if (c == 0xE2 && p + 2 < fe && P.data[p + 1] == 0x84 && P.data[p + 2] == 0xAA) {
+        c = 'k';
+        w = 3;
+      } else if (c >= 0x80) {
+        c = 0;  // breaker: never inside an ASCII keyword
+      }
+      const uint32_t nx = ac.delta[st * ac.nclasses + ac.cls[c]];
+      st = nx & 0x7FFFu;
+      if (nx & 0x8000u) {
+        for (uint32_t o = ac.out_off[st]; o < ac.out_off[st + 1]; ++o) {
+          const PatDev pd = ac.pats[ac.out_pat[o]];
+          if (pd.kw == kNoKw) continue;
+          if (pd.trunc) {  // confirm the rest of a long keyword on the lowered stream
+            const uint8_t* pb = ac.pat_bytes + pd.bytes_off;
+            uint64_t q = p + w;
+            bool ok = true;
+            for (uint32_t k = kAcMaxLit; k < pd.len && ok; ++k) {
+              if (q >= fe) { ok = false; break; }
+              uint32_t ch = P.data[q];
+              uint32_t cw = 1;
+              if (ch == 0xC4 && q + 1 < fe && P.data[q + 1] == 0xB0) { ch = 'i'; cw = 2; }
+              else if (ch == 0xE2 && q + 2 < fe && P.data[q + 1] == 0x84 && P.data[q + 2] == 0xAA) { ch = 'k'; cw = 3; }
+              else if (ch >= 0x80) { ok = false; break; }
+              ok = lower_ascii((uint8_t)ch) == pb[k];
+              q += cw;
+            }
+            if (!ok) continue;
+          }
+          atomicOr(&P.file_kw[(size_t)f * P.rs.kw_words + (pd.kw >> 5)], 1u << (pd.kw & 31));
+        }
+      }
+      p += w;
     }
   }
 }
@@ -284,6 +465,37 @@ __device__ inline bool match_string(const gre::ProgView& pv, const uint8_t* s, u
   return gre::vm_search(pv, s, n, 0, n, true, sc, &ms, &me);
 }
 
+// Literal prefilter for MatchString on short strings (paths, match texts):
+// a pattern with an anchor factor can only match a string that contains one
+// of its literals (case rules as in the scan).  Strings with bytes >= 0x80
+// skip the filter (fold-special runes).
+__device__ inline bool may_match(const RuleSetDev& rs, uint32_t prog, const uint8_t* s, uint32_t n) {
+  const uint32_t l0 = rs.prog_lit_off[prog], l1 = rs.prog_lit_off[prog + 1];
+  if (l0 == l1) return true;
+  for (uint32_t i = 0; i < n; ++i)
+    if (s[i] >= 0x80) return true;
+  for (uint32_t l = l0; l < l1; ++l) {
+    const uint8_t* rec = rs.prog_lits + (size_t)l * kLitRec;
+    const uint32_t len = rec[0];
+    const uint8_t* lo = rec + 1;
+    const uint8_t* rq = rec + 1 + 16;
+    for (uint32_t i = 0; i + len <= n; ++i) {
+      uint32_t k = 0;
+      for (; k < len; ++k) {
+        const uint8_t c = s[i + k];
+        if (lower_ascii(c) != lo[k] || (rq[k] && c != rq[k])) break;
+      }
+      if (k == len) return true;
+    }
+  }
+  return false;
+}
+
+__device__ inline bool match_string_pf(const RuleSetDev& rs, uint32_t prog, const uint8_t* s, uint32_t n,
+                                       gre::VmScratch& sc) {
+  return may_match(rs, prog, s, n) && match_string(rs.progs[prog], s, n, sc);
+}
+
 __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
   const uint32_t nthreads = gridDim.x * blockDim.x;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -293,7 +505,7 @@ __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
     const uint32_t plen = (uint32_t)(G.path_off[f + 1] - G.path_off[f]);
     bool allowed = false;
     for (uint32_t k = 0; k < G.n_gpath && !allowed; ++k)
-      allowed = match_string(G.rs.progs[G.gpath[k]], path, plen, sc);
+      allowed = match_string_pf(G.rs, G.gpath[k], path, plen, sc);
     if (allowed) {
       G.file_flags[f] |= kFileAllowed;
       continue;
@@ -301,9 +513,9 @@ __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
     if (!G.any_rule_paths) continue;
     for (uint32_t r = 0; r < G.rs.n_rules; ++r) {
       bool skip = false;
-      if (G.rule_path[r] >= 0) skip = !match_string(G.rs.progs[G.rule_path[r]], path, plen, sc);
+      if (G.rule_path[r] >= 0) skip = !match_string_pf(G.rs, (uint32_t)G.rule_path[r], path, plen, sc);
       for (uint32_t k = G.rule_apath_off[r]; k < G.rule_apath_off[r + 1] && !skip; ++k)
-        skip = match_string(G.rs.progs[G.rule_apath[k]], path, plen, sc);
+        skip = match_string_pf(G.rs, G.rule_apath[k], path, plen, sc);
       if (skip) G.path_mask[(size_t)f * G.rule_words + (r >> 5)] |= 1u << (r & 31);
     }
   }
@@ -388,13 +600,28 @@ __global__ __launch_bounds__(256) void k_full_jobs(ExpandParams E) {
   }
 }
 
-__global__ void k_mark_jobs(const uint64_t* keys, const uint32_t* vals, uint64_t n, uint8_t* flags) {
+// Job boundaries over the sorted candidates: a new (file, rule) pair starts a
+// job; inside a pair, a run of anchored candidates is split where the gap to
+// the previous candidate exceeds max_len + (off_max - off_min) and a 4 KiB
+// line is crossed — no match found before the split can reach a start
+// window after it, so the pieces replay Go's sequential FindAll exactly and
+// long files no longer serialise on one lane.
+__global__ void k_mark_jobs(const uint64_t* keys, const uint32_t* vals, uint64_t n, const RuleDev* rules,
+                            uint8_t* flags) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint8_t f = 1;
   if (i > 0) {
-    f = ((keys[i] >> kPosBits) != (keys[i - 1] >> kPosBits)) ||
-        ((vals[i] & ~kFullFlag) != (vals[i - 1] & ~kFullFlag));
+    const uint32_t r = (uint32_t)(keys[i] >> kPosBits);
+    f = (r != (uint32_t)(keys[i - 1] >> kPosBits)) || ((vals[i] & ~kFullFlag) != (vals[i - 1] & ~kFullFlag));
+    if (!f && !(vals[i] & kFullFlag) && !(vals[i - 1] & kFullFlag)) {
+      const RuleDev& rd = rules[r];
+      const uint64_t h0 = keys[i - 1] & kPosMask, h1 = keys[i] & kPosMask;
+      if (rd.max_len != gre::kInf && rd.off_max != gre::kInf && (h0 >> 12) != (h1 >> 12)) {
+        const uint64_t need = (uint64_t)rd.max_len + (rd.off_max - rd.off_min) + 8;
+        f = h1 - h0 > need;
+      }
+    }
   }
   flags[i] = f;
 }
@@ -544,9 +771,9 @@ __device__ void emit_match(const VerifyParams& V, const RuleDev& rd, uint32_t ru
                            gre::VmScratch& sc) {
   // AllowLocation (scanner.go:145-148): global then rule allow regexes on the whole match
   for (uint32_t k = 0; k < V.rs.n_global_allow; ++k)
-    if (match_string(V.rs.progs[V.rs.global_allow[k]], text + ms, me - ms, sc)) return;
+    if (match_string_pf(V.rs, V.rs.global_allow[k], text + ms, me - ms, sc)) return;
   for (uint32_t k = 0; k < rd.allow_n; ++k)
-    if (match_string(V.rs.progs[V.rs.allow_progs[rd.allow_off + k]], text + ms, me - ms, sc)) return;
+    if (match_string_pf(V.rs, V.rs.allow_progs[rd.allow_off + k], text + ms, me - ms, sc)) return;
   if (!rd.use_groups) {
     unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
     if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, ms, me, 0, 0, 0, 0};
@@ -582,7 +809,7 @@ __global__ __launch_bounds__(256) void k_verify(VerifyParams V) {
     const gre::ProgView& pv = V.rs.progs[rd.prog];
     const uint64_t fstart = V.off[fi];
     const uint8_t* text = V.data + fstart;
-    const uint32_t n = (uint32_t)(V.off[fi + 1] - fstart);
+    const uint32_t n = (uint32_t)(V.off[fi + 1] - 1 - fstart);  // NUL separator excluded
     uint32_t ms, me;
     if (full) {
       // regexp.go allMatches over the whole file
@@ -651,7 +878,7 @@ __global__ __launch_bounds__(256) void k_exclude(const uint8_t* data, const uint
   for (uint32_t j = t; j < n_jobs; j += nthreads) {
     const ExclJob jb = jobs[j];
     const uint8_t* text = data + off[jb.file];
-    const uint32_t n = (uint32_t)(off[jb.file + 1] - off[jb.file]);
+    const uint32_t n = (uint32_t)(off[jb.file + 1] - 1 - off[jb.file]);
     const gre::ProgView& pv = rs.progs[jb.prog];
     uint32_t pos = 0, ms, me;
     int64_t prev_end = -1;
@@ -677,28 +904,36 @@ __global__ __launch_bounds__(256) void k_exclude(const uint8_t* data, const uint
 }
 
 // ----------------------------------------------------------------- lines --
-// One wave per location: P(start) = count('\n' in [0,start)) and P(end) on the
+// Global newline prefix G(x) = count('\n' in data[0,x)) from the per-8KiB
+// block counts k_scan produced (nl_pre = their exclusive prefix sum) plus one
+// wave-cooperative count inside x's block (<= 8 KiB, 128 B per lane).
+__device__ inline uint32_t wave_nl_prefix(const uint8_t* data, const uint32_t* nl_pre, uint64_t x,
+                                          uint32_t lane) {
+  const uint64_t b0 = x & ~(uint64_t)(kNlBlock - 1);
+  uint32_t c = 0;
+  const uint64_t s = b0 + (uint64_t)lane * 128;
+  const uint64_t e = s + 128 < x ? s + 128 : x;
+  for (uint64_t i = s; i < e; ++i) c += data[i] == '\n';
+  for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
+  return nl_pre[x / kNlBlock] + c;
+}
+
+// One wave per location: P(start), P(end) relative to the file start on the
 // uncensored content; censored_lines() turns them into findLocation's numbers.
-__global__ __launch_bounds__(256) void k_lines(const uint8_t* data, const uint64_t* off, DevLoc* locs,
-                                               uint64_t n_locs) {
+__global__ __launch_bounds__(256) void k_lines(const uint8_t* data, const uint64_t* off, const uint32_t* nl_pre,
+                                               DevLoc* locs, uint64_t n_locs) {
   const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63;
   if (w >= n_locs) return;
-  DevLoc L = locs[w];
+  const DevLoc L = locs[w];
   if (L.flags) return;
-  const uint8_t* text = data + off[L.file];
-  uint32_t c1 = 0, c2 = 0;
-  for (uint64_t i = lane; i < L.end; i += 64) {
-    const uint32_t nl = text[i] == '\n';
-    if (i < L.start) c1 += nl; else c2 += nl;
-  }
-  for (int d = 32; d > 0; d >>= 1) {
-    c1 += __shfl_down(c1, d);
-    c2 += __shfl_down(c2, d);
-  }
+  const uint64_t fs = off[L.file];
+  const uint32_t g0 = wave_nl_prefix(data, nl_pre, fs, lane);
+  const uint32_t g1 = wave_nl_prefix(data, nl_pre, fs + L.start, lane);
+  const uint32_t g2 = wave_nl_prefix(data, nl_pre, fs + L.end, lane);
   if (lane == 0) {  // raw prefix counts P(start), P(end); see censored_lines()
-    locs[w].start_line = c1;
-    locs[w].end_line = c1 + c2;
+    locs[w].start_line = g1 - g0;
+    locs[w].end_line = g2 - g0;
   }
 }
 
@@ -746,13 +981,17 @@ struct DevImage {
   DBuf<PatDev> pats;
   DBuf<uint8_t> pat_bytes;
   DBuf<uint32_t> pat_rules;
+  DBuf<uint8_t> fast;
+  DBuf<uint32_t> prog_lit_off;
+  DBuf<uint8_t> prog_lits;
   RuleSetDev view{};
   // offsets into u32
   uint32_t o_gpath = 0, n_gpath = 0, o_apoff = 0, o_ap = 0, o_full = 0, n_full = 0;
   void release() {
     inst.release(); classes.release(); ranges.release(); progs.release(); rules.release();
     u32.release(); rule_path.release(); delta.release(); cls.release(); out_off.release();
-    out_pat.release(); pats.release(); pat_bytes.release(); pat_rules.release();
+    out_pat.release(); pats.release(); pat_bytes.release(); pat_rules.release(); fast.release();
+    prog_lit_off.release(); prog_lits.release();
   }
 };
 
@@ -778,6 +1017,9 @@ struct tsg_engine {
   DBuf<DevLoc> locs;
   DBuf<uint8_t> scratch;
   DBuf<Ctrl> ctrl;
+  DBuf<uint32_t> nl_blocks, nl_pre;
+  DBuf<uint8_t> tail;
+  uint32_t num_cus = 0;
   DBuf<ExclJob> excl_jobs;
   DBuf<ExclRange> excl_out;
   uint32_t vm_threads = 0;
@@ -829,6 +1071,26 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
     views.push_back(gre::ProgView{im.inst.p + offs[k].i, im.classes.p + offs[k].c, im.ranges.p,
                                   (uint32_t)p.inst.size(), p.start, (uint32_t)p.ncap});
   }
+  // per-program anchor literals for the MatchString prefilter
+  std::vector<uint32_t> lit_off{0};
+  std::vector<uint8_t> lits;
+  for (auto& rx : rs->regexes) {
+    const gre::Anchor& a = rx.c.anchor;
+    if (a.valid && a.lits.size() <= 32) {
+      for (auto& l : a.lits) {
+        uint8_t rec[kLitRec] = {0};
+        rec[0] = (uint8_t)l.lower.size();
+        memcpy(rec + 1, l.lower.data(), l.lower.size());
+        memcpy(rec + 17, l.req.data(), l.req.size());
+        lits.insert(lits.end(), rec, rec + kLitRec);
+      }
+    }
+    lit_off.push_back((uint32_t)(lits.size() / kLitRec));
+  }
+  HIP_TRY(im.prog_lit_off.ensure(lit_off.size()));
+  HIP_TRY(hipMemcpy(im.prog_lit_off.p, lit_off.data(), lit_off.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(im.prog_lits.ensure(lits.size() + kLitRec));
+  if (!lits.empty()) HIP_TRY(hipMemcpy(im.prog_lits.p, lits.data(), lits.size(), hipMemcpyHostToDevice));
   HIP_TRY(im.progs.ensure(views.size() + 1));
   if (!views.empty())
     HIP_TRY(hipMemcpy(im.progs.p, views.data(), views.size() * sizeof(gre::ProgView), hipMemcpyHostToDevice));
@@ -859,6 +1121,7 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
         for (int q = 0; q < 4; ++q) d.alpha[q] = c.anchor.alpha.w[q];
       }
       d.use_groups = !r.group_name.empty();
+      d.max_len = c.max_len;
       d.group_off = (uint32_t)group_slots.size();
       if (d.use_groups)
         for (size_t g = 0; g < c.prog.cap_names.size(); ++g)
@@ -938,6 +1201,8 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   // ---- view
   RuleSetDev& v = im.view;
   v.progs = im.progs.p;
+  v.prog_lit_off = im.prog_lit_off.p;
+  v.prog_lits = im.prog_lits.p;
   v.rules = im.rules.p;
   v.kw_ids = im.u32.p + o_kw;
   v.group_slots = im.u32.p + o_gs;
@@ -949,8 +1214,14 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   v.max_ninst = max_ninst;
   v.max_ncap = max_ncap;
   v.max_ninst_cap = max_ninst_cap;
+  const uint8_t* fast = nullptr;
+  if (!ac.fast.empty()) {
+    HIP_TRY(im.fast.ensure(ac.fast.size() + 16));
+    HIP_TRY(hipMemcpy(im.fast.p, ac.fast.data(), ac.fast.size(), hipMemcpyHostToDevice));
+    fast = im.fast.p;
+  }
   v.ac = AcDev{im.delta.p, im.cls.p, im.out_off.p, im.out_pat.p, im.pats.p, im.pat_bytes.p, im.pat_rules.p,
-               ac.nstates, ac.nclasses};
+               ac.nstates, ac.nclasses, fast, ac.fast_cls_off};
   im.rs_id = rs->id;
   // VM scratch
   e->scratch_stride = (scratch_bytes(max_ninst, max_ncap, max_ninst_cap) + 255) & ~255ull;
@@ -1006,6 +1277,51 @@ void censored_lines(std::vector<DevLoc>& locs) {
 int read_ctrl(tsg_engine* e, Ctrl* h) {
   HIP_TRY(hipMemcpyAsync(h, e->ctrl.p, sizeof(Ctrl), hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
+  return TSG_OK;
+}
+
+// Launch the AC pass: k_scan_fast when the automaton fits its LDS image,
+// else the generic kernel (transition table in LDS or, if too large, global).
+int launch_scan(tsg_engine* e, ScanParams P) {
+  hipStream_t s = e->stream;
+  if (!e->num_cus) {
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, e->device));
+    e->num_cus = (uint32_t)prop.multiProcessorCount;
+  }
+  const AcDev& ac = P.rs.ac;
+  if (ac.fast_lds) {
+    // final partial region: zero-padded copy (with 8 bytes of warm-up context)
+    P.tail_base = (P.nbytes / kFastRegion) * kFastRegion;
+    const uint64_t lead = P.tail_base >= 8 ? 8 : P.tail_base;
+    HIP_TRY(e->tail.ensure(8 + kFastRegion + 64));
+    HIP_TRY(hipMemsetAsync(e->tail.p, 0, 8 + kFastRegion + 64, s));
+    if (P.nbytes - P.tail_base + lead)
+      HIP_TRY(hipMemcpyAsync(e->tail.p + 8 - lead, P.data + P.tail_base - lead, P.nbytes - P.tail_base + lead,
+                             hipMemcpyDeviceToDevice, s));
+    P.tail = e->tail.p + 8 - P.tail_base;
+    const size_t lds = ac.fast_cls_off + 256;
+    const uint64_t nregions = (P.nbytes + kFastRegion - 1) / kFastRegion;
+    const uint64_t waves_per_block = kFastThreads / 64;
+    const uint32_t blocks = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>((nregions + waves_per_block - 1) / waves_per_block, (uint64_t)e->num_cus));
+    HIP_TRY(hipFuncSetAttribute((const void*)k_scan_fast, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_scan_fast, dim3(blocks), dim3(kFastThreads), lds, s, P);
+  } else {
+    const size_t table_bytes = (size_t)ac.nstates * ac.nclasses * 2;
+    const bool lds_table = table_bytes <= (size_t)kLdsTableMax;
+    const size_t lds = 256 + kTileLds + (lds_table ? table_bytes : 0);
+    const uint64_t nsteps = (P.nbytes + kBlockBytes - 1) / kBlockBytes;
+    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nsteps, (uint64_t)e->num_cus * 8));
+    if (lds_table) {
+      HIP_TRY(hipFuncSetAttribute((const void*)k_scan_generic<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(k_scan_generic<true>, dim3(blocks), dim3(kScanThreads), lds, s, P);
+    } else {
+      HIP_TRY(hipFuncSetAttribute((const void*)k_scan_generic<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(k_scan_generic<false>, dim3(blocks), dim3(kScanThreads), lds, s, P);
+    }
+  }
+  HIP_TRY(hipGetLastError());
   return TSG_OK;
 }
 
@@ -1081,24 +1397,17 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   P.hits = e->hits.p;
   P.hit_cap = hit_cap;
   P.ctrl = e->ctrl.p;
-  const size_t table_bytes = (size_t)RS.ac.nstates * RS.ac.nclasses * 2;
-  const bool lds_table = table_bytes <= (size_t)kLdsTableMax;
-  const size_t lds = 256 + kTileLds + (lds_table ? table_bytes : 0);
-  const uint64_t nsteps = (nbytes + kBlockBytes - 1) / kBlockBytes;
-  hipDeviceProp_t prop;
-  HIP_TRY(hipGetDeviceProperties(&prop, e->device));
-  const uint32_t scan_blocks = (uint32_t)std::min<uint64_t>(nsteps, (uint64_t)prop.multiProcessorCount * 8);
+  const uint64_t n_nlb = nbytes / kNlBlock + 2;
+  HIP_TRY(e->nl_blocks.ensure(n_nlb));
+  HIP_TRY(e->nl_pre.ensure(n_nlb));
+  P.nl_blocks = e->nl_blocks.p;
   for (int attempt = 0; attempt < 2 && nbytes; ++attempt) {
+    HIP_TRY(hipMemsetAsync(e->nl_blocks.p, 0, n_nlb * 4, s));
     HIP_TRY(hipEventRecord(e->ev[8], s));
-    if (lds_table) {
-      HIP_TRY(hipFuncSetAttribute((const void*)k_scan<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      hipLaunchKernelGGL(k_scan<true>, dim3(std::max(1u, scan_blocks)), dim3(kScanThreads), lds, s, P);
-    } else {
-      HIP_TRY(hipFuncSetAttribute((const void*)k_scan<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      hipLaunchKernelGGL(k_scan<false>, dim3(std::max(1u, scan_blocks)), dim3(kScanThreads), lds, s, P);
-    }
-    HIP_TRY(hipGetLastError());
+    if ((rc = launch_scan(e, P))) return rc;
     HIP_TRY(hipEventRecord(e->ev[9], s));
+    hipLaunchKernelGGL(k_special_gate, dim3(std::max(1u, std::min<uint32_t>((nf + 3) / 4, 4096))), dim3(256), 0, s, P);
+    HIP_TRY(hipGetLastError());
     Ctrl c;
     if ((rc = read_ctrl(e, &c))) return rc;
     if (c.hits <= hit_cap) break;
@@ -1162,7 +1471,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(e->job_start.ensure(n_cands));
     HIP_TRY(e->nsel.ensure(1));
     hipLaunchKernelGGL(k_mark_jobs, dim3((uint32_t)((n_cands + 255) / 256)), dim3(256), 0, s, e->keys2.p,
-                       e->vals2.p, n_cands, e->flags8.p);
+                       e->vals2.p, n_cands, RS.rules, e->flags8.p);
     hipcub::CountingInputIterator<uint32_t> cnt(0);
     size_t tmp2 = 0;
     HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tmp2, cnt, e->flags8.p, e->job_start.p, e->nsel.p,
@@ -1269,8 +1578,13 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   HIP_TRY(hipEventRecord(e->ev[6], s));
   // ---- 7. line numbers
   if (n_locs) {
+    const int n_nlb = (int)(nbytes / kNlBlock + 2);
+    size_t tmp = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->nl_blocks.p, e->nl_pre.p, n_nlb, s));
+    HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(e->cub_tmp.p, tmp, e->nl_blocks.p, e->nl_pre.p, n_nlb, s));
     hipLaunchKernelGGL(k_lines, dim3((uint32_t)((n_locs * 64 + 255) / 256)), dim3(256), 0, s, d_data, d_off,
-                       e->locs.p, n_locs);
+                       e->nl_pre.p, e->locs.p, n_locs);
     HIP_TRY(hipGetLastError());
     hl.resize(n_locs);
     HIP_TRY(hipMemcpyAsync(hl.data(), e->locs.p, n_locs * sizeof(DevLoc), hipMemcpyDeviceToHost, s));
@@ -1339,6 +1653,7 @@ void tsg_engine_free(tsg_engine* e) {
   e->keys.release(); e->keys2.release(); e->vals.release(); e->vals2.release(); e->flags8.release();
   e->job_start.release(); e->nsel.release(); e->cub_tmp.release(); e->locs.release();
   e->scratch.release(); e->ctrl.release(); e->excl_jobs.release(); e->excl_out.release();
+  e->nl_blocks.release(); e->nl_pre.release(); e->tail.release();
   if (e->events)
     for (auto& ev : e->ev) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream);
@@ -1377,14 +1692,14 @@ static int scan_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files
   std::lock_guard<std::mutex> lk(e->mu);
   *out = nullptr;
   HIP_TRY(hipSetDevice(e->device));
-  // pack contents and paths (pinned staging -> HBM)
+  // pack contents (each followed by one NUL separator) and paths: pinned staging -> HBM
   std::vector<uint64_t> off(n_files + 1, 0), poff(n_files + 1, 0);
   for (size_t i = 0; i < n_files; ++i) {
     if (files[i].len >= (1ull << 32)) {
       set_last_error("files of 4 GiB or more are outside this engine's coverage");
       return TSG_ERR_UNSUPPORTED;
     }
-    off[i + 1] = off[i] + files[i].len;
+    off[i + 1] = off[i] + files[i].len + 1;
     poff[i + 1] = poff[i] + (files[i].path ? strlen(files[i].path) : 0);
   }
   const uint64_t nbytes = off[n_files], pbytes = poff[n_files];
@@ -1393,6 +1708,7 @@ static int scan_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files
   HIP_TRY(hipHostMalloc((void**)&h, stage, hipHostMallocDefault));
   for (size_t i = 0; i < n_files; ++i) {
     if (files[i].len) memcpy(h + off[i], files[i].data, files[i].len);
+    h[off[i] + files[i].len] = 0;
     if (files[i].path) memcpy(h + nbytes + poff[i], files[i].path, poff[i + 1] - poff[i]);
   }
   auto cleanup = [&]() { (void)hipHostFree(h); };
@@ -1476,21 +1792,13 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
   P.hits = e->hits.p;
   P.hit_cap = 0;  // prefilter only: hits are counted, not stored
   P.ctrl = e->ctrl.p;
-  const size_t table_bytes = (size_t)RS.ac.nstates * RS.ac.nclasses * 2;
-  const bool lds_table = table_bytes <= (size_t)kLdsTableMax;
-  const size_t lds = 256 + kTileLds + (lds_table ? table_bytes : 0);
-  hipDeviceProp_t prop;
-  HIP_TRY(hipGetDeviceProperties(&prop, e->device));
-  const uint64_t nsteps = (nbytes + kBlockBytes - 1) / kBlockBytes;
-  const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nsteps, (uint64_t)prop.multiProcessorCount * 8));
+  const uint64_t n_nlb = nbytes / kNlBlock + 2;
+  HIP_TRY(e->nl_blocks.ensure(n_nlb));
+  HIP_TRY(hipMemsetAsync(e->nl_blocks.p, 0, n_nlb * 4, s));
+  P.nl_blocks = e->nl_blocks.p;
   if (nbytes) {
-    if (lds_table) {
-      HIP_TRY(hipFuncSetAttribute((const void*)k_scan<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      hipLaunchKernelGGL(k_scan<true>, dim3(blocks), dim3(kScanThreads), lds, s, P);
-    } else {
-      HIP_TRY(hipFuncSetAttribute((const void*)k_scan<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      hipLaunchKernelGGL(k_scan<false>, dim3(blocks), dim3(kScanThreads), lds, s, P);
-    }
+    if ((rc = launch_scan(e, P))) return rc;
+    hipLaunchKernelGGL(k_special_gate, dim3(std::max(1u, std::min<uint32_t>((nf + 3) / 4, 4096))), dim3(256), 0, s, P);
     HIP_TRY(hipGetLastError());
   }
   std::vector<uint32_t> kw((size_t)nf * RS.kw_words);

@@ -53,6 +53,10 @@ bool build_ac(tsg_ruleset* rs, std::string* err) {
     size_t L = std::min<size_t>(p.lower.size(), kAcMaxLit);
     for (size_t k = 0; k < L; ++k) {
       unsigned char c = p.lower[k];
+      if (c == 0) {
+        *err = "NUL bytes in keywords/literals are outside this engine's coverage (NUL separates files)";
+        return false;
+      }
       if (!cmap[c]) cmap[c] = ncls++;
     }
   }
@@ -133,6 +137,20 @@ bool build_ac(tsg_ruleset* rs, std::string* err) {
     for (auto x : outs[s]) ac.out_pat.push_back(x);
   }
   ac.out_off[S] = (uint32_t)ac.out_pat.size();
+  // fast image: rows padded to 64 classes, entries = next row byte offset | output bit
+  ac.fast.clear();
+  if (S <= (int)kFastMaxStates && ncls <= (int)kFastClasses) {
+    const size_t rows_bytes = (size_t)S * kFastClasses * 2;
+    ac.fast_cls_off = (uint32_t)rows_bytes;
+    ac.fast.assign(rows_bytes + 256, 0);
+    uint16_t* rows = reinterpret_cast<uint16_t*>(ac.fast.data());
+    for (int st = 0; st < S; ++st)
+      for (int c = 0; c < ncls; ++c) {
+        int t = go[st][c];
+        rows[(size_t)st * kFastClasses + c] = (uint16_t)(t * kFastClasses * 2 + (outs[t].empty() ? 0 : 1));
+      }
+    for (int b = 0; b < 256; ++b) ac.fast[rows_bytes + b] = (uint8_t)(2 * cmap[b]);
+  }
   return true;
 }
 }  // namespace tsg
