@@ -73,7 +73,7 @@ struct Ctrl {
   unsigned long long locs;
   unsigned long long excl;
   unsigned int err;
-  unsigned int pad;
+  unsigned int replays;  // diagnostic: 8-byte groups replayed by k_scan_fast
 };
 
 struct DevLoc {
@@ -99,7 +99,19 @@ struct ScanParams {
   uint32_t* nl_blocks;  // newline count per kNlBlock bytes of the batch
   const uint8_t* tail;  // virtual base of a zero-padded copy of data[tail_base-8, nbytes)
   uint64_t tail_base;   // first byte of the final partial fast region
+  const uint32_t* region_file;  // file containing byte r*kNlBlock, for r in [0, n_regions]
+  uint64_t n_regions;
 };
+
+// region_file[r] = index of the file holding byte r * kNlBlock (one pass over
+// files), so a report narrows its file lookup to the files of one 8 KiB region.
+__global__ __launch_bounds__(256) void k_region_index(const uint64_t* off, uint32_t n_files, uint64_t n_regions,
+                                                      uint32_t* region_file) {
+  const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= n_files) return;
+  const uint64_t a = off[f], b = off[f + 1];
+  for (uint64_t r = (a + kNlBlock - 1) / kNlBlock; r * kNlBlock < b && r < n_regions; ++r) region_file[r] = (uint32_t)f;
+}
 
 __device__ inline uint32_t find_file(const uint64_t* off, uint32_t lo, uint32_t hi, uint64_t pos) {
   // largest f in [lo, hi) with off[f] <= pos
@@ -116,7 +128,14 @@ __device__ inline uint8_t lower_ascii(uint8_t b) { return (b >= 'A' && b <= 'Z')
 // Files are NUL-separated, so the pattern lies inside file fi.
 __device__ __noinline__ void report(const ScanParams& P, uint32_t st, uint64_t p, uint64_t* last_kw) {
   const AcDev& ac = P.rs.ac;
-  const uint32_t fi = find_file(P.off, 0, P.n_files, p);
+  uint32_t lo = 0, hi = P.n_files;
+  if (P.region_file) {
+    const uint64_t r = p / kNlBlock;
+    lo = P.region_file[r];
+    hi = r + 1 < P.n_regions ? P.region_file[r + 1] + 1 : P.n_files;
+    if (hi > P.n_files) hi = P.n_files;
+  }
+  const uint32_t fi = find_file(P.off, lo, hi, p);
   const uint64_t fend = P.off[fi + 1] - 1;  // content end (separator excluded)
   uint32_t o0 = ac.out_off[st], o1 = ac.out_off[st + 1];
   for (uint32_t o = o0; o < o1; ++o) {
@@ -245,6 +264,7 @@ __device__ inline uint32_t byte_of(uint32_t w, int j) { return (w >> (8 * j)) & 
 
 __device__ __noinline__ void replay_group(const ScanParams& P, const uint8_t* lds, uint32_t e, uint64_t p,
                                           uint64_t* last_kw) {
+  atomicAdd(&P.ctrl->replays, 1u);
   const uint16_t* T = (const uint16_t*)lds;
   const uint8_t* cls2 = lds + P.rs.ac.fast_cls_off;
   for (int k = 0; k < 8; ++k) {
@@ -1019,6 +1039,7 @@ struct tsg_engine {
   DBuf<Ctrl> ctrl;
   DBuf<uint32_t> nl_blocks, nl_pre;
   DBuf<uint8_t> tail;
+  DBuf<uint32_t> region_file;
   uint32_t num_cus = 0;
   DBuf<ExclJob> excl_jobs;
   DBuf<ExclRange> excl_out;
@@ -1284,6 +1305,12 @@ int read_ctrl(tsg_engine* e, Ctrl* h) {
 // else the generic kernel (transition table in LDS or, if too large, global).
 int launch_scan(tsg_engine* e, ScanParams P) {
   hipStream_t s = e->stream;
+  P.n_regions = P.nbytes / kNlBlock + 1;
+  HIP_TRY(e->region_file.ensure(P.n_regions + 1));
+  P.region_file = e->region_file.p;
+  if (P.n_files)
+    hipLaunchKernelGGL(k_region_index, dim3((P.n_files + 255) / 256), dim3(256), 0, s, P.off, P.n_files,
+                       P.n_regions, e->region_file.p);
   if (!e->num_cus) {
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, e->device));
@@ -1352,7 +1379,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   }
   HIP_TRY(e->scratch.ensure((size_t)e->vm_threads * e->scratch_stride));
   std::vector<double>& tm = res->impl.timings;
-  tm.assign(8, 0.0);
+  tm.assign(13, 0.0);
   if (!e->events) {
     for (auto& ev : e->ev) HIP_TRY(hipEventCreate(&ev));
     e->events = true;
@@ -1421,6 +1448,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   Ctrl c;
   if ((rc = read_ctrl(e, &c))) return rc;
   const uint64_t n_hits = c.hits;
+  const uint32_t scan_replays = c.replays;
   // ---- 3. candidates
   uint64_t cand_cap = std::max<uint64_t>(1 << 16, n_hits * 2 + nf / 4);
   ExpandParams E{};
@@ -1598,6 +1626,11 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(hipEventElapsedTime(&ms, e->ev[k], e->ev[k + 1]));
     tm[k] = ms;
   }
+  tm[8] = (double)n_hits;
+  tm[9] = (double)n_cands;
+  tm[10] = (double)n_jobs;
+  tm[11] = (double)n_locs;
+  tm[12] = (double)scan_replays;
   if (nbytes) {  // k_scan alone (the dominant, HBM-bound kernel)
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, e->ev[8], e->ev[9]));
@@ -1653,7 +1686,7 @@ void tsg_engine_free(tsg_engine* e) {
   e->keys.release(); e->keys2.release(); e->vals.release(); e->vals2.release(); e->flags8.release();
   e->job_start.release(); e->nsel.release(); e->cub_tmp.release(); e->locs.release();
   e->scratch.release(); e->ctrl.release(); e->excl_jobs.release(); e->excl_out.release();
-  e->nl_blocks.release(); e->nl_pre.release(); e->tail.release();
+  e->nl_blocks.release(); e->nl_pre.release(); e->tail.release(); e->region_file.release();
   if (e->events)
     for (auto& ev : e->ev) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream);
