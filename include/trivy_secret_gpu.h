@@ -116,6 +116,11 @@ size_t tsg_ruleset_rule_count(const tsg_ruleset* rs);
 int tsg_ruleset_rule_info(const tsg_ruleset* rs, size_t i, int* mode, uint32_t* anchor_min,
                           uint32_t* anchor_max, size_t* n_literals);
 
+/* Automaton diagnostics: states/classes of the keyword+anchor automaton and
+ * whether it fits k_scan_fast's LDS image (fast_path = 1). */
+int tsg_ruleset_stats(const tsg_ruleset* rs, uint32_t* n_states, uint32_t* n_classes, uint32_t* n_patterns,
+                      uint32_t* n_keywords, int* fast_path);
+
 /* Engine bound to one GPU (one process per GPU; `device` is the HIP ordinal). */
 int tsg_engine_create(int device, tsg_engine** out);
 void tsg_engine_free(tsg_engine* e);

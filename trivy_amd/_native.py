@@ -86,6 +86,9 @@ _SIGS = {
     "tsg_ruleset_rule_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int),
                                              ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                                              ctypes.POINTER(ctypes.c_size_t)]),
+    "tsg_ruleset_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
+                                         ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                                         ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int)]),
     "tsg_engine_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "tsg_engine_free": (None, [ctypes.c_void_p]),
     "tsg_scan": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(FileC), ctypes.c_size_t,

@@ -12,8 +12,6 @@ namespace tsg {
 
 constexpr int kAcMaxLit = 8;   // trie depth; longer patterns are confirmed on hit
 constexpr uint32_t kNlBlock = 8192;  // newline-count granularity (bytes)
-constexpr uint32_t kFastClasses = 64;  // fast automaton rows are padded to 64 classes
-constexpr uint32_t kFastMaxStates = 511;  // 16-bit row byte offsets
 constexpr uint32_t kNoKw = 0xFFFFFFFFu;
 
 enum RuleMode : uint8_t { MODE_NEVER = 0, MODE_ANCHORED = 1, MODE_FULL = 2 };
@@ -53,7 +51,7 @@ struct AcDev {
   const uint8_t* pat_bytes;
   const uint32_t* pat_rules;
   uint32_t nstates, nclasses;
-  const uint8_t* fast_lds;  // LDS image for k_scan_fast: u16 rows [nstates][64] then cls2[256]; null if too big
+  const uint8_t* fast_lds;  // LDS image for k_scan_fast: u16 rows [nstates][nclasses] then cls2[256]; null if too big
   uint32_t fast_cls_off;    // byte offset of cls2 inside the image
 };
 

@@ -262,6 +262,11 @@ __device__ inline uint32_t nl_count_dword(uint32_t w) {
 
 __device__ inline uint32_t byte_of(uint32_t w, int j) { return (w >> (8 * j)) & 0xFFu; }
 
+// One automaton step on the LDS image: e = row byte offset | output bit.
+__device__ inline uint32_t ac_step(const uint16_t* T, const uint8_t* cls2, uint32_t e, uint32_t b) {
+  return *(const uint16_t*)((const uint8_t*)T + ((e & ~1u) + cls2[b]));
+}
+
 __device__ __noinline__ void replay_group(const ScanParams& P, const uint8_t* lds, uint32_t e, uint64_t p,
                                           uint64_t* last_kw) {
   atomicAdd(&P.ctrl->replays, 1u);
@@ -270,8 +275,8 @@ __device__ __noinline__ void replay_group(const ScanParams& P, const uint8_t* ld
   for (int k = 0; k < 8; ++k) {
     if (p + k >= P.nbytes) break;
     const uint32_t b = P.data[p + k];
-    e = T[((e & ~1u) | cls2[b]) >> 1];
-    if (e & 1u) report(P, e >> 7, p + k, last_kw);
+    e = ac_step(T, cls2, e, b);
+    if (e & 1u) report(P, (e & ~1u) / (2 * P.rs.ac.nclasses), p + k, last_kw);
   }
 }
 
@@ -289,9 +294,6 @@ __device__ inline void note_group(Flags2& f, int g, uint32_t acc, uint32_t gs) {
   }
 }
 
-__device__ inline uint32_t ac_step(const uint16_t* T, const uint8_t* cls2, uint32_t e, uint32_t b) {
-  return T[((e & ~1u) | cls2[b]) >> 1];
-}
 
 // `src` is P.data, or for the final partial region a zero-padded copy of it
 // addressed with the same offsets (ScanParams::tail), so loads need no bounds.

@@ -137,17 +137,18 @@ bool build_ac(tsg_ruleset* rs, std::string* err) {
     for (auto x : outs[s]) ac.out_pat.push_back(x);
   }
   ac.out_off[S] = (uint32_t)ac.out_pat.size();
-  // fast image: rows padded to 64 classes, entries = next row byte offset | output bit
+  // fast image: u16 rows of ncls entries, entry = next row's byte offset | output
+  // bit, followed by cls2[256] = 2 * class (see k_scan_fast).
   ac.fast.clear();
-  if (S <= (int)kFastMaxStates && ncls <= (int)kFastClasses) {
-    const size_t rows_bytes = (size_t)S * kFastClasses * 2;
+  const size_t rows_bytes = (size_t)S * ncls * 2;
+  if (ncls <= 127 && rows_bytes <= 65534) {
     ac.fast_cls_off = (uint32_t)rows_bytes;
     ac.fast.assign(rows_bytes + 256, 0);
     uint16_t* rows = reinterpret_cast<uint16_t*>(ac.fast.data());
     for (int st = 0; st < S; ++st)
       for (int c = 0; c < ncls; ++c) {
         int t = go[st][c];
-        rows[(size_t)st * kFastClasses + c] = (uint16_t)(t * kFastClasses * 2 + (outs[t].empty() ? 0 : 1));
+        rows[(size_t)st * ncls + c] = (uint16_t)(t * ncls * 2 + (outs[t].empty() ? 0 : 1));
       }
     for (int b = 0; b < 256; ++b) ac.fast[rows_bytes + b] = (uint8_t)(2 * cmap[b]);
   }
@@ -417,3 +418,14 @@ int tsg_regex_find_all(const char* pattern, const uint8_t* text, size_t len, int
 }
 
 }  // extern "C"
+
+extern "C" int tsg_ruleset_stats(const tsg_ruleset* rs, uint32_t* n_states, uint32_t* n_classes,
+                                 uint32_t* n_patterns, uint32_t* n_keywords, int* fast_path) {
+  if (!rs) return TSG_ERR_INVALID_ARG;
+  if (n_states) *n_states = rs->ac.nstates;
+  if (n_classes) *n_classes = rs->ac.nclasses;
+  if (n_patterns) *n_patterns = (uint32_t)rs->patterns.size();
+  if (n_keywords) *n_keywords = (uint32_t)rs->keywords.size();
+  if (fast_path) *fast_path = rs->ac.fast.empty() ? 0 : 1;
+  return TSG_OK;
+}
