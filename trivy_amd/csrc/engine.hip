@@ -73,7 +73,8 @@ struct Ctrl {
   unsigned long long locs;
   unsigned long long excl;
   unsigned int err;
-  unsigned int replays;  // diagnostic: 8-byte groups replayed by k_scan_fast
+  unsigned int pad;
+  unsigned long long ev_overflow;
 };
 
 struct DevLoc {
@@ -101,6 +102,11 @@ struct ScanParams {
   uint64_t tail_base;   // first byte of the final partial fast region
   const uint32_t* region_file;  // file containing byte r*kNlBlock, for r in [0, n_regions]
   uint64_t n_regions;
+  uint64_t* events;        // k_scan_fast output events, one segment per wave
+  uint32_t* ev_counts;     // events per wave
+  uint64_t ev_cap_per_wave;
+  uint64_t* ev_overflow;   // events beyond a wave's segment
+  uint64_t ev_overflow_cap;
 };
 
 // region_file[r] = index of the file holding byte r * kNlBlock (one pass over
@@ -267,19 +273,6 @@ __device__ inline uint32_t ac_step(const uint16_t* T, const uint8_t* cls2, uint3
   return *(const uint16_t*)((const uint8_t*)T + ((e & ~1u) + cls2[b]));
 }
 
-__device__ __noinline__ void replay_group(const ScanParams& P, const uint8_t* lds, uint32_t e, uint64_t p,
-                                          uint64_t* last_kw) {
-  atomicAdd(&P.ctrl->replays, 1u);
-  const uint16_t* T = (const uint16_t*)lds;
-  const uint8_t* cls2 = lds + P.rs.ac.fast_cls_off;
-  for (int k = 0; k < 8; ++k) {
-    if (p + k >= P.nbytes) break;
-    const uint32_t b = P.data[p + k];
-    e = ac_step(T, cls2, e, b);
-    if (e & 1u) report(P, (e & ~1u) / (2 * P.rs.ac.nclasses), p + k, last_kw);
-  }
-}
-
 // Flagged-group bookkeeping for one chain.
 struct Flags2 {
   int g1, g2, glast;
@@ -298,7 +291,7 @@ __device__ inline void note_group(Flags2& f, int g, uint32_t acc, uint32_t gs) {
 // `src` is P.data, or for the final partial region a zero-padded copy of it
 // addressed with the same offsets (ScanParams::tail), so loads need no bounds.
 __device__ inline void fast_region(const ScanParams& P, const uint8_t* smem, const uint8_t* src, uint64_t base,
-                                   uint32_t lane, uint64_t* last_kw) {
+                                   uint32_t lane, uint64_t* ev_seg, uint32_t* ev_count) {
   const uint16_t* T = (const uint16_t*)smem;
   const uint8_t* cls2 = smem + P.rs.ac.fast_cls_off;
   const uint64_t p0 = base + (uint64_t)lane * kFastChunk;
@@ -333,16 +326,47 @@ __device__ inline void fast_region(const ScanParams& P, const uint8_t* smem, con
   // newline count of this wave's 8 KiB block
   for (int o = 32; o > 0; o >>= 1) nl += __shfl_xor(nl, o);
   if (lane == 0 && base < P.nbytes) P.nl_blocks[base / kNlBlock] = nl;
-  // rare path: replay flagged groups with reporting
-  if (f.g1 >= 0) {
-    replay_group(P, smem, f.s1, p0 + 8 * f.g1, last_kw);
-    if (f.g2 >= 0) {
-      uint32_t es = f.s2;
-      for (int g = f.g2; g <= f.glast; ++g) {
-        replay_group(P, smem, es, p0 + 8 * g, last_kw);
-        for (int k = 0; k < 8; ++k) {
-          const uint64_t a = p0 + 8 * g + k;
-          es = ac_step(T, cls2, es, a < P.nbytes ? P.data[a] : 0u);
+  // rare path: replay the flagged 8-byte groups (LDS only) and append one
+  // event (position, output state) per output byte to this wave's private
+  // segment with ballot + popcount — no atomics; k_report resolves them.
+  const uint64_t lanes_lt = (1ull << lane) - 1;
+  if (__ballot(f.g1 >= 0)) {
+    // first flagged group, then the contiguous range [g2, glast]
+    int g = f.g1;
+    uint32_t es = f.s1;
+    int stop = f.g2 >= 0 ? f.glast : f.g1;  // last group to replay
+    bool jump = f.g2 >= 0;                  // after g1, continue at g2 with s2
+    bool live = f.g1 >= 0;
+    while (__ballot(live)) {
+      for (int k = 0; k < 8; ++k) {
+        bool ev = false;
+        uint64_t pos = 0;
+        if (live) {
+          pos = p0 + 8 * (uint32_t)g + k;
+          es = ac_step(T, cls2, es, src[pos]);
+          ev = (es & 1u) != 0;
+        }
+        const uint64_t m = __ballot(ev);
+        if (ev) {
+          const uint32_t slot = *ev_count + (uint32_t)__popcll(m & lanes_lt);
+          const uint64_t rec = (pos << 16) | ((es & ~1u) / (2 * P.rs.ac.nclasses));
+          if (slot < P.ev_cap_per_wave) ev_seg[slot] = rec;
+          else {
+            unsigned long long o = atomicAdd(&P.ctrl->ev_overflow, 1ull);
+            if (o < P.ev_overflow_cap) P.ev_overflow[o] = rec;
+          }
+        }
+        *ev_count += (uint32_t)__popcll(m);
+      }
+      if (live) {
+        if (g == f.g1 && jump) {
+          g = f.g2;
+          es = f.s2;
+          jump = false;
+        } else if (g < stop) {
+          ++g;
+        } else {
+          live = false;
         }
       }
     }
@@ -362,11 +386,36 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
   const uint32_t wave = (blockIdx.x * (kFastThreads / 64)) + (threadIdx.x >> 6);
   const uint32_t nwaves = gridDim.x * (kFastThreads / 64);
   const uint64_t nregions = (P.nbytes + kFastRegion - 1) / kFastRegion;
-  uint64_t last_kw = ~0ull;
+  uint64_t* ev_seg = P.events + (uint64_t)wave * P.ev_cap_per_wave;
+  uint32_t ev_count = 0;  // wave-uniform
   for (uint64_t rg = wave; rg < nregions; rg += nwaves) {
     const uint64_t base = rg * kFastRegion;
-    fast_region(P, smem, base >= P.tail_base ? P.tail : P.data, base, lane, &last_kw);
+    fast_region(P, smem, base >= P.tail_base ? P.tail : P.data, base, lane, ev_seg, &ev_count);
   }
+  if (lane == 0) P.ev_counts[wave] = ev_count < P.ev_cap_per_wave ? ev_count : P.ev_cap_per_wave;
+}
+
+// Resolve k_scan_fast's output events (one thread per event): file lookup,
+// keyword gate bits, special flag, anchor hit records.
+__global__ __launch_bounds__(256) void k_report(ScanParams P, uint32_t n_waves) {
+  const AcDev& ac = P.rs.ac;
+  uint64_t last_kw = ~0ull;
+  for (uint32_t w = blockIdx.x; w < n_waves + 1; w += gridDim.x) {
+    const uint64_t* seg;
+    uint64_t n;
+    if (w < n_waves) {
+      seg = P.events + (uint64_t)w * P.ev_cap_per_wave;
+      n = P.ev_counts[w];
+    } else {  // overflow bucket
+      seg = P.ev_overflow;
+      n = P.ctrl->ev_overflow < P.ev_overflow_cap ? P.ctrl->ev_overflow : P.ev_overflow_cap;
+    }
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint64_t rec = seg[i];
+      report(P, (uint32_t)(rec & 0xFFFF), rec >> 16, &last_kw);
+    }
+  }
+  (void)ac;
 }
 
 // Exact MatchKeywords for files holding U+0130 (C4 B0) or U+212A (E2 84 AA):
@@ -1042,6 +1091,8 @@ struct tsg_engine {
   DBuf<uint32_t> nl_blocks, nl_pre;
   DBuf<uint8_t> tail;
   DBuf<uint32_t> region_file;
+  DBuf<uint64_t> ev_buf, ev_overflow;
+  DBuf<uint32_t> ev_counts;
   uint32_t num_cus = 0;
   DBuf<ExclJob> excl_jobs;
   DBuf<ExclRange> excl_out;
@@ -1334,8 +1385,22 @@ int launch_scan(tsg_engine* e, ScanParams P) {
     const uint64_t waves_per_block = kFastThreads / 64;
     const uint32_t blocks = (uint32_t)std::max<uint64_t>(
         1, std::min<uint64_t>((nregions + waves_per_block - 1) / waves_per_block, (uint64_t)e->num_cus));
+    // per-wave event segments (expected ~1 output byte per KiB of text; 4x headroom)
+    const uint64_t n_waves = (uint64_t)blocks * (kFastThreads / 64);
+    P.ev_cap_per_wave = std::max<uint64_t>(1024, (P.nbytes / 256) / n_waves + 256);
+    HIP_TRY(e->ev_buf.ensure(n_waves * P.ev_cap_per_wave));
+    HIP_TRY(e->ev_counts.ensure(n_waves));
+    HIP_TRY(e->ev_overflow.ensure(1 << 20));
+    P.events = e->ev_buf.p;
+    P.ev_counts = e->ev_counts.p;
+    P.ev_overflow = e->ev_overflow.p;
+    P.ev_overflow_cap = e->ev_overflow.n;
+    HIP_TRY(hipMemsetAsync(&P.ctrl->ev_overflow, 0, 8, s));
     HIP_TRY(hipFuncSetAttribute((const void*)k_scan_fast, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(k_scan_fast, dim3(blocks), dim3(kFastThreads), lds, s, P);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_report, dim3((uint32_t)std::min<uint64_t>(n_waves + 1, 8192)), dim3(256), 0, s, P,
+                       (uint32_t)n_waves);
   } else {
     const size_t table_bytes = (size_t)ac.nstates * ac.nclasses * 2;
     const bool lds_table = table_bytes <= (size_t)kLdsTableMax;
@@ -1450,7 +1515,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   Ctrl c;
   if ((rc = read_ctrl(e, &c))) return rc;
   const uint64_t n_hits = c.hits;
-  const uint32_t scan_replays = c.replays;
+  const uint64_t scan_overflow = c.ev_overflow;
   // ---- 3. candidates
   uint64_t cand_cap = std::max<uint64_t>(1 << 16, n_hits * 2 + nf / 4);
   ExpandParams E{};
@@ -1632,7 +1697,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   tm[9] = (double)n_cands;
   tm[10] = (double)n_jobs;
   tm[11] = (double)n_locs;
-  tm[12] = (double)scan_replays;
+  tm[12] = (double)scan_overflow;
   if (nbytes) {  // k_scan alone (the dominant, HBM-bound kernel)
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, e->ev[8], e->ev[9]));
@@ -1689,6 +1754,7 @@ void tsg_engine_free(tsg_engine* e) {
   e->job_start.release(); e->nsel.release(); e->cub_tmp.release(); e->locs.release();
   e->scratch.release(); e->ctrl.release(); e->excl_jobs.release(); e->excl_out.release();
   e->nl_blocks.release(); e->nl_pre.release(); e->tail.release(); e->region_file.release();
+  e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release();
   if (e->events)
     for (auto& ev : e->ev) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream);
