@@ -132,7 +132,31 @@ __device__ inline uint8_t lower_ascii(uint8_t b) { return (b >= 'A' && b <= 'Z')
 
 // Report every pattern ending at global position p (AC state st has outputs).
 // Files are NUL-separated, so the pattern lies inside file fi.
-__device__ __noinline__ void report(const ScanParams& P, uint32_t st, uint64_t p, uint64_t* last_kw) {
+// Where anchor hit records go: straight to the global list, or staged in
+// LDS by k_report and flushed with one global atomic per block step.
+struct GlobalHitSink {
+  __device__ void push(const ScanParams& P, uint64_t rec) {
+    unsigned long long idx = atomicAdd(&P.ctrl->hits, 1ull);
+    if (idx < P.hit_cap) P.hits[idx] = rec;
+  }
+};
+struct LdsHitSink {
+  uint64_t* buf;
+  uint32_t* cnt;
+  uint32_t cap;
+  __device__ void push(const ScanParams& P, uint64_t rec) {
+    const uint32_t i = atomicAdd(cnt, 1u);
+    if (i < cap) {
+      buf[i] = rec;
+    } else {
+      GlobalHitSink g;
+      g.push(P, rec);
+    }
+  }
+};
+
+template <class Sink>
+__device__ inline void report_t(const ScanParams& P, uint32_t st, uint64_t p, uint64_t* last_kw, Sink& sink) {
   const AcDev& ac = P.rs.ac;
   uint32_t lo = 0, hi = P.n_files;
   if (P.region_file) {
@@ -161,7 +185,9 @@ __device__ __noinline__ void report(const ScanParams& P, uint32_t st, uint64_t p
       const uint64_t key = ((uint64_t)fi << 32) | pd.kw;  // per-lane dedupe of repeated keywords
       if (*last_kw != key) {
         *last_kw = key;
-        atomicOr(&P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)], 1u << (pd.kw & 31));
+        uint32_t* wp = &P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)];
+        const uint32_t bit = 1u << (pd.kw & 31);
+        if (!(__hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(wp, bit);
       }
     }
     if (pd.rule_n) {
@@ -171,10 +197,14 @@ __device__ __noinline__ void report(const ScanParams& P, uint32_t st, uint64_t p
         for (uint32_t k = 0; k < pd.len && ok; ++k) ok = rq[k] == 0 || P.data[start + k] == rq[k];
         if (!ok) continue;
       }
-      unsigned long long idx = atomicAdd(&P.ctrl->hits, 1ull);
-      if (idx < P.hit_cap) P.hits[idx] = (start << 16) | pid;
+      sink.push(P, (start << 16) | pid);
     }
   }
+}
+
+__device__ __noinline__ void report(const ScanParams& P, uint32_t st, uint64_t p, uint64_t* last_kw) {
+  GlobalHitSink g;
+  report_t(P, st, p, last_kw, g);
 }
 
 // Generic scan (any automaton size): one 128-byte chunk per lane, byte
@@ -397,9 +427,16 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
 
 // Resolve k_scan_fast's output events (one thread per event): file lookup,
 // keyword gate bits, special flag, anchor hit records.
+constexpr uint32_t kReportHitCap = 2048;
+
 __global__ __launch_bounds__(256) void k_report(ScanParams P, uint32_t n_waves) {
-  const AcDev& ac = P.rs.ac;
+  __shared__ uint64_t hbuf[kReportHitCap];
+  __shared__ uint32_t hcnt;
+  __shared__ unsigned long long hbase;
   uint64_t last_kw = ~0ull;
+  if (threadIdx.x == 0) hcnt = 0;
+  __syncthreads();
+  LdsHitSink sink{hbuf, &hcnt, kReportHitCap};
   for (uint32_t w = blockIdx.x; w < n_waves + 1; w += gridDim.x) {
     const uint64_t* seg;
     uint64_t n;
@@ -412,10 +449,19 @@ __global__ __launch_bounds__(256) void k_report(ScanParams P, uint32_t n_waves) 
     }
     for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
       const uint64_t rec = seg[i];
-      report(P, (uint32_t)(rec & 0xFFFF), rec >> 16, &last_kw);
+      report_t(P, (uint32_t)(rec & 0xFFFF), rec >> 16, &last_kw, sink);
     }
+    // flush staged hits with one global reservation per block step
+    __syncthreads();
+    const uint32_t nh = hcnt < kReportHitCap ? hcnt : kReportHitCap;
+    if (threadIdx.x == 0 && nh) hbase = atomicAdd(&P.ctrl->hits, (unsigned long long)nh);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nh; i += blockDim.x)
+      if (hbase + i < P.hit_cap) P.hits[hbase + i] = hbuf[i];
+    __syncthreads();
+    if (threadIdx.x == 0) hcnt = 0;
+    __syncthreads();
   }
-  (void)ac;
 }
 
 // Exact MatchKeywords for files holding U+0130 (C4 B0) or U+212A (E2 84 AA):
@@ -1442,7 +1488,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   if (!e->vm_threads) {
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, e->device));
-    e->vm_threads = (uint32_t)prop.multiProcessorCount * 128;  // 2 waves per CU
+    e->vm_threads = (uint32_t)prop.multiProcessorCount * 512;  // 8 waves per CU
   }
   HIP_TRY(e->scratch.ensure((size_t)e->vm_threads * e->scratch_stride));
   std::vector<double>& tm = res->impl.timings;
