@@ -116,6 +116,11 @@ size_t tsg_ruleset_rule_count(const tsg_ruleset* rs);
 int tsg_ruleset_rule_info(const tsg_ruleset* rs, size_t i, int* mode, uint32_t* anchor_min,
                           uint32_t* anchor_max, size_t* n_literals);
 
+/* Anchor literal k (< n_literals) of rule i: ASCII-lowercased bytes and the
+ * per-byte case requirement (0 = either case), each *len bytes (<= cap). */
+int tsg_ruleset_rule_literal(const tsg_ruleset* rs, size_t i, size_t k, char* lower, char* req, size_t cap,
+                             size_t* len);
+
 /* Automaton diagnostics: states/classes of the keyword+anchor automaton and
  * whether it fits k_scan_fast's LDS image (fast_path = 1). */
 int tsg_ruleset_stats(const tsg_ruleset* rs, uint32_t* n_states, uint32_t* n_classes, uint32_t* n_patterns,

@@ -340,6 +340,22 @@ int tsg_ruleset_rule_info(const tsg_ruleset* rs, size_t i, int* mode, uint32_t* 
   return TSG_OK;
 }
 
+// Anchor literal k of rule i: lowercased bytes and the case requirement
+// (0 = either case), both `len` bytes long (diagnostics / candidate studies).
+int tsg_ruleset_rule_literal(const tsg_ruleset* rs, size_t i, size_t k, char* lower, char* req, size_t cap,
+                             size_t* len) {
+  if (!rs || i >= rs->rules.size() || !len) return TSG_ERR_INVALID_ARG;
+  const RuleHost& r = rs->rules[i];
+  const gre::Anchor* a = r.regex >= 0 ? &rs->regexes[r.regex].c.anchor : nullptr;
+  if (!a || !a->valid || k >= a->lits.size()) return TSG_ERR_INVALID_ARG;
+  const gre::Lit& L = a->lits[k];
+  *len = L.lower.size();
+  if (cap < L.lower.size()) return TSG_ERR_INVALID_ARG;
+  if (lower) memcpy(lower, L.lower.data(), L.lower.size());
+  if (req) memcpy(req, L.req.data(), L.req.size());
+  return TSG_OK;
+}
+
 // ---- host regex diagnostics (compiler + VM on the CPU) ---------------------
 struct HostVm {
   std::vector<uint16_t> sp0, sp1, d0, d1, stk;
