@@ -121,6 +121,12 @@ int tsg_ruleset_rule_info(const tsg_ruleset* rs, size_t i, int* mode, uint32_t* 
 int tsg_ruleset_rule_literal(const tsg_ruleset* rs, size_t i, size_t k, char* lower, char* req, size_t cap,
                              size_t* len);
 
+/* Candidate filter of rule i, run on host text from anchor position h:
+ * *accept = 0 only when no match of the rule can contain an anchor hit at h
+ * (k_expand drops such hits); *n_states = its DFA size (0 = no filter). */
+int tsg_ruleset_follow_check(const tsg_ruleset* rs, size_t i, const uint8_t* text, size_t len, size_t h,
+                             int* accept, uint32_t* n_states);
+
 /* Automaton diagnostics: states/classes of the keyword+anchor automaton and
  * whether it fits k_scan_fast's LDS image (fast_path = 1). */
 int tsg_ruleset_stats(const tsg_ruleset* rs, uint32_t* n_states, uint32_t* n_classes, uint32_t* n_patterns,

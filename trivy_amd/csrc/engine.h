@@ -14,6 +14,10 @@ constexpr int kAcMaxLit = 8;   // trie depth; longer patterns are confirmed on h
 constexpr uint32_t kNlBlock = 8192;  // newline-count granularity (bytes)
 constexpr uint32_t kNoKw = 0xFFFFFFFFu;
 
+constexpr uint32_t kFollowMaxStates = 1024;  // follow-DFA subset-construction budget
+constexpr uint32_t kFollowDepth = 96;        // bytes a candidate filter reads past the hit
+constexpr uint32_t kNoFollow = 0xFFFFFFFFu;
+
 enum RuleMode : uint8_t { MODE_NEVER = 0, MODE_ANCHORED = 1, MODE_FULL = 2 };
 
 // ---- device-visible POD records ------------------------------------------
@@ -28,6 +32,10 @@ struct RuleDev {
   uint32_t allow_off, allow_n;  // per-rule allow regex progs
   uint32_t use_groups;          // SecretGroupName != ""
   uint32_t max_len;             // longest possible match in bytes (gre::kInf if unbounded)
+  uint32_t follow_off;          // candidate filter: first u16 of its table (kNoFollow = none)
+  uint32_t follow_ncls;         // its byte classes; class map at follow_cls_off (128 B)
+  uint32_t follow_cls_off;
+  uint32_t pad0;
 };
 
 struct PatDev {
@@ -58,6 +66,8 @@ struct AcDev {
 constexpr uint32_t kLitRec = 36;  // prefilter literal record: len, lower[16], req[16], pad
 
 struct RuleSetDev {
+  const uint16_t* follow_delta;  // all rules' candidate-filter tables (follow.cpp)
+  const uint8_t* follow_cls;
   const gre::ProgView* progs;
   const uint32_t* prog_lit_off;  // per program: range of prefilter literals (n_progs + 1)
   const uint8_t* prog_lits;      // kLitRec-byte records
@@ -81,6 +91,16 @@ struct RegexHost {
   gre::Compiled c;
 };
 
+// Per-rule candidate filter (follow.cpp): states 0 = DEAD, 1 = ACCEPT, 2 = start.
+struct FollowDfa {
+  bool valid = false;
+  uint32_t ncls = 0, nstates = 0;
+  uint8_t cls[128] = {};
+  std::vector<uint16_t> delta;  // [nstates][ncls]
+};
+bool build_follow(const gre::Compiled& c, FollowDfa* out);
+bool follow_accepts(const FollowDfa& f, const uint8_t* text, size_t n, size_t h);
+
 struct RuleHost {
   std::string id;
   int regex = -1;  // index into regexes, -1 => never matches
@@ -91,6 +111,7 @@ struct RuleHost {
   std::vector<int> allow_path;   // rule allow rules: path
   std::vector<int> exclude;
   RuleMode mode = MODE_NEVER;
+  FollowDfa follow;  // MODE_ANCHORED only
 };
 
 struct AcHost {

@@ -639,6 +639,7 @@ __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
 }
 
 struct ExpandParams {
+  const uint8_t* data;
   const uint64_t* off;
   uint32_t n_files;
   RuleSetDev rs;
@@ -665,6 +666,25 @@ __device__ inline bool rule_gate(const RuleSetDev& rs, const RuleDev& r, const u
   return false;
 }
 
+// Candidate filter (follow.cpp): may a match of rule `rd` contain the anchor
+// hit at text[h]?  false only when provably not.
+__device__ inline bool follow_accepts_dev(const RuleSetDev& rs, const RuleDev& rd, const uint8_t* data, uint64_t h,
+                                          uint64_t fend) {
+  if (rd.follow_off == kNoFollow) return true;
+  const uint16_t* T = rs.follow_delta + rd.follow_off;
+  const uint8_t* cls = rs.follow_cls + rd.follow_cls_off;
+  const uint32_t K = rd.follow_ncls;
+  uint32_t st = 2;
+  for (uint32_t i = 0; i < kFollowDepth; ++i) {
+    if (h + i >= fend) return false;
+    const uint8_t c = data[h + i];
+    if (c >= 0x80) return true;
+    st = T[st * K + cls[c]];
+    if (st < 2) return st == 1;
+  }
+  return true;
+}
+
 __device__ inline void emit_cand(const ExpandParams& E, uint32_t rule, uint64_t gpos, uint32_t val) {
   unsigned long long idx = atomicAdd(&E.ctrl->cands, 1ull);
   if (idx < E.cand_cap) {
@@ -684,10 +704,13 @@ __global__ __launch_bounds__(256) void k_expand(ExpandParams E) {
   if (fl & (kFileAllowed | kFileSpecial)) return;
   const PatDev pd = E.rs.ac.pats[pid];
   const uint32_t* kw = E.file_kw + (size_t)fi * E.rs.kw_words;
+  const uint64_t fend = E.off[fi + 1] - 1;
   for (uint32_t k = 0; k < pd.rule_n; ++k) {
     const uint32_t r = E.rs.ac.pat_rules[pd.rule_off + k];
     if (E.path_mask && ((E.path_mask[(size_t)fi * E.rule_words + (r >> 5)] >> (r & 31)) & 1)) continue;
-    if (!rule_gate(E.rs, E.rs.rules[r], kw)) continue;
+    const RuleDev& rd = E.rs.rules[r];
+    if (!rule_gate(E.rs, rd, kw)) continue;
+    if (!follow_accepts_dev(E.rs, rd, E.data, gpos, fend)) continue;
     emit_cand(E, r, gpos, fi);
   }
 }
@@ -1101,6 +1124,8 @@ struct DevImage {
   DBuf<uint8_t> fast;
   DBuf<uint32_t> prog_lit_off;
   DBuf<uint8_t> prog_lits;
+  DBuf<uint16_t> follow_delta;
+  DBuf<uint8_t> follow_cls;
   RuleSetDev view{};
   // offsets into u32
   uint32_t o_gpath = 0, n_gpath = 0, o_apoff = 0, o_ap = 0, o_full = 0, n_full = 0;
@@ -1108,7 +1133,7 @@ struct DevImage {
     inst.release(); classes.release(); ranges.release(); progs.release(); rules.release();
     u32.release(); rule_path.release(); delta.release(); cls.release(); out_off.release();
     out_pat.release(); pats.release(); pat_bytes.release(); pat_rules.release(); fast.release();
-    prog_lit_off.release(); prog_lits.release();
+    prog_lit_off.release(); prog_lits.release(); follow_delta.release(); follow_cls.release();
   }
 };
 
@@ -1221,9 +1246,19 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   std::map<std::string, uint32_t> kwid;
   for (size_t k = 0; k < rs->keywords.size(); ++k) kwid[rs->keywords[k]] = (uint32_t)k;
   std::vector<uint32_t> kw_ids, group_slots, allow_progs, apath_off, apath, full_rules;
+  std::vector<uint16_t> fdelta;
+  std::vector<uint8_t> fcls;
   for (size_t ri = 0; ri < rs->rules.size(); ++ri) {
     const RuleHost& r = rs->rules[ri];
     RuleDev d{};
+    d.follow_off = kNoFollow;
+    if (r.follow.valid) {
+      d.follow_off = (uint32_t)fdelta.size();
+      d.follow_ncls = r.follow.ncls;
+      d.follow_cls_off = (uint32_t)fcls.size();
+      fdelta.insert(fdelta.end(), r.follow.delta.begin(), r.follow.delta.end());
+      fcls.insert(fcls.end(), r.follow.cls, r.follow.cls + 128);
+    }
     d.prog = r.regex >= 0 ? (uint32_t)r.regex : 0;
     d.mode = r.mode;
     d.kw_off = (uint32_t)kw_ids.size();
@@ -1278,6 +1313,11 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   HIP_TRY(im.rules.ensure(rules.size() + 1));
   if (!rules.empty())
     HIP_TRY(hipMemcpy(im.rules.p, rules.data(), rules.size() * sizeof(RuleDev), hipMemcpyHostToDevice));
+  HIP_TRY(im.follow_delta.ensure(fdelta.size() + 1));
+  if (!fdelta.empty())
+    HIP_TRY(hipMemcpy(im.follow_delta.p, fdelta.data(), fdelta.size() * 2, hipMemcpyHostToDevice));
+  HIP_TRY(im.follow_cls.ensure(fcls.size() + 1));
+  if (!fcls.empty()) HIP_TRY(hipMemcpy(im.follow_cls.p, fcls.data(), fcls.size(), hipMemcpyHostToDevice));
   HIP_TRY(im.rule_path.ensure(rule_path.size() + 1));
   if (!rule_path.empty())
     HIP_TRY(hipMemcpy(im.rule_path.p, rule_path.data(), rule_path.size() * 4, hipMemcpyHostToDevice));
@@ -1320,6 +1360,8 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
     HIP_TRY(hipMemcpy(im.pat_rules.p, prules.data(), prules.size() * 4, hipMemcpyHostToDevice));
   // ---- view
   RuleSetDev& v = im.view;
+  v.follow_delta = im.follow_delta.p;
+  v.follow_cls = im.follow_cls.p;
   v.progs = im.progs.p;
   v.prog_lit_off = im.prog_lit_off.p;
   v.prog_lits = im.prog_lits.p;
@@ -1565,6 +1607,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   // ---- 3. candidates
   uint64_t cand_cap = std::max<uint64_t>(1 << 16, n_hits * 2 + nf / 4);
   ExpandParams E{};
+  E.data = d_data;
   E.off = d_off;
   E.n_files = nf;
   E.rs = RS;

@@ -275,6 +275,7 @@ int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_r
       // no group of that name => getMatchSubgroupsLocations yields nothing
       if (!has_group) r.mode = MODE_NEVER;
       else r.mode = c.anchor.valid ? MODE_ANCHORED : MODE_FULL;
+      if (r.mode == MODE_ANCHORED) build_follow(c, &r.follow);
     }
     for (auto& kw : r.keywords) {
       if (!kwid.count(kw) && !kw.empty()) {
@@ -353,6 +354,18 @@ int tsg_ruleset_rule_literal(const tsg_ruleset* rs, size_t i, size_t k, char* lo
   if (cap < L.lower.size()) return TSG_ERR_INVALID_ARG;
   if (lower) memcpy(lower, L.lower.data(), L.lower.size());
   if (req) memcpy(req, L.req.data(), L.req.size());
+  return TSG_OK;
+}
+
+// Candidate filter of rule i on host text (diagnostics / soundness tests):
+// *accept = 0 only if no match of the rule can contain an anchor hit at h.
+// *n_states = the filter's DFA states (0 = rule has no filter).
+int tsg_ruleset_follow_check(const tsg_ruleset* rs, size_t i, const uint8_t* text, size_t len, size_t h,
+                             int* accept, uint32_t* n_states) {
+  if (!rs || i >= rs->rules.size()) return TSG_ERR_INVALID_ARG;
+  const FollowDfa& f = rs->rules[i].follow;
+  if (n_states) *n_states = f.valid ? f.nstates : 0;
+  if (accept) *accept = follow_accepts(f, text, len, h) ? 1 : 0;
   return TSG_OK;
 }
 
