@@ -331,7 +331,7 @@ def main():
                          "avg_launch_ms": round(scan_kernel_ms, 3)},
             "stages_ms": {k: round(v, 3) for k, v in zip(
                 ["path_gate", "scan_total", "expand", "sort_jobs", "verify", "exclude", "lines", "k_scan"], stage)},
-            "counts": {k: int(v) for k, v in zip(["hits", "candidates", "jobs", "locs", "event_overflow"], stage[8:])},
+            "counts": {k: int(v) for k, v in zip(["hits", "candidates", "jobs", "locs", "event_overflow", "events", "outputs"], stage[8:])},
             "cpu_baseline": cpu,
             "parity": parity,
         }

@@ -18,7 +18,10 @@ import sys
 
 
 def short(name):
-    n = name.split("(")[0]
+    n = name.replace("(anonymous namespace)::", "")
+    if n.startswith("void "):
+        n = n[5:]
+    n = n.split("(")[0]
     return n.split("::")[-1] if "::" in n else n[:80]
 
 

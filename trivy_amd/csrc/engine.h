@@ -11,9 +11,12 @@
 namespace tsg {
 
 constexpr int kAcMaxLit = 8;   // trie depth; longer patterns are confirmed on hit
-constexpr uint32_t kNlBlock = 8192;  // newline-count granularity (bytes)
+constexpr uint32_t kNlBlock = 4096;  // newline-count granularity (bytes) = one k_scan_fast chain span
 constexpr uint32_t kNoKw = 0xFFFFFFFFu;
 
+constexpr uint32_t kFastRowBytes = 258;       // 128 u16 columns + 2 B: consecutive rows rotate LDS banks
+constexpr uint32_t kFastLdsMax = 160 * 1024;  // k_scan_fast image budget (one image per CU)
+constexpr uint32_t kFastSpecialEv = 0xFFFF;   // event tag: U+0130/U+017F/U+212A sequence ends here
 constexpr uint32_t kFollowMaxStates = 1024;  // follow-DFA subset-construction budget
 constexpr uint32_t kFollowDepth = 96;        // bytes a candidate filter reads past the hit
 constexpr uint32_t kNoFollow = 0xFFFFFFFFu;
@@ -35,7 +38,8 @@ struct RuleDev {
   uint32_t follow_off;          // candidate filter: first u16 of its table (kNoFollow = none)
   uint32_t follow_ncls;         // its byte classes; class map at follow_cls_off (128 B)
   uint32_t follow_cls_off;
-  uint32_t pad0;
+  uint32_t gate_implied;        // every anchor literal contains a keyword: on files without fold-special
+                                // bytes a match implies the MatchKeywords gate (scanner.go:169-181)
 };
 
 struct PatDev {
@@ -45,9 +49,9 @@ struct PatDev {
   uint32_t req_off;    // required-case bytes (0 = either case), valid if confirm
   uint32_t rule_off, rule_n;  // rules anchored on this pattern
   uint8_t special;
-  uint8_t confirm;  // anchor roles need a case check
-  uint8_t trunc;    // len > kAcMaxLit
-  uint8_t pad;
+  uint8_t confirm;     // anchor roles need a case check
+  uint8_t trunc;       // len > trie depth
+  uint8_t kw_needed;   // some rule whose gate is not implied uses this keyword
 };
 
 struct AcDev {
@@ -59,8 +63,13 @@ struct AcDev {
   const uint8_t* pat_bytes;
   const uint32_t* pat_rules;
   uint32_t nstates, nclasses;
-  const uint8_t* fast_lds;  // LDS image for k_scan_fast: u16 rows [nstates][nclasses] then cls2[256]; null if too big
-  uint32_t fast_cls_off;    // byte offset of cls2 inside the image
+  const uint8_t* fast_lds;   // LDS image for k_scan_fast (AcHost::fast); null => generic kernel
+  uint32_t fast_bytes;       // image size
+  uint32_t fast_out_entry;   // entries >= this are output states
+  uint32_t depth;            // trie depth
+  // k_report's LDS blob = fast image | out_off | out_pat | pats | pat_bytes
+  // (fast_lds is its start; offsets in bytes)
+  uint32_t rep_bytes, o_out_off, o_out_pat, o_pats, o_pat_bytes;
 };
 
 constexpr uint32_t kLitRec = 36;  // prefilter literal record: len, lower[16], req[16], pad
@@ -116,12 +125,13 @@ struct RuleHost {
 
 struct AcHost {
   std::vector<uint16_t> delta;  // generic: next state | 0x8000 output bit
-  std::vector<uint8_t> fast;    // fast image (see AcDev::fast_lds), empty if not representable
-  uint32_t fast_cls_off = 0;
+  std::vector<uint8_t> fast;    // k_scan_fast image: nstates rows of kFastRowBytes, empty if not representable
+  uint32_t fast_out_entry = 0;
   uint8_t cls[256];
   std::vector<uint32_t> out_off;
   std::vector<uint16_t> out_pat;
   uint32_t nstates = 0, nclasses = 0;
+  uint32_t depth = kAcMaxLit;  // trie depth (patterns longer than this are confirmed on hit)
 };
 
 struct PatternHost {

@@ -24,10 +24,13 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -75,6 +78,7 @@ struct Ctrl {
   unsigned int err;
   unsigned int pad;
   unsigned long long ev_overflow;
+  unsigned long long outputs;  // patterns k_report resolved (diagnostics)
 };
 
 struct DevLoc {
@@ -102,11 +106,12 @@ struct ScanParams {
   uint64_t tail_base;   // first byte of the final partial fast region
   const uint32_t* region_file;  // file containing byte r*kNlBlock, for r in [0, n_regions]
   uint64_t n_regions;
-  uint64_t* events;        // k_scan_fast output events, one segment per wave
-  uint32_t* ev_counts;     // events per wave
+  struct FastEvent* events;       // k_scan_fast events, one segment per wave
+  uint32_t* ev_counts;            // events per wave
   uint64_t ev_cap_per_wave;
-  uint64_t* ev_overflow;   // events beyond a wave's segment
+  struct FastEvent* ev_overflow;  // events beyond a wave's segment
   uint64_t ev_overflow_cap;
+  uint8_t* span_hi;               // per kNlBlock span: a byte >= 0x80 occurs (k_fold_special)
 };
 
 // region_file[r] = index of the file holding byte r * kNlBlock (one pass over
@@ -132,30 +137,17 @@ __device__ inline uint8_t lower_ascii(uint8_t b) { return (b >= 'A' && b <= 'Z')
 
 // Report every pattern ending at global position p (AC state st has outputs).
 // Files are NUL-separated, so the pattern lies inside file fi.
-// Where anchor hit records go: straight to the global list, or staged in
-// LDS by k_report and flushed with one global atomic per block step.
+// Where the generic kernel's anchor hit records go: the global list.
 struct GlobalHitSink {
   __device__ void push(const ScanParams& P, uint64_t rec) {
     unsigned long long idx = atomicAdd(&P.ctrl->hits, 1ull);
     if (idx < P.hit_cap) P.hits[idx] = rec;
   }
 };
-struct LdsHitSink {
-  uint64_t* buf;
-  uint32_t* cnt;
-  uint32_t cap;
-  __device__ void push(const ScanParams& P, uint64_t rec) {
-    const uint32_t i = atomicAdd(cnt, 1u);
-    if (i < cap) {
-      buf[i] = rec;
-    } else {
-      GlobalHitSink g;
-      g.push(P, rec);
-    }
-  }
-};
 
-template <class Sink>
+// kConfirm: the automaton ran on 7-bit aliased bytes (k_scan_fast), so each
+// reported pattern is re-checked on the real bytes first.
+template <bool kConfirm, class Sink>
 __device__ inline void report_t(const ScanParams& P, uint32_t st, uint64_t p, uint64_t* last_kw, Sink& sink) {
   const AcDev& ac = P.rs.ac;
   uint32_t lo = 0, hi = P.n_files;
@@ -171,13 +163,19 @@ __device__ inline void report_t(const ScanParams& P, uint32_t st, uint64_t p, ui
   for (uint32_t o = o0; o < o1; ++o) {
     uint32_t pid = ac.out_pat[o];
     PatDev pd = ac.pats[pid];
-    uint32_t tl = pd.len < (uint32_t)kAcMaxLit ? pd.len : (uint32_t)kAcMaxLit;
+    uint32_t tl = pd.len < ac.depth ? pd.len : ac.depth;
     uint64_t start = p + 1 - tl;
+    if (kConfirm) {
+      const uint8_t* pb = ac.pat_bytes + pd.bytes_off;
+      bool ok = true;
+      for (uint32_t k = 0; k < tl && ok; ++k) ok = lower_ascii(P.data[start + k]) == pb[k];
+      if (!ok) continue;
+    }
     if (pd.trunc) {
       if (start + pd.len > fend) continue;
       bool ok = true;
       const uint8_t* pb = ac.pat_bytes + pd.bytes_off;
-      for (uint32_t k = kAcMaxLit; k < pd.len && ok; ++k) ok = lower_ascii(P.data[start + k]) == pb[k];
+      for (uint32_t k = ac.depth; k < pd.len && ok; ++k) ok = lower_ascii(P.data[start + k]) == pb[k];
       if (!ok) continue;
     }
     if (pd.special) atomicOr(&P.file_flags[fi], kFileSpecial);
@@ -204,7 +202,7 @@ __device__ inline void report_t(const ScanParams& P, uint32_t st, uint64_t p, ui
 
 __device__ __noinline__ void report(const ScanParams& P, uint32_t st, uint64_t p, uint64_t* last_kw) {
   GlobalHitSink g;
-  report_t(P, st, p, last_kw, g);
+  report_t<false>(P, st, p, last_kw, g);
 }
 
 // Generic scan (any automaton size): one 128-byte chunk per lane, byte
@@ -273,22 +271,37 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_generic(ScanParams P) {
   }
 }
 
-// Fast scan: gfx950-tuned AC pass over the whole batch (the HBM-bound hot loop).
-//  * 1024-thread blocks, one LDS copy of the automaton per CU: transition rows
-//    padded to 64 classes (128 B), entry = next-row byte offset | output bit,
-//    class table after it holding 2*class, so one step is
-//      e = T[(e & ~1) | cls2[b]]   (v_and_or_b32 + 2 ds_reads)
-//  * each lane owns two independent 128-byte chunks (two dependency chains
-//    per lane hide the LDS latency), loaded straight into VGPRs with 16-byte
-//    loads; 7 bytes of warm-up from the previous chunk
-//  * outputs are OR-ed per 8-byte group; the (rare) flagged groups are
-//    replayed byte by byte with reporting afterwards, so the hot loop has no
-//    divergent branch
-//  * per 8 KiB block newline counts (SWAR) for StartLine/EndLine.
+// Fast scan: the HBM-bound hot loop — one pass of the keyword/anchor
+// Aho-Corasick automaton over the whole batch (MatchKeywords, scanner.go:169-181).
+//  * 1024-thread blocks, one LDS image of the automaton per CU (AcHost::fast):
+//    rows of 128 u16 columns indexed by the byte's low 7 bits (upper case
+//    shares the lower-case column), kFastRowBytes stride so consecutive rows
+//    rotate the LDS banks; an entry is the next row's byte offset / 4, so one
+//    step is  e = T[4e + 2(b & 0x7F)]  (one ds_read_u16, no class lookup),
+//    and output states are numbered last: one max() per byte flags outputs
+//  * every lane runs kFastChains independent chains (ILP against the LDS
+//    latency); a chain walks one kNlBlock-byte span per work unit with 7 bytes
+//    of warm-up (automaton depth <= kAcMaxLit), so spans need no stitching
+//  * each chain streams its span through a 128-byte register ring: a 16-byte
+//    vector is reloaded with the chain's next 128 bytes (or the next unit's
+//    first ones) as soon as it is consumed, so HBM latency hides behind a
+//    full ring of automaton work
+//  * per 8-byte group: an output (max >= fast_out_entry) or a byte >= 0x80
+//    flags the group; after each step a chain with flagged groups appends
+//    ONE event (first flagged group, group count, entry state) to the wave's
+//    segment with ballot/popcount (no atomics, no global reads in the scan);
+//    k_report replays those bytes.  Bytes >= 0x80 alias ASCII columns, so
+//    k_report confirms every pattern on the real bytes, and its replay finds
+//    the fold-special sequences C4B0 / C5BF / E284AA exactly
+//  * the newline count of each span goes straight to nl_blocks (one owner,
+//    plain store) and feeds StartLine/EndLine.
 constexpr int kFastThreads = 1024;
-constexpr int kFastChunk = 128;                          // bytes per lane
-constexpr int kFastRegion = 64 * kFastChunk;             // 8 KiB per wave iteration
-static_assert(kFastRegion == (int)kNlBlock, "newline blocks follow the wave layout");
+constexpr uint32_t kFastRowU16 = kFastRowBytes / 2;
+// Variant in use (chains per lane, 16-byte vectors per chain step); the
+// other shapes stay compilable for A/B runs (TSG_FAST_VARIANT).
+constexpr int kFastChains = 1;
+constexpr int kFastVecs = 8;
+constexpr uint32_t kFastUnitMax = 2 * kNlBlock;  // largest chains * span (tail buffer size)
 
 __device__ inline uint32_t nl_count_dword(uint32_t w) {
   const uint32_t t = w ^ 0x0A0A0A0Au;
@@ -296,149 +309,234 @@ __device__ inline uint32_t nl_count_dword(uint32_t w) {
   return __builtin_popcount(z);
 }
 
-__device__ inline uint32_t byte_of(uint32_t w, int j) { return (w >> (8 * j)) & 0xFFu; }
+// Column fold, four bytes at once: a byte with bit 6 set loses bit 5, so both
+// letter cases share columns 0x41-0x5A (LDS banks 0-15) while digits and
+// punctuation keep 0x20-0x3F (banks 16-31): the common text bytes no longer
+// collide on a bank.  (0x60/0x7B-0x7F alias 0x40/0x5B-0x5F; bytes >= 0x80 alias
+// too — their groups are replayed and reported patterns re-checked.)
+__device__ inline uint32_t fold4(uint32_t w) { return w & ~((w >> 1) & 0x20202020u); }
 
-// One automaton step on the LDS image: e = row byte offset | output bit.
-__device__ inline uint32_t ac_step(const uint16_t* T, const uint8_t* cls2, uint32_t e, uint32_t b) {
-  return *(const uint16_t*)((const uint8_t*)T + ((e & ~1u) + cls2[b]));
+// One automaton step on byte j of a folded dword w: e = T[e + (b & 0x7F)] (u16 units).
+__device__ inline uint32_t fstep(const uint8_t* T, uint32_t e, uint32_t w, int j) {
+  const uint32_t b = (w >> (8 * j)) & 0x7Fu;
+  uint32_t a;
+  asm("v_add_lshl_u32 %0, %1, %2, 1" : "=v"(a) : "v"(e), "v"(b));  // one VALU on the dependent chain
+  return *(const uint16_t*)(T + a);
 }
 
-// Flagged-group bookkeeping for one chain.
-struct Flags2 {
-  int g1, g2, glast;
-  uint32_t s1, s2;
+
+// `src` for a position: the batch, or for the final partial unit the
+// zero-padded copy addressed with the same offsets (ScanParams::tail).
+__device__ inline const uint8_t* fast_src(const ScanParams& P, uint64_t pos) {
+  return pos >= P.tail_base ? P.tail : P.data;
+}
+
+// A k_scan_fast event: one 8-byte group in which the automaton reached an
+// output state, with everything k_report needs to resolve it without touching
+// the batch again (32 bytes: two dwordx4 stores).
+struct FastEvent {
+  uint64_t pos;    // first byte of the group
+  uint32_t entry;  // automaton entry before the group
+  uint32_t pad;
+  uint2 prev;      // the 8 raw bytes before the group
+  uint2 cur;       // the group's 8 raw bytes
+};
+static_assert(sizeof(FastEvent) == 32, "two dwordx4");
+
+template <int V>
+struct FastChain {
+  uint4 cur[V];
+  uint64_t pos;  // first byte of the V*16 bytes in `cur`
+  uint32_t e;    // automaton entry
+  uint32_t nl;   // newlines of the current span
+  uint32_t hi;   // OR of the span's dwords: bit 7 of a byte = a byte >= 0x80
+  uint2 prev;    // the 8 raw bytes before the next group
 };
 
-__device__ inline void note_group(Flags2& f, int g, uint32_t acc, uint32_t gs) {
-  if (acc & 1u) {
-    if (f.g1 < 0) { f.g1 = g; f.s1 = gs; }
-    else if (f.g2 < 0) { f.g2 = g; f.s2 = gs; }
-    f.glast = g;
+// Walk one 8-byte group (d0, d1) of a chain; when the automaton reaches an
+// output state in it, append an event to the wave's segment (ballot +
+// popcount, no atomics; every lane calls this, so ev_count stays uniform).
+template <int V>
+__device__ inline void fast_group(const ScanParams& P, const uint8_t* T, uint32_t out_e, FastChain<V>& C, uint32_t d0,
+                                  uint32_t d1, uint64_t gpos, bool live, uint64_t lanes_lt, FastEvent* ev_seg,
+                                  uint32_t* ev_count) {
+  C.nl += nl_count_dword(d0) + nl_count_dword(d1);
+  C.hi |= d0 | d1;
+  const uint32_t f0 = fold4(d0), f1 = fold4(d1);
+  const uint32_t gs = C.e;
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    C.e = fstep(T, C.e, j < 4 ? f0 : f1, j & 3);
+    m = m > C.e ? m : C.e;
   }
-}
-
-
-// `src` is P.data, or for the final partial region a zero-padded copy of it
-// addressed with the same offsets (ScanParams::tail), so loads need no bounds.
-__device__ inline void fast_region(const ScanParams& P, const uint8_t* smem, const uint8_t* src, uint64_t base,
-                                   uint32_t lane, uint64_t* ev_seg, uint32_t* ev_count) {
-  const uint16_t* T = (const uint16_t*)smem;
-  const uint8_t* cls2 = smem + P.rs.ac.fast_cls_off;
-  const uint64_t p0 = base + (uint64_t)lane * kFastChunk;
-  // warm-up: the 7 bytes before the chunk
-  const uint2 h0 = p0 >= 8 ? *(const uint2*)(src + p0 - 8) : make_uint2(0, 0);
-  uint32_t e = 0;
-#pragma unroll
-  for (int j = 1; j < 8; ++j) e = ac_step(T, cls2, e, byte_of(j < 4 ? h0.x : h0.y, j & 3));
-  uint32_t nl = 0;
-  Flags2 f{-1, -1, -1, 0, 0};
-#pragma unroll
-  for (int k = 0; k < kFastChunk / 16; ++k) {
-    const uint4 v = *(const uint4*)(src + p0 + 16 * k);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {  // two 8-byte groups per 16-byte vector
-      const uint32_t gs = e;
-      uint32_t acc = 0;
-#pragma unroll
-      for (int dw = 0; dw < 2; ++dw) {
-        const uint32_t a = w[2 * h + dw];
-        nl += nl_count_dword(a);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          e = ac_step(T, cls2, e, byte_of(a, j));
-          acc |= e;
-        }
-      }
-      note_group(f, 2 * k + h, acc, gs);
-    }
-  }
-  // newline count of this wave's 8 KiB block
-  for (int o = 32; o > 0; o >>= 1) nl += __shfl_xor(nl, o);
-  if (lane == 0 && base < P.nbytes) P.nl_blocks[base / kNlBlock] = nl;
-  // rare path: replay the flagged 8-byte groups (LDS only) and append one
-  // event (position, output state) per output byte to this wave's private
-  // segment with ballot + popcount — no atomics; k_report resolves them.
-  const uint64_t lanes_lt = (1ull << lane) - 1;
-  if (__ballot(f.g1 >= 0)) {
-    // first flagged group, then the contiguous range [g2, glast]
-    int g = f.g1;
-    uint32_t es = f.s1;
-    int stop = f.g2 >= 0 ? f.glast : f.g1;  // last group to replay
-    bool jump = f.g2 >= 0;                  // after g1, continue at g2 with s2
-    bool live = f.g1 >= 0;
-    while (__ballot(live)) {
-      for (int k = 0; k < 8; ++k) {
-        bool ev = false;
-        uint64_t pos = 0;
-        if (live) {
-          pos = p0 + 8 * (uint32_t)g + k;
-          es = ac_step(T, cls2, es, src[pos]);
-          ev = (es & 1u) != 0;
-        }
-        const uint64_t m = __ballot(ev);
-        if (ev) {
-          const uint32_t slot = *ev_count + (uint32_t)__popcll(m & lanes_lt);
-          const uint64_t rec = (pos << 16) | ((es & ~1u) / (2 * P.rs.ac.nclasses));
-          if (slot < P.ev_cap_per_wave) ev_seg[slot] = rec;
-          else {
-            unsigned long long o = atomicAdd(&P.ctrl->ev_overflow, 1ull);
-            if (o < P.ev_overflow_cap) P.ev_overflow[o] = rec;
-          }
-        }
-        *ev_count += (uint32_t)__popcll(m);
-      }
-      if (live) {
-        if (g == f.g1 && jump) {
-          g = f.g2;
-          es = f.s2;
-          jump = false;
-        } else if (g < stop) {
-          ++g;
-        } else {
-          live = false;
-        }
+  const bool ev = live && m >= out_e;
+  const uint64_t b = __ballot(ev);
+  if (b) {
+    if (ev) {
+      FastEvent r;
+      r.pos = gpos;
+      r.entry = gs;
+      r.pad = 0;
+      r.prev = C.prev;
+      r.cur = make_uint2(d0, d1);
+      const uint32_t slot = *ev_count + (uint32_t)__popcll(b & lanes_lt);
+      if (slot < P.ev_cap_per_wave) {
+        ev_seg[slot] = r;
+      } else {
+        unsigned long long ov = atomicAdd(&P.ctrl->ev_overflow, 1ull);
+        if (ov < P.ev_overflow_cap) P.ev_overflow[ov] = r;
       }
     }
+    *ev_count += (uint32_t)__popcll(b);
   }
+  C.prev = make_uint2(d0, d1);
 }
 
+template <int CH, int V>
 __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
-  extern __shared__ __align__(16) uint8_t smem[];
+  constexpr uint32_t kUnit = CH * kNlBlock;          // bytes per lane per work unit
+  constexpr int kStep = V * 16;                      // bytes per chain step
+  constexpr int kSteps = kNlBlock / kStep;           // steps per span
+  __shared__ __align__(16) uint8_t smem[kFastLdsMax];  // static: LDS base folds to 0 in the step
   const AcDev& ac = P.rs.ac;
   {
-    const uint32_t words = (ac.fast_cls_off + 256) / 4;
+    const uint32_t words = ac.fast_bytes / 4;
     const uint32_t* src = (const uint32_t*)ac.fast_lds;
     for (uint32_t i = threadIdx.x; i < words; i += kFastThreads) ((uint32_t*)smem)[i] = src[i];
   }
   __syncthreads();
+  const uint8_t* T = smem;
+  const uint32_t out_e = ac.fast_out_entry;
   const uint32_t lane = threadIdx.x & 63;
+  const uint64_t lanes_lt = (1ull << lane) - 1;
   const uint32_t wave = (blockIdx.x * (kFastThreads / 64)) + (threadIdx.x >> 6);
-  const uint32_t nwaves = gridDim.x * (kFastThreads / 64);
-  const uint64_t nregions = (P.nbytes + kFastRegion - 1) / kFastRegion;
-  uint64_t* ev_seg = P.events + (uint64_t)wave * P.ev_cap_per_wave;
+  const uint64_t nlanes = (uint64_t)gridDim.x * kFastThreads;
+  const uint64_t units = (P.nbytes + kUnit - 1) / kUnit;
+  FastEvent* ev_seg = P.events + (uint64_t)wave * P.ev_cap_per_wave;
   uint32_t ev_count = 0;  // wave-uniform
-  for (uint64_t rg = wave; rg < nregions; rg += nwaves) {
-    const uint64_t base = rg * kFastRegion;
-    fast_region(P, smem, base >= P.tail_base ? P.tail : P.data, base, lane, ev_seg, &ev_count);
+  uint64_t u = (uint64_t)blockIdx.x * kFastThreads + threadIdx.x;
+  FastChain<V> C[CH];
+  uint4 nxt[CH][V];
+  if (u < units) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      C[c].pos = u * kUnit + (uint64_t)c * kNlBlock;
+      const uint8_t* src = fast_src(P, C[c].pos);
+#pragma unroll
+      for (int k = 0; k < V; ++k) nxt[c][k] = *(const uint4*)(src + C[c].pos + 16 * k);
+    }
+  }
+  // uniform per lane, not per wave: finished lanes walk stale bytes silently
+  while (__ballot(u < units)) {
+    const bool live = u < units;
+    const uint64_t un = u + nlanes;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      // warm-up: the 7 bytes before the span (automaton depth <= kAcMaxLit)
+      const uint64_t s0 = C[c].pos;
+      const uint2 h = live && s0 >= 8 ? *(const uint2*)(fast_src(P, s0 - 8) + s0 - 8) : make_uint2(0, 0);
+      uint32_t e = 0;
+#pragma unroll
+      for (int j = 1; j < 8; ++j) e = fstep(T, e, j < 4 ? fold4(h.x) : fold4(h.y), j & 3);
+      C[c].e = e;
+      C[c].prev = h;
+      C[c].nl = 0;
+      C[c].hi = 0;
+    }
+    for (int step = 0; step < kSteps; ++step) {
+      // take the prefetched bytes, then prefetch the chain's next step (same
+      // span, or the first step of the lane's next unit)
+      uint64_t np[CH];
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+#pragma unroll
+        for (int k = 0; k < V; ++k) C[c].cur[k] = nxt[c][k];
+        np[c] = step + 1 < kSteps ? C[c].pos + kStep : un * kUnit + (uint64_t)c * kNlBlock;
+      }
+      if (live && (step + 1 < kSteps || un < units)) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+          const uint8_t* src = fast_src(P, np[c]);
+#pragma unroll
+          for (int k = 0; k < V; ++k) nxt[c][k] = *(const uint4*)(src + np[c] + 16 * k);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < V; ++k)
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+          const uint4 v = C[c].cur[k];
+          fast_group(P, T, out_e, C[c], v.x, v.y, C[c].pos + 16 * k, live, lanes_lt, ev_seg, &ev_count);
+          fast_group(P, T, out_e, C[c], v.z, v.w, C[c].pos + 16 * k + 8, live, lanes_lt, ev_seg, &ev_count);
+        }
+#pragma unroll
+      for (int c = 0; c < CH; ++c) C[c].pos = np[c];
+    }
+    if (live) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const uint64_t s0 = u * kUnit + (uint64_t)c * kNlBlock;
+        if (s0 < P.nbytes) {
+          P.nl_blocks[s0 / kNlBlock] = C[c].nl;
+          P.span_hi[s0 / kNlBlock] = (C[c].hi & 0x80808080u) ? 1 : 0;
+        }
+      }
+    }
+    u = un;
   }
   if (lane == 0) P.ev_counts[wave] = ev_count < P.ev_cap_per_wave ? ev_count : P.ev_cap_per_wave;
 }
 
-// Resolve k_scan_fast's output events (one thread per event): file lookup,
-// keyword gate bits, special flag, anchor hit records.
+// Resolve k_scan_fast's events.  Each event is replayed on an LDS copy of the
+// scan image with the output tables (out_off/out_pat/pats/pat_bytes) behind
+// it; the event carries the group's bytes and the 8 before them, so a
+// pattern is confirmed on the real bytes (the scan folds/aliases bytes),
+// case requirement included, without touching the batch.  Per output:
+// keyword gate bit (only keywords some non-implied gate needs; fire-and-forget
+// atomic, file looked up once per event) and anchor hit (LDS-staged, one
+// global reservation per block step).
+constexpr uint32_t kReportThreads = 1024;
 constexpr uint32_t kReportHitCap = 2048;
+constexpr uint32_t kReportLds = kFastLdsMax - kReportHitCap * 8 - 64;
 
-__global__ __launch_bounds__(256) void k_report(ScanParams P, uint32_t n_waves) {
+__device__ inline uint32_t file_of_pos(const ScanParams& P, uint64_t pos) {
+  const uint64_t r = pos / kNlBlock;
+  const uint32_t hi = r + 1 < P.n_regions ? min(P.region_file[r + 1] + 1, P.n_files) : P.n_files;
+  return find_file(P.off, P.region_file[r], hi, pos);
+}
+
+// byte k (0 = oldest) of the last-8-bytes shift register
+__device__ inline uint32_t hist_byte(uint64_t h, uint32_t k) { return (uint32_t)(h >> (8 * k)) & 0xFFu; }
+
+__global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_t n_waves) {
+  __shared__ __align__(16) uint8_t L[kReportLds];
   __shared__ uint64_t hbuf[kReportHitCap];
   __shared__ uint32_t hcnt;
   __shared__ unsigned long long hbase;
-  uint64_t last_kw = ~0ull;
-  if (threadIdx.x == 0) hcnt = 0;
+  __shared__ uint32_t nout;
+  const AcDev& ac = P.rs.ac;
+  const bool in_lds = ac.rep_bytes <= kReportLds;
+  if (in_lds) {
+    const uint32_t words = ac.rep_bytes / 4;
+    const uint32_t* src = (const uint32_t*)ac.fast_lds;
+    for (uint32_t i = threadIdx.x; i < words; i += kReportThreads) ((uint32_t*)L)[i] = src[i];
+  }
+  const uint8_t* B = in_lds ? L : ac.fast_lds;  // blob base (LDS, or global when too big)
+  const uint32_t* out_off = (const uint32_t*)(B + ac.o_out_off);
+  const uint16_t* out_pat = (const uint16_t*)(B + ac.o_out_pat);
+  const PatDev* pats = (const PatDev*)(B + ac.o_pats);
+  const uint8_t* pbytes = B + ac.o_pat_bytes;
+  if (threadIdx.x == 0) {
+    hcnt = 0;
+    nout = 0;
+  }
   __syncthreads();
-  LdsHitSink sink{hbuf, &hcnt, kReportHitCap};
+  const uint32_t out_e = ac.fast_out_entry;
+  uint32_t my_out = 0;
+  uint64_t last_kw = ~0ull;
   for (uint32_t w = blockIdx.x; w < n_waves + 1; w += gridDim.x) {
-    const uint64_t* seg;
+    const FastEvent* seg;
     uint64_t n;
     if (w < n_waves) {
       seg = P.events + (uint64_t)w * P.ev_cap_per_wave;
@@ -448,8 +546,73 @@ __global__ __launch_bounds__(256) void k_report(ScanParams P, uint32_t n_waves) 
       n = P.ctrl->ev_overflow < P.ev_overflow_cap ? P.ctrl->ev_overflow : P.ev_overflow_cap;
     }
     for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
-      const uint64_t rec = seg[i];
-      report_t(P, (uint32_t)(rec & 0xFFFF), rec >> 16, &last_kw, sink);
+      const FastEvent ev = seg[i];
+      uint64_t hist = ((uint64_t)ev.prev.y << 32) | ev.prev.x;  // the 8 raw bytes before (oldest low)
+      uint32_t e = ev.entry;
+      const uint32_t fx = fold4(ev.cur.x), fy = fold4(ev.cur.y);
+      uint32_t fi = 0xFFFFFFFFu;
+      for (int j = 0; j < 8; ++j) {
+        e = fstep(B, e, j < 4 ? fx : fy, j & 3);
+        const uint32_t c = ((j < 4 ? ev.cur.x : ev.cur.y) >> (8 * (j & 3))) & 0xFFu;
+        hist = (hist >> 8) | ((uint64_t)c << 56);  // hist byte 7 = c
+        if (e < out_e || c >= 0x80) continue;  // an output ending on a byte >= 0x80 is an alias
+        const uint64_t pos = ev.pos + j;
+        const uint32_t st = e / kFastRowU16;
+        for (uint32_t o = out_off[st]; o < out_off[st + 1]; ++o) {
+          const uint32_t pid = out_pat[o];
+          const PatDev pd = pats[pid];
+          const uint32_t tl = pd.len < ac.depth ? pd.len : ac.depth;
+          // confirm the automaton's prefix on the real bytes (hist bytes 8-tl .. 7)
+          const uint8_t* pb = pbytes + pd.bytes_off;
+          bool ok = true;
+          for (uint32_t k = 0; k < tl && ok; ++k) ok = lower_ascii((uint8_t)hist_byte(hist, 8 - tl + k)) == pb[k];
+          if (!ok) continue;
+          const uint64_t start = pos + 1 - tl;
+          const bool want_kw = pd.kw_needed != 0;
+          bool want_hit = pd.rule_n != 0;
+          if (want_hit && pd.confirm) {  // case requirement of the anchor literal (first tl bytes)
+            const uint8_t* rq = pbytes + pd.req_off;
+            for (uint32_t k = 0; k < tl && want_hit; ++k) {
+              const uint32_t b = hist_byte(hist, 8 - tl + k);
+              want_hit = rq[k] == 0 || b == rq[k];
+            }
+          }
+          if (!want_kw && !want_hit) continue;
+          if (pd.trunc) {  // the rest of a long pattern, on the batch (rare)
+            if (fi == 0xFFFFFFFFu) fi = file_of_pos(P, pos);
+            const uint64_t fend = P.off[fi + 1] - 1;
+            if (start + pd.len > fend) continue;
+            for (uint32_t k = tl; k < pd.len && ok; ++k) {
+              const uint8_t b = P.data[start + k];
+              ok = lower_ascii(b) == pb[k];
+              if (want_hit && pd.confirm) {
+                const uint8_t r = pbytes[pd.req_off + k];
+                want_hit = r == 0 || b == r;
+              }
+            }
+            if (!ok) continue;
+          }
+          ++my_out;
+          if (want_kw) {
+            if (fi == 0xFFFFFFFFu) fi = file_of_pos(P, pos);
+            const uint64_t key = ((uint64_t)fi << 32) | pd.kw;  // per-lane dedupe of repeated keywords
+            if (last_kw != key) {
+              last_kw = key;
+              atomicOr(&P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)], 1u << (pd.kw & 31));
+            }
+          }
+          if (want_hit) {
+            const uint32_t slot = atomicAdd(&hcnt, 1u);
+            const uint64_t hrec = (start << 16) | pid;
+            if (slot < kReportHitCap) {
+              hbuf[slot] = hrec;
+            } else {
+              unsigned long long idx = atomicAdd(&P.ctrl->hits, 1ull);
+              if (idx < P.hit_cap) P.hits[idx] = hrec;
+            }
+          }
+        }
+      }
     }
     // flush staged hits with one global reservation per block step
     __syncthreads();
@@ -461,6 +624,32 @@ __global__ __launch_bounds__(256) void k_report(ScanParams P, uint32_t n_waves) 
     __syncthreads();
     if (threadIdx.x == 0) hcnt = 0;
     __syncthreads();
+  }
+  atomicAdd(&nout, my_out);
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(&P.ctrl->outputs, (unsigned long long)nout);
+}
+
+// Fold-special sequences (C4B0 U+0130, C5BF U+017F, E284AA U+212A) in the
+// spans k_scan_fast saw a byte >= 0x80 in: one wave per span, 64 bytes per
+// lane, flag the file so it takes the exact full-scan path (k_special_gate).
+__global__ __launch_bounds__(256) void k_fold_special(ScanParams P, uint64_t n_spans) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  constexpr uint32_t kPer = kNlBlock / 64;
+  for (uint64_t sp = w0; sp < n_spans; sp += nw) {
+    if (!P.span_hi[sp]) continue;
+    const uint64_t a = sp * kNlBlock + (uint64_t)lane * kPer;
+    const uint64_t b = a + kPer < P.nbytes ? a + kPer : P.nbytes;
+    uint32_t b1 = a >= 1 ? P.data[a - 1] : 0, b2 = a >= 2 ? P.data[a - 2] : 0;
+    for (uint64_t q = a; q < b; ++q) {
+      const uint32_t c = P.data[q];
+      if ((c == 0xB0 && b1 == 0xC4) || (c == 0xBF && b1 == 0xC5) || (c == 0xAA && b1 == 0x84 && b2 == 0xE2))
+        atomicOr(&P.file_flags[file_of_pos(P, q)], kFileSpecial);
+      b2 = b1;
+      b1 = c;
+    }
   }
 }
 
@@ -507,7 +696,7 @@ __global__ __launch_bounds__(256) void k_special_gate(ScanParams P) {
             const uint8_t* pb = ac.pat_bytes + pd.bytes_off;
             uint64_t q = p + w;
             bool ok = true;
-            for (uint32_t k = kAcMaxLit; k < pd.len && ok; ++k) {
+            for (uint32_t k = ac.depth; k < pd.len && ok; ++k) {
               if (q >= fe) { ok = false; break; }
               uint32_t ch = P.data[q];
               uint32_t cw = 1;
@@ -658,7 +847,7 @@ struct ExpandParams {
 };
 
 __device__ inline bool rule_gate(const RuleSetDev& rs, const RuleDev& r, const uint32_t* kw) {
-  if (r.kw_n == 0 || r.gate_always) return true;
+  if (r.kw_n == 0 || r.gate_always) return true;  // (gate_implied is applied by the callers that may use it)
   for (uint32_t k = 0; k < r.kw_n; ++k) {
     const uint32_t id = rs.kw_ids[r.kw_off + k];
     if ((kw[id >> 5] >> (id & 31)) & 1) return true;
@@ -709,7 +898,9 @@ __global__ __launch_bounds__(256) void k_expand(ExpandParams E) {
     const uint32_t r = E.rs.ac.pat_rules[pd.rule_off + k];
     if (E.path_mask && ((E.path_mask[(size_t)fi * E.rule_words + (r >> 5)] >> (r & 31)) & 1)) continue;
     const RuleDev& rd = E.rs.rules[r];
-    if (!rule_gate(E.rs, rd, kw)) continue;
+    // the file holds no fold-special byte here (those take k_full_jobs), so an
+    // implied gate needs no keyword bit
+    if (!rd.gate_implied && !rule_gate(E.rs, rd, kw)) continue;
     if (!follow_accepts_dev(E.rs, rd, E.data, gpos, fend)) continue;
     emit_cand(E, r, gpos, fi);
   }
@@ -1051,8 +1242,9 @@ __device__ inline uint32_t wave_nl_prefix(const uint8_t* data, const uint32_t* n
                                           uint32_t lane) {
   const uint64_t b0 = x & ~(uint64_t)(kNlBlock - 1);
   uint32_t c = 0;
-  const uint64_t s = b0 + (uint64_t)lane * 128;
-  const uint64_t e = s + 128 < x ? s + 128 : x;
+  constexpr uint32_t kPer = kNlBlock / 64;  // bytes per lane
+  const uint64_t s = b0 + (uint64_t)lane * kPer;
+  const uint64_t e = s + kPer < x ? s + kPer : x;
   for (uint64_t i = s; i < e; ++i) c += data[i] == '\n';
   for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
   return nl_pre[x / kNlBlock] + c;
@@ -1162,8 +1354,10 @@ struct tsg_engine {
   DBuf<uint32_t> nl_blocks, nl_pre;
   DBuf<uint8_t> tail;
   DBuf<uint32_t> region_file;
-  DBuf<uint64_t> ev_buf, ev_overflow;
+  DBuf<FastEvent> ev_buf, ev_overflow;
+  DBuf<uint8_t> span_hi;
   DBuf<uint32_t> ev_counts;
+  uint64_t ev_ovf_need = 0;  // overflow-event capacity learnt from a lost scan
   uint32_t num_cus = 0;
   DBuf<ExclJob> excl_jobs;
   DBuf<ExclRange> excl_out;
@@ -1248,6 +1442,7 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   std::vector<uint32_t> kw_ids, group_slots, allow_progs, apath_off, apath, full_rules;
   std::vector<uint16_t> fdelta;
   std::vector<uint8_t> fcls;
+  std::set<uint32_t> kw_needed_ids;
   for (size_t ri = 0; ri < rs->rules.size(); ++ri) {
     const RuleHost& r = rs->rules[ri];
     RuleDev d{};
@@ -1283,6 +1478,20 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
           if (c.prog.cap_names[g] == r.group_name) group_slots.push_back((uint32_t)g);
       d.group_n = (uint32_t)group_slots.size() - d.group_off;
     }
+    if (r.mode == MODE_ANCHORED && !d.gate_always && d.kw_n) {
+      // implied gate: every anchor literal contains one of the rule's keywords
+      const gre::Anchor& an = rs->regexes[r.regex].c.anchor;
+      bool all = !an.lits.empty();
+      for (auto& l : an.lits) {
+        bool has = false;
+        for (auto& kw : r.keywords) has |= !kw.empty() && l.lower.find(kw) != std::string::npos;
+        all &= has;
+      }
+      d.gate_implied = all;
+    }
+    if (!d.gate_implied)
+      for (auto& kw : r.keywords)
+        if (!kw.empty()) kw_needed_ids.insert(kwid[kw]);
     d.allow_off = (uint32_t)allow_progs.size();
     for (int x : r.allow_regex) allow_progs.push_back((uint32_t)x);
     d.allow_n = (uint32_t)allow_progs.size() - d.allow_off;
@@ -1348,7 +1557,8 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
     d.rule_n = (uint32_t)p.rules.size();
     d.special = p.special;
     d.confirm = p.confirm;
-    d.trunc = p.lower.size() > (size_t)kAcMaxLit;
+    d.kw_needed = p.kw >= 0 && kw_needed_ids.count((uint32_t)p.kw);
+    d.trunc = p.lower.size() > (size_t)ac.depth;
     pats.push_back(d);
   }
   HIP_TRY(im.pats.ensure(pats.size() + 1));
@@ -1377,13 +1587,29 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   v.max_ncap = max_ncap;
   v.max_ninst_cap = max_ninst_cap;
   const uint8_t* fast = nullptr;
+  uint32_t o_out_off = 0, o_out_pat = 0, o_pats = 0, o_pbytes = 0, rep_bytes = 0;
   if (!ac.fast.empty()) {
-    HIP_TRY(im.fast.ensure(ac.fast.size() + 16));
-    HIP_TRY(hipMemcpy(im.fast.p, ac.fast.data(), ac.fast.size(), hipMemcpyHostToDevice));
+    // k_report blob: the scan image followed by the small output tables
+    std::vector<uint8_t> blob(ac.fast.begin(), ac.fast.end());
+    auto put = [&](const void* p, size_t n) {
+      blob.resize((blob.size() + 15) & ~(size_t)15);
+      const uint32_t o = (uint32_t)blob.size();
+      blob.insert(blob.end(), (const uint8_t*)p, (const uint8_t*)p + n);
+      return o;
+    };
+    o_out_off = put(ac.out_off.data(), ac.out_off.size() * 4);
+    o_out_pat = put(ac.out_pat.data(), ac.out_pat.size() * 2);
+    o_pats = put(pats.data(), pats.size() * sizeof(PatDev));
+    o_pbytes = put(pbytes.data(), pbytes.size());
+    blob.resize((blob.size() + 15) & ~(size_t)15);
+    rep_bytes = (uint32_t)blob.size();
+    HIP_TRY(im.fast.ensure(blob.size() + 16));
+    HIP_TRY(hipMemcpy(im.fast.p, blob.data(), blob.size(), hipMemcpyHostToDevice));
     fast = im.fast.p;
   }
   v.ac = AcDev{im.delta.p, im.cls.p, im.out_off.p, im.out_pat.p, im.pats.p, im.pat_bytes.p, im.pat_rules.p,
-               ac.nstates, ac.nclasses, fast, ac.fast_cls_off};
+               ac.nstates, ac.nclasses, fast, (uint32_t)ac.fast.size(), ac.fast_out_entry, ac.depth,
+               rep_bytes, o_out_off, o_out_pat, o_pats, o_pbytes};
   im.rs_id = rs->id;
   // VM scratch
   e->scratch_stride = (scratch_bytes(max_ninst, max_ncap, max_ninst_cap) + 255) & ~255ull;
@@ -1460,35 +1686,49 @@ int launch_scan(tsg_engine* e, ScanParams P) {
   const AcDev& ac = P.rs.ac;
   if (ac.fast_lds) {
     // final partial region: zero-padded copy (with 8 bytes of warm-up context)
-    P.tail_base = (P.nbytes / kFastRegion) * kFastRegion;
+    // variant: chains per lane x 16-byte vectors per chain step (A/B via TSG_FAST_VARIANT)
+    int chains = kFastChains, vecs = kFastVecs;
+    if (const char* v = getenv("TSG_FAST_VARIANT")) sscanf(v, "%dx%d", &chains, &vecs);
+    if (!((chains == 1 && (vecs == 8 || vecs == 4)) || (chains == 2 && vecs == 4))) {
+      chains = kFastChains;
+      vecs = kFastVecs;
+    }
+    const uint64_t unit = (uint64_t)chains * kNlBlock;
+    P.tail_base = (P.nbytes / unit) * unit;
     const uint64_t lead = P.tail_base >= 8 ? 8 : P.tail_base;
-    HIP_TRY(e->tail.ensure(8 + kFastRegion + 64));
-    HIP_TRY(hipMemsetAsync(e->tail.p, 0, 8 + kFastRegion + 64, s));
+    HIP_TRY(e->tail.ensure(8 + kFastUnitMax + 64));
+    HIP_TRY(hipMemsetAsync(e->tail.p, 0, 8 + kFastUnitMax + 64, s));
     if (P.nbytes - P.tail_base + lead)
       HIP_TRY(hipMemcpyAsync(e->tail.p + 8 - lead, P.data + P.tail_base - lead, P.nbytes - P.tail_base + lead,
                              hipMemcpyDeviceToDevice, s));
     P.tail = e->tail.p + 8 - P.tail_base;
-    const size_t lds = ac.fast_cls_off + 256;
-    const uint64_t nregions = (P.nbytes + kFastRegion - 1) / kFastRegion;
-    const uint64_t waves_per_block = kFastThreads / 64;
+    const uint64_t units = (P.nbytes + unit - 1) / unit;
+    const uint64_t n_spans = (P.nbytes + kNlBlock - 1) / kNlBlock;
+    HIP_TRY(e->span_hi.ensure(n_spans + 1));
+    P.span_hi = e->span_hi.p;
     const uint32_t blocks = (uint32_t)std::max<uint64_t>(
-        1, std::min<uint64_t>((nregions + waves_per_block - 1) / waves_per_block, (uint64_t)e->num_cus));
-    // per-wave event segments (expected ~1 output byte per KiB of text; 4x headroom)
+        1, std::min<uint64_t>((units + kFastThreads - 1) / kFastThreads, (uint64_t)e->num_cus));
+    // per-wave event segments (an output group per ~KiB of source text; 4x headroom)
     const uint64_t n_waves = (uint64_t)blocks * (kFastThreads / 64);
     P.ev_cap_per_wave = std::max<uint64_t>(1024, (P.nbytes / 256) / n_waves + 256);
     HIP_TRY(e->ev_buf.ensure(n_waves * P.ev_cap_per_wave));
     HIP_TRY(e->ev_counts.ensure(n_waves));
-    HIP_TRY(e->ev_overflow.ensure(1 << 20));
+    HIP_TRY(e->ev_overflow.ensure(std::max<uint64_t>(1 << 20, e->ev_ovf_need)));
     P.events = e->ev_buf.p;
     P.ev_counts = e->ev_counts.p;
     P.ev_overflow = e->ev_overflow.p;
     P.ev_overflow_cap = e->ev_overflow.n;
     HIP_TRY(hipMemsetAsync(&P.ctrl->ev_overflow, 0, 8, s));
-    HIP_TRY(hipFuncSetAttribute((const void*)k_scan_fast, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_scan_fast, dim3(blocks), dim3(kFastThreads), lds, s, P);
+    // (the image lives in the kernel's static kFastLdsMax array: no dynamic LDS)
+    if (chains == 1 && vecs == 8) hipLaunchKernelGGL((k_scan_fast<1, 8>), dim3(blocks), dim3(kFastThreads), 0, s, P);
+    else if (chains == 1) hipLaunchKernelGGL((k_scan_fast<1, 4>), dim3(blocks), dim3(kFastThreads), 0, s, P);
+    else hipLaunchKernelGGL((k_scan_fast<2, 4>), dim3(blocks), dim3(kFastThreads), 0, s, P);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_report, dim3((uint32_t)std::min<uint64_t>(n_waves + 1, 8192)), dim3(256), 0, s, P,
+    hipLaunchKernelGGL(k_report, dim3((uint32_t)std::min<uint64_t>(n_waves + 1, e->num_cus)), dim3(kReportThreads), 0, s, P,
                        (uint32_t)n_waves);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_fold_special, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_spans + 3) / 4, 8192))),
+                       dim3(256), 0, s, P, n_spans);
   } else {
     const size_t table_bytes = (size_t)ac.nstates * ac.nclasses * 2;
     const bool lds_table = table_bytes <= (size_t)kLdsTableMax;
@@ -1534,7 +1774,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   }
   HIP_TRY(e->scratch.ensure((size_t)e->vm_threads * e->scratch_stride));
   std::vector<double>& tm = res->impl.timings;
-  tm.assign(13, 0.0);
+  tm.assign(15, 0.0);
   if (!e->events) {
     for (auto& ev : e->ev) HIP_TRY(hipEventCreate(&ev));
     e->events = true;
@@ -1592,8 +1832,10 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(hipGetLastError());
     Ctrl c;
     if ((rc = read_ctrl(e, &c))) return rc;
-    if (c.hits <= hit_cap) break;
+    const bool ev_lost = rs->ac.fast.size() && c.ev_overflow > e->ev_overflow.n;
+    if (c.hits <= hit_cap && !ev_lost) break;
     // overflow: grow and rescan (keyword bits are idempotent)
+    if (ev_lost) e->ev_ovf_need = c.ev_overflow + (c.ev_overflow >> 2);
     HIP_TRY(e->hits.ensure(c.hits));
     hit_cap = P.hit_cap = e->hits.n;
     P.hits = e->hits.p;
@@ -1604,6 +1846,13 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   if ((rc = read_ctrl(e, &c))) return rc;
   const uint64_t n_hits = c.hits;
   const uint64_t scan_overflow = c.ev_overflow;
+  const uint64_t n_outputs = c.outputs;
+  uint64_t n_events = scan_overflow;
+  if (rs->ac.fast.size() && e->ev_counts.n) {
+    std::vector<uint32_t> evc(e->ev_counts.n);
+    HIP_TRY(hipMemcpy(evc.data(), e->ev_counts.p, evc.size() * 4, hipMemcpyDeviceToHost));
+    for (uint32_t x : evc) n_events += x;
+  }
   // ---- 3. candidates
   uint64_t cand_cap = std::max<uint64_t>(1 << 16, n_hits * 2 + nf / 4);
   ExpandParams E{};
@@ -1787,6 +2036,8 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   tm[10] = (double)n_jobs;
   tm[11] = (double)n_locs;
   tm[12] = (double)scan_overflow;
+  tm[13] = (double)n_events;
+  tm[14] = (double)n_outputs;
   if (nbytes) {  // k_scan alone (the dominant, HBM-bound kernel)
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, e->ev[8], e->ev[9]));
@@ -1843,7 +2094,7 @@ void tsg_engine_free(tsg_engine* e) {
   e->job_start.release(); e->nsel.release(); e->cub_tmp.release(); e->locs.release();
   e->scratch.release(); e->ctrl.release(); e->excl_jobs.release(); e->excl_out.release();
   e->nl_blocks.release(); e->nl_pre.release(); e->tail.release(); e->region_file.release();
-  e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release();
+  e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release();
   if (e->events)
     for (auto& ev : e->ev) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream);
@@ -1986,10 +2237,15 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
   HIP_TRY(e->nl_blocks.ensure(n_nlb));
   HIP_TRY(hipMemsetAsync(e->nl_blocks.p, 0, n_nlb * 4, s));
   P.nl_blocks = e->nl_blocks.p;
-  if (nbytes) {
+  for (int attempt = 0; attempt < 2 && nbytes; ++attempt) {
     if ((rc = launch_scan(e, P))) return rc;
     hipLaunchKernelGGL(k_special_gate, dim3(std::max(1u, std::min<uint32_t>((nf + 3) / 4, 4096))), dim3(256), 0, s, P);
     HIP_TRY(hipGetLastError());
+    Ctrl c;
+    if ((rc = read_ctrl(e, &c))) return rc;
+    if (!rs->ac.fast.size() || c.ev_overflow <= e->ev_overflow.n) break;
+    e->ev_ovf_need = c.ev_overflow + (c.ev_overflow >> 2);  // events were lost: grow and rescan
+    HIP_TRY(hipMemsetAsync(e->ctrl.p, 0, sizeof(Ctrl), s));
   }
   std::vector<uint32_t> kw((size_t)nf * RS.kw_words);
   if (nf) HIP_TRY(hipMemcpyAsync(kw.data(), e->file_kw.p, kw.size() * 4, hipMemcpyDeviceToHost, s));

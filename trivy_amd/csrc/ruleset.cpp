@@ -41,16 +41,18 @@ bool is_ascii(const std::string& s) {
 namespace tsg {
 void set_last_error(const std::string& m) { g_last_error = m; }
 
-// Aho-Corasick over the lowercased patterns (truncated to kAcMaxLit bytes).
-bool build_ac(tsg_ruleset* rs, std::string* err) {
+// Aho-Corasick over the lowercased patterns (truncated to `depth` bytes).
+static bool build_ac_depth(tsg_ruleset* rs, int depth, std::string* err) {
   AcHost& ac = rs->ac;
+  ac = AcHost{};
+  ac.depth = (uint32_t)depth;
   // byte classes: every byte that appears in a (lowercased) pattern gets a
   // class; 'A'-'Z' share the class of their lowercase letter.
   int cmap[256];
   for (int b = 0; b < 256; ++b) cmap[b] = 0;
   int ncls = 1;
   for (auto& p : rs->patterns) {
-    size_t L = std::min<size_t>(p.lower.size(), kAcMaxLit);
+    size_t L = std::min<size_t>(p.lower.size(), (size_t)depth);
     for (size_t k = 0; k < L; ++k) {
       unsigned char c = p.lower[k];
       if (c == 0) {
@@ -73,7 +75,7 @@ bool build_ac(tsg_ruleset* rs, std::string* err) {
   term.emplace_back();
   for (size_t pi = 0; pi < rs->patterns.size(); ++pi) {
     auto& p = rs->patterns[pi];
-    size_t L = std::min<size_t>(p.lower.size(), kAcMaxLit);
+    size_t L = std::min<size_t>(p.lower.size(), (size_t)depth);
     int s = 0;
     for (size_t k = 0; k < L; ++k) {
       int c = cmap[(unsigned char)p.lower[k]];
@@ -120,6 +122,26 @@ bool build_ac(tsg_ruleset* rs, std::string* err) {
       }
     }
   }
+  // renumber: states without outputs first (root stays 0), output states
+  // last, so k_scan_fast detects an output with one max() per byte
+  {
+    std::vector<int> perm(S), inv;
+    for (int st = 0; st < S; ++st)
+      if (outs[st].empty()) { perm[st] = (int)inv.size(); inv.push_back(st); }
+    for (int st = 0; st < S; ++st)
+      if (!outs[st].empty()) { perm[st] = (int)inv.size(); inv.push_back(st); }
+    std::vector<std::vector<int>> go2(S);
+    std::vector<std::vector<uint16_t>> outs2(S);
+    for (int n = 0; n < S; ++n) {
+      go2[n] = go[inv[n]];
+      for (auto& t : go2[n]) t = perm[t];
+      outs2[n] = outs[inv[n]];
+    }
+    go.swap(go2);
+    outs.swap(outs2);
+  }
+  int first_out = S;
+  for (int st = S - 1; st >= 0 && !outs[st].empty(); --st) first_out = st;
   ac.nstates = (uint32_t)S;
   ac.nclasses = (uint32_t)ncls;
   ac.delta.assign((size_t)S * ncls, 0);
@@ -137,22 +159,55 @@ bool build_ac(tsg_ruleset* rs, std::string* err) {
     for (auto x : outs[s]) ac.out_pat.push_back(x);
   }
   ac.out_off[S] = (uint32_t)ac.out_pat.size();
-  // fast image: u16 rows of ncls entries, entry = next row's byte offset | output
-  // bit, followed by cls2[256] = 2 * class (see k_scan_fast).
+  // k_scan_fast LDS image: one kFastRowBytes row per state, 128 columns indexed
+  // by the folded byte (engine.hip fold4: both letter cases share a column;
+  // bytes >= 0x80 and a few rare ASCII bytes alias other columns, so their
+  // groups are replayed and every reported pattern is confirmed on the real
+  // bytes).  Entry = next row's offset / 2, so a step is T[2 * (e + col)].
+  // Only for all-ASCII pattern sets (the fold-special sequences are found by
+  // the replay instead) whose rows fit 16-bit entries and k_report's LDS.
   ac.fast.clear();
-  const size_t rows_bytes = (size_t)S * ncls * 2;
-  if (ncls <= 127 && rows_bytes <= 65534) {
-    ac.fast_cls_off = (uint32_t)rows_bytes;
-    ac.fast.assign(rows_bytes + 256, 0);
-    uint16_t* rows = reinterpret_cast<uint16_t*>(ac.fast.data());
-    for (int st = 0; st < S; ++st)
-      for (int c = 0; c < ncls; ++c) {
-        int t = go[st][c];
-        rows[(size_t)st * ncls + c] = (uint16_t)(t * ncls * 2 + (outs[t].empty() ? 0 : 1));
-      }
-    for (int b = 0; b < 256; ++b) ac.fast[rows_bytes + b] = (uint8_t)(2 * cmap[b]);
+  bool ascii_only = true;
+  for (auto& p : rs->patterns)
+    if (!p.special)
+      for (unsigned char c : p.lower) ascii_only &= c < 0x80;
+  constexpr uint32_t kRowU16 = kFastRowBytes / 2;
+  const size_t img = ((size_t)S * kFastRowBytes + 3) & ~(size_t)3;
+  // column of byte b after k_scan_fast's fold (bit 6 set clears bit 5, 7 bits
+  // kept); each column takes the class of the pattern bytes folding onto it,
+  // and two different pattern classes on one column rule the image out
+  int col_cls[128];
+  bool fold_ok = true;
+  for (int v = 0; v < 128; ++v) col_cls[v] = -1;
+  for (int b = 0; b < 256; ++b) {
+    const int v = ((b & 0x40) ? (b & ~0x20) : b) & 0x7F;
+    const int c = b < 128 ? cmap[b] : 0;  // bytes >= 0x80 never sit inside an ASCII pattern
+    if (c == 0) continue;
+    if (col_cls[v] >= 0 && col_cls[v] != c) fold_ok = false;
+    col_cls[v] = c;
+  }
+  for (int v = 0; v < 128; ++v)
+    if (col_cls[v] < 0) col_cls[v] = 0;
+  if (ascii_only && fold_ok && img <= kFastLdsMax - 16 * 1024 - 64 && (size_t)(S - 1) * kRowU16 < 65536) {
+    ac.fast.assign(img, 0);
+    for (int st = 0; st < S; ++st) {
+      uint16_t* row = reinterpret_cast<uint16_t*>(ac.fast.data() + (size_t)st * kFastRowBytes);
+      for (int v = 0; v < 128; ++v) row[v] = (uint16_t)(go[st][col_cls[v]] * kRowU16);
+    }
+    ac.fast_out_entry = (uint32_t)first_out * kRowU16;
   }
   return true;
+}
+
+// The deepest trie (<= kAcMaxLit) whose automaton fits k_scan_fast's LDS
+// image; longer patterns are confirmed on hit.  Falls back to depth
+// kAcMaxLit for the generic kernel when none fits.
+bool build_ac(tsg_ruleset* rs, std::string* err) {
+  for (int d = kAcMaxLit; d >= 4; --d) {
+    if (!build_ac_depth(rs, d, err)) return false;
+    if (!rs->ac.fast.empty()) return true;
+  }
+  return build_ac_depth(rs, kAcMaxLit, err);
 }
 }  // namespace tsg
 
