@@ -121,6 +121,9 @@ int tsg_ruleset_rule_info(const tsg_ruleset* rs, size_t i, int* mode, uint32_t* 
 int tsg_ruleset_rule_literal(const tsg_ruleset* rs, size_t i, size_t k, char* lower, char* req, size_t cap,
                              size_t* len);
 
+/* Instruction count and capture slots of rule i's compiled regex. */
+int tsg_ruleset_rule_prog(const tsg_ruleset* rs, size_t i, uint32_t* n_inst, uint32_t* n_cap);
+
 /* Candidate filter of rule i, run on host text from anchor position h:
  * *accept = 0 only when no match of the rule can contain an anchor hit at h
  * (k_expand drops such hits); *n_states = its DFA size (0 = no filter). */

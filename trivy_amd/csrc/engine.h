@@ -14,8 +14,10 @@ constexpr int kAcMaxLit = 8;   // trie depth; longer patterns are confirmed on h
 constexpr uint32_t kNlBlock = 4096;  // newline-count granularity (bytes) = one k_scan_fast chain span
 constexpr uint32_t kNoKw = 0xFFFFFFFFu;
 
-constexpr uint32_t kFastRowBytes = 258;       // 128 u16 columns + 2 B: consecutive rows rotate LDS banks
-constexpr uint32_t kFastLdsMax = 160 * 1024;  // k_scan_fast image budget (one image per CU)
+constexpr uint32_t kFastCols = 64;             // k_scan_fast columns (6-bit folded bytes, engine.hip fold6)
+constexpr uint32_t kFastRowBytes = 130;       // 64 u16 columns + 2 B: consecutive rows rotate LDS banks
+constexpr uint32_t kFastImgMax = 78 * 1024;   // k_scan_fast image budget: two images per CU's LDS
+constexpr uint32_t kLdsMax = 160 * 1024;      // LDS per CU
 constexpr uint32_t kFastSpecialEv = 0xFFFF;   // event tag: U+0130/U+017F/U+212A sequence ends here
 constexpr uint32_t kFollowMaxStates = 1024;  // follow-DFA subset-construction budget
 constexpr uint32_t kFollowDepth = 96;        // bytes a candidate filter reads past the hit

@@ -295,7 +295,6 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_generic(ScanParams P) {
 //    the fold-special sequences C4B0 / C5BF / E284AA exactly
 //  * the newline count of each span goes straight to nl_blocks (one owner,
 //    plain store) and feeds StartLine/EndLine.
-constexpr int kFastThreads = 1024;
 constexpr uint32_t kFastRowU16 = kFastRowBytes / 2;
 // Variant in use (chains per lane, 16-byte vectors per chain step); the
 // other shapes stay compilable for A/B runs (TSG_FAST_VARIANT).
@@ -309,16 +308,18 @@ __device__ inline uint32_t nl_count_dword(uint32_t w) {
   return __builtin_popcount(z);
 }
 
-// Column fold, four bytes at once: a byte with bit 6 set loses bit 5, so both
-// letter cases share columns 0x41-0x5A (LDS banks 0-15) while digits and
-// punctuation keep 0x20-0x3F (banks 16-31): the common text bytes no longer
-// collide on a bank.  (0x60/0x7B-0x7F alias 0x40/0x5B-0x5F; bytes >= 0x80 alias
-// too — their groups are replayed and reported patterns re-checked.)
-__device__ inline uint32_t fold4(uint32_t w) { return w & ~((w >> 1) & 0x20202020u); }
+// 6-bit column fold, four bytes at once: bits 0-4 kept, bit 6 moved to bit 5.
+// Both letter cases share columns 32-58, digits and punctuation sit in 0-31,
+// and a 64-column row spans the 32 LDS banks exactly once (two columns per
+// dword), so lanes in one state never collide on a bank, and the 130-byte
+// rows keep two images per CU.  Control bytes alias space/punctuation,
+// `{|}~ and DEL alias @[\]^_, bytes >= 0x80 alias ASCII: k_report re-checks
+// every pattern on the real bytes.
+__device__ inline uint32_t fold6(uint32_t w) { return (w & 0x1F1F1F1Fu) | ((w >> 1) & 0x20202020u); }
 
-// One automaton step on byte j of a folded dword w: e = T[e + (b & 0x7F)] (u16 units).
+// One automaton step on byte j of a folded dword w: e = T[e + col] (u16 units).
 __device__ inline uint32_t fstep(const uint8_t* T, uint32_t e, uint32_t w, int j) {
-  const uint32_t b = (w >> (8 * j)) & 0x7Fu;
+  const uint32_t b = (w >> (8 * j)) & 0x3Fu;
   uint32_t a;
   asm("v_add_lshl_u32 %0, %1, %2, 1" : "=v"(a) : "v"(e), "v"(b));  // one VALU on the dependent chain
   return *(const uint16_t*)(T + a);
@@ -353,23 +354,13 @@ struct FastChain {
   uint2 prev;    // the 8 raw bytes before the next group
 };
 
-// Walk one 8-byte group (d0, d1) of a chain; when the automaton reaches an
-// output state in it, append an event to the wave's segment (ballot +
-// popcount, no atomics; every lane calls this, so ev_count stays uniform).
+// Append an event for a group whose automaton max reached an output state
+// (ballot + popcount into the wave's segment, no atomics; every lane calls
+// this, so ev_count stays wave-uniform).
 template <int V>
-__device__ inline void fast_group(const ScanParams& P, const uint8_t* T, uint32_t out_e, FastChain<V>& C, uint32_t d0,
-                                  uint32_t d1, uint64_t gpos, bool live, uint64_t lanes_lt, FastEvent* ev_seg,
-                                  uint32_t* ev_count) {
-  C.nl += nl_count_dword(d0) + nl_count_dword(d1);
-  C.hi |= d0 | d1;
-  const uint32_t f0 = fold4(d0), f1 = fold4(d1);
-  const uint32_t gs = C.e;
-  uint32_t m = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    C.e = fstep(T, C.e, j < 4 ? f0 : f1, j & 3);
-    m = m > C.e ? m : C.e;
-  }
+__device__ inline void fast_event(const ScanParams& P, uint32_t out_e, const FastChain<V>& C, uint32_t m, uint32_t gs,
+                                  uint32_t d0, uint32_t d1, uint64_t gpos, bool live, uint64_t lanes_lt,
+                                  FastEvent* ev_seg, uint32_t* ev_count) {
   const bool ev = live && m >= out_e;
   const uint64_t b = __ballot(ev);
   if (b) {
@@ -390,15 +381,59 @@ __device__ inline void fast_group(const ScanParams& P, const uint8_t* T, uint32_
     }
     *ev_count += (uint32_t)__popcll(b);
   }
+}
+
+// Walk one 8-byte group (d0, d1) of a chain and report it if it hit an output.
+template <int V>
+__device__ inline void fast_group(const ScanParams& P, const uint8_t* T, uint32_t out_e, FastChain<V>& C, uint32_t d0,
+                                  uint32_t d1, uint64_t gpos, bool live, uint64_t lanes_lt, FastEvent* ev_seg,
+                                  uint32_t* ev_count) {
+  C.nl += nl_count_dword(d0) + nl_count_dword(d1);
+  C.hi |= d0 | d1;
+  const uint32_t f0 = fold6(d0), f1 = fold6(d1);
+  const uint32_t gs = C.e;
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    C.e = fstep(T, C.e, j < 4 ? f0 : f1, j & 3);
+    m = m > C.e ? m : C.e;
+  }
+  fast_event(P, out_e, C, m, gs, d0, d1, gpos, live, lanes_lt, ev_seg, ev_count);
   C.prev = make_uint2(d0, d1);
 }
 
-template <int CH, int V>
+// Two chains' groups walked in lock-step, so their LDS lookups overlap.
+template <int V>
+__device__ inline void fast_group2(const ScanParams& P, const uint8_t* T, uint32_t out_e, FastChain<V>& A,
+                                   FastChain<V>& B, uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1, uint64_t apos,
+                                   uint64_t bpos, bool live, uint64_t lanes_lt, FastEvent* ev_seg,
+                                   uint32_t* ev_count) {
+  A.nl += nl_count_dword(a0) + nl_count_dword(a1);
+  B.nl += nl_count_dword(b0) + nl_count_dword(b1);
+  A.hi |= a0 | a1;
+  B.hi |= b0 | b1;
+  const uint32_t fa0 = fold6(a0), fa1 = fold6(a1), fb0 = fold6(b0), fb1 = fold6(b1);
+  const uint32_t ga = A.e, gb = B.e;
+  uint32_t ma = 0, mb = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    A.e = fstep(T, A.e, j < 4 ? fa0 : fa1, j & 3);
+    B.e = fstep(T, B.e, j < 4 ? fb0 : fb1, j & 3);
+    ma = ma > A.e ? ma : A.e;
+    mb = mb > B.e ? mb : B.e;
+  }
+  fast_event(P, out_e, A, ma, ga, a0, a1, apos, live, lanes_lt, ev_seg, ev_count);
+  fast_event(P, out_e, B, mb, gb, b0, b1, bpos, live, lanes_lt, ev_seg, ev_count);
+  A.prev = make_uint2(a0, a1);
+  B.prev = make_uint2(b0, b1);
+}
+
+template <int CH, int V, int kFastThreads>
 __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
   constexpr uint32_t kUnit = CH * kNlBlock;          // bytes per lane per work unit
   constexpr int kStep = V * 16;                      // bytes per chain step
   constexpr int kSteps = kNlBlock / kStep;           // steps per span
-  __shared__ __align__(16) uint8_t smem[kFastLdsMax];  // static: LDS base folds to 0 in the step
+  __shared__ __align__(16) uint8_t smem[kFastImgMax];  // static: LDS base folds to 0 in the step
   const AcDev& ac = P.rs.ac;
   {
     const uint32_t words = ac.fast_bytes / 4;
@@ -438,7 +473,7 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
       const uint2 h = live && s0 >= 8 ? *(const uint2*)(fast_src(P, s0 - 8) + s0 - 8) : make_uint2(0, 0);
       uint32_t e = 0;
 #pragma unroll
-      for (int j = 1; j < 8; ++j) e = fstep(T, e, j < 4 ? fold4(h.x) : fold4(h.y), j & 3);
+      for (int j = 1; j < 8; ++j) e = fstep(T, e, j < 4 ? fold6(h.x) : fold6(h.y), j & 3);
       C[c].e = e;
       C[c].prev = h;
       C[c].nl = 0;
@@ -463,13 +498,19 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
         }
       }
 #pragma unroll
-      for (int k = 0; k < V; ++k)
-#pragma unroll
-        for (int c = 0; c < CH; ++c) {
-          const uint4 v = C[c].cur[k];
-          fast_group(P, T, out_e, C[c], v.x, v.y, C[c].pos + 16 * k, live, lanes_lt, ev_seg, &ev_count);
-          fast_group(P, T, out_e, C[c], v.z, v.w, C[c].pos + 16 * k + 8, live, lanes_lt, ev_seg, &ev_count);
+      for (int k = 0; k < V; ++k) {
+        if (CH == 2) {
+          const uint4 v = C[0].cur[k], w = C[CH - 1].cur[k];
+          fast_group2(P, T, out_e, C[0], C[CH - 1], v.x, v.y, w.x, w.y, C[0].pos + 16 * k, C[CH - 1].pos + 16 * k, live,
+                      lanes_lt, ev_seg, &ev_count);
+          fast_group2(P, T, out_e, C[0], C[CH - 1], v.z, v.w, w.z, w.w, C[0].pos + 16 * k + 8,
+                      C[CH - 1].pos + 16 * k + 8, live, lanes_lt, ev_seg, &ev_count);
+        } else {
+          const uint4 v = C[0].cur[k];
+          fast_group(P, T, out_e, C[0], v.x, v.y, C[0].pos + 16 * k, live, lanes_lt, ev_seg, &ev_count);
+          fast_group(P, T, out_e, C[0], v.z, v.w, C[0].pos + 16 * k + 8, live, lanes_lt, ev_seg, &ev_count);
         }
+      }
 #pragma unroll
       for (int c = 0; c < CH; ++c) C[c].pos = np[c];
     }
@@ -488,6 +529,101 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
   if (lane == 0) P.ev_counts[wave] = ev_count < P.ev_cap_per_wave ? ev_count : P.ev_cap_per_wave;
 }
 
+// Ring variant: every lane walks TWO chains in lock-step (ILP against the LDS
+// latency): chain c covers half c of the lane's kNlBlock span.  Each chain
+// streams through a 128-byte register ring — a 16-byte vector is reloaded
+// with the chain's next 128 bytes right after it is consumed, always (a
+// finished lane reloads its own bytes), so the compiler can count vmcnt
+// exactly across the loop and the HBM latency hides behind a full ring of
+// automaton work; every load completes whole 128-byte lines.
+constexpr uint32_t kRingHalf = kNlBlock / 2;
+
+__global__ __launch_bounds__(1024) void k_scan_ring(ScanParams P) {
+  constexpr int kSteps = kRingHalf / 128;
+  __shared__ __align__(16) uint8_t smem[kFastImgMax];
+  const AcDev& ac = P.rs.ac;
+  {
+    const uint32_t words = ac.fast_bytes / 4;
+    const uint32_t* src = (const uint32_t*)ac.fast_lds;
+    for (uint32_t i = threadIdx.x; i < words; i += 1024) ((uint32_t*)smem)[i] = src[i];
+  }
+  __syncthreads();
+  const uint8_t* T = smem;
+  const uint32_t out_e = ac.fast_out_entry;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t lanes_lt = (1ull << lane) - 1;
+  const uint32_t wave = (blockIdx.x * 16) + (threadIdx.x >> 6);
+  const uint64_t nlanes = (uint64_t)gridDim.x * 1024;
+  const uint64_t units = (P.nbytes + kNlBlock - 1) / kNlBlock;
+  FastEvent* ev_seg = P.events + (uint64_t)wave * P.ev_cap_per_wave;
+  uint32_t ev_count = 0;  // wave-uniform
+  uint64_t u = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+  FastChain<8> A, B;
+  // ring fill: the lane's first span (a lane with no span reloads span 0)
+  {
+    const uint64_t s0 = (u < units ? u : 0) * kNlBlock;
+    A.pos = s0;
+    B.pos = s0 + kRingHalf;
+    const uint8_t* sa = fast_src(P, A.pos);
+    const uint8_t* sb = fast_src(P, B.pos);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      A.cur[k] = *(const uint4*)(sa + A.pos + 16 * k);
+      B.cur[k] = *(const uint4*)(sb + B.pos + 16 * k);
+    }
+  }
+  while (__ballot(u < units)) {
+    const bool live = u < units;
+    const uint64_t un = u + nlanes;
+    const uint64_t s0 = A.pos;  // == u * kNlBlock for a live lane
+    {
+      // warm-up: the 7 bytes before each half (automaton depth <= kAcMaxLit)
+      const uint2 ha = s0 >= 8 ? *(const uint2*)(fast_src(P, s0 - 8) + s0 - 8) : make_uint2(0, 0);
+      const uint2 hb = *(const uint2*)(fast_src(P, B.pos - 8) + B.pos - 8);
+      uint32_t ea = 0, eb = 0;
+#pragma unroll
+      for (int j = 1; j < 8; ++j) {
+        ea = fstep(T, ea, j < 4 ? fold6(ha.x) : fold6(ha.y), j & 3);
+        eb = fstep(T, eb, j < 4 ? fold6(hb.x) : fold6(hb.y), j & 3);
+      }
+      A.e = ea;
+      B.e = eb;
+      A.prev = ha;
+      B.prev = hb;
+      A.nl = B.nl = 0;
+      A.hi = B.hi = 0;
+    }
+    // the unit after this one (or this one again: reloads stay unconditional)
+    const uint64_t nbase = (un < units ? un : (live ? u : 0)) * kNlBlock;
+    for (int step = 0; step < kSteps; ++step) {
+      const bool last = step + 1 == kSteps;
+      const uint64_t na = last ? nbase : A.pos + 128;
+      const uint64_t nb = last ? nbase + kRingHalf : B.pos + 128;
+      const uint8_t* sa = fast_src(P, na);
+      const uint8_t* sb = fast_src(P, nb);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint4 v = A.cur[k], w = B.cur[k];
+        A.cur[k] = *(const uint4*)(sa + na + 16 * k);
+        B.cur[k] = *(const uint4*)(sb + nb + 16 * k);
+        fast_group2(P, T, out_e, A, B, v.x, v.y, w.x, w.y, A.pos + 16 * k, B.pos + 16 * k, live, lanes_lt, ev_seg,
+                    &ev_count);
+        fast_group2(P, T, out_e, A, B, v.z, v.w, w.z, w.w, A.pos + 16 * k + 8, B.pos + 16 * k + 8, live, lanes_lt,
+                    ev_seg, &ev_count);
+      }
+      A.pos = na;
+      B.pos = nb;
+    }
+    if (live) {
+      const uint64_t sp = s0 / kNlBlock;
+      P.nl_blocks[sp] = A.nl + B.nl;
+      P.span_hi[sp] = ((A.hi | B.hi) & 0x80808080u) ? 1 : 0;
+    }
+    u = un;
+  }
+  if (lane == 0) P.ev_counts[wave] = ev_count < P.ev_cap_per_wave ? ev_count : P.ev_cap_per_wave;
+}
+
 // Resolve k_scan_fast's events.  Each event is replayed on an LDS copy of the
 // scan image with the output tables (out_off/out_pat/pats/pat_bytes) behind
 // it; the event carries the group's bytes and the 8 before them, so a
@@ -498,7 +634,7 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
 // global reservation per block step).
 constexpr uint32_t kReportThreads = 1024;
 constexpr uint32_t kReportHitCap = 2048;
-constexpr uint32_t kReportLds = kFastLdsMax - kReportHitCap * 8 - 64;
+constexpr uint32_t kReportLds = kLdsMax - kReportHitCap * 8 - 64;
 
 __device__ inline uint32_t file_of_pos(const ScanParams& P, uint64_t pos) {
   const uint64_t r = pos / kNlBlock;
@@ -549,7 +685,7 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
       const FastEvent ev = seg[i];
       uint64_t hist = ((uint64_t)ev.prev.y << 32) | ev.prev.x;  // the 8 raw bytes before (oldest low)
       uint32_t e = ev.entry;
-      const uint32_t fx = fold4(ev.cur.x), fy = fold4(ev.cur.y);
+      const uint32_t fx = fold6(ev.cur.x), fy = fold6(ev.cur.y);
       uint32_t fi = 0xFFFFFFFFu;
       for (int j = 0; j < 8; ++j) {
         e = fstep(B, e, j < 4 ? fx : fy, j & 3);
@@ -972,6 +1108,7 @@ struct VerifyParams {
   Ctrl* ctrl;
   uint8_t* scratch;
   uint64_t scratch_stride;
+  uint64_t* prof;  // diagnostics (TSG_PROFILE_VERIFY): per job {cycles, rule<<32 | candidates}
 };
 
 // Candidate start windows of one (file, rule) job, in increasing order
@@ -1130,9 +1267,21 @@ __global__ __launch_bounds__(256) void k_verify(VerifyParams V) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   gre::VmScratch sc = make_scratch(V.scratch + (uint64_t)t * V.scratch_stride, V.rs);
   for (uint32_t j = t; j < V.n_jobs; j += nthreads) {
+    const uint64_t t0 = V.prof ? clock64() : 0;
     const uint64_t c0 = V.job_start[j];
     const uint64_t c1 = (j + 1 < V.n_jobs) ? V.job_start[j + 1] : V.n_cands;
     const uint32_t rule = (uint32_t)(V.keys[c0] >> kPosBits);
+    struct ProfGuard {
+      const VerifyParams& V;
+      uint32_t j, rule;
+      uint64_t t0, nc;
+      __device__ ~ProfGuard() {
+        if (V.prof) {
+          V.prof[2 * j] = clock64() - t0;
+          V.prof[2 * j + 1] = ((uint64_t)rule << 32) | nc;
+        }
+      }
+    } pg{V, j, rule, t0, c1 - c0};
     const uint32_t fi = V.vals[c0] & ~kFullFlag;
     bool full = false;
     for (uint64_t c = c0; c < c1 && !full; ++c) full = (V.vals[c] & kFullFlag) != 0;
@@ -1355,6 +1504,7 @@ struct tsg_engine {
   DBuf<uint8_t> tail;
   DBuf<uint32_t> region_file;
   DBuf<FastEvent> ev_buf, ev_overflow;
+  DBuf<uint64_t> vprof;
   DBuf<uint8_t> span_hi;
   DBuf<uint32_t> ev_counts;
   uint64_t ev_ovf_need = 0;  // overflow-event capacity learnt from a lost scan
@@ -1688,12 +1838,13 @@ int launch_scan(tsg_engine* e, ScanParams P) {
     // final partial region: zero-padded copy (with 8 bytes of warm-up context)
     // variant: chains per lane x 16-byte vectors per chain step (A/B via TSG_FAST_VARIANT)
     int chains = kFastChains, vecs = kFastVecs;
-    if (const char* v = getenv("TSG_FAST_VARIANT")) sscanf(v, "%dx%d", &chains, &vecs);
-    if (!((chains == 1 && (vecs == 8 || vecs == 4)) || (chains == 2 && vecs == 4))) {
+    bool ring = false;  // TSG_FAST_VARIANT=ring: the two-chain register ring (A/B; spills today)
+    if (const char* v = getenv("TSG_FAST_VARIANT")) ring = sscanf(v, "%dx%d", &chains, &vecs) != 2;
+    if (!((chains == 1 && (vecs == 8 || vecs == 4)) || (chains == 2 && (vecs == 4 || vecs == 2)))) {
       chains = kFastChains;
       vecs = kFastVecs;
     }
-    const uint64_t unit = (uint64_t)chains * kNlBlock;
+    const uint64_t unit = ring ? (uint64_t)kNlBlock : (uint64_t)chains * kNlBlock;
     P.tail_base = (P.nbytes / unit) * unit;
     const uint64_t lead = P.tail_base >= 8 ? 8 : P.tail_base;
     HIP_TRY(e->tail.ensure(8 + kFastUnitMax + 64));
@@ -1706,10 +1857,14 @@ int launch_scan(tsg_engine* e, ScanParams P) {
     const uint64_t n_spans = (P.nbytes + kNlBlock - 1) / kNlBlock;
     HIP_TRY(e->span_hi.ensure(n_spans + 1));
     P.span_hi = e->span_hi.p;
+    // shape: 1x8 = 1024 threads, one block per CU (120 VGPRs); 1x4 = 768
+    // threads, two blocks per CU (two LDS images, 24 waves); 2x4 = 1024, one
+    const uint32_t nt = (!ring && ((chains == 1 && vecs == 4) || (chains == 2 && vecs == 2))) ? 768 : 1024;
+    const uint32_t per_cu = nt == 768 ? 2 : 1;
     const uint32_t blocks = (uint32_t)std::max<uint64_t>(
-        1, std::min<uint64_t>((units + kFastThreads - 1) / kFastThreads, (uint64_t)e->num_cus));
+        1, std::min<uint64_t>((units + nt - 1) / nt, (uint64_t)e->num_cus * per_cu));
     // per-wave event segments (an output group per ~KiB of source text; 4x headroom)
-    const uint64_t n_waves = (uint64_t)blocks * (kFastThreads / 64);
+    const uint64_t n_waves = (uint64_t)blocks * (nt / 64);
     P.ev_cap_per_wave = std::max<uint64_t>(1024, (P.nbytes / 256) / n_waves + 256);
     HIP_TRY(e->ev_buf.ensure(n_waves * P.ev_cap_per_wave));
     HIP_TRY(e->ev_counts.ensure(n_waves));
@@ -1719,10 +1874,12 @@ int launch_scan(tsg_engine* e, ScanParams P) {
     P.ev_overflow = e->ev_overflow.p;
     P.ev_overflow_cap = e->ev_overflow.n;
     HIP_TRY(hipMemsetAsync(&P.ctrl->ev_overflow, 0, 8, s));
-    // (the image lives in the kernel's static kFastLdsMax array: no dynamic LDS)
-    if (chains == 1 && vecs == 8) hipLaunchKernelGGL((k_scan_fast<1, 8>), dim3(blocks), dim3(kFastThreads), 0, s, P);
-    else if (chains == 1) hipLaunchKernelGGL((k_scan_fast<1, 4>), dim3(blocks), dim3(kFastThreads), 0, s, P);
-    else hipLaunchKernelGGL((k_scan_fast<2, 4>), dim3(blocks), dim3(kFastThreads), 0, s, P);
+    // (the image lives in the kernel's static kFastImgMax array: no dynamic LDS)
+    if (ring) hipLaunchKernelGGL(k_scan_ring, dim3(blocks), dim3(nt), 0, s, P);
+    else if (chains == 1 && vecs == 8) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024>), dim3(blocks), dim3(nt), 0, s, P);
+    else if (chains == 1) hipLaunchKernelGGL((k_scan_fast<1, 4, 768>), dim3(blocks), dim3(nt), 0, s, P);
+    else if (vecs == 4) hipLaunchKernelGGL((k_scan_fast<2, 4, 1024>), dim3(blocks), dim3(nt), 0, s, P);
+    else hipLaunchKernelGGL((k_scan_fast<2, 2, 768>), dim3(blocks), dim3(nt), 0, s, P);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_report, dim3((uint32_t)std::min<uint64_t>(n_waves + 1, e->num_cus)), dim3(kReportThreads), 0, s, P,
                        (uint32_t)n_waves);
@@ -1936,8 +2093,31 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     V.ctrl = e->ctrl.p;
     V.scratch = e->scratch.p;
     V.scratch_stride = e->scratch_stride;
+    const bool prof = getenv("TSG_PROFILE_VERIFY") != nullptr;
+    if (prof) HIP_TRY(e->vprof.ensure(2ull * n_jobs));
+    V.prof = prof ? e->vprof.p : nullptr;
     uint32_t blocks = std::min<uint32_t>((n_jobs + 255) / 256, e->vm_threads / 256);
     hipLaunchKernelGGL(k_verify, dim3(std::max(1u, blocks)), dim3(256), 0, s, V);
+    if (prof) {
+      std::vector<uint64_t> hp(2ull * n_jobs);
+      HIP_TRY(hipMemcpyAsync(hp.data(), e->vprof.p, hp.size() * 8, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      std::vector<uint32_t> idx(n_jobs);
+      for (uint32_t q = 0; q < n_jobs; ++q) idx[q] = q;
+      std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return hp[2 * a] > hp[2 * b]; });
+      std::map<uint32_t, std::pair<uint64_t, uint64_t>> per_rule;
+      for (uint32_t q = 0; q < n_jobs; ++q) {
+        auto& pr = per_rule[(uint32_t)(hp[2 * q + 1] >> 32)];
+        pr.first += hp[2 * q];
+        pr.second = std::max(pr.second, hp[2 * q]);
+      }
+      for (uint32_t q = 0; q < std::min<uint32_t>(10, n_jobs); ++q)
+        fprintf(stderr, "[verify] job %u cycles %llu rule %s cands %llu\n", idx[q], (unsigned long long)hp[2 * idx[q]],
+                rs->rules[hp[2 * idx[q] + 1] >> 32].id.c_str(), (unsigned long long)(hp[2 * idx[q] + 1] & 0xFFFFFFFF));
+      for (auto& kv : per_rule)
+        fprintf(stderr, "[verify] rule %s total %llu max %llu\n", rs->rules[kv.first].id.c_str(),
+                (unsigned long long)kv.second.first, (unsigned long long)kv.second.second);
+    }
     HIP_TRY(hipGetLastError());
     if ((rc = read_ctrl(e, &c))) return rc;
     n_locs = c.locs;
@@ -2094,7 +2274,7 @@ void tsg_engine_free(tsg_engine* e) {
   e->job_start.release(); e->nsel.release(); e->cub_tmp.release(); e->locs.release();
   e->scratch.release(); e->ctrl.release(); e->excl_jobs.release(); e->excl_out.release();
   e->nl_blocks.release(); e->nl_pre.release(); e->tail.release(); e->region_file.release();
-  e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release();
+  e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->vprof.release();
   if (e->events)
     for (auto& ev : e->ev) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream);

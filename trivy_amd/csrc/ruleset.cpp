@@ -159,11 +159,12 @@ static bool build_ac_depth(tsg_ruleset* rs, int depth, std::string* err) {
     for (auto x : outs[s]) ac.out_pat.push_back(x);
   }
   ac.out_off[S] = (uint32_t)ac.out_pat.size();
-  // k_scan_fast LDS image: one kFastRowBytes row per state, 128 columns indexed
-  // by the folded byte (engine.hip fold4: both letter cases share a column;
-  // bytes >= 0x80 and a few rare ASCII bytes alias other columns, so their
-  // groups are replayed and every reported pattern is confirmed on the real
-  // bytes).  Entry = next row's offset / 2, so a step is T[2 * (e + col)].
+  // k_scan_fast LDS image: one kFastRowBytes row per state, kFastCols columns
+  // indexed by the 6-bit folded byte (engine.hip fold6: both letter cases
+  // share a column; control bytes, bytes >= 0x80 and a few rare ASCII bytes
+  // alias other columns, so every reported pattern is confirmed on the real
+  // bytes by k_report).  Entry = next row's offset / 2, so a step is
+  // T[2 * (e + col)].
   // Only for all-ASCII pattern sets (the fold-special sequences are found by
   // the replay instead) whose rows fit 16-bit entries and k_report's LDS.
   ac.fast.clear();
@@ -173,26 +174,26 @@ static bool build_ac_depth(tsg_ruleset* rs, int depth, std::string* err) {
       for (unsigned char c : p.lower) ascii_only &= c < 0x80;
   constexpr uint32_t kRowU16 = kFastRowBytes / 2;
   const size_t img = ((size_t)S * kFastRowBytes + 3) & ~(size_t)3;
-  // column of byte b after k_scan_fast's fold (bit 6 set clears bit 5, 7 bits
-  // kept); each column takes the class of the pattern bytes folding onto it,
-  // and two different pattern classes on one column rule the image out
-  int col_cls[128];
+  // column of byte b after k_scan_fast's fold: bits 0-4 kept, bit 6 -> bit 5;
+  // each column takes the class of the pattern bytes folding onto it, and two
+  // different pattern classes on one column rule the image out
+  int col_cls[kFastCols];
   bool fold_ok = true;
-  for (int v = 0; v < 128; ++v) col_cls[v] = -1;
-  for (int b = 0; b < 256; ++b) {
-    const int v = ((b & 0x40) ? (b & ~0x20) : b) & 0x7F;
-    const int c = b < 128 ? cmap[b] : 0;  // bytes >= 0x80 never sit inside an ASCII pattern
+  for (uint32_t v = 0; v < kFastCols; ++v) col_cls[v] = -1;
+  for (int b = 0; b < 128; ++b) {  // bytes >= 0x80 never sit inside an ASCII pattern
+    const int v = (b & 0x1F) | ((b >> 1) & 0x20);
+    const int c = cmap[b];
     if (c == 0) continue;
     if (col_cls[v] >= 0 && col_cls[v] != c) fold_ok = false;
     col_cls[v] = c;
   }
-  for (int v = 0; v < 128; ++v)
+  for (uint32_t v = 0; v < kFastCols; ++v)
     if (col_cls[v] < 0) col_cls[v] = 0;
-  if (ascii_only && fold_ok && img <= kFastLdsMax - 16 * 1024 - 64 && (size_t)(S - 1) * kRowU16 < 65536) {
+  if (ascii_only && fold_ok && img <= kFastImgMax && (size_t)(S - 1) * kRowU16 < 65536) {
     ac.fast.assign(img, 0);
     for (int st = 0; st < S; ++st) {
       uint16_t* row = reinterpret_cast<uint16_t*>(ac.fast.data() + (size_t)st * kFastRowBytes);
-      for (int v = 0; v < 128; ++v) row[v] = (uint16_t)(go[st][col_cls[v]] * kRowU16);
+      for (uint32_t v = 0; v < kFastCols; ++v) row[v] = (uint16_t)(go[st][col_cls[v]] * kRowU16);
     }
     ac.fast_out_entry = (uint32_t)first_out * kRowU16;
   }
@@ -409,6 +410,15 @@ int tsg_ruleset_rule_literal(const tsg_ruleset* rs, size_t i, size_t k, char* lo
   if (cap < L.lower.size()) return TSG_ERR_INVALID_ARG;
   if (lower) memcpy(lower, L.lower.data(), L.lower.size());
   if (req) memcpy(req, L.req.data(), L.req.size());
+  return TSG_OK;
+}
+
+// Program size of rule i's regex (diagnostics: VM scratch sizing).
+int tsg_ruleset_rule_prog(const tsg_ruleset* rs, size_t i, uint32_t* n_inst, uint32_t* n_cap) {
+  if (!rs || i >= rs->rules.size()) return TSG_ERR_INVALID_ARG;
+  const RuleHost& r = rs->rules[i];
+  if (n_inst) *n_inst = r.regex >= 0 ? (uint32_t)rs->regexes[r.regex].c.prog.inst.size() : 0;
+  if (n_cap) *n_cap = r.regex >= 0 ? (uint32_t)rs->regexes[r.regex].c.prog.ncap : 0;
   return TSG_OK;
 }
 
