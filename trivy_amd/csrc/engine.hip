@@ -27,6 +27,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -870,6 +871,12 @@ struct GateParams {
   uint32_t rule_words;
   uint8_t* scratch;
   uint64_t scratch_stride;
+  // path literal automaton (PathAcHost): null => every path prog runs its VM
+  const uint8_t* pac;
+  uint32_t pac_states, pac_classes, pac_bytes;
+  uint32_t o_pac_cls, o_pac_out_off, o_pac_out, o_pac_lits, o_pac_req, o_pac_bit;
+  uint64_t pac_always;  // path progs without a literal filter
+  uint32_t n_progs;
 };
 
 __device__ inline gre::VmScratch make_scratch(uint8_t* base, const RuleSetDev& rs) {
@@ -938,16 +945,69 @@ __device__ inline bool match_string_pf(const RuleSetDev& rs, uint32_t prog, cons
   return may_match(rs, prog, s, n) && match_string(rs.progs[prog], s, n, sc);
 }
 
+// Path gates (Global.AllowPath / Rule.MatchPath / Rule.AllowPath,
+// scanner.go:375,391,397): one lane per file walks its path once through an
+// Aho-Corasick automaton over every path regex's anchor literals (LDS), and
+// only the regexes whose literal was seen (or that have none, or any path
+// with a byte >= 0x80) run the Pike VM.
+struct PacLit {
+  uint32_t bit;      // path-prog bit
+  uint32_t len;
+  uint32_t req_off;  // case requirement bytes (0 = either case)
+};
+
 __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
+  __shared__ __align__(16) uint8_t pl[16384];
+  const bool lds = G.pac && G.pac_bytes <= sizeof(pl);
+  if (lds) {
+    for (uint32_t i = threadIdx.x; i < G.pac_bytes / 4; i += blockDim.x) ((uint32_t*)pl)[i] = ((const uint32_t*)G.pac)[i];
+    __syncthreads();
+  }
+  const uint8_t* A = lds ? pl : G.pac;
+  const uint16_t* delta = (const uint16_t*)A;
+  const uint8_t* cls = A + G.o_pac_cls;
+  const uint32_t* out_off = (const uint32_t*)(A + G.o_pac_out_off);
+  const uint16_t* outs = (const uint16_t*)(A + G.o_pac_out);
+  const PacLit* lits = (const PacLit*)(A + G.o_pac_lits);
+  const uint8_t* req = A + G.o_pac_req;
+  const uint8_t* pbit = A + G.o_pac_bit;
   const uint32_t nthreads = gridDim.x * blockDim.x;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   gre::VmScratch sc = make_scratch(G.scratch + (uint64_t)t * G.scratch_stride, G.rs);
   for (uint32_t f = t; f < G.n_files; f += nthreads) {
     const uint8_t* path = G.paths + G.path_off[f];
     const uint32_t plen = (uint32_t)(G.path_off[f + 1] - G.path_off[f]);
+    uint64_t mask = ~0ull;
+    if (G.pac) {
+      mask = G.pac_always;
+      uint32_t st = 0;
+      bool hi = false;
+      for (uint32_t i = 0; i < plen; ++i) {
+        const uint8_t b = path[i];
+        hi |= b >= 0x80;
+        const uint32_t nx = delta[st * G.pac_classes + cls[b]];
+        st = nx & 0x7FFFu;
+        if (nx & 0x8000u) {
+          for (uint32_t o = out_off[st]; o < out_off[st + 1]; ++o) {
+            const PacLit L = lits[outs[o]];
+            bool ok = true;
+            for (uint32_t k = 0; k < L.len && ok; ++k) {
+              const uint8_t r = req[L.req_off + k];
+              ok = r == 0 || path[i + 1 - L.len + k] == r;
+            }
+            if (ok) mask |= 1ull << L.bit;
+          }
+        }
+      }
+      if (hi) mask = ~0ull;  // fold-special runes: no literal filter (as may_match)
+    }
+    auto may = [&](uint32_t prog) {
+      const uint32_t b = prog < G.n_progs ? pbit[prog] : 0xFFu;
+      return b == 0xFFu || ((mask >> b) & 1);
+    };
     bool allowed = false;
     for (uint32_t k = 0; k < G.n_gpath && !allowed; ++k)
-      allowed = match_string_pf(G.rs, G.gpath[k], path, plen, sc);
+      allowed = may(G.gpath[k]) && match_string(G.rs.progs[G.gpath[k]], path, plen, sc);
     if (allowed) {
       G.file_flags[f] |= kFileAllowed;
       continue;
@@ -955,9 +1015,12 @@ __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
     if (!G.any_rule_paths) continue;
     for (uint32_t r = 0; r < G.rs.n_rules; ++r) {
       bool skip = false;
-      if (G.rule_path[r] >= 0) skip = !match_string_pf(G.rs, (uint32_t)G.rule_path[r], path, plen, sc);
+      if (G.rule_path[r] >= 0) {
+        const uint32_t pp = (uint32_t)G.rule_path[r];
+        skip = !(may(pp) && match_string(G.rs.progs[pp], path, plen, sc));
+      }
       for (uint32_t k = G.rule_apath_off[r]; k < G.rule_apath_off[r + 1] && !skip; ++k)
-        skip = match_string_pf(G.rs, G.rule_apath[k], path, plen, sc);
+        skip = may(G.rule_apath[k]) && match_string(G.rs.progs[G.rule_apath[k]], path, plen, sc);
       if (skip) G.path_mask[(size_t)f * G.rule_words + (r >> 5)] |= 1u << (r & 31);
     }
   }
@@ -1467,6 +1530,10 @@ struct DevImage {
   DBuf<uint8_t> prog_lits;
   DBuf<uint16_t> follow_delta;
   DBuf<uint8_t> follow_cls;
+  DBuf<uint8_t> pac;  // path literal automaton blob (k_path_gate)
+  uint32_t pac_states = 0, pac_classes = 0, pac_bytes = 0;
+  uint32_t o_pac_cls = 0, o_pac_out_off = 0, o_pac_out = 0, o_pac_lits = 0, o_pac_req = 0, o_pac_bit = 0;
+  uint64_t pac_always = 0;
   RuleSetDev view{};
   // offsets into u32
   uint32_t o_gpath = 0, n_gpath = 0, o_apoff = 0, o_ap = 0, o_full = 0, n_full = 0;
@@ -1474,7 +1541,7 @@ struct DevImage {
     inst.release(); classes.release(); ranges.release(); progs.release(); rules.release();
     u32.release(); rule_path.release(); delta.release(); cls.release(); out_off.release();
     out_pat.release(); pats.release(); pat_bytes.release(); pat_rules.release(); fast.release();
-    prog_lit_off.release(); prog_lits.release(); follow_delta.release(); follow_cls.release();
+    prog_lit_off.release(); prog_lits.release(); follow_delta.release(); follow_cls.release(); pac.release();
   }
 };
 
@@ -1718,6 +1785,128 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   HIP_TRY(im.pat_rules.ensure(prules.size() + 1));
   if (!prules.empty())
     HIP_TRY(hipMemcpy(im.pat_rules.p, prules.data(), prules.size() * 4, hipMemcpyHostToDevice));
+  // ---- path literal automaton (k_path_gate)
+  im.pac_bytes = 0;
+  {
+    std::vector<uint32_t> pprogs(rs->global_allow_path.begin(), rs->global_allow_path.end());
+    for (auto& r : rs->rules) {
+      if (r.path >= 0) pprogs.push_back((uint32_t)r.path);
+      for (int x : r.allow_path) pprogs.push_back((uint32_t)x);
+    }
+    std::sort(pprogs.begin(), pprogs.end());
+    pprogs.erase(std::unique(pprogs.begin(), pprogs.end()), pprogs.end());
+    if (!pprogs.empty() && pprogs.size() <= 64) {
+      std::vector<uint8_t> bit(rs->regexes.size(), 0xFF);
+      uint64_t always = 0;
+      std::vector<std::string> lit_lower, lit_req;
+      std::vector<uint32_t> lit_bit;
+      for (size_t i = 0; i < pprogs.size(); ++i) {
+        bit[pprogs[i]] = (uint8_t)i;
+        const gre::Anchor& a = rs->regexes[pprogs[i]].c.anchor;
+        bool ascii = a.valid && a.lits.size() <= 32;
+        for (auto& l : a.lits)
+          for (unsigned char c : l.lower) ascii &= c < 0x80 && c != 0;
+        if (!ascii) {
+          always |= 1ull << i;
+          continue;
+        }
+        for (auto& l : a.lits) {
+          lit_lower.push_back(l.lower);
+          lit_req.push_back(l.req);
+          lit_bit.push_back((uint32_t)i);
+        }
+      }
+      // trie over lowercased literals; classes: literal bytes, 'A'-'Z' share lower case
+      int cmap[256] = {0};
+      int K = 1;
+      for (auto& l : lit_lower)
+        for (unsigned char c : l)
+          if (!cmap[c]) cmap[c] = K++;
+      for (int b = 'A'; b <= 'Z'; ++b) cmap[b] = cmap[b + 32];
+      std::vector<std::vector<int>> go(1, std::vector<int>(K, -1));
+      std::vector<std::vector<uint16_t>> term(1);
+      for (size_t li = 0; li < lit_lower.size(); ++li) {
+        int st = 0;
+        for (unsigned char c : lit_lower[li]) {
+          const int k = cmap[c];
+          if (go[st][k] < 0) {
+            go[st][k] = (int)go.size();
+            go.emplace_back(K, -1);
+            term.emplace_back();
+          }
+          st = go[st][k];
+        }
+        term[st].push_back((uint16_t)li);
+      }
+      const int S = (int)go.size();
+      std::vector<int> fail(S, 0);
+      std::vector<std::vector<uint16_t>> outs(S);
+      std::deque<int> q;
+      for (int k = 0; k < K; ++k) {
+        if (go[0][k] < 0) go[0][k] = 0;
+        else q.push_back(go[0][k]);
+      }
+      while (!q.empty()) {
+        const int st = q.front();
+        q.pop_front();
+        outs[st] = term[st];
+        for (auto x : outs[fail[st]]) outs[st].push_back(x);
+        for (int k = 0; k < K; ++k) {
+          const int t2 = go[st][k];
+          if (t2 >= 0) {
+            fail[t2] = go[fail[st]][k];
+            q.push_back(t2);
+          } else {
+            go[st][k] = go[fail[st]][k];
+          }
+        }
+      }
+      if (S < 32768 && lit_lower.size() < 65536) {
+        std::vector<uint8_t> blob;
+        auto put = [&](const void* p, size_t n) {
+          blob.resize((blob.size() + 15) & ~(size_t)15);
+          const uint32_t o = (uint32_t)blob.size();
+          blob.insert(blob.end(), (const uint8_t*)p, (const uint8_t*)p + n);
+          return o;
+        };
+        std::vector<uint16_t> delta((size_t)S * K);
+        for (int st = 0; st < S; ++st)
+          for (int k = 0; k < K; ++k) {
+            const int t2 = go[st][k];
+            delta[(size_t)st * K + k] = (uint16_t)(t2 | (outs[t2].empty() ? 0 : 0x8000));
+          }
+        put(delta.data(), delta.size() * 2);
+        uint8_t cl[256];
+        for (int b = 0; b < 256; ++b) cl[b] = (uint8_t)cmap[b];
+        im.o_pac_cls = put(cl, 256);
+        std::vector<uint32_t> ooff(S + 1, 0);
+        std::vector<uint16_t> oo;
+        for (int st = 0; st < S; ++st) {
+          ooff[st] = (uint32_t)oo.size();
+          oo.insert(oo.end(), outs[st].begin(), outs[st].end());
+        }
+        ooff[S] = (uint32_t)oo.size();
+        im.o_pac_out_off = put(ooff.data(), ooff.size() * 4);
+        im.o_pac_out = put(oo.data(), oo.size() * 2 + 2);
+        std::vector<uint8_t> reqb;
+        std::vector<PacLit> pls;
+        for (size_t li = 0; li < lit_lower.size(); ++li) {
+          pls.push_back(PacLit{lit_bit[li], (uint32_t)lit_lower[li].size(), (uint32_t)reqb.size()});
+          reqb.insert(reqb.end(), lit_req[li].begin(), lit_req[li].end());
+        }
+        im.o_pac_lits = put(pls.data(), pls.size() * sizeof(PacLit) + 4);
+        im.o_pac_req = put(reqb.data(), reqb.size() + 1);
+        im.o_pac_bit = put(bit.data(), bit.size());
+        blob.resize((blob.size() + 15) & ~(size_t)15);
+        HIP_TRY(im.pac.ensure(blob.size()));
+        HIP_TRY(hipMemcpy(im.pac.p, blob.data(), blob.size(), hipMemcpyHostToDevice));
+        im.pac_bytes = (uint32_t)blob.size();
+        im.pac_states = (uint32_t)S;
+        im.pac_classes = (uint32_t)K;
+        im.pac_always = always;
+      }
+    }
+  }
   // ---- view
   RuleSetDev& v = im.view;
   v.follow_delta = im.follow_delta.p;
@@ -1956,6 +2145,18 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     G.rule_words = rule_words;
     G.scratch = e->scratch.p;
     G.scratch_stride = e->scratch_stride;
+    G.pac = im.pac_bytes ? im.pac.p : nullptr;
+    G.pac_states = im.pac_states;
+    G.pac_classes = im.pac_classes;
+    G.pac_bytes = im.pac_bytes;
+    G.o_pac_cls = im.o_pac_cls;
+    G.o_pac_out_off = im.o_pac_out_off;
+    G.o_pac_out = im.o_pac_out;
+    G.o_pac_lits = im.o_pac_lits;
+    G.o_pac_req = im.o_pac_req;
+    G.o_pac_bit = im.o_pac_bit;
+    G.pac_always = im.pac_always;
+    G.n_progs = (uint32_t)rs->regexes.size();
     uint32_t blocks = std::min<uint32_t>((nf + 255) / 256, e->vm_threads / 256);
     hipLaunchKernelGGL(k_path_gate, dim3(std::max(1u, blocks)), dim3(256), 0, s, G);
     HIP_TRY(hipGetLastError());
