@@ -130,6 +130,12 @@ int tsg_ruleset_rule_prog(const tsg_ruleset* rs, size_t i, uint32_t* n_inst, uin
 int tsg_ruleset_follow_check(const tsg_ruleset* rs, size_t i, const uint8_t* text, size_t len, size_t h,
                              int* accept, uint32_t* n_states);
 
+/* Verify DFA of rule i, anchored at s on host text: *result = 1 (match
+ * [s, *me)), 0 (none) or 2 (undecidable by the DFA: the Pike VM decides);
+ * *n_states = its size (0 = the rule always uses the VM). */
+int tsg_ruleset_dfa_check(const tsg_ruleset* rs, size_t i, const uint8_t* text, size_t len, size_t s,
+                          int* result, size_t* me, uint32_t* n_states);
+
 /* Automaton diagnostics: states/classes of the keyword+anchor automaton and
  * whether it fits k_scan_fast's LDS image (fast_path = 1). */
 int tsg_ruleset_stats(const tsg_ruleset* rs, uint32_t* n_states, uint32_t* n_classes, uint32_t* n_patterns,

@@ -1,0 +1,85 @@
+"""Verify-DFA exactness (dfa.cpp, the host build of the tables k_verify walks):
+Go's FindAllIndex rebuilt from the anchored leftmost-first DFA (leftmost
+start = first start position with a match, end = the DFA's match end) must
+equal the host Go-semantics Pike VM's FindAllIndex on ASCII text, for every
+builtin rule and a few hand-picked priority/assertion patterns.  CPU only."""
+import ctypes
+import os
+import random
+
+import pytest
+
+from trivy_amd import _native as N
+import trivy_amd.secret as S
+
+from . import corpus_gen
+from .conftest import GOLDEN
+
+
+def _dfa_find_all(rs, i, t):
+    res, me, ns = ctypes.c_int(), ctypes.c_size_t(), ctypes.c_uint32()
+    out, pos, n = [], 0, len(t)
+    while pos < n:
+        hit = None
+        for s in range(pos, n):
+            N.check(N.lib.tsg_ruleset_dfa_check(rs, i, t, n, s, ctypes.byref(res), ctypes.byref(me), ctypes.byref(ns)))
+            assert res.value != 2, "ASCII text must be decidable"
+            if res.value == 1:
+                hit = (s, me.value)
+                break
+        if hit is None:
+            break
+        assert hit[1] > hit[0], "anchored builtin rules never match empty"
+        out.append(list(hit))
+        pos = hit[1]
+    return out
+
+
+def _ascii_texts():
+    rng = random.Random(5)
+    tpl = corpus_gen.secret_instances(rng)
+    texts = [d for _, d in corpus_gen.make_corpus(3, 40) if max(d, default=0) < 0x80]
+    texts += [open(os.path.join(GOLDEN, "secret_testdata", c), "rb").read()
+              for c in sorted(os.listdir(os.path.join(GOLDEN, "secret_testdata"))) if not c.endswith(".yaml")]
+    texts = [t for t in texts if max(t, default=0) < 0x80 and len(t) < 6000]
+    for _ in range(60):
+        parts = [tpl[rng.randrange(len(tpl))]() for _ in range(5)]
+        t = rng.choice(["", " ", "\n", "'", "=", "\t\n  "]).join(parts).encode()
+        if max(t, default=0) < 0x80:
+            texts.append(t)
+    return texts
+
+
+def test_verify_dfa_equals_vm_on_builtin_rules():
+    sc = S.new_scanner(None)
+    rs = sc._rs.handle
+    res, me, ns = ctypes.c_int(), ctypes.c_size_t(), ctypes.c_uint32()
+    texts = _ascii_texts()
+    total = 0
+    for i, r in enumerate(sc.rules):
+        N.check(N.lib.tsg_ruleset_dfa_check(rs, i, b"x", 1, 0, ctypes.byref(res), ctypes.byref(me), ctypes.byref(ns)))
+        if ns.value == 0:
+            continue
+        for t in texts:
+            want = N.regex_find_all(r.regex, t)
+            if not want and r.keywords and not any(k.lower().encode() in t.lower() for k in r.keywords):
+                continue  # keep the O(n^2) reference walk to texts that matter
+            assert _dfa_find_all(rs, i, t) == want, (r.id, t[:120])
+            total += len(want)
+    assert total > 200
+
+
+@pytest.mark.parametrize("pat,text", [
+    (r"(a|ab)(c|bcd)(d*)", b"abcd xabcdd"), (r"x*?y", b"xxy xy"), (r"a+?", b"aaa"), (r"(?U)a+", b"aaa b"),
+    (r"^abc", b"abc abc"), (r"abc$", b"abc abc"), (r"(^|\s+)k(\s+|$)", b"k  k \n k"), (r"a{2,3}", b"aaaaaaa"),
+    (r"(?i)key[a-z]{0,3}=", b"KEYab= keyabcd="), (r"([^0-9A-Za-z]|^)(LTAI)(?i)[a-z0-9]{4}([^0-9A-Za-z]|$)", b"LTAIabcd xLTAI1234 LTAIzzzz"),
+])
+def test_verify_dfa_priorities(pat, text):
+    rules = [S.Rule(id="t", category="c", title="t", severity="HIGH", regex=pat, keywords=[])]
+    sc = S.Scanner(rules, [], S.ExcludeBlock())
+    rs = sc._rs.handle
+    res, me, ns = ctypes.c_int(), ctypes.c_size_t(), ctypes.c_uint32()
+    N.check(N.lib.tsg_ruleset_dfa_check(rs, 0, b"x", 1, 0, ctypes.byref(res), ctypes.byref(me), ctypes.byref(ns)))
+    if ns.value == 0:
+        pytest.skip("no DFA for this pattern (VM path)")
+    assert _dfa_find_all(rs, 0, text) == N.regex_find_all(pat, text)

@@ -22,6 +22,7 @@ constexpr uint32_t kFastSpecialEv = 0xFFFF;   // event tag: U+0130/U+017F/U+212A
 constexpr uint32_t kFollowMaxStates = 1024;  // follow-DFA subset-construction budget
 constexpr uint32_t kFollowDepth = 96;        // bytes a candidate filter reads past the hit
 constexpr uint32_t kNoFollow = 0xFFFFFFFFu;
+constexpr uint32_t kDfaMaxStates = 4096;     // verify-DFA budget per rule (else the Pike VM)
 
 enum RuleMode : uint8_t { MODE_NEVER = 0, MODE_ANCHORED = 1, MODE_FULL = 2 };
 
@@ -42,6 +43,9 @@ struct RuleDev {
   uint32_t follow_cls_off;
   uint32_t gate_implied;        // every anchor literal contains a keyword: on files without fold-special
                                 // bytes a match implies the MatchKeywords gate (scanner.go:169-181)
+  uint32_t dfa_off;             // verify DFA (dfa.cpp): first u16 of its table (kNoFollow = none)
+  uint32_t dfa_ncls, dfa_cls_off, dfa_match_off;
+  uint32_t dfa_start0, dfa_start1;  // start state at s > 0 / s == 0 (BeginText)
 };
 
 struct PatDev {
@@ -79,6 +83,8 @@ constexpr uint32_t kLitRec = 36;  // prefilter literal record: len, lower[16], r
 struct RuleSetDev {
   const uint16_t* follow_delta;  // all rules' candidate-filter tables (follow.cpp)
   const uint8_t* follow_cls;
+  const uint16_t* dfa_delta;     // all rules' verify DFAs (dfa.cpp)
+  const uint8_t* dfa_bytes;      // their class maps and match flags
   const gre::ProgView* progs;
   const uint32_t* prog_lit_off;  // per program: range of prefilter literals (n_progs + 1)
   const uint8_t* prog_lits;      // kLitRec-byte records
@@ -110,6 +116,20 @@ struct FollowDfa {
   std::vector<uint16_t> delta;  // [nstates][ncls]
 };
 bool build_follow(const gre::Compiled& c, FollowDfa* out);
+
+// Anchored leftmost-first DFA over ASCII for k_verify (dfa.cpp): state 0 =
+// dead; entry = next state | 0x8000 when that byte, as the text's last,
+// completes a match ($ satisfied); match[state] = a match ends here.
+struct DfaHost {
+  bool valid = false;
+  uint32_t ncls = 0, nstates = 0;
+  uint32_t start[2] = {0, 0};
+  uint8_t cls[128] = {};
+  std::vector<uint16_t> delta;
+  std::vector<uint8_t> match;
+};
+bool build_dfa(const gre::Compiled& c, DfaHost* out);
+int dfa_anchored(const DfaHost& d, const uint8_t* text, size_t n, size_t s, size_t* me);
 bool follow_accepts(const FollowDfa& f, const uint8_t* text, size_t n, size_t h);
 
 struct RuleHost {
@@ -123,6 +143,7 @@ struct RuleHost {
   std::vector<int> exclude;
   RuleMode mode = MODE_NEVER;
   FollowDfa follow;  // MODE_ANCHORED only
+  DfaHost dfa;       // MODE_ANCHORED only
 };
 
 struct AcHost {

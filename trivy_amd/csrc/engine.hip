@@ -1297,9 +1297,121 @@ __device__ bool vm_search_starts(const gre::ProgView& p, const uint8_t* text, ui
   return matched;
 }
 
+// Anchored leftmost-first DFA walk from s (dfa.cpp): 1 = match [s, *me),
+// 0 = none, 2 = undecidable here (byte >= 0x80) -> the Pike VM decides.
+__device__ inline int dfa_anchored_dev(const RuleSetDev& rs, const RuleDev& rd, const uint8_t* text, uint32_t n,
+                                       uint32_t s, uint32_t* me) {
+  const uint16_t* T = rs.dfa_delta + rd.dfa_off;
+  const uint8_t* cls = rs.dfa_bytes + rd.dfa_cls_off;
+  const uint8_t* mt = rs.dfa_bytes + rd.dfa_match_off;
+  const uint32_t K = rd.dfa_ncls;
+  uint32_t st = s == 0 ? rd.dfa_start1 : rd.dfa_start0;
+  int64_t last = mt[st] ? (int64_t)s : -1;
+  for (uint32_t q = s; q < n && st; ++q) {
+    const uint8_t c = text[q];
+    if (c >= 0x80) return 2;
+    const uint32_t e = T[st * K + cls[c]];
+    if (q + 1 == n) {
+      if (e & 0x8000u) last = n;
+      break;
+    }
+    st = e & 0x7FFFu;
+    if (st && mt[st]) last = q + 1;
+  }
+  if (last < 0) return 0;
+  *me = (uint32_t)last;
+  return 1;
+}
+
+// Bit-state backtracker (go1.22 regexp/backtrack.go semantics: depth-first in
+// priority order, each (pc, pos) visited once, so the first MATCH reached is
+// the leftmost-first match and its captures are Go's) for the secret-group
+// spans of a match [ms, me) the DFA or VM already found.  Visited bits, job
+// stack and the tracked capture slots live in the lane's LDS arena; only the
+// SecretGroupName slots are tracked (captures never steer the search).
+// Returns false when the match does not fit the arena (the caller then runs
+// the Pike capture VM) — never a different answer.
+constexpr uint32_t kVerifyThreads = 64;
+constexpr uint32_t kBsWords = 560;  // LDS words per lane: 140 KiB per block
+
+__device__ bool bitstate_captures(const gre::ProgView& p, const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me,
+                                  const uint32_t* gnum, uint32_t ng, uint32_t* area, int32_t* gcap) {
+  const uint32_t P = p.ninst;
+  const uint32_t end = me + 16 < n ? me + 16 : n;  // positions the search may visit: [ms, end]
+  const uint32_t W = end - ms + 1;
+  const uint32_t vis_words = (P * W + 31) / 32;
+  if (2 * ng > 8 || P >= 0x4000 || W >= 0xFFFF || vis_words + 32 > kBsWords) return false;
+  uint32_t* vis = area;
+  uint32_t* stk = area + vis_words;
+  const uint32_t stk_cap = kBsWords - vis_words;
+  for (uint32_t i = 0; i < vis_words; ++i) vis[i] = 0;
+  for (uint32_t k = 0; k < 2 * ng; ++k) gcap[k] = -1;
+  auto local = [&](uint32_t slot) -> int {  // tracked index of capture slot, or -1
+    for (uint32_t g = 0; g < ng; ++g)
+      if (slot == 2 * gnum[g] || slot == 2 * gnum[g] + 1) return (int)(2 * g + (slot & 1));
+    return -1;
+  };
+  uint32_t sp = 0;
+  stk[sp++] = (p.start << 16);
+  while (sp) {
+    const uint32_t j = stk[--sp];
+    const uint32_t kind = j >> 30, pc0 = (j >> 16) & 0x3FFFu, v = j & 0xFFFFu;
+    if (kind == 2) {  // capture restore
+      const int l = local(p.inst[pc0].arg);
+      if (l >= 0) gcap[l] = v == 0xFFFFu ? -1 : (int32_t)(ms + v);
+      continue;
+    }
+    uint32_t pos = ms + v;
+    uint32_t pc = kind == 1 ? p.inst[pc0].arg : pc0;  // ALT: the second branch
+    for (;;) {
+      if (pc == 0) break;
+      if (pos > end) return false;
+      const uint32_t bit = pc * W + (pos - ms);
+      if (vis[bit >> 5] & (1u << (bit & 31))) break;
+      vis[bit >> 5] |= 1u << (bit & 31);
+      const gre::Inst in = p.inst[pc];
+      if (in.op == gre::I_ALT) {
+        if (sp >= stk_cap) return false;
+        stk[sp++] = (1u << 30) | (pc << 16) | (pos - ms);
+        pc = in.out;
+        continue;
+      }
+      if (in.op == gre::I_CAP) {
+        const int l = local(in.arg);
+        if (l >= 0) {
+          if (sp >= stk_cap) return false;
+          const int32_t old = gcap[l];
+          stk[sp++] = (2u << 30) | (pc << 16) | (old < 0 ? 0xFFFFu : (uint32_t)(old - (int32_t)ms));
+          gcap[l] = (int32_t)pos;
+        }
+        pc = in.out;
+        continue;
+      }
+      if (in.op == gre::I_EMPTY) {
+        uint32_t w;
+        const int r = gre::decode_rune(text, n, pos, &w);
+        if ((in.empty & ~gre::empty_ctx(gre::prev_ctx_rune(text, pos), r)) != 0) break;
+        pc = in.out;
+        continue;
+      }
+      if (in.op == gre::I_NOP) {
+        pc = in.out;
+        continue;
+      }
+      if (in.op == gre::I_MATCH) return pos == me;
+      uint32_t w;
+      const int r = gre::decode_rune(text, n, pos, &w);
+      if (!gre::inst_consumes(in, p, r)) break;
+      pos += w;
+      pc = in.out;
+    }
+  }
+  return false;
+}
+
 __device__ void emit_match(const VerifyParams& V, const RuleDev& rd, uint32_t rule, uint32_t fi,
                            const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me,
-                           gre::VmScratch& sc) {
+                           gre::VmScratch& sc, uint32_t* bs_area) {
   // AllowLocation (scanner.go:145-148): global then rule allow regexes on the whole match
   for (uint32_t k = 0; k < V.rs.n_global_allow; ++k)
     if (match_string_pf(V.rs, V.rs.global_allow[k], text + ms, me - ms, sc)) return;
@@ -1311,11 +1423,24 @@ __device__ void emit_match(const VerifyParams& V, const RuleDev& rd, uint32_t ru
     return;
   }
   const gre::ProgView& pv = V.rs.progs[rd.prog];
+  const uint32_t* gnum = V.rs.group_slots + rd.group_off;
+  int32_t* gcap = (int32_t*)(bs_area + kBsWords - 8);  // tracked slots (the arena's last 8 words)
+  if (bitstate_captures(pv, text, n, ms, me, gnum, rd.group_n, bs_area, gcap)) {
+    for (uint32_t g = 0; g < rd.group_n; ++g) {
+      const int32_t s = gcap[2 * g], e = gcap[2 * g + 1];
+      unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
+      if (idx < V.loc_cap) {
+        if (s < 0 || e < 0) V.locs[idx] = DevLoc{fi, rule, 0, 0, 0, 0, 1, 0};
+        else V.locs[idx] = DevLoc{fi, rule, (uint64_t)s, (uint64_t)e, 0, 0, 0, 0};
+      }
+    }
+    return;
+  }
   int32_t out[kMaxCap];  // ncap <= kMaxCap is enforced by the rule compiler
   bool ok = gre::vm_captures(pv, text, n, ms, sc, out);
   if (!ok || (uint32_t)out[1] != me) atomicOr(&V.ctrl->err, 1u);
   for (uint32_t g = 0; g < rd.group_n; ++g) {
-    const uint32_t slot = V.rs.group_slots[rd.group_off + g];
+    const uint32_t slot = gnum[g];
     const int32_t s = out[2 * slot], e = out[2 * slot + 1];
     unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
     if (idx < V.loc_cap) {
@@ -1325,7 +1450,9 @@ __device__ void emit_match(const VerifyParams& V, const RuleDev& rd, uint32_t ru
   }
 }
 
-__global__ __launch_bounds__(256) void k_verify(VerifyParams V) {
+__global__ __launch_bounds__(kVerifyThreads) void k_verify(VerifyParams V) {
+  __shared__ uint32_t bs_lds[kVerifyThreads * kBsWords];
+  uint32_t* bs_area = bs_lds + threadIdx.x * kBsWords;
   const uint32_t nthreads = gridDim.x * blockDim.x;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   gre::VmScratch sc = make_scratch(V.scratch + (uint64_t)t * V.scratch_stride, V.rs);
@@ -1371,7 +1498,7 @@ __global__ __launch_bounds__(256) void k_verify(VerifyParams V) {
           pos = me;
         }
         prev_end = me;
-        if (accept) emit_match(V, rd, rule, fi, text, n, ms, me, sc);
+        if (accept) emit_match(V, rd, rule, fi, text, n, ms, me, sc, bs_area);
       }
     } else {
       IvIter it;
@@ -1388,9 +1515,37 @@ __global__ __launch_bounds__(256) void k_verify(VerifyParams V) {
       it.h_prev = it.p_prev = 0;
       it.advance();
       uint32_t pos = 0;
+      if (rd.dfa_off != kNoFollow) {
+        // FindAll over the permitted starts with the verify DFA: the first
+        // start (>= pos) that matches is Go's leftmost match; a byte >= 0x80
+        // hands the rest of the job to the Pike VM below
+        bool vm = false;
+        while (it.have && !vm) {
+          bool found = false;
+          uint32_t s0 = it.cs > pos ? it.cs : pos;
+          for (uint32_t sp = s0; sp <= it.ce && sp < n; ++sp) {
+            if (!gre::is_rune_start(text, n, sp)) continue;
+            const int r = dfa_anchored_dev(V.rs, rd, text, n, sp, &me);
+            if (r == 2) {
+              vm = true;
+              break;
+            }
+            if (r == 1) {
+              emit_match(V, rd, rule, fi, text, n, sp, me, sc, bs_area);
+              pos = me;
+              found = true;
+              break;
+            }
+          }
+          if (vm) break;
+          if (!found) it.advance();
+          else while (it.have && it.ce < pos) it.advance();
+        }
+        if (!vm) continue;
+      }
       while (it.have) {
         if (!vm_search_starts(pv, text, n, pos, it, sc, &ms, &me)) break;
-        emit_match(V, rd, rule, fi, text, n, ms, me, sc);
+        emit_match(V, rd, rule, fi, text, n, ms, me, sc, bs_area);
         if (me == ms) break;  // cannot happen for anchored rules (non-empty literal)
         pos = me;
       }
@@ -1531,6 +1686,8 @@ struct DevImage {
   DBuf<uint16_t> follow_delta;
   DBuf<uint8_t> follow_cls;
   DBuf<uint8_t> pac;  // path literal automaton blob (k_path_gate)
+  DBuf<uint16_t> dfa_delta;
+  DBuf<uint8_t> dfa_bytes;
   uint32_t pac_states = 0, pac_classes = 0, pac_bytes = 0;
   uint32_t o_pac_cls = 0, o_pac_out_off = 0, o_pac_out = 0, o_pac_lits = 0, o_pac_req = 0, o_pac_bit = 0;
   uint64_t pac_always = 0;
@@ -1541,7 +1698,7 @@ struct DevImage {
     inst.release(); classes.release(); ranges.release(); progs.release(); rules.release();
     u32.release(); rule_path.release(); delta.release(); cls.release(); out_off.release();
     out_pat.release(); pats.release(); pat_bytes.release(); pat_rules.release(); fast.release();
-    prog_lit_off.release(); prog_lits.release(); follow_delta.release(); follow_cls.release(); pac.release();
+    prog_lit_off.release(); prog_lits.release(); follow_delta.release(); follow_cls.release(); pac.release(); dfa_delta.release(); dfa_bytes.release();
   }
 };
 
@@ -1657,13 +1814,25 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   std::map<std::string, uint32_t> kwid;
   for (size_t k = 0; k < rs->keywords.size(); ++k) kwid[rs->keywords[k]] = (uint32_t)k;
   std::vector<uint32_t> kw_ids, group_slots, allow_progs, apath_off, apath, full_rules;
-  std::vector<uint16_t> fdelta;
-  std::vector<uint8_t> fcls;
+  std::vector<uint16_t> fdelta, ddelta;
+  std::vector<uint8_t> fcls, dbytes;
   std::set<uint32_t> kw_needed_ids;
   for (size_t ri = 0; ri < rs->rules.size(); ++ri) {
     const RuleHost& r = rs->rules[ri];
     RuleDev d{};
     d.follow_off = kNoFollow;
+    d.dfa_off = kNoFollow;
+    if (r.dfa.valid) {
+      d.dfa_off = (uint32_t)ddelta.size();
+      d.dfa_ncls = r.dfa.ncls;
+      d.dfa_cls_off = (uint32_t)dbytes.size();
+      dbytes.insert(dbytes.end(), r.dfa.cls, r.dfa.cls + 128);
+      d.dfa_match_off = (uint32_t)dbytes.size();
+      dbytes.insert(dbytes.end(), r.dfa.match.begin(), r.dfa.match.end());
+      d.dfa_start0 = r.dfa.start[0];
+      d.dfa_start1 = r.dfa.start[1];
+      ddelta.insert(ddelta.end(), r.dfa.delta.begin(), r.dfa.delta.end());
+    }
     if (r.follow.valid) {
       d.follow_off = (uint32_t)fdelta.size();
       d.follow_ncls = r.follow.ncls;
@@ -1742,6 +1911,11 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   HIP_TRY(im.follow_delta.ensure(fdelta.size() + 1));
   if (!fdelta.empty())
     HIP_TRY(hipMemcpy(im.follow_delta.p, fdelta.data(), fdelta.size() * 2, hipMemcpyHostToDevice));
+  HIP_TRY(im.dfa_delta.ensure(ddelta.size() + 1));
+  if (!ddelta.empty())
+    HIP_TRY(hipMemcpy(im.dfa_delta.p, ddelta.data(), ddelta.size() * 2, hipMemcpyHostToDevice));
+  HIP_TRY(im.dfa_bytes.ensure(dbytes.size() + 1));
+  if (!dbytes.empty()) HIP_TRY(hipMemcpy(im.dfa_bytes.p, dbytes.data(), dbytes.size(), hipMemcpyHostToDevice));
   HIP_TRY(im.follow_cls.ensure(fcls.size() + 1));
   if (!fcls.empty()) HIP_TRY(hipMemcpy(im.follow_cls.p, fcls.data(), fcls.size(), hipMemcpyHostToDevice));
   HIP_TRY(im.rule_path.ensure(rule_path.size() + 1));
@@ -1911,6 +2085,8 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   RuleSetDev& v = im.view;
   v.follow_delta = im.follow_delta.p;
   v.follow_cls = im.follow_cls.p;
+  v.dfa_delta = im.dfa_delta.p;
+  v.dfa_bytes = im.dfa_bytes.p;
   v.progs = im.progs.p;
   v.prog_lit_off = im.prog_lit_off.p;
   v.prog_lits = im.prog_lits.p;
@@ -2297,8 +2473,11 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     const bool prof = getenv("TSG_PROFILE_VERIFY") != nullptr;
     if (prof) HIP_TRY(e->vprof.ensure(2ull * n_jobs));
     V.prof = prof ? e->vprof.p : nullptr;
-    uint32_t blocks = std::min<uint32_t>((n_jobs + 255) / 256, e->vm_threads / 256);
-    hipLaunchKernelGGL(k_verify, dim3(std::max(1u, blocks)), dim3(256), 0, s, V);
+    // one wave per block spreads the (latency-bound, divergent) lanes over
+    // every CU and its L1; each block's LDS holds its lanes' bit-state arenas
+    const uint32_t vb = kVerifyThreads;
+    uint32_t blocks = std::min<uint32_t>((n_jobs + vb - 1) / vb, e->vm_threads / vb);
+    hipLaunchKernelGGL(k_verify, dim3(std::max(1u, blocks)), dim3(vb), 0, s, V);
     if (prof) {
       std::vector<uint64_t> hp(2ull * n_jobs);
       HIP_TRY(hipMemcpyAsync(hp.data(), e->vprof.p, hp.size() * 8, hipMemcpyDeviceToHost, s));

@@ -331,7 +331,10 @@ int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_r
       // no group of that name => getMatchSubgroupsLocations yields nothing
       if (!has_group) r.mode = MODE_NEVER;
       else r.mode = c.anchor.valid ? MODE_ANCHORED : MODE_FULL;
-      if (r.mode == MODE_ANCHORED) build_follow(c, &r.follow);
+      if (r.mode == MODE_ANCHORED) {
+        build_follow(c, &r.follow);
+        build_dfa(c, &r.dfa);
+      }
     }
     for (auto& kw : r.keywords) {
       if (!kwid.count(kw) && !kw.empty()) {
@@ -419,6 +422,19 @@ int tsg_ruleset_rule_prog(const tsg_ruleset* rs, size_t i, uint32_t* n_inst, uin
   const RuleHost& r = rs->rules[i];
   if (n_inst) *n_inst = r.regex >= 0 ? (uint32_t)rs->regexes[r.regex].c.prog.inst.size() : 0;
   if (n_cap) *n_cap = r.regex >= 0 ? (uint32_t)rs->regexes[r.regex].c.prog.ncap : 0;
+  return TSG_OK;
+}
+
+// Verify DFA of rule i on host text: 1 = match [s, *me), 0 = none, 2 = not
+// decidable by the DFA (no DFA, byte >= 0x80, s at the end) -> Pike VM.
+int tsg_ruleset_dfa_check(const tsg_ruleset* rs, size_t i, const uint8_t* text, size_t len, size_t s,
+                          int* result, size_t* me, uint32_t* n_states) {
+  if (!rs || i >= rs->rules.size() || !result) return TSG_ERR_INVALID_ARG;
+  const DfaHost& d = rs->rules[i].dfa;
+  if (n_states) *n_states = d.valid ? d.nstates : 0;
+  size_t e = 0;
+  *result = dfa_anchored(d, text, len, s, &e);
+  if (me) *me = e;
   return TSG_OK;
 }
 
