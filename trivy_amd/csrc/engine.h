@@ -58,6 +58,10 @@ struct PatDev {
   uint8_t confirm;     // anchor roles need a case check
   uint8_t trunc;       // len > trie depth
   uint8_t kw_needed;   // some rule whose gate is not implied uses this keyword
+  // k_report's branch-free confirm of the first min(len, depth) bytes against
+  // the last 8 bytes (byte 7 = the pattern's last automaton byte)
+  uint64_t lo64, m64;    // lowered pattern bytes / their mask, top-aligned
+  uint64_t rq64, rqm64;  // case requirement bytes / their mask (0 = none)
 };
 
 struct AcDev {

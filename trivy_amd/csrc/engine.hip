@@ -643,8 +643,12 @@ __device__ inline uint32_t file_of_pos(const ScanParams& P, uint64_t pos) {
   return find_file(P.off, P.region_file[r], hi, pos);
 }
 
-// byte k (0 = oldest) of the last-8-bytes shift register
-__device__ inline uint32_t hist_byte(uint64_t h, uint32_t k) { return (uint32_t)(h >> (8 * k)) & 0xFFu; }
+// ASCII lowercase of 8 bytes at once (bytes 'A'-'Z' gain 0x20)
+__device__ inline uint64_t lower64(uint64_t x) {
+  const uint64_t t = x & 0x7F7F7F7F7F7F7F7Full;
+  const uint64_t up = ((t + 0x3F3F3F3F3F3F3F3Full) ^ (t + 0x2525252525252525ull)) & ~x & 0x8080808080808080ull;
+  return x | (up >> 2);
+}
 
 __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_t n_waves) {
   __shared__ __align__(16) uint8_t L[kReportLds];
@@ -682,85 +686,86 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
       seg = P.ev_overflow;
       n = P.ctrl->ev_overflow < P.ev_overflow_cap ? P.ctrl->ev_overflow : P.ev_overflow_cap;
     }
-    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
-      const FastEvent ev = seg[i];
-      uint64_t hist = ((uint64_t)ev.prev.y << 32) | ev.prev.x;  // the 8 raw bytes before (oldest low)
-      uint32_t e = ev.entry;
-      const uint32_t fx = fold6(ev.cur.x), fy = fold6(ev.cur.y);
-      uint32_t fi = 0xFFFFFFFFu;
-      for (int j = 0; j < 8; ++j) {
-        e = fstep(B, e, j < 4 ? fx : fy, j & 3);
-        const uint32_t c = ((j < 4 ? ev.cur.x : ev.cur.y) >> (8 * (j & 3))) & 0xFFu;
-        hist = (hist >> 8) | ((uint64_t)c << 56);  // hist byte 7 = c
-        if (e < out_e || c >= 0x80) continue;  // an output ending on a byte >= 0x80 is an alias
-        const uint64_t pos = ev.pos + j;
-        const uint32_t st = e / kFastRowU16;
-        for (uint32_t o = out_off[st]; o < out_off[st + 1]; ++o) {
-          const uint32_t pid = out_pat[o];
-          const PatDev pd = pats[pid];
-          const uint32_t tl = pd.len < ac.depth ? pd.len : ac.depth;
-          // confirm the automaton's prefix on the real bytes (hist bytes 8-tl .. 7)
-          const uint8_t* pb = pbytes + pd.bytes_off;
-          bool ok = true;
-          for (uint32_t k = 0; k < tl && ok; ++k) ok = lower_ascii((uint8_t)hist_byte(hist, 8 - tl + k)) == pb[k];
-          if (!ok) continue;
-          const uint64_t start = pos + 1 - tl;
-          const bool want_kw = pd.kw_needed != 0;
-          bool want_hit = pd.rule_n != 0;
-          if (want_hit && pd.confirm) {  // case requirement of the anchor literal (first tl bytes)
-            const uint8_t* rq = pbytes + pd.req_off;
-            for (uint32_t k = 0; k < tl && want_hit; ++k) {
-              const uint32_t b = hist_byte(hist, 8 - tl + k);
-              want_hit = rq[k] == 0 || b == rq[k];
+    const uint32_t rounds = (uint32_t)((n + blockDim.x - 1) / blockDim.x);
+    for (uint32_t rd_i = 0; rd_i < rounds; ++rd_i) {
+      const uint64_t i = (uint64_t)rd_i * blockDim.x + threadIdx.x;
+      if (i < n) {
+        const FastEvent ev = seg[i];
+        uint64_t hist = ((uint64_t)ev.prev.y << 32) | ev.prev.x;  // the 8 raw bytes before (oldest low)
+        uint64_t hlow = lower64(hist);
+        uint32_t e = ev.entry;
+        const uint32_t fx = fold6(ev.cur.x), fy = fold6(ev.cur.y);
+        uint32_t fi = 0xFFFFFFFFu;
+  #pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          e = fstep(B, e, j < 4 ? fx : fy, j & 3);
+          const uint32_t c = ((j < 4 ? ev.cur.x : ev.cur.y) >> (8 * (j & 3))) & 0xFFu;
+          hist = (hist >> 8) | ((uint64_t)c << 56);  // hist byte 7 = c
+          hlow = (hlow >> 8) | ((uint64_t)lower_ascii((uint8_t)c) << 56);
+          if (e < out_e || c >= 0x80) continue;  // an output ending on a byte >= 0x80 is an alias
+          const uint64_t pos = ev.pos + j;
+          const uint32_t st = e / kFastRowU16;
+          for (uint32_t o = out_off[st]; o < out_off[st + 1]; ++o) {
+            const uint32_t pid = out_pat[o];
+            const PatDev& pd = pats[pid];
+            // the automaton's prefix on the real bytes (it ran on folded ones)
+            if ((hlow & pd.m64) != pd.lo64) continue;
+            const bool want_kw = pd.kw_needed != 0;
+            bool want_hit = pd.rule_n != 0 && (hist & pd.rqm64) == pd.rq64;
+            if (!want_kw && !want_hit) continue;
+            const uint32_t tl = pd.len < ac.depth ? pd.len : ac.depth;
+            const uint64_t start = pos + 1 - tl;
+            if (pd.trunc) {  // the rest of a long pattern, on the batch (rare)
+              if (fi == 0xFFFFFFFFu) fi = file_of_pos(P, pos);
+              const uint64_t fend = P.off[fi + 1] - 1;
+              if (start + pd.len > fend) continue;
+              bool ok = true;
+              const uint8_t* pb = pbytes + pd.bytes_off;
+              for (uint32_t k = tl; k < pd.len && ok; ++k) {
+                const uint8_t b = P.data[start + k];
+                ok = lower_ascii(b) == pb[k];
+                if (want_hit && pd.confirm) {
+                  const uint8_t r = pbytes[pd.req_off + k];
+                  want_hit = r == 0 || b == r;
+                }
+              }
+              if (!ok) continue;
             }
-          }
-          if (!want_kw && !want_hit) continue;
-          if (pd.trunc) {  // the rest of a long pattern, on the batch (rare)
-            if (fi == 0xFFFFFFFFu) fi = file_of_pos(P, pos);
-            const uint64_t fend = P.off[fi + 1] - 1;
-            if (start + pd.len > fend) continue;
-            for (uint32_t k = tl; k < pd.len && ok; ++k) {
-              const uint8_t b = P.data[start + k];
-              ok = lower_ascii(b) == pb[k];
-              if (want_hit && pd.confirm) {
-                const uint8_t r = pbytes[pd.req_off + k];
-                want_hit = r == 0 || b == r;
+            ++my_out;
+            if (want_kw) {
+              if (fi == 0xFFFFFFFFu) fi = file_of_pos(P, pos);
+              const uint64_t key = ((uint64_t)fi << 32) | pd.kw;  // per-lane dedupe of repeated keywords
+              if (last_kw != key) {
+                last_kw = key;
+                atomicOr(&P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)], 1u << (pd.kw & 31));
               }
             }
-            if (!ok) continue;
-          }
-          ++my_out;
-          if (want_kw) {
-            if (fi == 0xFFFFFFFFu) fi = file_of_pos(P, pos);
-            const uint64_t key = ((uint64_t)fi << 32) | pd.kw;  // per-lane dedupe of repeated keywords
-            if (last_kw != key) {
-              last_kw = key;
-              atomicOr(&P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)], 1u << (pd.kw & 31));
-            }
-          }
-          if (want_hit) {
-            const uint32_t slot = atomicAdd(&hcnt, 1u);
-            const uint64_t hrec = (start << 16) | pid;
-            if (slot < kReportHitCap) {
-              hbuf[slot] = hrec;
-            } else {
-              unsigned long long idx = atomicAdd(&P.ctrl->hits, 1ull);
-              if (idx < P.hit_cap) P.hits[idx] = hrec;
+            if (want_hit) {
+              const uint32_t slot = atomicAdd(&hcnt, 1u);
+              const uint64_t hrec = (start << 16) | pid;
+              if (slot < kReportHitCap) {
+                hbuf[slot] = hrec;
+              } else {
+                unsigned long long idx = atomicAdd(&P.ctrl->hits, 1ull);
+                if (idx < P.hit_cap) P.hits[idx] = hrec;
+              }
             }
           }
         }
       }
+      // stage -> global with one reservation per half-full buffer (uniform decision)
+      __syncthreads();
+      if (hcnt >= kReportHitCap / 2 || rd_i + 1 == rounds) {
+        const uint32_t nh = hcnt < kReportHitCap ? hcnt : kReportHitCap;
+        if (threadIdx.x == 0 && nh) hbase = atomicAdd(&P.ctrl->hits, (unsigned long long)nh);
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < nh; q += blockDim.x)
+          if (hbase + q < P.hit_cap) P.hits[hbase + q] = hbuf[q];
+        __syncthreads();
+        if (threadIdx.x == 0) hcnt = 0;
+        __syncthreads();
+      }
     }
-    // flush staged hits with one global reservation per block step
-    __syncthreads();
-    const uint32_t nh = hcnt < kReportHitCap ? hcnt : kReportHitCap;
-    if (threadIdx.x == 0 && nh) hbase = atomicAdd(&P.ctrl->hits, (unsigned long long)nh);
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nh; i += blockDim.x)
-      if (hbase + i < P.hit_cap) P.hits[hbase + i] = hbuf[i];
-    __syncthreads();
-    if (threadIdx.x == 0) hcnt = 0;
-    __syncthreads();
   }
   atomicAdd(&nout, my_out);
   __syncthreads();
@@ -1950,6 +1955,18 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
     d.confirm = p.confirm;
     d.kw_needed = p.kw >= 0 && kw_needed_ids.count((uint32_t)p.kw);
     d.trunc = p.lower.size() > (size_t)ac.depth;
+    {
+      const size_t tl = std::min<size_t>(p.lower.size(), ac.depth);
+      for (size_t k = 0; k < tl; ++k) {
+        const int sh = 8 * (int)(8 - tl + k);
+        d.lo64 |= (uint64_t)(uint8_t)p.lower[k] << sh;
+        d.m64 |= 0xFFull << sh;
+        if (p.confirm && p.req[k]) {
+          d.rq64 |= (uint64_t)(uint8_t)p.req[k] << sh;
+          d.rqm64 |= 0xFFull << sh;
+        }
+      }
+    }
     pats.push_back(d);
   }
   HIP_TRY(im.pats.ensure(pats.size() + 1));
