@@ -102,10 +102,10 @@ def read_result(N, res):
     dt = np.dtype([("file", "<u4"), ("rule", "<u4"), ("start", "<u8"), ("end", "<u8"),
                    ("start_line", "<u4"), ("end_line", "<u4")])
     locs = np.frombuffer(arr.tobytes(), dtype=dt)
-    tm = (ctypes.c_double * 16)()
+    tm = (ctypes.c_double * 32)()
     nt = ctypes.c_size_t()
-    N.lib.tsg_result_timings(res, tm, 16, ctypes.byref(nt))
-    return locs, [tm[i] for i in range(nt.value)]
+    N.lib.tsg_result_timings(res, tm, 32, ctypes.byref(nt))
+    return locs, [tm[i] for i in range(min(32, nt.value))]
 
 
 def parity_checks(N, S, c, locs, rules, seed, density, n_sample=300):
@@ -148,6 +148,18 @@ def parity_checks(N, S, c, locs, rules, seed, density, n_sample=300):
     return dict(planted=int(len(real)), planted_found=int(found), decoys=int(len(decoys)),
                 decoys_found=int(decoy_hits), spot_files=len(cand), spot_findings=spot_findings,
                 spot_mismatched_files=mismatched, total_findings=int(len(locs)))
+
+
+def traffic_bytes(content_bytes):
+    """HBM bytes per k_scan_fast launch from the committed rocprofv3 FETCH_SIZE
+    pass (profiles/traffic_k_scan_fast.json, written by tools/prof_summary.py:
+    FETCH_SIZE KiB x 1024 x 2, the gfx950 correction), scaled to this launch's
+    content bytes when the profiled corpus differs.  None without a profile."""
+    p = os.path.join(ROOT, "profiles", "traffic_k_scan_fast.json")
+    if not os.path.exists(p):
+        return None
+    t = json.load(open(p))
+    return round(t["hbm_read_bytes_per_launch"] * content_bytes / t["algorithmic_bytes_per_launch"])
 
 
 def cpu_baseline(N, c, seed, density, seconds, cores):
@@ -278,7 +290,7 @@ def main():
     for i in range(args.steps):
         res = scan_device(N, eng, rs, c)
         locs, tm = read_result(N, res)
-        scan_ms.append(tm[7])
+        scan_ms.append(tm[17] if len(tm) > 17 and tm[17] > 0 else tm[7])
         stage = tm
         N.lib.tsg_result_free(res)
     torch.cuda.synchronize()
@@ -325,13 +337,14 @@ def main():
                        "gb_per_gpu": round(c["total"] / 1e9, 3), "files_per_gpu": c["n_files"],
                        "density": args.density, "parallelism": f"file shards x{world}, no collective"},
             "pct_hbm_peak": round(100.0 * value / (HBM_PEAK_GBPS * world), 2),
-            "roofline": {"bound": "hbm", "kernel": "k_scan", "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": "k_scan_fast", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": None, "algorithmic_bytes_per_launch": c["total"],
+                         "traffic": traffic_bytes(c["total"]), "algorithmic_bytes_per_launch": c["total"],
                          "avg_launch_ms": round(scan_kernel_ms, 3)},
             "stages_ms": {k: round(v, 3) for k, v in zip(
-                ["path_gate", "scan_total", "expand", "sort_jobs", "verify", "exclude", "lines", "k_scan"], stage)},
-            "counts": {k: int(v) for k, v in zip(["hits", "candidates", "jobs", "locs", "event_overflow", "events", "outputs"], stage[8:])},
+                ["path_gate", "scan_total", "expand", "sort_jobs", "verify", "exclude", "lines", "scan_kernels"], stage)},
+            "counts": {k: int(v) for k, v in zip(["hits", "candidates", "jobs", "locs", "event_overflow", "events", "outputs"], stage[8:15])},
+            "host_ms": {"call_wall": round(stage[15], 3), "post": round(stage[16], 3)},
             "cpu_baseline": cpu,
             "parity": parity,
         }

@@ -1606,6 +1606,24 @@ __global__ __launch_bounds__(256) void k_exclude(const uint8_t* data, const uint
   }
 }
 
+// (file, start) sort keys of the kept locations (files < 4 GiB: start fits 32 bits)
+__global__ void k_loc_keys(const DevLoc* locs, uint64_t n, uint64_t* keys, uint32_t* idx) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  keys[i] = ((uint64_t)locs[i].file << 32) | (uint32_t)locs[i].start;
+  idx[i] = (uint32_t)i;
+}
+
+__global__ void k_loc_gather(const DevLoc* locs, const uint32_t* idx, uint64_t n, DevLoc* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = locs[idx[i]];
+}
+
+__global__ void k_flags8(const uint32_t* flags, uint8_t* out, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (uint8_t)flags[i];
+}
+
 // ----------------------------------------------------------------- lines --
 // Global newline prefix G(x) = count('\n' in data[0,x)) from the per-8KiB
 // block counts k_scan produced (nl_pre = their exclusive prefix sum) plus one
@@ -1726,7 +1744,7 @@ struct tsg_engine {
   DBuf<uint32_t> job_start;
   DBuf<uint32_t> nsel;
   DBuf<uint8_t> cub_tmp;
-  DBuf<DevLoc> locs;
+  DBuf<DevLoc> locs, locs2;
   DBuf<uint8_t> scratch;
   DBuf<Ctrl> ctrl;
   DBuf<uint32_t> nl_blocks, nl_pre;
@@ -1737,6 +1755,10 @@ struct tsg_engine {
   DBuf<uint8_t> span_hi;
   DBuf<uint32_t> ev_counts;
   uint64_t ev_ovf_need = 0;  // overflow-event capacity learnt from a lost scan
+  bool fast_timed = false;   // ev[10..11] bracket the last k_scan_fast launch
+  DBuf<uint8_t> fflags8;     // per-file result flags, u8
+  uint8_t* h_flags = nullptr;  // pinned staging for them
+  size_t h_flags_n = 0;
   uint32_t num_cus = 0;
   DBuf<ExclJob> excl_jobs;
   DBuf<ExclRange> excl_out;
@@ -2153,39 +2175,33 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
 // So StartLine = 1 + P(start) - (newlines censored before start), and
 // EndLine == StartLine because [start,end) itself is censored.  P(x) are the
 // raw prefix counts k_lines produced at every location boundary.
+// `locs` arrive ordered by (file, start) (k_loc_keys + radix sort on the device).
 void censored_lines(std::vector<DevLoc>& locs) {
-  std::vector<size_t> idx(locs.size());
-  for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
-  std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {
-    const DevLoc &x = locs[a], &y = locs[b];
-    if (x.file != y.file) return x.file < y.file;
-    if (x.start != y.start) return x.start < y.start;
-    return x.end < y.end;
-  });
   size_t i = 0;
-  while (i < idx.size()) {
+  std::vector<uint64_t> ia, ib;
+  std::vector<uint32_t> ipa, ipb;
+  while (i < locs.size()) {
     size_t j = i;
-    while (j < idx.size() && locs[idx[j]].file == locs[idx[i]].file) ++j;
+    while (j < locs.size() && locs[j].file == locs[i].file) ++j;
     // merged censored intervals of this file: (a, b, P(a), P(b))
-    struct Iv { uint64_t a, b; uint32_t pa, pb; };
-    std::vector<Iv> iv;
+    ia.clear(); ib.clear(); ipa.clear(); ipb.clear();
     for (size_t k = i; k < j; ++k) {
-      const DevLoc& L = locs[idx[k]];
+      const DevLoc& L = locs[k];
       if (L.flags) continue;
-      if (!iv.empty() && L.start <= iv.back().b) {
-        if (L.end > iv.back().b) { iv.back().b = L.end; iv.back().pb = L.end_line; }
+      if (!ia.empty() && L.start <= ib.back()) {
+        if (L.end > ib.back()) { ib.back() = L.end; ipb.back() = L.end_line; }
       } else {
-        iv.push_back(Iv{L.start, L.end, L.start_line, L.end_line});
+        ia.push_back(L.start); ib.push_back(L.end); ipa.push_back(L.start_line); ipb.push_back(L.end_line);
       }
     }
     size_t m = 0;
     uint32_t before = 0;  // newlines censored in intervals entirely before the current one
     for (size_t k = i; k < j; ++k) {
-      DevLoc& L = locs[idx[k]];
+      DevLoc& L = locs[k];
       if (L.flags) continue;
-      while (m < iv.size() && iv[m].b <= L.start) { before += iv[m].pb - iv[m].pa; ++m; }
+      while (m < ia.size() && ib[m] <= L.start) { before += ipb[m] - ipa[m]; ++m; }
       uint32_t hidden = before;
-      if (m < iv.size() && iv[m].a < L.start) hidden += L.start_line - iv[m].pa;
+      if (m < ia.size() && ia[m] < L.start) hidden += L.start_line - ipa[m];
       const uint32_t line = L.start_line - hidden + 1;
       L.start_line = line;
       L.end_line = line;
@@ -2257,12 +2273,15 @@ int launch_scan(tsg_engine* e, ScanParams P) {
     P.ev_overflow_cap = e->ev_overflow.n;
     HIP_TRY(hipMemsetAsync(&P.ctrl->ev_overflow, 0, 8, s));
     // (the image lives in the kernel's static kFastImgMax array: no dynamic LDS)
+    if (e->events) HIP_TRY(hipEventRecord(e->ev[10], s));
     if (ring) hipLaunchKernelGGL(k_scan_ring, dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1 && vecs == 8) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1) hipLaunchKernelGGL((k_scan_fast<1, 4, 768>), dim3(blocks), dim3(nt), 0, s, P);
     else if (vecs == 4) hipLaunchKernelGGL((k_scan_fast<2, 4, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     else hipLaunchKernelGGL((k_scan_fast<2, 2, 768>), dim3(blocks), dim3(nt), 0, s, P);
     HIP_TRY(hipGetLastError());
+    if (e->events) HIP_TRY(hipEventRecord(e->ev[11], s));
+    e->fast_timed = e->events;
     hipLaunchKernelGGL(k_report, dim3((uint32_t)std::min<uint64_t>(n_waves + 1, e->num_cus)), dim3(kReportThreads), 0, s, P,
                        (uint32_t)n_waves);
     HIP_TRY(hipGetLastError());
@@ -2290,6 +2309,8 @@ int launch_scan(tsg_engine* e, ScanParams P) {
 int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, const uint64_t* d_off,
                  const uint8_t* d_paths, const uint64_t* d_path_off, size_t n_files, uint64_t nbytes,
                  tsg_result* res) {
+  const auto wall0 = std::chrono::steady_clock::now();
+  e->fast_timed = false;
   int rc = upload_ruleset(e, rs);
   if (rc) return rc;
   const DevImage& im = e->img;
@@ -2313,7 +2334,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   }
   HIP_TRY(e->scratch.ensure((size_t)e->vm_threads * e->scratch_stride));
   std::vector<double>& tm = res->impl.timings;
-  tm.assign(15, 0.0);
+  tm.assign(18, 0.0);
   if (!e->events) {
     for (auto& ev : e->ev) HIP_TRY(hipEventCreate(&ev));
     e->events = true;
@@ -2596,13 +2617,43 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     hipLaunchKernelGGL(k_lines, dim3((uint32_t)((n_locs * 64 + 255) / 256)), dim3(256), 0, s, d_data, d_off,
                        e->nl_pre.p, e->locs.p, n_locs);
     HIP_TRY(hipGetLastError());
+    // order by (file, start) on the device (censored_lines walks files in order)
+    HIP_TRY(e->keys.ensure(n_locs));
+    HIP_TRY(e->keys2.ensure(n_locs));
+    HIP_TRY(e->vals.ensure(n_locs));
+    HIP_TRY(e->vals2.ensure(n_locs));
+    HIP_TRY(e->locs2.ensure(n_locs));
+    hipLaunchKernelGGL(k_loc_keys, dim3((uint32_t)((n_locs + 255) / 256)), dim3(256), 0, s, e->locs.p, n_locs,
+                       e->keys.p, e->vals.p);
+    size_t tmp2 = 0;
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
+                                               (int)n_locs, 0, 64, s));
+    HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
+                                               (int)n_locs, 0, 64, s));
+    hipLaunchKernelGGL(k_loc_gather, dim3((uint32_t)((n_locs + 255) / 256)), dim3(256), 0, s, e->locs.p,
+                       e->vals2.p, n_locs, e->locs2.p);
+    HIP_TRY(hipGetLastError());
     hl.resize(n_locs);
-    HIP_TRY(hipMemcpyAsync(hl.data(), e->locs.p, n_locs * sizeof(DevLoc), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(hl.data(), e->locs2.p, n_locs * sizeof(DevLoc), hipMemcpyDeviceToHost, s));
   }
   HIP_TRY(hipEventRecord(e->ev[7], s));
-  std::vector<uint32_t> flags(nf);
-  if (nf) HIP_TRY(hipMemcpyAsync(flags.data(), e->file_flags.p, nf * 4, hipMemcpyDeviceToHost, s));
+  // per-file flags as bytes through pinned staging
+  if (nf) {
+    HIP_TRY(e->fflags8.ensure(nf));
+    hipLaunchKernelGGL(k_flags8, dim3((nf + 255) / 256), dim3(256), 0, s, e->file_flags.p, e->fflags8.p, nf);
+    HIP_TRY(hipGetLastError());
+    if (e->h_flags_n < nf) {
+      if (e->h_flags) HIP_TRY(hipHostFree(e->h_flags));
+      e->h_flags = nullptr;
+      e->h_flags_n = 0;
+      HIP_TRY(hipHostMalloc((void**)&e->h_flags, (size_t)nf + (nf >> 2) + 64, hipHostMallocDefault));
+      e->h_flags_n = (size_t)nf + (nf >> 2) + 64;
+    }
+    HIP_TRY(hipMemcpyAsync(e->h_flags, e->fflags8.p, nf, hipMemcpyDeviceToHost, s));
+  }
   HIP_TRY(hipStreamSynchronize(s));
+  const auto wall1 = std::chrono::steady_clock::now();
   for (int k = 0; k < 7; ++k) {
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, e->ev[k], e->ev[k + 1]));
@@ -2620,9 +2671,13 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(hipEventElapsedTime(&ms, e->ev[8], e->ev[9]));
     tm[7] = ms;
   }
+  if (e->fast_timed) {  // k_scan_fast alone
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, e->ev[10], e->ev[11]));
+    tm[17] = ms;
+  }
   auto& R = res->impl;
-  R.file_flags.resize(nf);
-  for (uint32_t f = 0; f < nf; ++f) R.file_flags[f] = (uint8_t)flags[f];
+  R.file_flags.assign(e->h_flags, e->h_flags + nf);
   censored_lines(hl);
   R.locs.clear();
   for (auto& L : hl) {
@@ -2632,6 +2687,9 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     }
     R.locs.push_back(tsg_loc{L.file, L.rule, L.start, L.end, L.start_line, L.end_line});
   }
+  const auto wall2 = std::chrono::steady_clock::now();
+  tm[15] = std::chrono::duration<double, std::milli>(wall2 - wall0).count();  // whole call, host clock
+  tm[16] = std::chrono::duration<double, std::milli>(wall2 - wall1).count();  // host post-processing
   return TSG_OK;
 }
 
@@ -2668,10 +2726,11 @@ void tsg_engine_free(tsg_engine* e) {
   e->data.release(); e->off.release(); e->paths.release(); e->path_off.release();
   e->file_kw.release(); e->file_flags.release(); e->path_mask.release(); e->hits.release();
   e->keys.release(); e->keys2.release(); e->vals.release(); e->vals2.release(); e->flags8.release();
-  e->job_start.release(); e->nsel.release(); e->cub_tmp.release(); e->locs.release();
+  e->job_start.release(); e->nsel.release(); e->cub_tmp.release(); e->locs.release(); e->locs2.release();
   e->scratch.release(); e->ctrl.release(); e->excl_jobs.release(); e->excl_out.release();
   e->nl_blocks.release(); e->nl_pre.release(); e->tail.release(); e->region_file.release();
-  e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->vprof.release();
+  e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->vprof.release(); e->fflags8.release();
+  if (e->h_flags) (void)hipHostFree(e->h_flags);
   if (e->events)
     for (auto& ev : e->ev) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream);
