@@ -115,14 +115,15 @@ struct ScanParams {
   uint8_t* span_hi;               // per kNlBlock span: a byte >= 0x80 occurs (k_fold_special)
 };
 
-// region_file[r] = index of the file holding byte r * kNlBlock (one pass over
-// files), so a report narrows its file lookup to the files of one 8 KiB region.
-__global__ __launch_bounds__(256) void k_region_index(const uint64_t* off, uint32_t n_files, uint64_t n_regions,
-                                                      uint32_t* region_file) {
+// region_file[r] = index of the file holding byte r * kNlBlock = the largest f
+// with off[f] <= r * kNlBlock: each file marks the first region boundary at or
+// after its start (atomicMax), an inclusive max-scan fills the rest.
+__global__ __launch_bounds__(256) void k_region_mark(const uint64_t* off, uint32_t n_files, uint64_t n_regions,
+                                                     uint32_t* region_file) {
   const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= n_files) return;
-  const uint64_t a = off[f], b = off[f + 1];
-  for (uint64_t r = (a + kNlBlock - 1) / kNlBlock; r * kNlBlock < b && r < n_regions; ++r) region_file[r] = (uint32_t)f;
+  const uint64_t r = (off[f] + kNlBlock - 1) / kNlBlock;
+  if (r < n_regions) atomicMax(&region_file[r], (uint32_t)f);
 }
 
 __device__ inline uint32_t find_file(const uint64_t* off, uint32_t lo, uint32_t hi, uint64_t pos) {
@@ -780,17 +781,21 @@ __global__ __launch_bounds__(256) void k_fold_special(ScanParams P, uint64_t n_s
   const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   constexpr uint32_t kPer = kNlBlock / 64;
-  for (uint64_t sp = w0; sp < n_spans; sp += nw) {
-    if (!P.span_hi[sp]) continue;
-    const uint64_t a = sp * kNlBlock + (uint64_t)lane * kPer;
-    const uint64_t b = a + kPer < P.nbytes ? a + kPer : P.nbytes;
-    uint32_t b1 = a >= 1 ? P.data[a - 1] : 0, b2 = a >= 2 ? P.data[a - 2] : 0;
-    for (uint64_t q = a; q < b; ++q) {
-      const uint32_t c = P.data[q];
-      if ((c == 0xB0 && b1 == 0xC4) || (c == 0xBF && b1 == 0xC5) || (c == 0xAA && b1 == 0x84 && b2 == 0xE2))
-        atomicOr(&P.file_flags[file_of_pos(P, q)], kFileSpecial);
-      b2 = b1;
-      b1 = c;
+  for (uint64_t g = w0 * 64; g < n_spans; g += nw * 64) {  // 64 spans per wave step
+    uint64_t m = __ballot(g + lane < n_spans && P.span_hi[g + lane]);
+    while (m) {
+      const uint64_t sp = g + (uint64_t)__ffsll((long long)m) - 1;
+      m &= m - 1;
+      const uint64_t a = sp * kNlBlock + (uint64_t)lane * kPer;
+      const uint64_t b = a + kPer < P.nbytes ? a + kPer : P.nbytes;
+      uint32_t b1 = a >= 1 && a - 1 < P.nbytes ? P.data[a - 1] : 0, b2 = a >= 2 && a - 2 < P.nbytes ? P.data[a - 2] : 0;
+      for (uint64_t q = a; q < b; ++q) {
+        const uint32_t c = P.data[q];
+        if ((c == 0xB0 && b1 == 0xC4) || (c == 0xBF && b1 == 0xC5) || (c == 0xAA && b1 == 0x84 && b2 == 0xE2))
+          atomicOr(&P.file_flags[file_of_pos(P, q)], kFileSpecial);
+        b2 = b1;
+        b1 = c;
+      }
     }
   }
 }
@@ -1034,6 +1039,8 @@ __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
 struct ExpandParams {
   const uint8_t* data;
   const uint64_t* off;
+  const uint32_t* region_file;  // launch_scan's region -> file index
+  uint64_t n_regions;
   uint32_t n_files;
   RuleSetDev rs;
   const uint32_t* file_kw;
@@ -1092,7 +1099,9 @@ __global__ __launch_bounds__(256) void k_expand(ExpandParams E) {
   const uint64_t h = E.hits[i];
   const uint64_t gpos = h >> 16;
   const uint32_t pid = (uint32_t)(h & 0xFFFF);
-  const uint32_t fi = find_file(E.off, 0, E.n_files, gpos);
+  const uint64_t rg = gpos / kNlBlock;
+  const uint32_t fhi = rg + 1 < E.n_regions ? min(E.region_file[rg + 1] + 1, E.n_files) : E.n_files;
+  const uint32_t fi = find_file(E.off, E.region_file[rg], fhi, gpos);
   const uint32_t fl = E.file_flags[fi];
   if (fl & (kFileAllowed | kFileSpecial)) return;
   const PatDev pd = E.rs.ac.pats[pid];
@@ -1749,7 +1758,7 @@ struct tsg_engine {
   DBuf<Ctrl> ctrl;
   DBuf<uint32_t> nl_blocks, nl_pre;
   DBuf<uint8_t> tail;
-  DBuf<uint32_t> region_file;
+  DBuf<uint32_t> region_file, region_tmp;
   DBuf<FastEvent> ev_buf, ev_overflow;
   DBuf<uint64_t> vprof;
   DBuf<uint8_t> span_hi;
@@ -2223,9 +2232,19 @@ int launch_scan(tsg_engine* e, ScanParams P) {
   P.n_regions = P.nbytes / kNlBlock + 1;
   HIP_TRY(e->region_file.ensure(P.n_regions + 1));
   P.region_file = e->region_file.p;
-  if (P.n_files)
-    hipLaunchKernelGGL(k_region_index, dim3((P.n_files + 255) / 256), dim3(256), 0, s, P.off, P.n_files,
-                       P.n_regions, e->region_file.p);
+  if (P.n_files) {
+    HIP_TRY(e->region_tmp.ensure(P.n_regions + 1));
+    HIP_TRY(hipMemsetAsync(e->region_tmp.p, 0, (P.n_regions + 1) * 4, s));
+    hipLaunchKernelGGL(k_region_mark, dim3((P.n_files + 255) / 256), dim3(256), 0, s, P.off, P.n_files,
+                       P.n_regions, e->region_tmp.p);
+    HIP_TRY(hipGetLastError());
+    size_t tmp = 0;
+    HIP_TRY(hipcub::DeviceScan::InclusiveScan(nullptr, tmp, e->region_tmp.p, e->region_file.p, hipcub::Max(),
+                                              (int)P.n_regions, s));
+    HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+    HIP_TRY(hipcub::DeviceScan::InclusiveScan(e->cub_tmp.p, tmp, e->region_tmp.p, e->region_file.p, hipcub::Max(),
+                                              (int)P.n_regions, s));
+  }
   if (!e->num_cus) {
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, e->device));
@@ -2285,7 +2304,7 @@ int launch_scan(tsg_engine* e, ScanParams P) {
     hipLaunchKernelGGL(k_report, dim3((uint32_t)std::min<uint64_t>(n_waves + 1, e->num_cus)), dim3(kReportThreads), 0, s, P,
                        (uint32_t)n_waves);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_fold_special, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_spans + 3) / 4, 8192))),
+    hipLaunchKernelGGL(k_fold_special, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_spans + 255) / 256, 2048))),
                        dim3(256), 0, s, P, n_spans);
   } else {
     const size_t table_bytes = (size_t)ac.nstates * ac.nclasses * 2;
@@ -2430,6 +2449,8 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   ExpandParams E{};
   E.data = d_data;
   E.off = d_off;
+  E.region_file = e->region_file.p;
+  E.n_regions = nbytes / kNlBlock + 1;
   E.n_files = nf;
   E.rs = RS;
   E.file_kw = e->file_kw.p;
@@ -2728,7 +2749,7 @@ void tsg_engine_free(tsg_engine* e) {
   e->keys.release(); e->keys2.release(); e->vals.release(); e->vals2.release(); e->flags8.release();
   e->job_start.release(); e->nsel.release(); e->cub_tmp.release(); e->locs.release(); e->locs2.release();
   e->scratch.release(); e->ctrl.release(); e->excl_jobs.release(); e->excl_out.release();
-  e->nl_blocks.release(); e->nl_pre.release(); e->tail.release(); e->region_file.release();
+  e->nl_blocks.release(); e->nl_pre.release(); e->tail.release(); e->region_file.release(); e->region_tmp.release();
   e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->vprof.release(); e->fflags8.release();
   if (e->h_flags) (void)hipHostFree(e->h_flags);
   if (e->events)
