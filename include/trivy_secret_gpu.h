@@ -121,6 +121,13 @@ int tsg_ruleset_rule_info(const tsg_ruleset* rs, size_t i, int* mode, uint32_t* 
 int tsg_ruleset_rule_literal(const tsg_ruleset* rs, size_t i, size_t k, char* lower, char* req, size_t cap,
                              size_t* len);
 
+/* Scan-automaton pattern k (k < n_patterns of tsg_ruleset_stats): its
+ * lowercased literal (*len bytes into `lower`), the class positions the
+ * k_scan_fast automaton requires right after it (*ext <= 8) with their 6-bit
+ * fold-column masks (cols[0..ext)), and the automaton's state count. */
+int tsg_ruleset_scan_pattern(const tsg_ruleset* rs, size_t k, char* lower, size_t cap, size_t* len, uint32_t* ext,
+                             uint64_t* cols, uint32_t* fast_states);
+
 /* Instruction count and capture slots of rule i's compiled regex. */
 int tsg_ruleset_rule_prog(const tsg_ruleset* rs, size_t i, uint32_t* n_inst, uint32_t* n_cap);
 

@@ -88,6 +88,9 @@ _SIGS = {
                                              ctypes.POINTER(ctypes.c_size_t)]),
     "tsg_ruleset_rule_literal": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_char_p,
                                                 ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
+    "tsg_ruleset_scan_pattern": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                                                ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_uint32),
+                                                ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
     "tsg_ruleset_rule_prog": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32),
                                              ctypes.POINTER(ctypes.c_uint32)]),
     "tsg_ruleset_dfa_check": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,

@@ -11,12 +11,13 @@
 namespace tsg {
 
 constexpr int kAcMaxLit = 8;   // trie depth; longer patterns are confirmed on hit
+constexpr int kFastExtTo = 6;  // scan automaton: short anchor literals extended by classes up to this length
 constexpr uint32_t kNlBlock = 4096;  // newline-count granularity (bytes) = one k_scan_fast chain span
 constexpr uint32_t kNoKw = 0xFFFFFFFFu;
 
 constexpr uint32_t kFastCols = 64;             // k_scan_fast columns (6-bit folded bytes, engine.hip fold6)
 constexpr uint32_t kFastRowBytes = 130;       // 64 u16 columns + 2 B: consecutive rows rotate LDS banks
-constexpr uint32_t kFastImgMax = 78 * 1024;   // k_scan_fast image budget: two images per CU's LDS
+constexpr uint32_t kFastImgMax = 132 * 1024;  // k_scan_fast image budget (1008 rows: 16-bit entries)
 constexpr uint32_t kLdsMax = 160 * 1024;      // LDS per CU
 constexpr uint32_t kFastSpecialEv = 0xFFFF;   // event tag: U+0130/U+017F/U+212A sequence ends here
 constexpr uint32_t kFollowMaxStates = 1024;  // follow-DFA subset-construction budget
@@ -58,6 +59,8 @@ struct PatDev {
   uint8_t confirm;     // anchor roles need a case check
   uint8_t trunc;       // len > trie depth
   uint8_t kw_needed;   // some rule whose gate is not implied uses this keyword
+  uint8_t ext;         // scan-automaton class positions after the literal (k_scan_fast image only)
+  uint8_t pad[7];
   // k_report's branch-free confirm of the first min(len, depth) bytes against
   // the last 8 bytes (byte 7 = the pattern's last automaton byte)
   uint64_t lo64, m64;    // lowered pattern bytes / their mask, top-aligned
@@ -120,6 +123,8 @@ struct FollowDfa {
   std::vector<uint16_t> delta;  // [nstates][ncls]
 };
 bool build_follow(const gre::Compiled& c, FollowDfa* out);
+// Fold-column sets required right after anchor literal `lit` (follow.cpp).
+std::vector<uint64_t> follow_ext(const gre::Compiled& c, const gre::Lit& lit, int max_ext);
 
 // Anchored leftmost-first DFA over ASCII for k_verify (dfa.cpp): state 0 =
 // dead; entry = next state | 0x8000 when that byte, as the text's last,
@@ -148,6 +153,7 @@ struct RuleHost {
   RuleMode mode = MODE_NEVER;
   FollowDfa follow;  // MODE_ANCHORED only
   DfaHost dfa;       // MODE_ANCHORED only
+  bool gate_implied = false;  // every anchor literal contains one of the keywords
 };
 
 struct AcHost {
@@ -159,6 +165,12 @@ struct AcHost {
   std::vector<uint16_t> out_pat;
   uint32_t nstates = 0, nclasses = 0;
   uint32_t depth = kAcMaxLit;  // trie depth (patterns longer than this are confirmed on hit)
+  // k_scan_fast image's own automaton (fold columns, literal + class
+  // extensions): per-state outputs and, per pattern, the extension it carries
+  std::vector<uint32_t> fast_out_off;
+  std::vector<uint16_t> fast_out_pat;
+  std::vector<uint8_t> fast_ext;
+  uint32_t fast_states = 0;
 };
 
 struct PatternHost {
@@ -169,6 +181,7 @@ struct PatternHost {
   bool confirm = false;
   bool any_anchor = false;
   std::vector<uint32_t> rules;
+  std::vector<uint64_t> ext_cols;  // fold columns every anchored use requires after the literal
 };
 
 }  // namespace tsg

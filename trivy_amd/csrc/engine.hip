@@ -386,11 +386,14 @@ __device__ inline void fast_event(const ScanParams& P, uint32_t out_e, const Fas
 }
 
 // Walk one 8-byte group (d0, d1) of a chain and report it if it hit an output.
-template <int V>
+// kMode (timing experiments only, TSG_SCAN_MODE; results are wrong unless 0):
+// 1 = no events, 2 = no newline count, 4 = loads from the batch's first MiB
+// (L2-resident: takes HBM out of the picture).
+template <int V, int kMode = 0>
 __device__ inline void fast_group(const ScanParams& P, const uint8_t* T, uint32_t out_e, FastChain<V>& C, uint32_t d0,
                                   uint32_t d1, uint64_t gpos, bool live, uint64_t lanes_lt, FastEvent* ev_seg,
                                   uint32_t* ev_count) {
-  C.nl += nl_count_dword(d0) + nl_count_dword(d1);
+  if (!(kMode & 2)) C.nl += nl_count_dword(d0) + nl_count_dword(d1);
   C.hi |= d0 | d1;
   const uint32_t f0 = fold6(d0), f1 = fold6(d1);
   const uint32_t gs = C.e;
@@ -400,7 +403,7 @@ __device__ inline void fast_group(const ScanParams& P, const uint8_t* T, uint32_
     C.e = fstep(T, C.e, j < 4 ? f0 : f1, j & 3);
     m = m > C.e ? m : C.e;
   }
-  fast_event(P, out_e, C, m, gs, d0, d1, gpos, live, lanes_lt, ev_seg, ev_count);
+  if (!(kMode & 1)) fast_event(P, out_e, C, m, gs, d0, d1, gpos, live, lanes_lt, ev_seg, ev_count);
   C.prev = make_uint2(d0, d1);
 }
 
@@ -430,7 +433,7 @@ __device__ inline void fast_group2(const ScanParams& P, const uint8_t* T, uint32
   B.prev = make_uint2(b0, b1);
 }
 
-template <int CH, int V, int kFastThreads>
+template <int CH, int V, int kFastThreads, int kMode = 0>
 __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
   constexpr uint32_t kUnit = CH * kNlBlock;          // bytes per lane per work unit
   constexpr int kStep = V * 16;                      // bytes per chain step
@@ -496,7 +499,10 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
         for (int c = 0; c < CH; ++c) {
           const uint8_t* src = fast_src(P, np[c]);
 #pragma unroll
-          for (int k = 0; k < V; ++k) nxt[c][k] = *(const uint4*)(src + np[c] + 16 * k);
+          for (int k = 0; k < V; ++k) {
+            if (kMode & 4) nxt[c][k] = *(const uint4*)(P.data + ((np[c] + 16 * k) & 0xFFFF0ull));
+            else nxt[c][k] = *(const uint4*)(src + np[c] + 16 * k);
+          }
         }
       }
 #pragma unroll
@@ -509,8 +515,8 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
                       C[CH - 1].pos + 16 * k + 8, live, lanes_lt, ev_seg, &ev_count);
         } else {
           const uint4 v = C[0].cur[k];
-          fast_group(P, T, out_e, C[0], v.x, v.y, C[0].pos + 16 * k, live, lanes_lt, ev_seg, &ev_count);
-          fast_group(P, T, out_e, C[0], v.z, v.w, C[0].pos + 16 * k + 8, live, lanes_lt, ev_seg, &ev_count);
+          fast_group<V, kMode>(P, T, out_e, C[0], v.x, v.y, C[0].pos + 16 * k, live, lanes_lt, ev_seg, &ev_count);
+          fast_group<V, kMode>(P, T, out_e, C[0], v.z, v.w, C[0].pos + 16 * k + 8, live, lanes_lt, ev_seg, &ev_count);
         }
       }
 #pragma unroll
@@ -525,6 +531,94 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
           P.span_hi[s0 / kNlBlock] = (C[c].hi & 0x80808080u) ? 1 : 0;
         }
       }
+    }
+    u = un;
+  }
+  if (lane == 0) P.ev_counts[wave] = ev_count < P.ev_cap_per_wave ? ev_count : P.ev_cap_per_wave;
+}
+
+// Deep-prefetch shape of k_scan_fast (one chain per lane): the lane's span
+// streams through a ring of R = D + 1 register sets of V 16-byte vectors, and
+// step s issues the loads of step s + D before walking set s mod R — so every
+// load has D steps of automaton work to land in, for the same registers as
+// the 1x8 cur/nxt pair when R * V = 16.  The ring runs on across the lane's
+// units (kSteps is a multiple of R), so a unit's first steps were prefetched
+// during the previous unit.
+template <int V, int D, int kFastThreads, int kMode = 0>
+__global__ __launch_bounds__(kFastThreads) void k_scan_deep(ScanParams P) {
+  constexpr uint32_t kUnit = kNlBlock;
+  constexpr int kStep = V * 16;
+  constexpr int kSteps = kNlBlock / kStep;
+  constexpr int R = D + 1;
+  static_assert(kSteps % R == 0 && D < kSteps, "ring must tile the span");
+  __shared__ __align__(16) uint8_t smem[kFastImgMax];
+  const AcDev& ac = P.rs.ac;
+  {
+    const uint32_t words = ac.fast_bytes / 4;
+    const uint32_t* src = (const uint32_t*)ac.fast_lds;
+    for (uint32_t i = threadIdx.x; i < words; i += kFastThreads) ((uint32_t*)smem)[i] = src[i];
+  }
+  __syncthreads();
+  const uint8_t* T = smem;
+  const uint32_t out_e = ac.fast_out_entry;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t lanes_lt = (1ull << lane) - 1;
+  const uint32_t wave = (blockIdx.x * (kFastThreads / 64)) + (threadIdx.x >> 6);
+  const uint64_t nlanes = (uint64_t)gridDim.x * kFastThreads;
+  const uint64_t units = (P.nbytes + kUnit - 1) / kUnit;
+  FastEvent* ev_seg = P.events + (uint64_t)wave * P.ev_cap_per_wave;
+  uint32_t ev_count = 0;  // wave-uniform
+  uint64_t u = (uint64_t)blockIdx.x * kFastThreads + threadIdx.x;
+  FastChain<V> C;
+  uint4 buf[R][V];
+  auto load = [&](uint4(&b)[V], uint64_t pos) {
+    const uint8_t* src = fast_src(P, pos);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      if (kMode & 4) b[k] = *(const uint4*)(P.data + ((pos + 16 * k) & 0xFFFF0ull));
+      else b[k] = *(const uint4*)(src + pos + 16 * k);
+    }
+  };
+  if (u < units) {
+#pragma unroll
+    for (int r = 0; r < D; ++r) load(buf[r], u * kUnit + (uint64_t)r * kStep);
+  }
+  // uniform per lane, not per wave: finished lanes walk stale bytes silently
+  while (__ballot(u < units)) {
+    const bool live = u < units;
+    const uint64_t un = u + nlanes;
+    const uint64_t base = u * kUnit;
+    {
+      // warm-up: the 7 bytes before the span (automaton depth <= kAcMaxLit)
+      const uint2 h = live && base >= 8 ? *(const uint2*)(fast_src(P, base - 8) + base - 8) : make_uint2(0, 0);
+      uint32_t e = 0;
+#pragma unroll
+      for (int j = 1; j < 8; ++j) e = fstep(T, e, j < 4 ? fold6(h.x) : fold6(h.y), j & 3);
+      C.e = e;
+      C.prev = h;
+      C.nl = 0;
+      C.hi = 0;
+    }
+    for (int s0 = 0; s0 < kSteps; s0 += R) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int st = s0 + r;
+        const int ps = st + D;  // the step whose loads go out now
+        if (live && (ps < kSteps || un < units))
+          load(buf[(r + D) % R], ps < kSteps ? base + (uint64_t)ps * kStep : un * kUnit + (uint64_t)(ps - kSteps) * kStep);
+        const uint64_t pos = base + (uint64_t)st * kStep;
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+          const uint4 v = buf[r][k];
+          fast_group<V, kMode>(P, T, out_e, C, v.x, v.y, pos + 16 * k, live, lanes_lt, ev_seg, &ev_count);
+          fast_group<V, kMode>(P, T, out_e, C, v.z, v.w, pos + 16 * k + 8, live, lanes_lt, ev_seg, &ev_count);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // no hoisting across steps (register pressure)
+      }
+    }
+    if (live && base < P.nbytes) {
+      P.nl_blocks[base / kNlBlock] = C.nl;
+      P.span_hi[base / kNlBlock] = (C.hi & 0x80808080u) ? 1 : 0;
     }
     u = un;
   }
@@ -715,7 +809,7 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
             bool want_hit = pd.rule_n != 0 && (hist & pd.rqm64) == pd.rq64;
             if (!want_kw && !want_hit) continue;
             const uint32_t tl = pd.len < ac.depth ? pd.len : ac.depth;
-            const uint64_t start = pos + 1 - tl;
+            const uint64_t start = pos + 1 - tl - pd.ext;
             if (pd.trunc) {  // the rest of a long pattern, on the batch (rare)
               if (fi == 0xFFFFFFFFu) fi = file_of_pos(P, pos);
               const uint64_t fend = P.off[fi + 1] - 1;
@@ -1900,17 +1994,7 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
           if (c.prog.cap_names[g] == r.group_name) group_slots.push_back((uint32_t)g);
       d.group_n = (uint32_t)group_slots.size() - d.group_off;
     }
-    if (r.mode == MODE_ANCHORED && !d.gate_always && d.kw_n) {
-      // implied gate: every anchor literal contains one of the rule's keywords
-      const gre::Anchor& an = rs->regexes[r.regex].c.anchor;
-      bool all = !an.lits.empty();
-      for (auto& l : an.lits) {
-        bool has = false;
-        for (auto& kw : r.keywords) has |= !kw.empty() && l.lower.find(kw) != std::string::npos;
-        all &= has;
-      }
-      d.gate_implied = all;
-    }
+    d.gate_implied = r.gate_implied;  // ruleset.cpp: every anchor literal contains a keyword
     if (!d.gate_implied)
       for (auto& kw : r.keywords)
         if (!kw.empty()) kw_needed_ids.insert(kwid[kw]);
@@ -1986,10 +2070,13 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
     d.confirm = p.confirm;
     d.kw_needed = p.kw >= 0 && kw_needed_ids.count((uint32_t)p.kw);
     d.trunc = p.lower.size() > (size_t)ac.depth;
+    d.ext = ac.fast.empty() ? 0 : ac.fast_ext[pats.size()];
     {
+      // window = the 8 bytes ending at the automaton's output byte: the
+      // literal sits `ext` class positions before it
       const size_t tl = std::min<size_t>(p.lower.size(), ac.depth);
       for (size_t k = 0; k < tl; ++k) {
-        const int sh = 8 * (int)(8 - tl + k);
+        const int sh = 8 * (int)(8 - d.ext - tl + k);
         d.lo64 |= (uint64_t)(uint8_t)p.lower[k] << sh;
         d.m64 |= 0xFFull << sh;
         if (p.confirm && p.req[k]) {
@@ -2160,8 +2247,8 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
       blob.insert(blob.end(), (const uint8_t*)p, (const uint8_t*)p + n);
       return o;
     };
-    o_out_off = put(ac.out_off.data(), ac.out_off.size() * 4);
-    o_out_pat = put(ac.out_pat.data(), ac.out_pat.size() * 2);
+    o_out_off = put(ac.fast_out_off.data(), ac.fast_out_off.size() * 4);
+    o_out_pat = put(ac.fast_out_pat.data(), ac.fast_out_pat.size() * 2);
     o_pats = put(pats.data(), pats.size() * sizeof(PatDev));
     o_pbytes = put(pbytes.data(), pbytes.size());
     blob.resize((blob.size() + 15) & ~(size_t)15);
@@ -2256,7 +2343,15 @@ int launch_scan(tsg_engine* e, ScanParams P) {
     // variant: chains per lane x 16-byte vectors per chain step (A/B via TSG_FAST_VARIANT)
     int chains = kFastChains, vecs = kFastVecs;
     bool ring = false;  // TSG_FAST_VARIANT=ring: the two-chain register ring (A/B; spills today)
-    if (const char* v = getenv("TSG_FAST_VARIANT")) ring = sscanf(v, "%dx%d", &chains, &vecs) != 2;
+    int deep_v = 0, deep_d = 0;  // TSG_FAST_VARIANT=d<V>x<D>: k_scan_deep
+    int mode = 0;                // TSG_SCAN_MODE: timing experiments only (see fast_group)
+    if (const char* m = getenv("TSG_SCAN_MODE")) mode = atoi(m);
+    if (const char* v = getenv("TSG_FAST_VARIANT")) {
+      if (sscanf(v, "d%dx%d", &deep_v, &deep_d) != 2) {
+        deep_v = 0;
+        ring = sscanf(v, "%dx%d", &chains, &vecs) != 2;
+      }
+    }
     if (!((chains == 1 && (vecs == 8 || vecs == 4)) || (chains == 2 && (vecs == 4 || vecs == 2)))) {
       chains = kFastChains;
       vecs = kFastVecs;
@@ -2294,6 +2389,15 @@ int launch_scan(tsg_engine* e, ScanParams P) {
     // (the image lives in the kernel's static kFastImgMax array: no dynamic LDS)
     if (e->events) HIP_TRY(hipEventRecord(e->ev[10], s));
     if (ring) hipLaunchKernelGGL(k_scan_ring, dim3(blocks), dim3(nt), 0, s, P);
+#define TSG_DEEP(VV, DD, M)                                                                 \
+  else if (deep_v == VV && deep_d == DD && mode == M)                                      \
+      hipLaunchKernelGGL((k_scan_deep<VV, DD, 1024, M>), dim3(blocks), dim3(nt), 0, s, P);
+    TSG_DEEP(8, 1, 0) TSG_DEEP(4, 3, 0) TSG_DEEP(4, 1, 0) TSG_DEEP(2, 3, 0)
+#undef TSG_DEEP
+#define TSG_MODE(M) \
+  else if (chains == 1 && vecs == 8 && mode == M) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, M>), dim3(blocks), dim3(nt), 0, s, P);
+    TSG_MODE(1) TSG_MODE(2) TSG_MODE(3) TSG_MODE(4) TSG_MODE(5) TSG_MODE(6) TSG_MODE(7)
+#undef TSG_MODE
     else if (chains == 1 && vecs == 8) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1) hipLaunchKernelGGL((k_scan_fast<1, 4, 768>), dim3(blocks), dim3(nt), 0, s, P);
     else if (vecs == 4) hipLaunchKernelGGL((k_scan_fast<2, 4, 1024>), dim3(blocks), dim3(nt), 0, s, P);

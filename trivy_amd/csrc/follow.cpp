@@ -87,21 +87,15 @@ struct SetBuilder {
   void reset() { std::fill(seen.begin(), seen.end(), 0); }
 };
 
-}  // namespace
-
-bool build_follow(const gre::Compiled& c, FollowDfa* out) {
-  *out = FollowDfa{};
+// Q_h: closure of start, then alphabet steps (lengths 1..off_max).
+void anchor_entry(const gre::Compiled& c, SetBuilder& sb, std::vector<uint32_t>* qp, bool* qmatch) {
   const gre::Prog& p = c.prog;
-  if (!c.anchor.valid || p.inst.empty() || p.start == 0) return false;
   const gre::Anchor& a = c.anchor;
-  SetBuilder sb(p);
-  // ---- Q_h: closure of start, then alphabet steps (lengths 1..off_max)
-  std::vector<uint32_t> q;
-  bool qmatch = false;
-  sb.add(p.start, &q, &qmatch);
+  std::vector<uint32_t>& q = *qp;
+  sb.add(p.start, &q, qmatch);
   bool alpha_hi = false;
   for (int b = 128; b < 256; ++b) alpha_hi |= a.alpha.has(b);
-  for (uint32_t k = 0; k < a.off_max && !qmatch; ++k) {
+  for (uint32_t k = 0; k < a.off_max && !*qmatch; ++k) {
     const size_t before = q.size();
     std::vector<uint32_t> nxt;
     for (uint32_t pc : q) {
@@ -111,9 +105,114 @@ bool build_follow(const gre::Compiled& c, FollowDfa* out) {
       if (!step && alpha_hi) step = consumes_some_nonascii(p, in);
       if (step) nxt.push_back(in.out);
     }
-    for (uint32_t pc : nxt) sb.add(pc, &q, &qmatch);  // `seen` keeps q duplicate-free
+    for (uint32_t pc : nxt) sb.add(pc, &q, qmatch);  // `seen` keeps q duplicate-free
     if (q.size() == before) break;  // fixpoint
   }
+}
+
+inline uint32_t fold_col(int b) { return (uint32_t)((b & 0x1F) | ((b >> 1) & 0x20)); }
+
+// The fold-special runes: a file holding one (C4B0 / C5BF / E284AA) is
+// flagged by k_fold_special and scanned whole for every rule (k_full_jobs),
+// its anchor hits dropped — so the scan automaton may assume they are absent.
+inline bool fold_special_rune(uint32_t r) { return r == 0x130 || r == 0x17F || r == 0x212A; }
+
+// Can `in` consume a non-ASCII rune other than the fold-special ones?
+bool consumes_other_nonascii(const gre::Prog& p, const Inst& in) {
+  switch (in.op) {
+    case gre::I_RUNE: {
+      const gre::ClassDesc& cd = p.classes[in.arg];
+      for (uint32_t k = 0; k < cd.nranges; ++k) {
+        const uint32_t lo = p.ranges[cd.range_off + 2 * k], hi = p.ranges[cd.range_off + 2 * k + 1];
+        for (uint32_t r = lo; r <= hi; ++r)
+          if (!fold_special_rune(r)) return true;
+      }
+      return false;
+    }
+    case gre::I_RUNE1: return in.arg >= 128 && !fold_special_rune(in.arg);
+    case gre::I_ANY:
+    case gre::I_ANYNL: return true;
+  }
+  return false;
+}
+
+}  // namespace
+
+// Column sets that every match of the rule must show right after an
+// occurrence of anchor literal `lit` (for the scan automaton: a pattern
+// "literal + classes" fires far less often than the bare literal — e.g.
+// twilio's `SK` followed by two hex digits instead of every "sk" in text).
+// Position j's set is the 6-bit fold columns (k_scan_fast's fold6) of every
+// ASCII byte some NFA state alive there consumes; extension stops at the
+// first position where a non-ASCII rune could be consumed (its bytes alias
+// arbitrary columns), where a match may already have ended, or where the set
+// is every column.  Sound like build_follow: assertions count as satisfied and
+// the alive set is a union over all paths.
+std::vector<uint64_t> follow_ext(const gre::Compiled& c, const gre::Lit& lit, int max_ext) {
+  std::vector<uint64_t> cols;
+  const gre::Prog& p = c.prog;
+  if (!c.anchor.valid || p.inst.empty() || p.start == 0 || max_ext <= 0) return cols;
+  SetBuilder sb(p);
+  std::vector<uint32_t> q;
+  bool m = false;
+  anchor_entry(c, sb, &q, &m);
+  if (m) return cols;
+  auto step = [&](const std::vector<uint32_t>& from, const bool* bytes, std::vector<uint32_t>* to) {
+    sb.reset();
+    to->clear();
+    bool mm = false;
+    for (uint32_t pc : from) {
+      const Inst& in = p.inst[pc];
+      bool any = false;
+      for (int ch = 0; ch < 128 && !any; ++ch) any = bytes[ch] && consumes_ascii(p, in, ch);
+      if (any) sb.add(in.out, to, &mm);
+    }
+    return mm;
+  };
+  std::vector<uint32_t> nx;
+  for (size_t k = 0; k < lit.lower.size(); ++k) {
+    bool bytes[128] = {false};
+    const unsigned char lo = (unsigned char)lit.lower[k], rq = (unsigned char)lit.req[k];
+    if (lo >= 0x80) return cols;
+    if (rq) {
+      bytes[rq & 0x7F] = true;
+    } else {
+      bytes[lo] = true;
+      if (lo >= 'a' && lo <= 'z') bytes[lo - 32] = true;
+    }
+    if (step(q, bytes, &nx)) return cols;  // a match can end inside the literal
+    q.swap(nx);
+    if (q.empty()) return cols;
+  }
+  for (int j = 0; j < max_ext; ++j) {
+    bool bytes[128] = {false};
+    uint64_t mask = 0;
+    for (uint32_t pc : q) {
+      const Inst& in = p.inst[pc];
+      if (consumes_other_nonascii(p, in)) return cols;
+      for (int ch = 0; ch < 128; ++ch)
+        if (consumes_ascii(p, in, ch)) {
+          bytes[ch] = true;
+          mask |= 1ull << fold_col(ch);
+        }
+    }
+    if (mask == ~0ull || mask == 0) return cols;
+    cols.push_back(mask);
+    if (step(q, bytes, &nx)) return cols;  // a match may end here: nothing after is required
+    q.swap(nx);
+    if (q.empty()) return cols;
+  }
+  return cols;
+}
+
+bool build_follow(const gre::Compiled& c, FollowDfa* out) {
+  *out = FollowDfa{};
+  const gre::Prog& p = c.prog;
+  if (!c.anchor.valid || p.inst.empty() || p.start == 0) return false;
+  SetBuilder sb(p);
+  std::vector<uint32_t> q;
+  bool qmatch = false;
+  anchor_entry(c, sb, &q, &qmatch);
   if (qmatch) return false;  // a match can end right at h: nothing to filter
   std::sort(q.begin(), q.end());
   // ---- byte classes over ASCII: bytes accepted by the same consuming insts

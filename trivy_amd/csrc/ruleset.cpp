@@ -2,6 +2,7 @@
 // pkg/fanal/secret/scanner.go:84-95,191-221 into the engine's compiled form:
 // Go-RE2 programs (gre.cpp), anchor literals, and one Aho-Corasick automaton
 // over every keyword (MatchKeywords, scanner.go:169-181) and anchor literal.
+#include <algorithm>
 #include <atomic>
 #include <cstring>
 #include <deque>
@@ -159,54 +160,159 @@ static bool build_ac_depth(tsg_ruleset* rs, int depth, std::string* err) {
     for (auto x : outs[s]) ac.out_pat.push_back(x);
   }
   ac.out_off[S] = (uint32_t)ac.out_pat.size();
-  // k_scan_fast LDS image: one kFastRowBytes row per state, kFastCols columns
-  // indexed by the 6-bit folded byte (engine.hip fold6: both letter cases
-  // share a column; control bytes, bytes >= 0x80 and a few rare ASCII bytes
-  // alias other columns, so every reported pattern is confirmed on the real
-  // bytes by k_report).  Entry = next row's offset / 2, so a step is
-  // T[2 * (e + col)].
-  // Only for all-ASCII pattern sets (the fold-special sequences are found by
-  // the replay instead) whose rows fit 16-bit entries and k_report's LDS.
+  return true;
+}
+
+// k_scan_fast's automaton: a DFA over the 64 fold columns (engine.hip fold6:
+// both letter cases share a column; control bytes, bytes >= 0x80 and a few
+// rare ASCII bytes alias other columns, so every reported pattern is
+// confirmed on the real bytes by k_report) for the patterns truncated to
+// `depth`, each anchor-only literal followed by plan[pattern] of its required
+// column sets (PatternHost::ext_cols).  Built by subset construction
+// over items (pattern, columns matched); a state's outputs are the patterns
+// completed on entering it, and output states are numbered last so the scan
+// detects an output with one max() per byte.  Entry = next row's offset / 2,
+// so a step is T[2 * (e + col)].  Only for all-ASCII pattern sets whose rows
+// fit 16-bit entries and the LDS image (the fold-special sequences are found
+// by k_fold_special instead).
+static bool build_fast(tsg_ruleset* rs, int depth, const std::vector<uint8_t>& plan) {
+  AcHost& ac = rs->ac;
   ac.fast.clear();
-  bool ascii_only = true;
+  ac.fast_out_off.clear();
+  ac.fast_out_pat.clear();
+  ac.fast_states = 0;
+  ac.fast_out_entry = 0;
+  ac.fast_ext.assign(rs->patterns.size(), 0);
   for (auto& p : rs->patterns)
     if (!p.special)
-      for (unsigned char c : p.lower) ascii_only &= c < 0x80;
+      for (unsigned char c : p.lower)
+        if (c >= 0x80) return false;
   constexpr uint32_t kRowU16 = kFastRowBytes / 2;
-  const size_t img = ((size_t)S * kFastRowBytes + 3) & ~(size_t)3;
-  // column of byte b after k_scan_fast's fold: bits 0-4 kept, bit 6 -> bit 5;
-  // each column takes the class of the pattern bytes folding onto it, and two
-  // different pattern classes on one column rule the image out
-  int col_cls[kFastCols];
-  bool fold_ok = true;
-  for (uint32_t v = 0; v < kFastCols; ++v) col_cls[v] = -1;
-  for (int b = 0; b < 128; ++b) {  // bytes >= 0x80 never sit inside an ASCII pattern
-    const int v = (b & 0x1F) | ((b >> 1) & 0x20);
-    const int c = cmap[b];
-    if (c == 0) continue;
-    if (col_cls[v] >= 0 && col_cls[v] != c) fold_ok = false;
-    col_cls[v] = c;
-  }
-  for (uint32_t v = 0; v < kFastCols; ++v)
-    if (col_cls[v] < 0) col_cls[v] = 0;
-  if (ascii_only && fold_ok && img <= kFastImgMax && (size_t)(S - 1) * kRowU16 < 65536) {
-    ac.fast.assign(img, 0);
-    for (int st = 0; st < S; ++st) {
-      uint16_t* row = reinterpret_cast<uint16_t*>(ac.fast.data() + (size_t)st * kFastRowBytes);
-      for (uint32_t v = 0; v < kFastCols; ++v) row[v] = (uint16_t)(go[st][col_cls[v]] * kRowU16);
+  const size_t max_rows = std::min<size_t>(kFastImgMax / kFastRowBytes, 65536 / kRowU16);
+  // per pattern: the column-mask sequence the automaton walks
+  std::vector<std::vector<uint64_t>> seq(rs->patterns.size());
+  std::vector<std::vector<uint32_t>> starts(kFastCols);  // patterns whose first mask holds column v
+  for (size_t pi = 0; pi < rs->patterns.size(); ++pi) {
+    const PatternHost& p = rs->patterns[pi];
+    if (p.special) continue;
+    const size_t tl = std::min<size_t>(p.lower.size(), (size_t)depth);
+    for (size_t k = 0; k < tl; ++k) {
+      const int b = (unsigned char)p.lower[k];
+      seq[pi].push_back(1ull << ((b & 0x1F) | ((b >> 1) & 0x20)));
     }
-    ac.fast_out_entry = (uint32_t)first_out * kRowU16;
+    if (plan[pi] && p.lower.size() < (size_t)depth) {
+      const size_t e = std::min<size_t>({p.ext_cols.size(), (size_t)plan[pi], (size_t)depth - p.lower.size()});
+      for (size_t j = 0; j < e; ++j) seq[pi].push_back(p.ext_cols[j]);
+      ac.fast_ext[pi] = (uint8_t)e;
+    }
+    for (uint32_t v = 0; v < kFastCols; ++v)
+      if (!seq[pi].empty() && ((seq[pi][0] >> v) & 1)) starts[v].push_back((uint32_t)pi);
   }
+  using Item = uint32_t;  // pattern << 4 | columns matched (1..7)
+  struct Key {
+    std::vector<Item> items;
+    std::vector<uint16_t> outs;
+    bool operator<(const Key& o) const { return items != o.items ? items < o.items : outs < o.outs; }
+  };
+  std::map<Key, int> ids;
+  std::vector<Key> states;
+  states.push_back(Key{});
+  ids[states[0]] = 0;
+  std::vector<std::vector<int>> go;
+  for (size_t s = 0; s < states.size(); ++s) {
+    if (states.size() > max_rows) return false;
+    go.emplace_back(kFastCols, 0);
+    const std::vector<Item> cur = states[s].items;
+    for (uint32_t v = 0; v < kFastCols; ++v) {
+      Key k;
+      auto advance = [&](uint32_t pi, uint32_t i) {  // pattern pi matched i columns, column v next
+        if (!((seq[pi][i] >> v) & 1)) return;
+        if (i + 1 == seq[pi].size()) k.outs.push_back((uint16_t)pi);
+        else k.items.push_back((pi << 4) | (i + 1));
+      };
+      for (Item it : cur) advance(it >> 4, it & 15);
+      for (uint32_t pi : starts[v]) advance(pi, 0);
+      std::sort(k.items.begin(), k.items.end());
+      k.items.erase(std::unique(k.items.begin(), k.items.end()), k.items.end());
+      std::sort(k.outs.begin(), k.outs.end());
+      k.outs.erase(std::unique(k.outs.begin(), k.outs.end()), k.outs.end());
+      auto it = ids.find(k);
+      int t;
+      if (it != ids.end()) {
+        t = it->second;
+      } else {
+        t = (int)states.size();
+        ids.emplace(k, t);
+        states.push_back(std::move(k));
+      }
+      go[s][v] = t;
+    }
+  }
+  const int S = (int)states.size();
+  if ((size_t)S > max_rows) return false;
+  // renumber: start first, states without outputs, then output states
+  std::vector<int> perm(S), inv;
+  for (int st = 0; st < S; ++st)
+    if (states[st].outs.empty()) { perm[st] = (int)inv.size(); inv.push_back(st); }
+  const int first_out = (int)inv.size();
+  for (int st = 0; st < S; ++st)
+    if (!states[st].outs.empty()) { perm[st] = (int)inv.size(); inv.push_back(st); }
+  const size_t img = ((size_t)S * kFastRowBytes + 3) & ~(size_t)3;
+  ac.fast.assign(img, 0);
+  ac.fast_out_off.assign(S + 1, 0);
+  for (int n = 0; n < S; ++n) {
+    uint16_t* row = reinterpret_cast<uint16_t*>(ac.fast.data() + (size_t)n * kFastRowBytes);
+    for (uint32_t v = 0; v < kFastCols; ++v) row[v] = (uint16_t)(perm[go[inv[n]][v]] * kRowU16);
+    ac.fast_out_off[n] = (uint32_t)ac.fast_out_pat.size();
+    for (auto x : states[inv[n]].outs) ac.fast_out_pat.push_back(x);
+  }
+  ac.fast_out_off[S] = (uint32_t)ac.fast_out_pat.size();
+  ac.fast_out_entry = (uint32_t)first_out * kRowU16;
+  ac.fast_states = (uint32_t)S;
   return true;
 }
 
 // The deepest trie (<= kAcMaxLit) whose automaton fits k_scan_fast's LDS
 // image; longer patterns are confirmed on hit.  Falls back to depth
 // kAcMaxLit for the generic kernel when none fits.
+//
+// Scan-automaton extensions are tried longest first at each depth: they cut
+// the scan's events (and k_report's work) by the selectivity of the classes.
 bool build_ac(tsg_ruleset* rs, std::string* err) {
   for (int d = kAcMaxLit; d >= 4; --d) {
     if (!build_ac_depth(rs, d, err)) return false;
-    if (!rs->ac.fast.empty()) return true;
+    std::vector<uint8_t> plan(rs->patterns.size(), 0);
+    if (!build_fast(rs, d, plan)) continue;
+    // greedy, shortest literals first (the frequent ones): extend every
+    // literal shorter than t to t columns where the automaton still fits
+    for (int t = 3; t <= kFastExtTo; ++t) {
+      std::vector<uint8_t> want = plan;
+      std::vector<size_t> grow;
+      for (size_t pi = 0; pi < rs->patterns.size(); ++pi) {
+        const PatternHost& p = rs->patterns[pi];
+        const size_t e = std::min<size_t>(p.ext_cols.size(), p.lower.size() < (size_t)t ? t - p.lower.size() : 0);
+        if (e > want[pi]) {
+          want[pi] = (uint8_t)e;
+          grow.push_back(pi);
+        }
+      }
+      if (grow.empty()) continue;
+      if (build_fast(rs, d, want)) {
+        plan = want;
+        continue;
+      }
+      std::stable_sort(grow.begin(), grow.end(), [&](size_t a, size_t b) {
+        return rs->patterns[a].lower.size() < rs->patterns[b].lower.size();
+      });
+      for (size_t pi : grow) {
+        std::vector<uint8_t> one = plan;
+        one[pi] = want[pi];
+        if (build_fast(rs, d, one)) plan = one;
+      }
+      break;
+    }
+    if (!build_fast(rs, d, plan)) return false;  // cannot happen: plan was built
+    return true;
   }
   return build_ac_depth(rs, kAcMaxLit, err);
 }
@@ -335,6 +441,19 @@ int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_r
         build_follow(c, &r.follow);
         build_dfa(c, &r.dfa);
       }
+      // implied gate: every anchor literal contains one of the rule's keywords
+      // (so a hit proves MatchKeywords, scanner.go:169-181)
+      bool kw_ok = !r.keywords.empty();
+      for (auto& kw : r.keywords) kw_ok &= !kw.empty();
+      if (r.mode == MODE_ANCHORED && kw_ok) {
+        bool all = !c.anchor.lits.empty();
+        for (auto& l : c.anchor.lits) {
+          bool has = false;
+          for (auto& kw : r.keywords) has |= l.lower.find(kw) != std::string::npos;
+          all &= has;
+        }
+        r.gate_implied = all;
+      }
     }
     for (auto& kw : r.keywords) {
       if (!kwid.count(kw) && !kw.empty()) {
@@ -375,9 +494,37 @@ int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_r
         ph.rules.push_back((uint32_t)ri);
     }
   }
-  if (rs->patterns.size() >= 65535) {
+  if (rs->patterns.size() >= 4095) {  // build_fast items: pattern << 4
     e = "too many keyword/anchor literals";
     return fail(TSG_ERR_UNSUPPORTED);
+  }
+  // scan-automaton extensions: for anchor-only patterns (no keyword some
+  // non-implied gate needs), the column sets every anchored use requires next
+  {
+    std::vector<uint8_t> kw_needed(rs->keywords.size(), 0);
+    for (auto& r : rs->rules)
+      if (!r.gate_implied)
+        for (auto& kw : r.keywords)
+          for (size_t k = 0; k < rs->keywords.size(); ++k)
+            if (!kw.empty() && rs->keywords[k] == kw) kw_needed[k] = 1;
+    for (auto& ph : rs->patterns) {
+      if (ph.special || ph.rules.empty() || (ph.kw >= 0 && kw_needed[ph.kw])) continue;
+      bool first = true;
+      for (uint32_t ri : ph.rules) {
+        const gre::Compiled& c = rs->regexes[rs->rules[ri].regex].c;
+        for (auto& lit : c.anchor.lits) {
+          if (lit.lower != ph.lower) continue;
+          std::vector<uint64_t> cols = follow_ext(c, lit, kAcMaxLit);
+          if (first) {
+            ph.ext_cols = cols;
+            first = false;
+          } else {
+            if (cols.size() < ph.ext_cols.size()) ph.ext_cols.resize(cols.size());
+            for (size_t j = 0; j < ph.ext_cols.size(); ++j) ph.ext_cols[j] |= cols[j];
+          }
+        }
+      }
+    }
   }
   if (!build_ac(rs, &e)) return fail(TSG_ERR_UNSUPPORTED);
   *out = rs;
@@ -413,6 +560,26 @@ int tsg_ruleset_rule_literal(const tsg_ruleset* rs, size_t i, size_t k, char* lo
   if (cap < L.lower.size()) return TSG_ERR_INVALID_ARG;
   if (lower) memcpy(lower, L.lower.data(), L.lower.size());
   if (req) memcpy(req, L.req.data(), L.req.size());
+  return TSG_OK;
+}
+
+// Scan-automaton pattern k (diagnostics / soundness tests): its lowercased
+// literal, the class positions k_scan_fast's automaton requires after it
+// (*ext, 0 without a fast image) and their fold-column masks (cols[0..ext)).
+int tsg_ruleset_scan_pattern(const tsg_ruleset* rs, size_t k, char* lower, size_t cap, size_t* len, uint32_t* ext,
+                             uint64_t* cols, uint32_t* fast_states) {
+  if (!rs || k >= rs->patterns.size() || !len) return TSG_ERR_INVALID_ARG;
+  const PatternHost& p = rs->patterns[k];
+  *len = p.lower.size();
+  if (lower) {
+    if (cap < p.lower.size()) return TSG_ERR_INVALID_ARG;
+    memcpy(lower, p.lower.data(), p.lower.size());
+  }
+  const uint32_t e = rs->ac.fast.empty() ? 0 : rs->ac.fast_ext[k];
+  if (ext) *ext = e;
+  if (cols)
+    for (uint32_t j = 0; j < e; ++j) cols[j] = p.ext_cols[j];
+  if (fast_states) *fast_states = rs->ac.fast_states;
   return TSG_OK;
 }
 
