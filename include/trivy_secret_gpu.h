@@ -128,6 +128,10 @@ int tsg_ruleset_rule_literal(const tsg_ruleset* rs, size_t i, size_t k, char* lo
 int tsg_ruleset_scan_pattern(const tsg_ruleset* rs, size_t k, char* lower, size_t cap, size_t* len, uint32_t* ext,
                              uint64_t* cols, uint32_t* fast_states);
 
+/* k_scan_fast's LDS image: up to cap bytes into buf, *len = its size (0 when
+ * the ruleset has no fast image), *out_entry = the first output state's entry. */
+int tsg_ruleset_scan_image(const tsg_ruleset* rs, uint8_t* buf, size_t cap, size_t* len, uint32_t* out_entry);
+
 /* Instruction count and capture slots of rule i's compiled regex. */
 int tsg_ruleset_rule_prog(const tsg_ruleset* rs, size_t i, uint32_t* n_inst, uint32_t* n_cap);
 

@@ -16,8 +16,9 @@ constexpr uint32_t kNlBlock = 4096;  // newline-count granularity (bytes) = one 
 constexpr uint32_t kNoKw = 0xFFFFFFFFu;
 
 constexpr uint32_t kFastCols = 64;             // k_scan_fast columns (6-bit folded bytes, engine.hip fold6)
-constexpr uint32_t kFastRowBytes = 130;       // 64 u16 columns + 2 B: consecutive rows rotate LDS banks
-constexpr uint32_t kFastImgMax = 132 * 1024;  // k_scan_fast image budget (1008 rows: 16-bit entries)
+constexpr uint32_t kFastRowBytes = 134;       // 64 u16 columns + 6 B: consecutive rows rotate LDS banks
+constexpr uint32_t kFastMaxRows = 1008;
+constexpr uint32_t kFastImgMax = kFastMaxRows * kFastRowBytes;  // k_scan_fast image budget (LDS)
 constexpr uint32_t kLdsMax = 160 * 1024;      // LDS per CU
 constexpr uint32_t kFastSpecialEv = 0xFFFF;   // event tag: U+0130/U+017F/U+212A sequence ends here
 constexpr uint32_t kFollowMaxStates = 1024;  // follow-DFA subset-construction budget

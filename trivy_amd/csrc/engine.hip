@@ -297,7 +297,6 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_generic(ScanParams P) {
 //    the fold-special sequences C4B0 / C5BF / E284AA exactly
 //  * the newline count of each span goes straight to nl_blocks (one owner,
 //    plain store) and feeds StartLine/EndLine.
-constexpr uint32_t kFastRowU16 = kFastRowBytes / 2;
 // Variant in use (chains per lane, 16-byte vectors per chain step); the
 // other shapes stay compilable for A/B runs (TSG_FAST_VARIANT).
 constexpr int kFastChains = 1;
@@ -310,21 +309,25 @@ __device__ inline uint32_t nl_count_dword(uint32_t w) {
   return __builtin_popcount(z);
 }
 
-// 6-bit column fold, four bytes at once: bits 0-4 kept, bit 6 moved to bit 5.
-// Both letter cases share columns 32-58, digits and punctuation sit in 0-31,
-// and a 64-column row spans the 32 LDS banks exactly once (two columns per
-// dword), so lanes in one state never collide on a bank, and the 130-byte
-// rows keep two images per CU.  Control bytes alias space/punctuation,
-// `{|}~ and DEL alias @[\]^_, bytes >= 0x80 alias ASCII: k_report re-checks
-// every pattern on the real bytes.
-__device__ inline uint32_t fold6(uint32_t w) { return (w & 0x1F1F1F1Fu) | ((w >> 1) & 0x20202020u); }
+// 6-bit column fold, four bytes at once, each byte = 2 x column (the byte
+// offset of its u16 entry in a row): column = bits 0-4 kept, bit 6 moved to
+// bit 5.  Both letter cases share columns 32-58, digits and punctuation sit
+// in 0-31, and a row's 64 entries cover the 32 LDS banks once (two columns
+// per dword), so lanes in one state never collide on a bank.  Control bytes
+// alias space/punctuation, `{|}~ and DEL alias @[\]^_, bytes >= 0x80 alias
+// ASCII: k_report re-checks every pattern on the real bytes.
+__device__ inline uint32_t fold6(uint32_t w) { return ((w << 1) & 0x3E3E3E3Eu) | (w & 0x40404040u); }
 
-// One automaton step on byte j of a folded dword w: e = T[e + col] (u16 units).
+// One automaton step on byte j of a folded dword w: e = T[e * row + 2 col].
+// Entries are row indices and rows are kFastRowBytes apart (a stride an LDS
+// bank-conflict simulation of the scan picked: 134 B conflicts ~13 % less
+// than packed 130 B rows); the address is one v_mad_u32_u24 on the chain.
 __device__ inline uint32_t fstep(const uint8_t* T, uint32_t e, uint32_t w, int j) {
-  const uint32_t b = (w >> (8 * j)) & 0x3Fu;
-  uint32_t a;
-  asm("v_add_lshl_u32 %0, %1, %2, 1" : "=v"(a) : "v"(e), "v"(b));  // one VALU on the dependent chain
-  return *(const uint16_t*)(T + a);
+  uint32_t c2;  // byte j (one VALU; the compiler splits a masked shift in two)
+  if (j == 0) c2 = w & 0xFFu;
+  else if (j == 3) c2 = w >> 24;
+  else asm("v_bfe_u32 %0, %1, %2, 8" : "=v"(c2) : "v"(w), "i"(8 * j));
+  return *(const uint16_t*)(T + (e * kFastRowBytes + c2));
 }
 
 
@@ -729,7 +732,7 @@ __global__ __launch_bounds__(1024) void k_scan_ring(ScanParams P) {
 // atomic, file looked up once per event) and anchor hit (LDS-staged, one
 // global reservation per block step).
 constexpr uint32_t kReportThreads = 1024;
-constexpr uint32_t kReportHitCap = 2048;
+constexpr uint32_t kReportHitCap = 1024;
 constexpr uint32_t kReportLds = kLdsMax - kReportHitCap * 8 - 64;
 
 __device__ inline uint32_t file_of_pos(const ScanParams& P, uint64_t pos) {
@@ -799,7 +802,7 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
           hlow = (hlow >> 8) | ((uint64_t)lower_ascii((uint8_t)c) << 56);
           if (e < out_e || c >= 0x80) continue;  // an output ending on a byte >= 0x80 is an alias
           const uint64_t pos = ev.pos + j;
-          const uint32_t st = e / kFastRowU16;
+          const uint32_t st = e;
           for (uint32_t o = out_off[st]; o < out_off[st + 1]; ++o) {
             const uint32_t pid = out_pat[o];
             const PatDev& pd = pats[pid];
@@ -2371,8 +2374,9 @@ int launch_scan(tsg_engine* e, ScanParams P) {
     P.span_hi = e->span_hi.p;
     // shape: 1x8 = 1024 threads, one block per CU (120 VGPRs); 1x4 = 768
     // threads, two blocks per CU (two LDS images, 24 waves); 2x4 = 1024, one
-    const uint32_t nt = (!ring && ((chains == 1 && vecs == 4) || (chains == 2 && vecs == 2))) ? 768 : 1024;
-    const uint32_t per_cu = nt == 768 ? 2 : 1;
+    // every shape: 1024 threads, one block per CU (the image takes most of the LDS)
+    const uint32_t nt = 1024;
+    const uint32_t per_cu = 1;
     const uint32_t blocks = (uint32_t)std::max<uint64_t>(
         1, std::min<uint64_t>((units + nt - 1) / nt, (uint64_t)e->num_cus * per_cu));
     // per-wave event segments (an output group per ~KiB of source text; 4x headroom)
@@ -2399,9 +2403,9 @@ int launch_scan(tsg_engine* e, ScanParams P) {
     TSG_MODE(1) TSG_MODE(2) TSG_MODE(3) TSG_MODE(4) TSG_MODE(5) TSG_MODE(6) TSG_MODE(7)
 #undef TSG_MODE
     else if (chains == 1 && vecs == 8) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024>), dim3(blocks), dim3(nt), 0, s, P);
-    else if (chains == 1) hipLaunchKernelGGL((k_scan_fast<1, 4, 768>), dim3(blocks), dim3(nt), 0, s, P);
+    else if (chains == 1) hipLaunchKernelGGL((k_scan_fast<1, 4, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     else if (vecs == 4) hipLaunchKernelGGL((k_scan_fast<2, 4, 1024>), dim3(blocks), dim3(nt), 0, s, P);
-    else hipLaunchKernelGGL((k_scan_fast<2, 2, 768>), dim3(blocks), dim3(nt), 0, s, P);
+    else hipLaunchKernelGGL((k_scan_fast<2, 2, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     HIP_TRY(hipGetLastError());
     if (e->events) HIP_TRY(hipEventRecord(e->ev[11], s));
     e->fast_timed = e->events;

@@ -171,8 +171,8 @@ static bool build_ac_depth(tsg_ruleset* rs, int depth, std::string* err) {
 // column sets (PatternHost::ext_cols).  Built by subset construction
 // over items (pattern, columns matched); a state's outputs are the patterns
 // completed on entering it, and output states are numbered last so the scan
-// detects an output with one max() per byte.  Entry = next row's offset / 2,
-// so a step is T[2 * (e + col)].  Only for all-ASCII pattern sets whose rows
+// detects an output with one max() per byte.  Entry = next row's index, so a
+// step reads the u16 at e * kFastRowBytes + 2 * col.  Only for all-ASCII pattern sets whose rows
 // fit 16-bit entries and the LDS image (the fold-special sequences are found
 // by k_fold_special instead).
 static bool build_fast(tsg_ruleset* rs, int depth, const std::vector<uint8_t>& plan) {
@@ -187,8 +187,7 @@ static bool build_fast(tsg_ruleset* rs, int depth, const std::vector<uint8_t>& p
     if (!p.special)
       for (unsigned char c : p.lower)
         if (c >= 0x80) return false;
-  constexpr uint32_t kRowU16 = kFastRowBytes / 2;
-  const size_t max_rows = std::min<size_t>(kFastImgMax / kFastRowBytes, 65536 / kRowU16);
+  const size_t max_rows = kFastMaxRows;
   // per pattern: the column-mask sequence the automaton walks
   std::vector<std::vector<uint64_t>> seq(rs->patterns.size());
   std::vector<std::vector<uint32_t>> starts(kFastCols);  // patterns whose first mask holds column v
@@ -262,12 +261,12 @@ static bool build_fast(tsg_ruleset* rs, int depth, const std::vector<uint8_t>& p
   ac.fast_out_off.assign(S + 1, 0);
   for (int n = 0; n < S; ++n) {
     uint16_t* row = reinterpret_cast<uint16_t*>(ac.fast.data() + (size_t)n * kFastRowBytes);
-    for (uint32_t v = 0; v < kFastCols; ++v) row[v] = (uint16_t)(perm[go[inv[n]][v]] * kRowU16);
+    for (uint32_t v = 0; v < kFastCols; ++v) row[v] = (uint16_t)perm[go[inv[n]][v]];
     ac.fast_out_off[n] = (uint32_t)ac.fast_out_pat.size();
     for (auto x : states[inv[n]].outs) ac.fast_out_pat.push_back(x);
   }
   ac.fast_out_off[S] = (uint32_t)ac.fast_out_pat.size();
-  ac.fast_out_entry = (uint32_t)first_out * kRowU16;
+  ac.fast_out_entry = (uint32_t)first_out;
   ac.fast_states = (uint32_t)S;
   return true;
 }
@@ -580,6 +579,17 @@ int tsg_ruleset_scan_pattern(const tsg_ruleset* rs, size_t k, char* lower, size_
   if (cols)
     for (uint32_t j = 0; j < e; ++j) cols[j] = p.ext_cols[j];
   if (fast_states) *fast_states = rs->ac.fast_states;
+  return TSG_OK;
+}
+
+// k_scan_fast's LDS image (diagnostics / layout studies): copies up to cap
+// bytes, *len = image bytes (0 = no fast image), *out_entry = first output
+// state's entry (entries are row offsets / 2).
+int tsg_ruleset_scan_image(const tsg_ruleset* rs, uint8_t* buf, size_t cap, size_t* len, uint32_t* out_entry) {
+  if (!rs || !len) return TSG_ERR_INVALID_ARG;
+  *len = rs->ac.fast.size();
+  if (out_entry) *out_entry = rs->ac.fast_out_entry;
+  if (buf) memcpy(buf, rs->ac.fast.data(), std::min(cap, rs->ac.fast.size()));
   return TSG_OK;
 }
 
