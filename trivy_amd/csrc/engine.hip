@@ -80,6 +80,7 @@ struct Ctrl {
   unsigned int pad;
   unsigned long long ev_overflow;
   unsigned long long outputs;  // patterns k_report resolved (diagnostics)
+  unsigned long long n_special;  // files flagged kFileSpecial (ScanParams::special_files)
 };
 
 struct DevLoc {
@@ -113,7 +114,20 @@ struct ScanParams {
   struct FastEvent* ev_overflow;  // events beyond a wave's segment
   uint64_t ev_overflow_cap;
   uint8_t* span_hi;               // per kNlBlock span: a byte >= 0x80 occurs (k_fold_special)
+  uint32_t* special_files;        // files flagged kFileSpecial, ctrl->n_special of them
 };
+
+// Flag a file as holding a fold-special sequence; the first flagger lists it
+// for k_special_gate (so that kernel visits flagged files only).
+__device__ inline void mark_special(const ScanParams& P, uint32_t fi) {
+  if (P.file_flags[fi] & kFileSpecial) return;
+  const uint32_t old = atomicOr(&P.file_flags[fi], kFileSpecial);
+  if (!(old & kFileSpecial)) {
+    const unsigned long long k = atomicAdd(&P.ctrl->n_special, 1ull);
+    if (k < P.n_files) P.special_files[k] = fi;
+  }
+}
+
 
 // region_file[r] = index of the file holding byte r * kNlBlock = the largest f
 // with off[f] <= r * kNlBlock: each file marks the first region boundary at or
@@ -180,7 +194,7 @@ __device__ inline void report_t(const ScanParams& P, uint32_t st, uint64_t p, ui
       for (uint32_t k = ac.depth; k < pd.len && ok; ++k) ok = lower_ascii(P.data[start + k]) == pb[k];
       if (!ok) continue;
     }
-    if (pd.special) atomicOr(&P.file_flags[fi], kFileSpecial);
+    if (pd.special) mark_special(P, fi);
     if (pd.kw != kNoKw) {
       const uint64_t key = ((uint64_t)fi << 32) | pd.kw;  // per-lane dedupe of repeated keywords
       if (*last_kw != key) {
@@ -366,10 +380,10 @@ template <int V>
 __device__ inline void fast_event(const ScanParams& P, uint32_t out_e, const FastChain<V>& C, uint32_t m, uint32_t gs,
                                   uint32_t d0, uint32_t d1, uint64_t gpos, bool live, uint64_t lanes_lt,
                                   FastEvent* ev_seg, uint32_t* ev_count) {
-  const bool ev = live && m >= out_e;
-  const uint64_t b = __ballot(ev);
+  // lane mask straight from the compare (uge), live lanes only
+  const uint64_t b = __builtin_amdgcn_uicmp(m, out_e, 35) & __ballot(live);
   if (b) {
-    if (ev) {
+    if ((b >> __lane_id()) & 1) {
       FastEvent r;
       r.pos = gpos;
       r.entry = gs;
@@ -889,7 +903,7 @@ __global__ __launch_bounds__(256) void k_fold_special(ScanParams P, uint64_t n_s
       for (uint64_t q = a; q < b; ++q) {
         const uint32_t c = P.data[q];
         if ((c == 0xB0 && b1 == 0xC4) || (c == 0xBF && b1 == 0xC5) || (c == 0xAA && b1 == 0x84 && b2 == 0xE2))
-          atomicOr(&P.file_flags[file_of_pos(P, q)], kFileSpecial);
+          mark_special(P, file_of_pos(P, q));
         b2 = b1;
         b1 = c;
       }
@@ -1116,7 +1130,7 @@ __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
     for (uint32_t k = 0; k < G.n_gpath && !allowed; ++k)
       allowed = may(G.gpath[k]) && match_string(G.rs.progs[G.gpath[k]], path, plen, sc);
     if (allowed) {
-      G.file_flags[f] |= kFileAllowed;
+      atomicOr(&G.file_flags[f], kFileAllowed);  // the scan flags files concurrently (side stream)
       continue;
     }
     if (!G.any_rule_paths) continue;
@@ -1859,6 +1873,7 @@ struct tsg_engine {
   DBuf<FastEvent> ev_buf, ev_overflow;
   DBuf<uint64_t> vprof;
   DBuf<uint8_t> span_hi;
+  DBuf<uint32_t> special_files;
   DBuf<uint32_t> ev_counts;
   uint64_t ev_ovf_need = 0;  // overflow-event capacity learnt from a lost scan
   bool fast_timed = false;   // ev[10..11] bracket the last k_scan_fast launch
@@ -2433,6 +2448,15 @@ int launch_scan(tsg_engine* e, ScanParams P) {
 }
 
 // Run the device pipeline on a batch already in HBM.  Fills r->impl.locs and flags.
+// Exact keyword gates of the files mark_special listed: one wave per file.
+int launch_special_gate(tsg_engine* e, const ScanParams& P, uint64_t n_special) {
+  if (!n_special) return TSG_OK;
+  const uint64_t waves = std::min<uint64_t>(std::min<uint64_t>(n_special, P.n_files), 16384);
+  hipLaunchKernelGGL(k_special_gate, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, e->stream, P);
+  HIP_TRY(hipGetLastError());
+  return TSG_OK;
+}
+
 int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, const uint64_t* d_off,
                  const uint8_t* d_paths, const uint64_t* d_path_off, size_t n_files, uint64_t nbytes,
                  tsg_result* res) {
@@ -2467,8 +2491,10 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     e->events = true;
   }
   HIP_TRY(hipEventRecord(e->ev[0], s));
-  // ---- 1. path gates
-  if (nf && (im.n_gpath || rs->any_path_rules)) {
+  // ---- 1. path gates (per file).  Not overlapped with the scan: the scan
+  // fills every CU's VGPRs, so a side-stream launch only delays k_report.
+  const bool path_gates = nf && (im.n_gpath || rs->any_path_rules);
+  if (path_gates) {
     GateParams G{};
     G.off = d_off;
     G.paths = d_paths;
@@ -2518,6 +2544,8 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   P.hits = e->hits.p;
   P.hit_cap = hit_cap;
   P.ctrl = e->ctrl.p;
+  HIP_TRY(e->special_files.ensure(nf + 1));
+  P.special_files = e->special_files.p;
   const uint64_t n_nlb = nbytes / kNlBlock + 2;
   HIP_TRY(e->nl_blocks.ensure(n_nlb));
   HIP_TRY(e->nl_pre.ensure(n_nlb));
@@ -2527,18 +2555,19 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(hipEventRecord(e->ev[8], s));
     if ((rc = launch_scan(e, P))) return rc;
     HIP_TRY(hipEventRecord(e->ev[9], s));
-    hipLaunchKernelGGL(k_special_gate, dim3(std::max(1u, std::min<uint32_t>((nf + 3) / 4, 4096))), dim3(256), 0, s, P);
-    HIP_TRY(hipGetLastError());
     Ctrl c;
     if ((rc = read_ctrl(e, &c))) return rc;
     const bool ev_lost = rs->ac.fast.size() && c.ev_overflow > e->ev_overflow.n;
-    if (c.hits <= hit_cap && !ev_lost) break;
+    if (c.hits <= hit_cap && !ev_lost) {
+      if ((rc = launch_special_gate(e, P, c.n_special))) return rc;
+      break;
+    }
     // overflow: grow and rescan (keyword bits are idempotent)
     if (ev_lost) e->ev_ovf_need = c.ev_overflow + (c.ev_overflow >> 2);
     HIP_TRY(e->hits.ensure(c.hits));
     hit_cap = P.hit_cap = e->hits.n;
     P.hits = e->hits.p;
-    HIP_TRY(hipMemsetAsync(e->ctrl.p, 0, sizeof(Ctrl), s));
+    HIP_TRY(hipMemsetAsync(e->ctrl.p, 0, offsetof(Ctrl, n_special), s));  // keep the special-file list
   }
   HIP_TRY(hipEventRecord(e->ev[2], s));
   Ctrl c;
@@ -2788,6 +2817,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(hipEventElapsedTime(&ms, e->ev[k], e->ev[k + 1]));
     tm[k] = ms;
   }
+
   tm[8] = (double)n_hits;
   tm[9] = (double)n_cands;
   tm[10] = (double)n_jobs;
@@ -2858,7 +2888,7 @@ void tsg_engine_free(tsg_engine* e) {
   e->job_start.release(); e->nsel.release(); e->cub_tmp.release(); e->locs.release(); e->locs2.release();
   e->scratch.release(); e->ctrl.release(); e->excl_jobs.release(); e->excl_out.release();
   e->nl_blocks.release(); e->nl_pre.release(); e->tail.release(); e->region_file.release(); e->region_tmp.release();
-  e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->vprof.release(); e->fflags8.release();
+  e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->special_files.release(); e->vprof.release(); e->fflags8.release();
   if (e->h_flags) (void)hipHostFree(e->h_flags);
   if (e->events)
     for (auto& ev : e->ev) (void)hipEventDestroy(ev);
@@ -2998,19 +3028,22 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
   P.hits = e->hits.p;
   P.hit_cap = 0;  // prefilter only: hits are counted, not stored
   P.ctrl = e->ctrl.p;
+  HIP_TRY(e->special_files.ensure(nf + 1));
+  P.special_files = e->special_files.p;
   const uint64_t n_nlb = nbytes / kNlBlock + 2;
   HIP_TRY(e->nl_blocks.ensure(n_nlb));
   HIP_TRY(hipMemsetAsync(e->nl_blocks.p, 0, n_nlb * 4, s));
   P.nl_blocks = e->nl_blocks.p;
   for (int attempt = 0; attempt < 2 && nbytes; ++attempt) {
     if ((rc = launch_scan(e, P))) return rc;
-    hipLaunchKernelGGL(k_special_gate, dim3(std::max(1u, std::min<uint32_t>((nf + 3) / 4, 4096))), dim3(256), 0, s, P);
-    HIP_TRY(hipGetLastError());
     Ctrl c;
     if ((rc = read_ctrl(e, &c))) return rc;
-    if (!rs->ac.fast.size() || c.ev_overflow <= e->ev_overflow.n) break;
+    if (!rs->ac.fast.size() || c.ev_overflow <= e->ev_overflow.n) {
+      if ((rc = launch_special_gate(e, P, c.n_special))) return rc;
+      break;
+    }
     e->ev_ovf_need = c.ev_overflow + (c.ev_overflow >> 2);  // events were lost: grow and rescan
-    HIP_TRY(hipMemsetAsync(e->ctrl.p, 0, sizeof(Ctrl), s));
+    HIP_TRY(hipMemsetAsync(e->ctrl.p, 0, offsetof(Ctrl, n_special), s));  // keep the special-file list
   }
   std::vector<uint32_t> kw((size_t)nf * RS.kw_words);
   if (nf) HIP_TRY(hipMemcpyAsync(kw.data(), e->file_kw.p, kw.size() * 4, hipMemcpyDeviceToHost, s));
