@@ -167,6 +167,16 @@ bool build_dfa(const gre::Compiled& c, DfaHost* out) {
   }
   if (overflow) return false;
   delta.resize(lists.size() * K, 0);
+  // bit 14: the target state is a match state (saves the walk a dependent load)
+  for (auto& v : delta)
+    if (match[v & kDfaStateMask]) v |= 0x4000;
+  // first-byte filter: a start position whose byte kills both start states
+  // (and does not end a match as the last byte) cannot match
+  for (int c = 0; c < 128; ++c)
+    for (int bt = 0; bt < 2; ++bt) {
+      const uint16_t e = delta[(size_t)out->start[bt] * K + out->cls[c]];
+      if ((e & kDfaStateMask) || (e & 0x8000) || match[out->start[bt]]) out->first[c >> 5] |= 1u << (c & 31);
+    }
   out->delta = std::move(delta);
   out->match = std::move(match);
   out->ncls = K;
@@ -189,8 +199,8 @@ int dfa_anchored(const DfaHost& d, const uint8_t* text, size_t n, size_t s, size
       if (e & 0x8000) last = (int64_t)n;
       break;
     }
-    st = e & 0x7FFF;
-    if (st && d.match[st]) last = (int64_t)(q + 1);
+    st = e & kDfaStateMask;
+    if (e & 0x4000) last = (int64_t)(q + 1);
   }
   if (last < 0) return 0;
   *me = (size_t)last;

@@ -25,6 +25,7 @@ constexpr uint32_t kFollowMaxStates = 1024;  // follow-DFA subset-construction b
 constexpr uint32_t kFollowDepth = 96;        // bytes a candidate filter reads past the hit
 constexpr uint32_t kNoFollow = 0xFFFFFFFFu;
 constexpr uint32_t kDfaMaxStates = 4096;     // verify-DFA budget per rule (else the Pike VM)
+constexpr uint32_t kDfaStateMask = 0x3FFF;  // verify-DFA entry: bit15 end-match, bit14 match state
 
 enum RuleMode : uint8_t { MODE_NEVER = 0, MODE_ANCHORED = 1, MODE_FULL = 2 };
 
@@ -48,6 +49,9 @@ struct RuleDev {
   uint32_t dfa_off;             // verify DFA (dfa.cpp): first u16 of its table (kNoFollow = none)
   uint32_t dfa_ncls, dfa_cls_off, dfa_match_off;
   uint32_t dfa_start0, dfa_start1;  // start state at s > 0 / s == 0 (BeginText)
+  uint32_t dfa_first[4];        // ASCII bytes on which a start state does not die (k_verify start skip)
+  uint32_t dfa_size;            // u16 entries of its table (k_verify stages it in LDS when it fits)
+  uint32_t dfa_smatch;          // bit 0/1: start0/start1 is a match state
 };
 
 struct PatDev {
@@ -134,6 +138,7 @@ struct DfaHost {
   bool valid = false;
   uint32_t ncls = 0, nstates = 0;
   uint32_t start[2] = {0, 0};
+  uint32_t first[4] = {0, 0, 0, 0};  // ASCII first bytes that keep some start state alive
   uint8_t cls[128] = {};
   std::vector<uint16_t> delta;
   std::vector<uint8_t> match;

@@ -81,6 +81,7 @@ struct Ctrl {
   unsigned long long ev_overflow;
   unsigned long long outputs;  // patterns k_report resolved (diagnostics)
   unsigned long long n_special;  // files flagged kFileSpecial (ScanParams::special_files)
+  unsigned long long n_caps;     // matches whose secret-group spans k_captures resolves
 };
 
 struct DevLoc {
@@ -1297,6 +1298,10 @@ struct VerifyParams {
   uint8_t* scratch;
   uint64_t scratch_stride;
   uint64_t* prof;  // diagnostics (TSG_PROFILE_VERIFY): per job {cycles, rule<<32 | candidates}
+  uint64_t* dbg;   // diagnostics: [0] dfa starts [1] dfa cycles [2] bitstate ok [3] bitstate cycles
+                   // [4] vm captures [5] vm capture cycles [6] vm searches [7] vm search cycles [8] allow cycles
+  uint4* caps;     // deferred capture jobs {file, rule, ms, me} (k_captures)
+  uint64_t cap_cap;
 };
 
 // Candidate start windows of one (file, rule) job, in increasing order
@@ -1424,24 +1429,62 @@ __device__ bool vm_search_starts(const gre::ProgView& p, const uint8_t* text, ui
 
 // Anchored leftmost-first DFA walk from s (dfa.cpp): 1 = match [s, *me),
 // 0 = none, 2 = undecidable here (byte >= 0x80) -> the Pike VM decides.
-__device__ inline int dfa_anchored_dev(const RuleSetDev& rs, const RuleDev& rd, const uint8_t* text, uint32_t n,
-                                       uint32_t s, uint32_t* me) {
-  const uint16_t* T = rs.dfa_delta + rd.dfa_off;
-  const uint8_t* cls = rs.dfa_bytes + rd.dfa_cls_off;
-  const uint8_t* mt = rs.dfa_bytes + rd.dfa_match_off;
-  const uint32_t K = rd.dfa_ncls;
-  uint32_t st = s == 0 ? rd.dfa_start1 : rd.dfa_start0;
-  int64_t last = mt[st] ? (int64_t)s : -1;
-  for (uint32_t q = s; q < n && st; ++q) {
-    const uint8_t c = text[q];
-    if (c >= 0x80) return 2;
-    const uint32_t e = T[st * K + cls[c]];
-    if (q + 1 == n) {
-      if (e & 0x8000u) last = n;
-      break;
+// T / cls: the rule's table and class map, in global memory or staged in LDS.
+// Plain scalars (no RuleDev reference: a by-reference struct lands in scratch
+// and its fields get reloaded inside the walk).
+struct DfaRef {
+  const uint16_t* T;
+  const uint8_t* cls;
+  uint32_t K, start0, start1, smatch;
+};
+
+// Global / LDS address spaces spelled out: through generic pointers the
+// compiler emits flat loads that wait on both counters.
+typedef __attribute__((address_space(1))) const uint8_t gu8;
+typedef __attribute__((address_space(1))) const uint16_t gu16;
+template <typename T>
+__device__ inline T* as_global(const void* p) { return reinterpret_cast<T*>(reinterpret_cast<uintptr_t>(p)); }
+
+constexpr uint32_t kVerifyDfaLds = 48 * 1024;  // bytes of LDS for the block's verify DFA
+__shared__ __align__(16) uint16_t g_vdfa[kVerifyDfaLds / 2];  // k_verify's staged DFA table
+__shared__ __align__(16) uint8_t g_vcls[128];                 // and its class map
+
+// kLds: the rule's table / class map are the block's staged copy (g_vdfa,
+// g_vcls); else d.T / d.cls in global memory.
+template <bool kLds>
+__device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, uint32_t n, uint32_t s, uint32_t* me) {
+  gu16* Tg = as_global<gu16>(d.T);
+  gu8* cg = as_global<gu8>(d.cls);
+  gu8* tx = as_global<gu8>(text);
+  const uint32_t K = d.K;
+  uint32_t st = s == 0 ? d.start1 : d.start0;
+  int64_t last = ((d.smatch >> (s == 0 ? 1 : 0)) & 1) ? (int64_t)s : -1;
+  // 16 bytes at a time: the byte loads issue together (unconditionally when
+  // the chunk lies inside the file), only the transition loads are chained
+  for (uint32_t q0 = s; q0 < n && st; q0 += 16) {
+    uint32_t c[16];
+    if (q0 + 16 <= n) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) c[i] = tx[q0 + i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) c[i] = q0 + i < n ? (uint32_t)tx[q0 + i] : 0u;
     }
-    st = e & 0x7FFFu;
-    if (st && mt[st]) last = q + 1;
+    const uint32_t m = n - q0 < 16 ? n - q0 : 16;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if ((uint32_t)i >= m || !st) break;
+      if (c[i] >= 0x80) return 2;  // runes / case folding: the Pike VM decides
+      const uint32_t k = kLds ? (uint32_t)g_vcls[c[i]] : (uint32_t)cg[c[i]];
+      const uint32_t e = kLds ? (uint32_t)g_vdfa[st * K + k] : (uint32_t)Tg[st * K + k];
+      if (q0 + i + 1 == n) {
+        if (e & 0x8000u) last = n;
+        st = 0;
+        break;
+      }
+      st = e & kDfaStateMask;
+      if (e & 0x4000u) last = q0 + i + 1;
+    }
   }
   if (last < 0) return 0;
   *me = (uint32_t)last;
@@ -1457,7 +1500,10 @@ __device__ inline int dfa_anchored_dev(const RuleSetDev& rs, const RuleDev& rd, 
 // Returns false when the match does not fit the arena (the caller then runs
 // the Pike capture VM) — never a different answer.
 constexpr uint32_t kVerifyThreads = 64;
-constexpr uint32_t kBsWords = 560;  // LDS words per lane: 140 KiB per block
+#ifndef TSG_BS_WORDS
+#define TSG_BS_WORDS 560
+#endif
+constexpr uint32_t kBsWords = TSG_BS_WORDS;  // LDS words per lane: 140 KiB per block
 
 __device__ bool bitstate_captures(const gre::ProgView& p, const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me,
                                   const uint32_t* gnum, uint32_t ng, uint32_t* area, int32_t* gcap) {
@@ -1534,23 +1580,22 @@ __device__ bool bitstate_captures(const gre::ProgView& p, const uint8_t* text, u
   return false;
 }
 
-__device__ void emit_match(const VerifyParams& V, const RuleDev& rd, uint32_t rule, uint32_t fi,
-                           const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me,
-                           gre::VmScratch& sc, uint32_t* bs_area) {
-  // AllowLocation (scanner.go:145-148): global then rule allow regexes on the whole match
-  for (uint32_t k = 0; k < V.rs.n_global_allow; ++k)
-    if (match_string_pf(V.rs, V.rs.global_allow[k], text + ms, me - ms, sc)) return;
-  for (uint32_t k = 0; k < rd.allow_n; ++k)
-    if (match_string_pf(V.rs, V.rs.allow_progs[rd.allow_off + k], text + ms, me - ms, sc)) return;
-  if (!rd.use_groups) {
-    unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
-    if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, ms, me, 0, 0, 0, 0};
-    return;
-  }
+// Secret-group spans of one kept match (getMatchSubgroupsLocations,
+// scanner.go:150-163): bit-state backtracker in the lane's LDS arena, the
+// capture VM when the match does not fit it.
+__device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t rule, uint32_t fi,
+                            const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me, gre::VmScratch& sc,
+                            uint32_t* bs_area) {
   const gre::ProgView& pv = V.rs.progs[rd.prog];
   const uint32_t* gnum = V.rs.group_slots + rd.group_off;
   int32_t* gcap = (int32_t*)(bs_area + kBsWords - 8);  // tracked slots (the arena's last 8 words)
-  if (bitstate_captures(pv, text, n, ms, me, gnum, rd.group_n, bs_area, gcap)) {
+  const uint64_t tb0 = V.dbg ? clock64() : 0;
+  const bool bs_ok = bitstate_captures(pv, text, n, ms, me, gnum, rd.group_n, bs_area, gcap);
+  if (V.dbg) {
+    atomicAdd((unsigned long long*)&V.dbg[2], bs_ok ? 1ull : 0ull);
+    atomicAdd((unsigned long long*)&V.dbg[3], (unsigned long long)(clock64() - tb0));
+  }
+  if (bs_ok) {
     for (uint32_t g = 0; g < rd.group_n; ++g) {
       const int32_t s = gcap[2 * g], e = gcap[2 * g + 1];
       unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
@@ -1562,7 +1607,12 @@ __device__ void emit_match(const VerifyParams& V, const RuleDev& rd, uint32_t ru
     return;
   }
   int32_t out[kMaxCap];  // ncap <= kMaxCap is enforced by the rule compiler
+  const uint64_t tv0 = V.dbg ? clock64() : 0;
   bool ok = gre::vm_captures(pv, text, n, ms, sc, out);
+  if (V.dbg) {
+    atomicAdd((unsigned long long*)&V.dbg[4], 1ull);
+    atomicAdd((unsigned long long*)&V.dbg[5], (unsigned long long)(clock64() - tv0));
+  }
   if (!ok || (uint32_t)out[1] != me) atomicOr(&V.ctrl->err, 1u);
   for (uint32_t g = 0; g < rd.group_n; ++g) {
     const uint32_t slot = gnum[g];
@@ -1575,13 +1625,100 @@ __device__ void emit_match(const VerifyParams& V, const RuleDev& rd, uint32_t ru
   }
 }
 
-__global__ __launch_bounds__(kVerifyThreads) void k_verify(VerifyParams V) {
+// A match k_verify found: allow rules, then the whole-match location or, for
+// rules with a secret group, a capture job for k_captures (the bit-state
+// arenas need ~140 KiB of LDS per wave, which would cap k_verify at one wave
+// per CU; split off, the match search runs at full occupancy).
+__device__ void emit_match(const VerifyParams& V, const RuleDev& rd, uint32_t rule, uint32_t fi,
+                           const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me, gre::VmScratch& sc,
+                           uint32_t* bs_area) {
+  // AllowLocation (scanner.go:145-148): global then rule allow regexes on the whole match
+  for (uint32_t k = 0; k < V.rs.n_global_allow; ++k)
+    if (match_string_pf(V.rs, V.rs.global_allow[k], text + ms, me - ms, sc)) return;
+  for (uint32_t k = 0; k < rd.allow_n; ++k)
+    if (match_string_pf(V.rs, V.rs.allow_progs[rd.allow_off + k], text + ms, me - ms, sc)) return;
+  if (!rd.use_groups) {
+    unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
+    if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, ms, me, 0, 0, 0, 0};
+    return;
+  }
+  if (bs_area) {  // combined shape: resolve the groups here
+    emit_groups(V, rd, rule, fi, text, n, ms, me, sc, bs_area);
+    return;
+  }
+  unsigned long long idx = atomicAdd(&V.ctrl->n_caps, 1ull);
+  if (idx < V.cap_cap) V.caps[idx] = make_uint4(fi, rule, ms, me);
+}
+
+__global__ __launch_bounds__(kVerifyThreads) void k_captures(VerifyParams V, uint32_t n_caps) {
   __shared__ uint32_t bs_lds[kVerifyThreads * kBsWords];
   uint32_t* bs_area = bs_lds + threadIdx.x * kBsWords;
   const uint32_t nthreads = gridDim.x * blockDim.x;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   gre::VmScratch sc = make_scratch(V.scratch + (uint64_t)t * V.scratch_stride, V.rs);
-  for (uint32_t j = t; j < V.n_jobs; j += nthreads) {
+  for (uint32_t i = t; i < n_caps; i += nthreads) {
+    const uint4 c = V.caps[i];
+    const RuleDev rd = V.rs.rules[c.y];
+    const uint64_t fstart = V.off[c.x];
+    const uint32_t n = (uint32_t)(V.off[c.x + 1] - 1 - fstart);
+    emit_groups(V, rd, c.y, c.x, V.data + fstart, n, c.z, c.w, sc, bs_area);
+  }
+}
+
+// Pull the rule tables k_verify walks (programs, classes, verify DFAs, rule
+// records) back into every XCD's L2 after the scan streamed the batch through
+// it: k_verify's walks are chains of dependent loads, and a cold line there
+// costs an HBM round trip per step.  Block b serves XCD b % 8 (round-robin
+// dispatch), part b / 8 of each range; nothing is written.
+struct WarmRanges {
+  const uint8_t* p[8];
+  uint64_t n[8];
+  uint32_t k;
+};
+constexpr uint32_t kWarmParts = 8;
+
+__global__ __launch_bounds__(256) void k_warm(WarmRanges R, uint32_t* sink) {
+  const uint32_t part = blockIdx.x / 8;
+  uint32_t acc = 0;
+  for (uint32_t r = 0; r < R.k; ++r) {
+    const uint64_t lines = (R.n[r] + 127) / 128;
+    const uint64_t per = (lines + kWarmParts - 1) / kWarmParts;
+    const uint64_t l0 = part * per, l1 = l0 + per < lines ? l0 + per : lines;
+    for (uint64_t l = l0 + threadIdx.x; l < l1; l += blockDim.x) acc = acc * 31u + R.p[r][l * 128];
+  }
+  if (acc == 0x5EED1234u) sink[0] = acc;  // keeps the loads alive
+}
+
+constexpr uint32_t kVerifyBlock = 256;
+
+// kInline: one wave per block with the bit-state arenas in LDS, groups
+// resolved in place (default); else (TSG_VERIFY_SPLIT) the search runs at
+// full occupancy and defers group captures to k_captures.
+template <bool kInline>
+__global__ __launch_bounds__(kInline ? kVerifyThreads : kVerifyBlock) void k_verify(VerifyParams V) {
+  uint32_t* bs_area = nullptr;
+  if constexpr (kInline) {
+    __shared__ uint32_t bs_lds[kVerifyThreads * kBsWords];
+    bs_area = bs_lds + threadIdx.x * kBsWords;
+  }
+  const uint32_t nthreads = gridDim.x * blockDim.x;
+  gre::VmScratch sc = make_scratch(V.scratch + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * V.scratch_stride, V.rs);
+  // block-uniform loop: jobs are sorted by rule, so the block's first job's
+  // rule is (nearly) every lane's; its verify DFA goes to LDS when it fits,
+  // turning each dependent step's L2 round trip into an LDS read
+  for (uint32_t base = blockIdx.x * blockDim.x; base < V.n_jobs; base += nthreads) {
+    const uint32_t r0 = (uint32_t)(V.keys[V.job_start[base]] >> kPosBits);
+    const RuleDev& rd0 = V.rs.rules[r0];
+    const bool stage = !kInline && rd0.dfa_off != kNoFollow && rd0.dfa_size * 2 <= kVerifyDfaLds;
+    __syncthreads();  // previous iteration's readers are done
+    if constexpr (!kInline) if (stage) {
+      const uint16_t* src = V.rs.dfa_delta + rd0.dfa_off;
+      for (uint32_t i = threadIdx.x; i < rd0.dfa_size; i += blockDim.x) g_vdfa[i] = src[i];
+      if (threadIdx.x < 128) g_vcls[threadIdx.x] = V.rs.dfa_bytes[rd0.dfa_cls_off + threadIdx.x];
+    }
+    __syncthreads();
+    const uint32_t j = base + threadIdx.x;
+    if (j >= V.n_jobs) continue;
     const uint64_t t0 = V.prof ? clock64() : 0;
     const uint64_t c0 = V.job_start[j];
     const uint64_t c1 = (j + 1 < V.n_jobs) ? V.job_start[j + 1] : V.n_cands;
@@ -1596,11 +1733,13 @@ __global__ __launch_bounds__(kVerifyThreads) void k_verify(VerifyParams V) {
           V.prof[2 * j + 1] = ((uint64_t)rule << 32) | nc;
         }
       }
-    } pg{V, j, rule, t0, c1 - c0};
+    } pg{V, j, rule, t0, 0};  // nc: DFA starts tried (diagnostics), bit 31 = full-file job
     const uint32_t fi = V.vals[c0] & ~kFullFlag;
     bool full = false;
     for (uint64_t c = c0; c < c1 && !full; ++c) full = (V.vals[c] & kFullFlag) != 0;
+    if (full) pg.nc |= 1u << 31;
     const RuleDev rd = V.rs.rules[rule];
+    const bool in_lds = stage && rule == r0;
     const gre::ProgView& pv = V.rs.progs[rd.prog];
     const uint64_t fstart = V.off[fi];
     const uint8_t* text = V.data + fstart;
@@ -1641,6 +1780,9 @@ __global__ __launch_bounds__(kVerifyThreads) void k_verify(VerifyParams V) {
       it.advance();
       uint32_t pos = 0;
       if (rd.dfa_off != kNoFollow) {
+        const DfaRef dref{V.rs.dfa_delta + rd.dfa_off, V.rs.dfa_bytes + rd.dfa_cls_off, rd.dfa_ncls, rd.dfa_start0,
+                          rd.dfa_start1, rd.dfa_smatch};
+        const uint32_t fm0 = rd.dfa_first[0], fm1 = rd.dfa_first[1], fm2 = rd.dfa_first[2], fm3 = rd.dfa_first[3];
         // FindAll over the permitted starts with the verify DFA: the first
         // start (>= pos) that matches is Go's leftmost match; a byte >= 0x80
         // hands the rest of the job to the Pike VM below
@@ -1650,7 +1792,23 @@ __global__ __launch_bounds__(kVerifyThreads) void k_verify(VerifyParams V) {
           uint32_t s0 = it.cs > pos ? it.cs : pos;
           for (uint32_t sp = s0; sp <= it.ce && sp < n; ++sp) {
             if (!gre::is_rune_start(text, n, sp)) continue;
-            const int r = dfa_anchored_dev(V.rs, rd, text, n, sp, &me);
+            {
+              const uint32_t c0 = as_global<gu8>(text)[sp];  // first-byte skip (no dependent table loads)
+              const uint32_t fw = c0 < 32 ? fm0 : c0 < 64 ? fm1 : c0 < 96 ? fm2 : fm3;
+              if (c0 < 0x80 && !((fw >> (c0 & 31)) & 1)) continue;
+            }
+            const uint64_t td0 = V.dbg ? clock64() : 0;
+            int r;
+            if constexpr (kInline) r = dfa_anchored_dev<false>(dref, text, n, sp, &me);
+            else r = in_lds ? dfa_anchored_dev<true>(dref, text, n, sp, &me) : dfa_anchored_dev<false>(dref, text, n, sp, &me);
+            if (V.dbg) {
+              atomicAdd((unsigned long long*)&V.dbg[0], 1ull);
+              atomicAdd((unsigned long long*)&V.dbg[1], (unsigned long long)(clock64() - td0));
+              atomicAdd((unsigned long long*)&V.dbg[9 + (r == 1 ? 1 : r == 2 ? 2 : 0)], 1ull);
+              if (r == 1) atomicAdd((unsigned long long*)&V.dbg[12], (unsigned long long)(me - sp));
+              ++pg.nc;
+              if (rule < 64) atomicAdd((unsigned long long*)&V.dbg[13], 0ull);
+            }
             if (r == 2) {
               vm = true;
               break;
@@ -1669,7 +1827,13 @@ __global__ __launch_bounds__(kVerifyThreads) void k_verify(VerifyParams V) {
         if (!vm) continue;
       }
       while (it.have) {
-        if (!vm_search_starts(pv, text, n, pos, it, sc, &ms, &me)) break;
+        const uint64_t ts0 = V.dbg ? clock64() : 0;
+        const bool got = vm_search_starts(pv, text, n, pos, it, sc, &ms, &me);
+        if (V.dbg) {
+          atomicAdd((unsigned long long*)&V.dbg[6], 1ull);
+          atomicAdd((unsigned long long*)&V.dbg[7], (unsigned long long)(clock64() - ts0));
+        }
+        if (!got) break;
         emit_match(V, rd, rule, fi, text, n, ms, me, sc, bs_area);
         if (me == ms) break;  // cannot happen for anchored rules (non-empty literal)
         pos = me;
@@ -1874,6 +2038,7 @@ struct tsg_engine {
   DBuf<uint64_t> vprof;
   DBuf<uint8_t> span_hi;
   DBuf<uint32_t> special_files;
+  DBuf<uint4> caps;
   DBuf<uint32_t> ev_counts;
   uint64_t ev_ovf_need = 0;  // overflow-event capacity learnt from a lost scan
   bool fast_timed = false;   // ev[10..11] bracket the last k_scan_fast launch
@@ -1979,6 +2144,9 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
       dbytes.insert(dbytes.end(), r.dfa.match.begin(), r.dfa.match.end());
       d.dfa_start0 = r.dfa.start[0];
       d.dfa_start1 = r.dfa.start[1];
+      for (int q = 0; q < 4; ++q) d.dfa_first[q] = r.dfa.first[q];
+      d.dfa_size = (uint32_t)r.dfa.delta.size();
+      d.dfa_smatch = (r.dfa.match[r.dfa.start[0]] ? 1u : 0u) | (r.dfa.match[r.dfa.start[1]] ? 2u : 0u);
       ddelta.insert(ddelta.end(), r.dfa.delta.begin(), r.dfa.delta.end());
     }
     if (r.follow.valid) {
@@ -2648,10 +2816,13 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   HIP_TRY(hipEventRecord(e->ev[4], s));
   // ---- 5. verify
   uint64_t loc_cap = std::max<uint64_t>(1 << 16, n_jobs);
+  uint64_t caps_cap = std::max<uint64_t>(1 << 14, n_jobs / 4);
   uint64_t n_locs = 0;
-  for (int attempt = 0; attempt < 3 && n_jobs; ++attempt) {
+  for (int attempt = 0; attempt < 4 && n_jobs; ++attempt) {
     HIP_TRY(e->locs.ensure(loc_cap));
+    HIP_TRY(e->caps.ensure(caps_cap));
     HIP_TRY(hipMemsetAsync(&e->ctrl.p->locs, 0, 8, s));
+    HIP_TRY(hipMemsetAsync(&e->ctrl.p->n_caps, 0, 8, s));
     VerifyParams V{};
     V.data = d_data;
     V.off = d_off;
@@ -2666,16 +2837,56 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     V.ctrl = e->ctrl.p;
     V.scratch = e->scratch.p;
     V.scratch_stride = e->scratch_stride;
+    V.caps = e->caps.p;
+    V.cap_cap = e->caps.n;
     const bool prof = getenv("TSG_PROFILE_VERIFY") != nullptr;
-    if (prof) HIP_TRY(e->vprof.ensure(2ull * n_jobs));
-    V.prof = prof ? e->vprof.p : nullptr;
-    // one wave per block spreads the (latency-bound, divergent) lanes over
-    // every CU and its L1; each block's LDS holds its lanes' bit-state arenas
-    const uint32_t vb = kVerifyThreads;
-    uint32_t blocks = std::min<uint32_t>((n_jobs + vb - 1) / vb, e->vm_threads / vb);
-    hipLaunchKernelGGL(k_verify, dim3(std::max(1u, blocks)), dim3(vb), 0, s, V);
     if (prof) {
-      std::vector<uint64_t> hp(2ull * n_jobs);
+      HIP_TRY(e->vprof.ensure(2ull * n_jobs + 16));
+      HIP_TRY(hipMemsetAsync(e->vprof.p + 2ull * n_jobs, 0, 16 * 8, s));
+    }
+    V.prof = prof ? e->vprof.p : nullptr;
+    V.dbg = prof ? e->vprof.p + 2ull * n_jobs : nullptr;
+    // rule tables back into L2, then the match search (no LDS: full occupancy)
+    if (attempt == 0) {
+      WarmRanges W{};
+      auto add = [&](const void* ptr, uint64_t bytes) {
+        if (ptr && bytes && W.k < 8) {
+          W.p[W.k] = (const uint8_t*)ptr;
+          W.n[W.k++] = bytes;
+        }
+      };
+      add(im.inst.p, im.inst.n * sizeof(gre::Inst));
+      add(im.classes.p, im.classes.n * sizeof(gre::ClassDesc));
+      add(im.ranges.p, im.ranges.n * 4);
+      add(im.progs.p, im.progs.n * sizeof(gre::ProgView));
+      add(im.rules.p, im.rules.n * sizeof(RuleDev));
+      add(im.dfa_delta.p, im.dfa_delta.n * 2);
+      add(im.dfa_bytes.p, im.dfa_bytes.n);
+      add(im.u32.p, im.u32.n * 4);
+      hipLaunchKernelGGL(k_warm, dim3(8 * kWarmParts), dim3(256), 0, s, W, (uint32_t*)e->nsel.p);
+      HIP_TRY(hipGetLastError());
+    }
+    // default: one kernel (measured 0.67 ms vs 0.48 + 0.21 ms split at 50 GB);
+    // TSG_VERIFY_SPLIT=1 runs the full-occupancy search + k_captures instead
+    static const bool inl = getenv("TSG_VERIFY_SPLIT") == nullptr;
+    const uint32_t vb = inl ? kVerifyThreads : kVerifyBlock;
+    uint32_t blocks = std::min<uint32_t>((n_jobs + vb - 1) / vb, e->vm_threads / vb);
+    if (inl) hipLaunchKernelGGL(k_verify<true>, dim3(std::max(1u, blocks)), dim3(vb), 0, s, V);
+    else hipLaunchKernelGGL(k_verify<false>, dim3(std::max(1u, blocks)), dim3(vb), 0, s, V);
+    HIP_TRY(hipGetLastError());
+    if ((rc = read_ctrl(e, &c))) return rc;
+    if (c.n_caps > e->caps.n) {  // capture list overflow: grow and re-run the search
+      caps_cap = c.n_caps;
+      continue;
+    }
+    if (c.n_caps) {
+      // one wave per block: each block's LDS holds its lanes' bit-state arenas
+      const uint32_t cb = std::min<uint32_t>((uint32_t)((c.n_caps + kVerifyThreads - 1) / kVerifyThreads),
+                                             e->vm_threads / kVerifyThreads);
+      hipLaunchKernelGGL(k_captures, dim3(std::max(1u, cb)), dim3(kVerifyThreads), 0, s, V, (uint32_t)c.n_caps);
+    }
+    if (prof) {
+      std::vector<uint64_t> hp(2ull * n_jobs + 16);
       HIP_TRY(hipMemcpyAsync(hp.data(), e->vprof.p, hp.size() * 8, hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
       std::vector<uint32_t> idx(n_jobs);
@@ -2688,11 +2899,17 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
         pr.second = std::max(pr.second, hp[2 * q]);
       }
       for (uint32_t q = 0; q < std::min<uint32_t>(10, n_jobs); ++q)
-        fprintf(stderr, "[verify] job %u cycles %llu rule %s cands %llu\n", idx[q], (unsigned long long)hp[2 * idx[q]],
+        fprintf(stderr, "[verify] job %u cycles %llu rule %s starts %llx\n", idx[q], (unsigned long long)hp[2 * idx[q]],
                 rs->rules[hp[2 * idx[q] + 1] >> 32].id.c_str(), (unsigned long long)(hp[2 * idx[q] + 1] & 0xFFFFFFFF));
       for (auto& kv : per_rule)
         fprintf(stderr, "[verify] rule %s total %llu max %llu\n", rs->rules[kv.first].id.c_str(),
                 (unsigned long long)kv.second.first, (unsigned long long)kv.second.second);
+      const uint64_t* d = hp.data() + 2ull * n_jobs;
+      fprintf(stderr, "[verify] dfa starts %llu cycles %llu | bitstate ok %llu cycles %llu | vm captures %llu cycles %llu | vm searches %llu cycles %llu\n",
+              (unsigned long long)d[0], (unsigned long long)d[1], (unsigned long long)d[2], (unsigned long long)d[3],
+              (unsigned long long)d[4], (unsigned long long)d[5], (unsigned long long)d[6], (unsigned long long)d[7]);
+      fprintf(stderr, "[verify] dfa results none %llu match %llu vm %llu match bytes %llu\n", (unsigned long long)d[9],
+              (unsigned long long)d[10], (unsigned long long)d[11], (unsigned long long)d[12]);
     }
     HIP_TRY(hipGetLastError());
     if ((rc = read_ctrl(e, &c))) return rc;
@@ -2888,7 +3105,7 @@ void tsg_engine_free(tsg_engine* e) {
   e->job_start.release(); e->nsel.release(); e->cub_tmp.release(); e->locs.release(); e->locs2.release();
   e->scratch.release(); e->ctrl.release(); e->excl_jobs.release(); e->excl_out.release();
   e->nl_blocks.release(); e->nl_pre.release(); e->tail.release(); e->region_file.release(); e->region_tmp.release();
-  e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->special_files.release(); e->vprof.release(); e->fflags8.release();
+  e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->special_files.release(); e->caps.release(); e->vprof.release(); e->fflags8.release();
   if (e->h_flags) (void)hipHostFree(e->h_flags);
   if (e->events)
     for (auto& ev : e->ev) (void)hipEventDestroy(ev);
