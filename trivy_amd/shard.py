@@ -1,0 +1,83 @@
+"""Multi-GPU sharding of a scan batch.
+
+Files are independent in `Scanner.Scan` (pkg/fanal/secret/scanner.go:371-452
+keeps no cross-file state), so a batch shards by file with no data-path
+collective: each rank (one process per GPU) scans its own files on its own
+engine, and only the per-file results are merged on the host, in input
+order, the way the analyzer concatenates per-file `types.Secret`s
+(pkg/fanal/analyzer/analyzer.go:403-444, sort at :218-229).
+
+  partition(sizes, n)        greedy LPT by byte size: files largest first, each
+                             to the least-loaded rank (ties: lowest rank), so
+                             every rank gets about total/n bytes
+  scan_sharded(fn, batch)    rank r runs fn(its files); results are exchanged
+                             with all_gather_object (host objects only: tens of
+                             bytes per finding) and returned in batch order
+
+The merge is the only communication; with world size 1 (or no process group)
+it is a plain call.
+"""
+from __future__ import annotations
+
+import heapq
+from typing import Any, Callable, List, Optional, Sequence
+
+
+def partition(sizes: Sequence[int], n_ranks: int) -> List[List[int]]:
+    """Greedy LPT: indices of the files each rank scans (each file exactly
+    once; rank loads differ by at most the largest file)."""
+    if n_ranks < 1:
+        raise ValueError("n_ranks must be >= 1")
+    order = sorted(range(len(sizes)), key=lambda i: (-int(sizes[i]), i))
+    heap = [(0, r) for r in range(n_ranks)]
+    parts: List[List[int]] = [[] for _ in range(n_ranks)]
+    for i in order:
+        load, r = heapq.heappop(heap)
+        parts[r].append(i)
+        heapq.heappush(heap, (load + int(sizes[i]), r))
+    for p in parts:
+        p.sort()  # keep input order inside a shard (batch locality, stable merge)
+    return parts
+
+
+def _dist():
+    try:
+        import torch.distributed as dist
+    except ImportError:  # pragma: no cover - torch is part of this image
+        return None
+    return dist if dist.is_available() and dist.is_initialized() else None
+
+
+def scan_sharded(scan_fn: Callable[[List[Any]], List[Any]], batch: Sequence[Any],
+                 sizes: Optional[Sequence[int]] = None, group=None) -> List[Any]:
+    """Scan `batch` across the ranks of the default (or given) process group.
+
+    scan_fn(sub_batch) -> one result per item, in order (e.g.
+    `Scanner.scan_batch` on this rank's engine).  sizes: bytes per item
+    (default: len(item.content)).  Every rank must call this with the same
+    batch; every rank returns the full, input-ordered result list.
+    """
+    dist = _dist()
+    world = dist.get_world_size(group) if dist else 1
+    rank = dist.get_rank(group) if dist else 0
+    if sizes is None:
+        sizes = [len(getattr(b, "content", b"")) for b in batch]
+    parts = partition(sizes, world)
+    mine = parts[rank]
+    local = scan_fn([batch[i] for i in mine]) if mine else []
+    if len(local) != len(mine):
+        raise RuntimeError(f"scan_fn returned {len(local)} results for {len(mine)} files")
+    if world == 1:
+        gathered = [list(zip(mine, local))]
+    else:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, list(zip(mine, local)), group=group)
+    out: List[Any] = [None] * len(batch)
+    seen = 0
+    for shard in gathered:
+        for i, res in shard:
+            out[i] = res
+            seen += 1
+    if seen != len(batch):
+        raise RuntimeError(f"merge saw {seen} results for {len(batch)} files")
+    return out
