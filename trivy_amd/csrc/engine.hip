@@ -94,6 +94,7 @@ struct DevLoc {
 };
 
 struct ScanParams {
+  uint32_t report_mode;  // timing experiments only (TSG_REPORT_MODE): 1 = no file lookups in k_report
   const uint8_t* data;
   const uint64_t* off;  // n_files + 1
   uint64_t nbytes;
@@ -829,7 +830,7 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
             const uint32_t tl = pd.len < ac.depth ? pd.len : ac.depth;
             const uint64_t start = pos + 1 - tl - pd.ext;
             if (pd.trunc) {  // the rest of a long pattern, on the batch (rare)
-              if (fi == 0xFFFFFFFFu) fi = file_of_pos(P, pos);
+              if (fi == 0xFFFFFFFFu) fi = (P.report_mode & 1) ? (uint32_t)((pos >> 12) % P.n_files) : file_of_pos(P, pos);
               const uint64_t fend = P.off[fi + 1] - 1;
               if (start + pd.len > fend) continue;
               bool ok = true;
@@ -846,7 +847,7 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
             }
             ++my_out;
             if (want_kw) {
-              if (fi == 0xFFFFFFFFu) fi = file_of_pos(P, pos);
+              if (fi == 0xFFFFFFFFu) fi = (P.report_mode & 1) ? (uint32_t)((pos >> 12) % P.n_files) : file_of_pos(P, pos);
               const uint64_t key = ((uint64_t)fi << 32) | pd.kw;  // per-lane dedupe of repeated keywords
               if (last_kw != key) {
                 last_kw = key;
@@ -2714,6 +2715,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   P.ctrl = e->ctrl.p;
   HIP_TRY(e->special_files.ensure(nf + 1));
   P.special_files = e->special_files.p;
+  if (const char* m = getenv("TSG_REPORT_MODE")) P.report_mode = (uint32_t)atoi(m);
   const uint64_t n_nlb = nbytes / kNlBlock + 2;
   HIP_TRY(e->nl_blocks.ensure(n_nlb));
   HIP_TRY(e->nl_pre.ensure(n_nlb));
