@@ -8,6 +8,11 @@ GPU; one step = one complete Scanner.Scan pass over every file of the shard
 (tsg_scan_device).  Multi-GPU: one process per GPU, each scanning its own
 shard (independent files: no data-path collective) -> weak scaling.
 
+Other BASELINE configs (`--config N`, extra measurement lines, not the
+headline): 1 = keyword prefilter only (tsg_gate_device, 20 GB), 4 = stress:
+builtin + 1000 generated gitleaks-style custom rules (tests/stress_rules.py;
+the automaton no longer fits k_scan_fast's LDS image).
+
 Prints ONE JSON line (rank 0).  Roofline is reported for the dominant kernel
 (k_scan, the HBM pass).  cpu_baseline times the CPU oracle (a Python port of
 the Go scanner; Go is not installed) on a bounded sample of the same corpus.
@@ -33,6 +38,14 @@ TPL_RULES = ["aws-access-key-id", "aws-secret-access-key", "github-pat", "github
              "hugging-face-access-token", "slack-access-token", "stripe-secret-token", "sendgrid-api-token",
              "npm-access-token", "facebook-token", "twilio-api-key", "shopify-token", "age-secret-key",
              "rubygems-api-token", "pulumi-api-token"]
+WORKLOADS = {
+    1: "configs[1]: keyword prefilter only (Aho-Corasick over all builtin rule keywords, per-file rule gates), "
+       "mixed text corpus resident in HBM",
+    2: "configs[2]: full builtin ruleset (prefilter + regex + line numbers + allow rules), mixed text corpus "
+       "resident in HBM",
+    4: "configs[4]: stress, builtin + generated gitleaks-style custom rules (explosion rules, keyword-less rules), "
+       "mixed text corpus resident in HBM",
+}
 HBM_PEAK_GBPS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 
 
@@ -108,7 +121,7 @@ def read_result(N, res):
     return locs, [tm[i] for i in range(min(32, nt.value))]
 
 
-def parity_checks(N, S, c, locs, rules, seed, density, n_sample=300):
+def parity_checks(N, S, c, locs, rules, seed, density, n_sample=300, oracle_cfg=None):
     """Full-size properties + oracle spot checks on sample files."""
     from oracle import secret_oracle as O
 
@@ -130,7 +143,7 @@ def parity_checks(N, S, c, locs, rules, seed, density, n_sample=300):
     for L in locs:
         by_file.setdefault(int(L["file"]), []).append(
             (rules[int(L["rule"])].id, int(L["start"]), int(L["end"]), int(L["start_line"]), int(L["end_line"])))
-    oracle = O.Scanner(None)
+    oracle = O.Scanner(O.parse_config(oracle_cfg) if oracle_cfg else None)
     mismatched = 0
     spot_findings = 0
     for f in cand:
@@ -148,6 +161,38 @@ def parity_checks(N, S, c, locs, rules, seed, density, n_sample=300):
     return dict(planted=int(len(real)), planted_found=int(found), decoys=int(len(decoys)),
                 decoys_found=int(decoy_hits), spot_files=len(cand), spot_findings=spot_findings,
                 spot_mismatched_files=mismatched, total_findings=int(len(locs)))
+
+
+def gate_timings(N, eng):
+    """Timings of the engine's last tsg_gate_device call (tsg_engine_gate_timings)."""
+    tm = (ctypes.c_double * 32)()
+    nt = ctypes.c_size_t()
+    N.check(N.lib.tsg_engine_gate_timings(eng, tm, 32, ctypes.byref(nt)))
+    return [tm[i] for i in range(min(32, nt.value))]
+
+
+def gate_checks(N, c, rules, gates, words, seed, density, n_sample=200):
+    """configs[1] parity: gate bits of sample files against the oracle's MatchKeywords."""
+    from oracle import secret_oracle as O
+
+    g = np.frombuffer(bytes(gates), dtype=np.uint32).reshape(c["n_files"], words)
+    orules = O.Scanner(None).rules
+    rng = np.random.default_rng(seed + 9)
+    cand = [int(f) for f in np.unique(rng.integers(0, c["n_files"], n_sample)) if c["sizes"][f] <= (4 << 20)]
+    bad = 0
+    passed = 0
+    for f in cand:
+        n = int(c["sizes"][f])
+        buf = (ctypes.c_uint8 * max(1, n))()
+        N.check(N.lib.tsg_gen_file(seed, f, n, density, buf))
+        data = bytes(buf)[:n]
+        low = O.go_bytes_to_lower(data)
+        want = [O.Scanner.match_keywords(r, data, low) for r in orules]
+        got = [bool((g[f, i // 32] >> (i % 32)) & 1) for i in range(len(rules))]
+        passed += sum(want)
+        bad += want != got
+    return dict(spot_files=len(cand), spot_gate_bits_set=passed, spot_mismatched_files=bad,
+                files_with_any_keyword_rule=int(sum(bool(x.any()) for x in g)))
 
 
 def traffic_bytes(content_bytes):
@@ -243,7 +288,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--gb", type=float, default=50.0, help="corpus GB per GPU (configs[2]: 50)")
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 4],
+                    help="BASELINE.json configs index: 2 full ruleset (default), 1 prefilter only, 4 stress rules")
+    ap.add_argument("--gb", type=float, default=None, help="corpus GB per GPU (configs[2]: 50, configs[1]: 20)")
+    ap.add_argument("--stress-rules", type=int, default=1000)
     ap.add_argument("--density", type=float, default=1e-6)
     ap.add_argument("--seed", type=int, default=20261015 + 2)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -251,6 +299,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     args = ap.parse_args()
+    if args.gb is None:
+        args.gb = 20.0 if args.config == 1 else 50.0
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -275,24 +325,52 @@ def main():
     seed = args.seed + 1000 * rank
     c = build_corpus(N, torch, seed, args.gb, args.density, local_rank)
     torch.cuda.synchronize()
-    sc = S.new_scanner(None, device=local_rank)
+    cfg = None
+    if args.config == 4:
+        import tempfile
+
+        from tests import stress_rules
+
+        cfg_path = os.path.join(tempfile.mkdtemp(), "trivy-secret.yaml")
+        stress_rules.write_config(cfg_path, stress_rules.make_rules(20261019, args.stress_rules))
+        cfg = S.parse_config(cfg_path)
+    sc = S.new_scanner(cfg, device=local_rank)
     eng = S.get_engine(local_rank)
     rs = sc._rs.handle
+    st = [ctypes.c_uint32() for _ in range(4)]
+    fast = ctypes.c_int()
+    N.check(N.lib.tsg_ruleset_stats(rs, *[ctypes.byref(x) for x in st], ctypes.byref(fast)))
+    scan_kernel = "k_scan_fast" if fast.value else "k_scan_generic"
+    gate_words = (len(sc.rules) + 31) // 32
+    gates = (ctypes.c_uint32 * (c["n_files"] * gate_words))() if args.config == 1 else None
+
+    def one_step():
+        if args.config == 1:
+            N.check(N.lib.tsg_gate_device(eng, rs, ctypes.c_void_p(c["d_data"].data_ptr()),
+                                          ctypes.c_void_p(c["d_off"].data_ptr()), c["n_files"], gates, gate_words))
+            return None
+        return scan_device(N, eng, rs, c)
 
     for _ in range(args.warmup):
-        N.lib.tsg_result_free(scan_device(N, eng, rs, c))
+        r = one_step()
+        if r is not None:
+            N.lib.tsg_result_free(r)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     stage = None
     scan_ms = []
+    locs = None
     for i in range(args.steps):
-        res = scan_device(N, eng, rs, c)
-        locs, tm = read_result(N, res)
+        res = one_step()
+        if res is None:  # prefilter only: timings of the engine's last call
+            tm = gate_timings(N, eng)
+        else:
+            locs, tm = read_result(N, res)
+            N.lib.tsg_result_free(res)
         scan_ms.append(tm[17] if len(tm) > 17 and tm[17] > 0 else tm[7])
         stage = tm
-        N.lib.tsg_result_free(res)
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
@@ -312,9 +390,13 @@ def main():
     achieved = c["total"] / (scan_kernel_ms / 1e3) / 1e9
     parity = None
     if rank == 0 and not args.no_parity:
-        parity = parity_checks(N, S, c, locs, sc.rules, seed, args.density)
+        if args.config == 1:
+            parity = gate_checks(N, c, sc.rules, gates, gate_words, seed, args.density)
+        else:
+            parity = parity_checks(N, S, c, locs, sc.rules, seed, args.density,
+                                   n_sample=300 if args.config == 2 else 24, oracle_cfg=cfg_path if cfg else None)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and args.config == 2:
         cores = args.cpu_cores or min(16, os.cpu_count() or 1)
         cpu = cpu_baseline(N, c, seed, args.density, args.cpu_seconds, cores)
     if rank == 0:
@@ -332,14 +414,14 @@ def main():
             "dtype": "u8",
             "data": "synthetic (seeded SURVEY.md §8(d) text model, builtin-rule secrets planted at "
                     f"{args.density:g}/byte, generated in HBM)",
-            "config": {"workload": "configs[2]: full builtin ruleset (prefilter + regex + line numbers + "
-                                   "allow rules), mixed text corpus resident in HBM",
+            "config": {"workload": WORKLOADS[args.config] + (f" ({args.stress_rules} generated rules)"
+                                                              if args.config == 4 else ""),
                        "gb_per_gpu": round(c["total"] / 1e9, 3), "files_per_gpu": c["n_files"],
                        "density": args.density, "parallelism": f"file shards x{world}, no collective"},
             "pct_hbm_peak": round(100.0 * value / (HBM_PEAK_GBPS * world), 2),
-            "roofline": {"bound": "hbm", "kernel": "k_scan_fast", "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": scan_kernel, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic_bytes(c["total"]), "algorithmic_bytes_per_launch": c["total"],
+                         "traffic": traffic_bytes(c["total"]) if args.config == 2 else None, "algorithmic_bytes_per_launch": c["total"],
                          "avg_launch_ms": round(scan_kernel_ms, 3)},
             "stages_ms": {k: round(v, 3) for k, v in zip(
                 ["path_gate", "scan_total", "expand", "sort_jobs", "verify", "exclude", "lines", "scan_kernels"], stage)},

@@ -187,6 +187,11 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
                     const uint64_t* d_offsets, size_t n_files, uint32_t* h_gates_out,
                     size_t gate_words_per_file);
 
+/* Timings of the engine's last tsg_gate_device call, milliseconds, in the
+ * tsg_result_timings layout: [0] scan + report + special gate, [7] generic scan
+ * kernel, [17] k_scan_fast alone, [15] whole call (host clock). */
+int tsg_engine_gate_timings(const tsg_engine* e, double* ms, size_t n, size_t* n_out);
+
 /* Host-side path regex evaluation (per-file, not per-byte): Go MatchString. */
 int tsg_regex_match(const char* pattern, const uint8_t* text, size_t len, int* matched);
 /* Host-side FindAllIndex for diagnostics/tests of the compiler + VM: writes

@@ -1,0 +1,116 @@
+"""GPU parity for BASELINE configs[1] (prefilter only) and configs[4] (stress).
+
+* `tsg_gate_device` -- the per-file rule gate bits of the keyword prefilter --
+  against the oracle's `Rule.MatchKeywords` (scanner.go:169-181) for every
+  (file, rule), on the builtin rules and on a 1000-rule generated set.
+* 1000 generated gitleaks-style custom rules on top of the builtins
+  (tests/stress_rules.py): the scan automaton no longer fits k_scan_fast's
+  LDS image, explosion rules exceed the verify-DFA state cap, keyword-less
+  rules force full-file jobs; findings compared field by field with the
+  oracle on text, one minified long-line file and binary-ish files.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from oracle import secret_oracle as o
+
+from . import corpus_gen, stress_rules
+from .test_gpu_parity import _canon, _oracle_plain, _plain
+
+pytestmark = pytest.mark.gpu
+
+S = pytest.importorskip("trivy_amd.secret")
+N = pytest.importorskip("trivy_amd._native")
+# Device buffers come from the engine's own HIP runtime (the libamdhip64 the
+# .so links), not torch's: a batch handed over as raw device pointers.
+_hip = ctypes.CDLL("libamdhip64.so.7")
+_hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+_hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+_hip.hipFree.argtypes = [ctypes.c_void_p]
+
+
+class _DevBuf:
+    def __init__(self, data: bytes):
+        self.p = ctypes.c_void_p()
+        assert _hip.hipMalloc(ctypes.byref(self.p), max(1, len(data))) == 0
+        src = ctypes.create_string_buffer(data, len(data))
+        assert _hip.hipMemcpy(self.p, src, len(data), 1) == 0  # hipMemcpyHostToDevice
+
+    def __del__(self):
+        _hip.hipFree(self.p)
+
+
+@pytest.fixture(scope="module")
+def stress_cfg(tmp_path_factory):
+    rules = stress_rules.make_rules(20261019, 1000)
+    path = str(tmp_path_factory.mktemp("stress") / "trivy-secret.yaml")
+    stress_rules.write_config(path, rules)
+    return path, rules
+
+
+def _pack(files):
+    """Device batch layout of include/trivy_secret_gpu.h: content + one NUL per file."""
+    sizes = np.array([len(d) for _, d in files], dtype=np.uint64)
+    off = np.zeros(len(files) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(sizes + 1)
+    buf = bytearray(int(off[-1]) + 64)
+    for (_, d), s in zip(files, off[:-1]):
+        buf[int(s):int(s) + len(d)] = d
+    return _DevBuf(bytes(buf)), _DevBuf(off.tobytes())
+
+
+def _gates(sc, files):
+    eng = S.get_engine(0)
+    d_data, d_off = _pack(files)
+    nr = len(sc.rules)
+    words = (nr + 31) // 32
+    out = (ctypes.c_uint32 * (len(files) * words))()
+    N.check(N.lib.tsg_gate_device(eng, sc._rs.handle, d_data.p, d_off.p, len(files), out, words))
+    g = np.frombuffer(bytes(out), dtype=np.uint32).reshape(len(files), words)
+    return [[bool((g[f, r // 32] >> (r % 32)) & 1) for r in range(nr)] for f in range(len(files))]
+
+
+def _check_gates(cfg_path, files):
+    sc = S.new_scanner(S.parse_config(cfg_path) if cfg_path else None, device=0)
+    oc = o.Scanner(o.parse_config(cfg_path) if cfg_path else None)
+    assert [r.id for r in sc.rules] == [r.id for r in oc.rules]
+    got = _gates(sc, files)
+    n_pass = 0
+    for (p, d), g in zip(files, got):
+        low = o.go_bytes_to_lower(d)
+        want = [o.Scanner.match_keywords(r, d, low) for r in oc.rules]
+        bad = [oc.rules[i].id for i in range(len(want)) if want[i] != g[i]]
+        assert not bad, f"gate mismatch on {p}: {bad[:8]}"
+        n_pass += sum(want)
+    return n_pass
+
+
+def test_gate_device_builtin_vs_oracle():
+    files = corpus_gen.make_corpus(77, 600)
+    files += [("kelvin.txt", "K key".encode()), ("longs.txt", "ſk_live_ token".encode()),
+              ("idot.txt", "İ private KEY".encode()), ("empty.txt", b""), ("nul.txt", b"\x00ghp_\x00aws")]
+    assert _check_gates(None, files) > 0
+
+
+def test_gate_device_stress_rules_vs_oracle(stress_cfg):
+    path, rules = stress_cfg
+    files = stress_rules.make_corpus(5, rules, 40, long_line_bytes=50_000)
+    assert _check_gates(path, files) > 0
+
+
+def test_stress_1000_rules_vs_oracle(stress_cfg):
+    path, rules = stress_cfg
+    files = stress_rules.make_corpus(11, rules, 60)
+    sc_o = o.Scanner(o.parse_config(path))
+    sc_g = S.new_scanner(S.parse_config(path), device=0)
+    got = sc_g.scan_batch([S.ScanArgs(p, d) for p, d in files])
+    n_find, custom = 0, 0
+    for (p, d), g in zip(files, got):
+        want = _oracle_plain(sc_o.scan(p, d))
+        n_find += len(want["Findings"])
+        custom += sum(f["RuleID"].startswith("stress-") for f in want["Findings"])
+        assert _canon(_plain(g)) == _canon(want), f"stress file {p}"
+    assert custom > 200  # the generated rules really fire

@@ -120,6 +120,8 @@ _SIGS = {
     "tsg_result_timings": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_size_t,
                                           ctypes.POINTER(ctypes.c_size_t)]),
     "tsg_result_free": (None, [ctypes.c_void_p]),
+    "tsg_engine_gate_timings": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_size_t,
+                                               ctypes.POINTER(ctypes.c_size_t)]),
     "tsg_gate_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t]),
     "tsg_gen_corpus_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,

@@ -2,6 +2,8 @@
 #pragma once
 #include <cstdint>
 #include <deque>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -194,6 +196,7 @@ struct PatternHost {
 
 struct tsg_ruleset {
   std::vector<tsg::RegexHost> regexes;
+  std::map<std::string, int> regex_ids;  // source -> regexes index
   std::vector<tsg::RuleHost> rules;
   std::vector<int> global_allow_regex;  // AllowRules with Regex
   std::vector<int> global_allow_path;   // AllowRules with Path
@@ -204,10 +207,18 @@ struct tsg_ruleset {
   bool any_path_rules = false;  // some rule has Path or per-rule allow paths
   bool any_exclude = false;
   uint64_t id = 0;  // unique id for device-image caching
+  // keyword-only shadow for tsg_gate_device (configs[1]): same rules and
+  // keywords, no regex, so no gate is implied by an anchor and every keyword
+  // is a scan pattern of its own.  Built on first use.
+  mutable std::mutex gate_mu;
+  mutable tsg_ruleset* gate_rs = nullptr;
+  ~tsg_ruleset();
 };
 
 namespace tsg {
 bool build_ac(tsg_ruleset* rs, std::string* err);
+// The keyword-only shadow of rs (owned by rs), or nullptr with *err set.
+const tsg_ruleset* gate_ruleset(const tsg_ruleset* rs, std::string* err);
 }
 
 namespace tsg {

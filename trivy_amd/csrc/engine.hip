@@ -1125,6 +1125,7 @@ __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
       if (hi) mask = ~0ull;  // fold-special runes: no literal filter (as may_match)
     }
     auto may = [&](uint32_t prog) {
+      if (!G.pac) return true;  // no literal prefilter (e.g. > 64 path programs)
       const uint32_t b = prog < G.n_progs ? pbit[prog] : 0xFFu;
       return b == 0xFFu || ((mask >> b) & 1);
     };
@@ -1512,10 +1513,11 @@ __device__ bool bitstate_captures(const gre::ProgView& p, const uint8_t* text, u
   const uint32_t end = me + 16 < n ? me + 16 : n;  // positions the search may visit: [ms, end]
   const uint32_t W = end - ms + 1;
   const uint32_t vis_words = (P * W + 31) / 32;
-  if (2 * ng > 8 || P >= 0x4000 || W >= 0xFFFF || vis_words + 32 > kBsWords) return false;
+  // arena: visited bits | job stack | the 8 tracked capture slots (gcap, the last 8 words)
+  if (2 * ng > 8 || P >= 0x4000 || W >= 0xFFFF || vis_words + 8 + 32 > kBsWords) return false;
   uint32_t* vis = area;
   uint32_t* stk = area + vis_words;
-  const uint32_t stk_cap = kBsWords - vis_words;
+  const uint32_t stk_cap = kBsWords - 8 - vis_words;
   for (uint32_t i = 0; i < vis_words; ++i) vis[i] = 0;
   for (uint32_t k = 0; k < 2 * ng; ++k) gcap[k] = -1;
   auto local = [&](uint32_t slot) -> int {  // tracked index of capture slot, or -1
@@ -1935,6 +1937,7 @@ __global__ __launch_bounds__(256) void k_lines(const uint8_t* data, const uint64
   const DevLoc L = locs[w];
   if (L.flags) return;
   const uint64_t fs = off[L.file];
+  if (L.start > L.end || fs + L.end >= off[L.file + 1]) return;  // never read outside the file
   const uint32_t g0 = wave_nl_prefix(data, nl_pre, fs, lane);
   const uint32_t g1 = wave_nl_prefix(data, nl_pre, fs + L.start, lane);
   const uint32_t g2 = wave_nl_prefix(data, nl_pre, fs + L.end, lane);
@@ -2053,9 +2056,38 @@ struct tsg_engine {
   uint64_t scratch_stride = 0;
   hipEvent_t ev[12];
   bool events = false;
+  DBuf<uint32_t> gate_out, gate_rules;  // tsg_gate_device: rule gate words, rule -> keyword-id CSR
+  std::vector<double> gate_tm;          // timings of the last tsg_gate_device call
 };
 
 namespace {
+
+// Rule gate words of tsg_gate_device, one lane per file: rule r passes iff it
+// has no keywords or one of its keyword ids is set in the file's keyword bits
+// (Rule.MatchKeywords, scanner.go:169-181).  `rules` is a CSR: rules[0..R]
+// offsets into rules[R+1..], a keyword id or 0xFFFFFFFF for "always".
+__global__ void k_rule_gates(const uint32_t* __restrict__ file_kw, uint32_t kw_words, uint32_t n_files,
+                             const uint32_t* __restrict__ rules, uint32_t n_rules, uint32_t* __restrict__ out,
+                             uint32_t words) {
+  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= n_files) return;
+  const uint32_t* kw = file_kw + (uint64_t)f * kw_words;
+  const uint32_t* ids = rules + n_rules + 1;
+  uint32_t w = 0;
+  for (uint32_t r = 0; r < n_rules; ++r) {
+    bool pass = rules[r] == rules[r + 1];
+    for (uint32_t k = rules[r]; k < rules[r + 1] && !pass; ++k) {
+      const uint32_t id = ids[k];
+      pass = id == 0xFFFFFFFFu || ((kw[id >> 5] >> (id & 31)) & 1);
+    }
+    if (pass) w |= 1u << (r & 31);
+    if ((r & 31) == 31 || r + 1 == n_rules) {
+      if ((r >> 5) < words) out[(uint64_t)f * words + (r >> 5)] = w;
+      w = 0;
+    }
+  }
+  for (uint32_t j = (n_rules + 31) >> 5; j < words; ++j) out[(uint64_t)f * words + j] = 0;
+}
 
 int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   DevImage& im = e->img;
@@ -3220,6 +3252,15 @@ static int scan_device_impl(tsg_engine* e, const tsg_ruleset* rs, const uint8_t*
 int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, const uint64_t* d_offsets,
                     size_t n_files, uint32_t* h_gates_out, size_t gate_words_per_file) {
   if (!e || !rs || !d_offsets) return TSG_ERR_INVALID_ARG;
+  {
+    std::string err;
+    const tsg_ruleset* g = gate_ruleset(rs, &err);
+    if (!g) {
+      set_last_error(err);
+      return TSG_ERR_INTERNAL;
+    }
+    rs = g;
+  }
   std::lock_guard<std::mutex> lk(e->mu);
   HIP_TRY(hipSetDevice(e->device));
   int rc = upload_ruleset(e, rs);
@@ -3229,6 +3270,12 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
   uint64_t nbytes = 0;
   HIP_TRY(hipMemcpy(&nbytes, d_offsets + n_files, 8, hipMemcpyDeviceToHost));
   hipStream_t s = e->stream;
+  const auto wall0 = std::chrono::steady_clock::now();
+  if (!e->events) {
+    for (auto& ev : e->ev) HIP_TRY(hipEventCreate(&ev));
+    e->events = true;
+  }
+  e->fast_timed = false;
   HIP_TRY(e->ctrl.ensure(1));
   HIP_TRY(e->file_kw.ensure((size_t)nf * RS.kw_words + 1));
   HIP_TRY(e->file_flags.ensure(nf + 1));
@@ -3253,6 +3300,7 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
   HIP_TRY(e->nl_blocks.ensure(n_nlb));
   HIP_TRY(hipMemsetAsync(e->nl_blocks.p, 0, n_nlb * 4, s));
   P.nl_blocks = e->nl_blocks.p;
+  HIP_TRY(hipEventRecord(e->ev[8], s));
   for (int attempt = 0; attempt < 2 && nbytes; ++attempt) {
     if ((rc = launch_scan(e, P))) return rc;
     Ctrl c;
@@ -3264,26 +3312,52 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
     e->ev_ovf_need = c.ev_overflow + (c.ev_overflow >> 2);  // events were lost: grow and rescan
     HIP_TRY(hipMemsetAsync(e->ctrl.p, 0, offsetof(Ctrl, n_special), s));  // keep the special-file list
   }
-  std::vector<uint32_t> kw((size_t)nf * RS.kw_words);
-  if (nf) HIP_TRY(hipMemcpyAsync(kw.data(), e->file_kw.p, kw.size() * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  if (h_gates_out) {
-    // rule gate bits from keyword bits (host: per file x rule, not per byte)
-    for (uint32_t f = 0; f < nf; ++f) {
-      uint32_t* g = h_gates_out + (size_t)f * gate_words_per_file;
-      memset(g, 0, gate_words_per_file * 4);
-      for (size_t r = 0; r < rs->rules.size() && r / 32 < gate_words_per_file; ++r) {
-        const RuleHost& rh = rs->rules[r];
-        bool pass = rh.keywords.empty();
-        for (auto& k : rh.keywords) {
-          if (k.empty()) { pass = true; break; }
-          size_t id = std::find(rs->keywords.begin(), rs->keywords.end(), k) - rs->keywords.begin();
-          if ((kw[(size_t)f * RS.kw_words + id / 32] >> (id % 32)) & 1) { pass = true; break; }
-        }
-        if (pass) g[r / 32] |= 1u << (r % 32);
+  if (e->events) HIP_TRY(hipEventRecord(e->ev[9], s));
+  if (h_gates_out && nf && gate_words_per_file) {
+    // rule -> keyword-id CSR (host, per ruleset: not per byte), gates on the GPU
+    const uint32_t R = (uint32_t)rs->rules.size();
+    std::vector<uint32_t> csr(R + 1);
+    std::vector<uint32_t> ids;
+    for (uint32_t r = 0; r < R; ++r) {
+      csr[r] = (uint32_t)ids.size();
+      for (auto& k : rs->rules[r].keywords) {
+        if (k.empty()) { ids.push_back(0xFFFFFFFFu); continue; }
+        ids.push_back((uint32_t)(std::find(rs->keywords.begin(), rs->keywords.end(), k) - rs->keywords.begin()));
       }
     }
+    csr[R] = (uint32_t)ids.size();
+    csr.insert(csr.end(), ids.begin(), ids.end());
+    HIP_TRY(e->gate_rules.ensure(csr.size()));
+    HIP_TRY(hipMemcpyAsync(e->gate_rules.p, csr.data(), csr.size() * 4, hipMemcpyHostToDevice, s));
+    const size_t words = gate_words_per_file;
+    HIP_TRY(e->gate_out.ensure((size_t)nf * words));
+    hipLaunchKernelGGL(k_rule_gates, dim3((nf + 255) / 256), dim3(256), 0, s, e->file_kw.p, RS.kw_words, nf,
+                       e->gate_rules.p, R, e->gate_out.p, (uint32_t)words);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(h_gates_out, e->gate_out.p, (size_t)nf * words * 4, hipMemcpyDeviceToHost, s));
   }
+  HIP_TRY(hipStreamSynchronize(s));
+  e->gate_tm.assign(18, 0.0);
+  if (e->events && nbytes) {
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, e->ev[8], e->ev[9]));
+    e->gate_tm[0] = ms;  // scan + report + special gate
+    if (e->fast_timed) {
+      HIP_TRY(hipEventElapsedTime(&ms, e->ev[10], e->ev[11]));
+      e->gate_tm[17] = ms;
+    } else {
+      e->gate_tm[7] = e->gate_tm[0];
+    }
+  }
+  e->gate_tm[15] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - wall0).count();
+  return TSG_OK;
+}
+
+int tsg_engine_gate_timings(const tsg_engine* e, double* ms, size_t n, size_t* n_out) {
+  if (!e || (!ms && n)) return TSG_ERR_INVALID_ARG;
+  const size_t k = std::min(n, e->gate_tm.size());
+  for (size_t i = 0; i < k; ++i) ms[i] = e->gate_tm[i];
+  if (n_out) *n_out = k;
   return TSG_OK;
 }
 

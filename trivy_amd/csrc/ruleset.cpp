@@ -320,6 +320,9 @@ bool build_ac(tsg_ruleset* rs, std::string* err) {
 using namespace tsg;
 
 static int add_regex(tsg_ruleset* rs, const char* src, std::string* err) {
+  // one program per distinct source (custom rule sets repeat path and allow regexes)
+  auto it = rs->regex_ids.find(src);
+  if (it != rs->regex_ids.end()) return it->second;
   RegexHost r;
   r.src = src;
   if (!gre::compile(r.src, &r.c, err)) {
@@ -327,6 +330,7 @@ static int add_regex(tsg_ruleset* rs, const char* src, std::string* err) {
     return -1;
   }
   rs->regexes.push_back(std::move(r));
+  rs->regex_ids[src] = (int)rs->regexes.size() - 1;
   return (int)rs->regexes.size() - 1;
 }
 
@@ -532,6 +536,10 @@ int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_r
 
 void tsg_ruleset_free(tsg_ruleset* rs) { delete rs; }
 
+tsg_ruleset::~tsg_ruleset() { delete gate_rs; }
+
+
+
 size_t tsg_ruleset_rule_count(const tsg_ruleset* rs) { return rs ? rs->rules.size() : 0; }
 
 int tsg_ruleset_rule_info(const tsg_ruleset* rs, size_t i, int* mode, uint32_t* amin,
@@ -705,6 +713,35 @@ int tsg_regex_find_all(const char* pattern, const uint8_t* text, size_t len, int
 }
 
 }  // extern "C"
+
+namespace tsg {
+const tsg_ruleset* gate_ruleset(const tsg_ruleset* rs, std::string* err) {
+  std::lock_guard<std::mutex> lk(rs->gate_mu);
+  if (rs->gate_rs) return rs->gate_rs;
+  // rules keep their keywords (already lowercased: ToLower is idempotent on
+  // them) and lose the regex; allow rules, paths and excludes do not touch
+  // MatchKeywords (scanner.go:169-181)
+  std::vector<tsg_rule> rules(rs->rules.size());
+  std::vector<std::vector<const char*>> kws(rs->rules.size());
+  for (size_t i = 0; i < rs->rules.size(); ++i) {
+    const RuleHost& r = rs->rules[i];
+    for (auto& k : r.keywords) kws[i].push_back(k.c_str());
+    tsg_rule& t = rules[i];
+    memset(&t, 0, sizeof(t));
+    t.id = r.id.c_str();
+    t.keywords = kws[i].data();
+    t.n_keywords = kws[i].size();
+  }
+  tsg_ruleset* g = nullptr;
+  char ebuf[512] = {0};
+  if (tsg_ruleset_compile(rules.data(), rules.size(), nullptr, 0, nullptr, 0, &g, ebuf, sizeof(ebuf)) != TSG_OK) {
+    *err = std::string("gate ruleset: ") + ebuf;
+    return nullptr;
+  }
+  rs->gate_rs = g;
+  return g;
+}
+}  // namespace tsg
 
 extern "C" int tsg_ruleset_stats(const tsg_ruleset* rs, uint32_t* n_states, uint32_t* n_classes,
                                  uint32_t* n_patterns, uint32_t* n_keywords, int* fast_path) {
