@@ -423,9 +423,12 @@ def main():
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic_bytes(c["total"]) if args.config == 2 else None, "algorithmic_bytes_per_launch": c["total"],
                          "avg_launch_ms": round(scan_kernel_ms, 3)},
-            "stages_ms": {k: round(v, 3) for k, v in zip(
-                ["path_gate", "scan_total", "expand", "sort_jobs", "verify", "exclude", "lines", "scan_kernels"], stage)},
-            "counts": {k: int(v) for k, v in zip(["hits", "candidates", "jobs", "locs", "event_overflow", "events", "outputs"], stage[8:15])},
+            "stages_ms": ({"prefilter_total": round(stage[0], 3), "scan_kernel": round(scan_kernel_ms, 3)}
+                          if args.config == 1 else {k: round(v, 3) for k, v in zip(
+                              ["path_gate", "scan_total", "expand", "sort_jobs", "verify", "exclude", "lines",
+                               "scan_kernels"], stage)}),
+            "counts": None if args.config == 1 else {k: int(v) for k, v in zip(
+                ["hits", "candidates", "jobs", "locs", "event_overflow", "events", "outputs"], stage[8:15])},
             "host_ms": {"call_wall": round(stage[15], 3), "post": round(stage[16], 3)},
             "cpu_baseline": cpu,
             "parity": parity,

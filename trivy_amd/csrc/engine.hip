@@ -95,6 +95,7 @@ struct DevLoc {
 
 struct ScanParams {
   uint32_t report_mode;  // timing experiments only (TSG_REPORT_MODE): 1 = no file lookups in k_report
+  uint32_t gen_lds_rows;  // k_scan_generic<false>: automaton rows staged in LDS (the shallow ones)
   const uint8_t* data;
   const uint64_t* off;  // n_files + 1
   uint64_t nbytes;
@@ -235,11 +236,19 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_generic(ScanParams P) {
   const AcDev& ac = P.rs.ac;
   const uint32_t K = ac.nclasses;
   for (int i = threadIdx.x; i < 256; i += kScanThreads) cls[i] = ac.cls[i];
-  if (kLdsTable) {
-    const uint32_t n = ac.nstates * K;
+  // kLdsTable: the whole table in LDS; else its first gen_lds_rows rows (states
+  // are numbered breadth-first, so those are where text keeps the automaton)
+  // and the deep rest from global memory (L2-resident)
+  const uint32_t lds_rows = kLdsTable ? ac.nstates : P.gen_lds_rows;
+  {
+    const uint32_t n = lds_rows * K;
     for (uint32_t i = threadIdx.x; i < n; i += kScanThreads) dl[i] = ac.delta[i];
   }
-  const uint16_t* delta = kLdsTable ? dl : ac.delta;
+  auto next = [&](uint32_t st, uint32_t c) -> uint32_t {
+    const uint32_t i = st * K + c;
+    if (kLdsTable) return dl[i];
+    return st < lds_rows ? (uint32_t)dl[i] : (uint32_t)ac.delta[i];
+  };
   const uint32_t tid = threadIdx.x;
   const uint64_t nsteps = (P.nbytes + kBlockBytes - 1) / kBlockBytes;
   uint64_t last_kw = ~0ull;
@@ -276,12 +285,12 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_generic(ScanParams P) {
     // warm-up: the automaton restarted kAcMaxLit-1 bytes earlier (a NUL
     // separator inside the window resets it, so files never leak)
     const uint64_t w0 = p0 >= (uint64_t)(kAcMaxLit - 1) ? p0 - (kAcMaxLit - 1) : 0;
-    for (uint64_t p = w0; p < p0; ++p) st = delta[st * K + cls[row[(int64_t)p - (int64_t)p0]]] & 0x7FFFu;
+    for (uint64_t p = w0; p < p0; ++p) st = next(st, cls[row[(int64_t)p - (int64_t)p0]]) & 0x7FFFu;
     uint32_t nl = 0;
     for (uint64_t p = p0; p < pend; ++p) {
       const uint8_t b = row[p - p0];
       nl += b == '\n';
-      const uint32_t nx = delta[st * K + cls[b]];
+      const uint32_t nx = next(st, cls[b]);
       st = nx & 0x7FFFu;
       if (nx & 0x8000u) report(P, st, p, &last_kw);
     }
@@ -317,6 +326,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_generic(ScanParams P) {
 // other shapes stay compilable for A/B runs (TSG_FAST_VARIANT).
 constexpr int kFastChains = 1;
 constexpr int kFastVecs = 8;
+constexpr int kFastEventWin = 4;  // 8-byte groups per wave-level event check
 constexpr uint32_t kFastUnitMax = 2 * kNlBlock;  // largest chains * span (tail buffer size)
 
 __device__ inline uint32_t nl_count_dword(uint32_t w) {
@@ -452,7 +462,47 @@ __device__ inline void fast_group2(const ScanParams& P, const uint8_t* T, uint32
   B.prev = make_uint2(b0, b1);
 }
 
-template <int CH, int V, int kFastThreads, int kMode = 0>
+// G consecutive 8-byte groups of a chain with ONE wave-level event check:
+// the per-group maxima are kept, and only when some live lane reached an
+// output state anywhere in the window (rare: ~one group in 10^3) are the
+// groups' events appended in order.  Cuts the compare / ballot / branch per
+// group that otherwise sits on every chain step.
+template <int V, int kMode, int G>
+__device__ inline void fast_window(const ScanParams& P, const uint8_t* T, uint32_t out_e, FastChain<V>& C,
+                                   const uint32_t (&d)[2 * G], uint64_t gpos, bool live, uint64_t lanes_lt,
+                                   FastEvent* ev_seg, uint32_t* ev_count) {
+  uint32_t gs[G], m[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const uint32_t d0 = d[2 * g], d1 = d[2 * g + 1];
+    if (!(kMode & 2)) C.nl += nl_count_dword(d0) + nl_count_dword(d1);
+    C.hi |= d0 | d1;
+    const uint32_t f0 = fold6(d0), f1 = fold6(d1);
+    gs[g] = C.e;
+    uint32_t mm = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      C.e = fstep(T, C.e, j < 4 ? f0 : f1, j & 3);
+      mm = mm > C.e ? mm : C.e;
+    }
+    m[g] = mm;
+  }
+  if (!(kMode & 1)) {
+    uint32_t mx = m[0];
+#pragma unroll
+    for (int g = 1; g < G; ++g) mx = mx > m[g] ? mx : m[g];
+    if (__builtin_amdgcn_uicmp(mx, out_e, 35) & __ballot(live)) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        fast_event(P, out_e, C, m[g], gs[g], d[2 * g], d[2 * g + 1], gpos + 8 * g, live, lanes_lt, ev_seg, ev_count);
+        C.prev = make_uint2(d[2 * g], d[2 * g + 1]);
+      }
+    }
+  }
+  C.prev = make_uint2(d[2 * G - 2], d[2 * G - 1]);
+}
+
+template <int CH, int V, int kFastThreads, int kMode = 0, int kWin = 1>
 __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
   constexpr uint32_t kUnit = CH * kNlBlock;          // bytes per lane per work unit
   constexpr int kStep = V * 16;                      // bytes per chain step
@@ -532,6 +582,16 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
                       lanes_lt, ev_seg, &ev_count);
           fast_group2(P, T, out_e, C[0], C[CH - 1], v.z, v.w, w.z, w.w, C[0].pos + 16 * k + 8,
                       C[CH - 1].pos + 16 * k + 8, live, lanes_lt, ev_seg, &ev_count);
+        } else if (kWin == 2) {
+          const uint4 v = C[0].cur[k];
+          const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+          fast_window<V, kMode, 2>(P, T, out_e, C[0], d, C[0].pos + 16 * k, live, lanes_lt, ev_seg, &ev_count);
+        } else if (kWin == 4) {
+          if (k % 2 == 0) {
+            const uint4 v = C[0].cur[k], w = C[0].cur[k + 1 < V ? k + 1 : k];
+            const uint32_t d[8] = {v.x, v.y, v.z, v.w, w.x, w.y, w.z, w.w};
+            fast_window<V, kMode, 4>(P, T, out_e, C[0], d, C[0].pos + 16 * k, live, lanes_lt, ev_seg, &ev_count);
+          }
         } else {
           const uint4 v = C[0].cur[k];
           fast_group<V, kMode>(P, T, out_e, C[0], v.x, v.y, C[0].pos + 16 * k, live, lanes_lt, ev_seg, &ev_count);
@@ -1137,14 +1197,22 @@ __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
       continue;
     }
     if (!G.any_rule_paths) continue;
+    // rules share path programs (identical sources compile once): the last
+    // evaluated program's answer is reused for the runs of rules naming it
+    uint32_t memo_prog = 0xFFFFFFFFu;
+    bool memo_res = false;
+    auto path_match = [&](uint32_t prog) {
+      if (prog != memo_prog) {
+        memo_prog = prog;
+        memo_res = may(prog) && match_string(G.rs.progs[prog], path, plen, sc);
+      }
+      return memo_res;
+    };
     for (uint32_t r = 0; r < G.rs.n_rules; ++r) {
       bool skip = false;
-      if (G.rule_path[r] >= 0) {
-        const uint32_t pp = (uint32_t)G.rule_path[r];
-        skip = !(may(pp) && match_string(G.rs.progs[pp], path, plen, sc));
-      }
+      if (G.rule_path[r] >= 0) skip = !path_match((uint32_t)G.rule_path[r]);
       for (uint32_t k = G.rule_apath_off[r]; k < G.rule_apath_off[r + 1] && !skip; ++k)
-        skip = may(G.rule_apath[k]) && match_string(G.rs.progs[G.rule_apath[k]], path, plen, sc);
+        skip = path_match(G.rule_apath[k]);
       if (skip) G.path_mask[(size_t)f * G.rule_words + (r >> 5)] |= 1u << (r & 31);
     }
   }
@@ -2565,6 +2633,8 @@ int launch_scan(tsg_engine* e, ScanParams P) {
     int deep_v = 0, deep_d = 0;  // TSG_FAST_VARIANT=d<V>x<D>: k_scan_deep
     int mode = 0;                // TSG_SCAN_MODE: timing experiments only (see fast_group)
     if (const char* m = getenv("TSG_SCAN_MODE")) mode = atoi(m);
+    int win = kFastEventWin;     // groups per event check (fast_window; A/B via TSG_EVENT_WIN)
+    if (const char* w = getenv("TSG_EVENT_WIN")) win = atoi(w);
     if (const char* v = getenv("TSG_FAST_VARIANT")) {
       if (sscanf(v, "d%dx%d", &deep_v, &deep_d) != 2) {
         deep_v = 0;
@@ -2618,6 +2688,8 @@ int launch_scan(tsg_engine* e, ScanParams P) {
   else if (chains == 1 && vecs == 8 && mode == M) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, M>), dim3(blocks), dim3(nt), 0, s, P);
     TSG_MODE(1) TSG_MODE(2) TSG_MODE(3) TSG_MODE(4) TSG_MODE(5) TSG_MODE(6) TSG_MODE(7)
 #undef TSG_MODE
+    else if (chains == 1 && vecs == 8 && win == 2) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 2>), dim3(blocks), dim3(nt), 0, s, P);
+    else if (chains == 1 && vecs == 8 && win == 4) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 4>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1 && vecs == 8) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1) hipLaunchKernelGGL((k_scan_fast<1, 4, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     else if (vecs == 4) hipLaunchKernelGGL((k_scan_fast<2, 4, 1024>), dim3(blocks), dim3(nt), 0, s, P);
@@ -2633,7 +2705,16 @@ int launch_scan(tsg_engine* e, ScanParams P) {
   } else {
     const size_t table_bytes = (size_t)ac.nstates * ac.nclasses * 2;
     const bool lds_table = table_bytes <= (size_t)kLdsTableMax;
-    const size_t lds = 256 + kTileLds + (lds_table ? table_bytes : 0);
+    // a table too large for LDS is read from global memory (L2-resident).
+    // Measured on configs[4] (6669 states x 46 classes): staging its 445
+    // shallowest rows in LDS is slower (46.7 vs 35.8 ms / 10 GB) -- a wave
+    // still waits on the rare lane in a deep state at almost every byte, and
+    // the LDS halves the blocks per CU.  TSG_GEN_LDS_KB re-enables it for A/B.
+    P.gen_lds_rows = lds_table ? ac.nstates : 0;
+    if (!lds_table)
+      if (const char* kb = getenv("TSG_GEN_LDS_KB"))
+        P.gen_lds_rows = (uint32_t)std::min<size_t>(ac.nstates, ((size_t)atoi(kb) << 10) / (2u * ac.nclasses));
+    const size_t lds = 256 + kTileLds + (size_t)P.gen_lds_rows * ac.nclasses * 2;
     const uint64_t nsteps = (P.nbytes + kBlockBytes - 1) / kBlockBytes;
     const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nsteps, (uint64_t)e->num_cus * 8));
     if (lds_table) {

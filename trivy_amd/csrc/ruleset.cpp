@@ -124,12 +124,17 @@ static bool build_ac_depth(tsg_ruleset* rs, int depth, std::string* err) {
     }
   }
   // renumber: states without outputs first (root stays 0), output states
-  // last, so k_scan_fast detects an output with one max() per byte
+  // last, each part in breadth-first order, so shallow states (where text
+  // keeps the automaton) have the smallest ids: k_scan_generic keeps the
+  // first rows of a table too large for LDS in LDS
   {
+    std::vector<int> bfs;
+    bfs.push_back(0);
+    bfs.insert(bfs.end(), order.begin(), order.end());
     std::vector<int> perm(S), inv;
-    for (int st = 0; st < S; ++st)
+    for (int st : bfs)
       if (outs[st].empty()) { perm[st] = (int)inv.size(); inv.push_back(st); }
-    for (int st = 0; st < S; ++st)
+    for (int st : bfs)
       if (!outs[st].empty()) { perm[st] = (int)inv.size(); inv.push_back(st); }
     std::vector<std::vector<int>> go2(S);
     std::vector<std::vector<uint16_t>> outs2(S);
