@@ -100,6 +100,7 @@ typedef struct tsg_finding {
 /* Per-file flags in a result. */
 #define TSG_FILE_PATH_ALLOWED 1u /* Global.AllowPath matched: Secret{FilePath} without findings (scanner.go:375-379) */
 #define TSG_FILE_SPECIAL 2u      /* content holds U+0130/U+017F/U+212A: scanned on the exact full-scan path */
+#define TSG_FILE_BINARY 4u       /* tsg_analyze: utils.IsBinary (utils.go:77-95) -> skipped, Analyze returns nil */
 
 const char* tsg_version(void);
 const char* tsg_last_error(void);
@@ -180,6 +181,17 @@ size_t tsg_result_findings(const tsg_result* r, size_t file, const tsg_finding**
 /* Per-stage device timings of the last scan, milliseconds. */
 int tsg_result_timings(const tsg_result* r, double* ms, size_t n, size_t* n_out);
 void tsg_result_free(tsg_result* r);
+
+/* SecretAnalyzer.Analyze (pkg/fanal/analyzer/secret/secret.go:79-113) over a
+ * batch of RAW files, the per-file work on the GPU: the utils.IsBinary gate on
+ * the first min(len, 300) bytes (utils.go:77-95; binary files get
+ * TSG_FILE_BINARY and no locations), deletion of every '\r'
+ * (secret.go:91, bytes.ReplaceAll) by stream compaction in HBM, then the scan.
+ * files[i].path is the FilePath the findings carry: the caller applies
+ * secret.go:95-98 (the '/' prefix when AnalysisInput.Dir is empty).  Offsets
+ * and line numbers of the result refer to the CR-stripped content, exactly as
+ * Analyze hands it to Scan; findings are built from it. */
+int tsg_analyze(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, size_t n_files, tsg_result** out);
 
 /* Prefilter-only pass (BASELINE config 2): per-file rule gate bitmasks
  * (rule i passes iff bit i set), exactly MatchKeywords (scanner.go:169-181). */

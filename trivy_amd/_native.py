@@ -31,6 +31,7 @@ TSG_ERR_PANIC = 7
 
 TSG_FILE_PATH_ALLOWED = 1
 TSG_FILE_SPECIAL = 2
+TSG_FILE_BINARY = 4
 
 c_char_pp = ctypes.POINTER(ctypes.c_char_p)
 
@@ -120,6 +121,8 @@ _SIGS = {
     "tsg_result_timings": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_size_t,
                                           ctypes.POINTER(ctypes.c_size_t)]),
     "tsg_result_free": (None, [ctypes.c_void_p]),
+    "tsg_analyze": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(FileC), ctypes.c_size_t,
+                                   ctypes.POINTER(ctypes.c_void_p)]),
     "tsg_engine_gate_timings": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_size_t,
                                                ctypes.POINTER(ctypes.c_size_t)]),
     "tsg_gate_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

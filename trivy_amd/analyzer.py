@@ -82,19 +82,13 @@ class SecretAnalyzer:
         return self.analyze_batch([(file_path, content, dir_)])[0]
 
     def analyze_batch(self, inputs: Sequence[Tuple[str, bytes, str]]) -> List[Optional[List[Secret]]]:
-        """Batched Analyze: binary gate, CR strip and '/' prefix per file, then
-        one GPU scan over all remaining files."""
+        """Batched Analyze (secret.go:79-113): the '/' prefix of secret.go:95-98
+        on the path here; the IsBinary gate, '\r' deletion and Scan of every
+        file in one GPU call (tsg_analyze)."""
+        batch = [S.ScanArgs(path if dir_ != "" else "/" + path, content) for path, content, dir_ in inputs]
         out: List[Optional[List[Secret]]] = [None] * len(inputs)
-        batch, where = [], []
-        for i, (path, content, dir_) in enumerate(inputs):
-            if is_binary(content, len(content)):
-                continue
-            content = content.replace(b"\r", b"")
-            fp = path if dir_ != "" else "/" + path
-            batch.append(S.ScanArgs(fp, content))
-            where.append(i)
         if batch:
-            for i, res in zip(where, self.scanner.scan_batch(batch)):
-                if res.Findings:
+            for i, res in enumerate(self.scanner.analyze_batch(batch)):
+                if res is not None and res.Findings:
                     out[i] = [res]
         return out

@@ -2015,6 +2015,120 @@ __global__ __launch_bounds__(256) void k_lines(const uint8_t* data, const uint64
   }
 }
 
+// ---- SecretAnalyzer front end (tsg_analyze) --------------------------------
+// utils.IsBinary (utils.go:77-95) per byte of the head.
+__device__ inline bool is_binary_byte(uint32_t b) {
+  return b < 7 || b == 11 || (b > 13 && b < 27) || (b > 27 && b < 0x20) || b == 0x7F;
+}
+
+// One wave per file: the first min(len, 300) bytes decide IsBinary; a binary
+// file's bytes become '\r', so the compaction drops it to an empty file.
+__global__ __launch_bounds__(256) void k_binary(uint8_t* data, const uint64_t* off, uint32_t n_files,
+                                                uint8_t* bin_flags, unsigned long long* n_drop) {
+  const uint32_t f = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // wave-uniform
+  const uint32_t lane = threadIdx.x & 63;
+  if (f >= n_files) return;
+  const uint64_t s = off[f], len = off[f + 1] - 1 - s;
+  const uint32_t head = len < 300 ? (uint32_t)len : 300u;
+  bool bin = false;
+  for (uint32_t i = lane; i < head; i += 64) bin |= is_binary_byte(data[s + i]);
+  bin = __ballot(bin) != 0;
+  if (lane == 0) {
+    bin_flags[f] = bin ? 1 : 0;
+    if (bin && len) atomicAdd(n_drop, 1ull);
+  }
+  if (bin)
+    for (uint64_t i = lane; i < len; i += 64) data[s + i] = '\r';
+}
+
+__device__ inline uint32_t cr_count_dword(uint32_t w) {  // bytes == 0x0D (exact SWAR)
+  const uint32_t t = w ^ 0x0D0D0D0Du;
+  const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
+  return __builtin_popcount(z);
+}
+
+constexpr uint32_t kStripBlock = 4096;  // bytes per block (256 threads x 16)
+
+// 16 bytes of the batch for thread t of block b (zero past the end) and how
+// many of them survive the '\r' deletion.
+__device__ inline uint32_t strip_chunk(const uint8_t* data, uint64_t nbytes, uint64_t g, uint4* v) {
+  if (g + 16 <= nbytes) {
+    *v = *(const uint4*)(data + g);
+    return 16 - cr_count_dword(v->x) - cr_count_dword(v->y) - cr_count_dword(v->z) - cr_count_dword(v->w);
+  }
+  uint8_t tmp[16] = {0};
+  uint32_t kept = 0;
+  for (uint32_t i = 0; i < 16; ++i) {
+    const uint64_t q = g + i;
+    tmp[i] = q < nbytes ? data[q] : '\r';
+    kept += tmp[i] != '\r';
+  }
+  memcpy(v, tmp, 16);
+  return kept;
+}
+
+__device__ inline uint32_t block_excl_scan(uint32_t x, uint32_t* total) {
+  __shared__ uint32_t wsum[4];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, 64);
+    if (lane >= (uint32_t)d) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t base = 0, all = 0;
+  for (uint32_t k = 0; k < 4; ++k) {
+    if (k < w) base += wsum[k];
+    all += wsum[k];
+  }
+  __syncthreads();
+  *total = all;
+  return base + inc - x;
+}
+
+__global__ __launch_bounds__(256) void k_strip_count(const uint8_t* data, uint64_t nbytes, uint64_t* blk_kept) {
+  const uint64_t g = (uint64_t)blockIdx.x * kStripBlock + threadIdx.x * 16;
+  uint4 v;
+  const uint32_t kept = strip_chunk(data, nbytes, g, &v);
+  uint32_t total;
+  (void)block_excl_scan(kept, &total);
+  if (threadIdx.x == 0) blk_kept[blockIdx.x] = total;
+}
+
+// Writes the kept bytes at their compacted positions and, per 16-byte chunk,
+// the compacted position of its first byte (for the file offsets).
+__global__ __launch_bounds__(256) void k_strip_compact(const uint8_t* data, uint64_t nbytes, const uint64_t* blk_base,
+                                                       uint8_t* out, uint64_t* chunk_pos) {
+  const uint64_t chunk = (uint64_t)blockIdx.x * (kStripBlock / 16) + threadIdx.x;
+  const uint64_t g = chunk * 16;
+  uint4 v;
+  const uint32_t kept = strip_chunk(data, nbytes, g, &v);
+  uint32_t total;
+  const uint64_t pos = blk_base[blockIdx.x] + block_excl_scan(kept, &total);
+  if (g < nbytes) chunk_pos[chunk] = pos;
+  const uint8_t* b = (const uint8_t*)&v;
+  uint64_t o = pos;
+  for (uint32_t i = 0; i < 16; ++i)
+    if (b[i] != '\r' && g + i < nbytes) out[o++] = b[i];
+}
+
+// off'[f] = compacted position of byte off[f].
+__global__ void k_strip_offsets(const uint8_t* data, const uint64_t* off, uint32_t n_files, const uint64_t* chunk_pos,
+                                uint64_t total_kept, uint64_t* off_out) {
+  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f > n_files) return;
+  if (f == n_files) {
+    off_out[f] = total_kept;
+    return;
+  }
+  const uint64_t p = off[f], c = p / 16;
+  uint64_t q = chunk_pos[c];
+  for (uint64_t i = c * 16; i < p; ++i) q += data[i] != '\r';
+  off_out[f] = q;
+}
+
 }  // namespace
 
 // =========================================================== host side ======
@@ -2125,6 +2239,10 @@ struct tsg_engine {
   hipEvent_t ev[12];
   bool events = false;
   DBuf<uint32_t> gate_out, gate_rules;  // tsg_gate_device: rule gate words, rule -> keyword-id CSR
+  // tsg_analyze: IsBinary flags, '\r'-stripped batch and its offsets, block sums, chunk positions
+  DBuf<uint8_t> bin8, strip_out;
+  DBuf<uint64_t> strip_off, blk_kept, blk_base, chunk_pos;
+  DBuf<unsigned long long> n_drop;
   std::vector<double> gate_tm;          // timings of the last tsg_gate_device call
 };
 
@@ -3328,6 +3446,128 @@ static int scan_device_impl(tsg_engine* e, const tsg_ruleset* rs, const uint8_t*
   }
   *out = res;
   return TSG_OK;
+}
+
+// SecretAnalyzer.Analyze over raw files (secret.go:79-113): pack -> H2D ->
+// IsBinary (k_binary) -> '\r' deletion by compaction (k_strip_*) -> scan.
+static int analyze_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, size_t n_files,
+                        tsg_result** out) {
+  if (!e || !rs || !out || (n_files && !files)) return TSG_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(e->mu);
+  *out = nullptr;
+  HIP_TRY(hipSetDevice(e->device));
+  std::vector<uint64_t> off(n_files + 1, 0), poff(n_files + 1, 0);
+  for (size_t i = 0; i < n_files; ++i) {
+    if (files[i].len >= (1ull << 32)) {
+      set_last_error("files of 4 GiB or more are outside this engine's coverage");
+      return TSG_ERR_UNSUPPORTED;
+    }
+    off[i + 1] = off[i] + files[i].len + 1;
+    poff[i + 1] = poff[i] + (files[i].path ? strlen(files[i].path) : 0);
+  }
+  const uint64_t nbytes = off[n_files], pbytes = poff[n_files];
+  uint8_t* h = nullptr;
+  HIP_TRY(hipHostMalloc((void**)&h, nbytes + pbytes + 16, hipHostMallocDefault));
+  for (size_t i = 0; i < n_files; ++i) {
+    if (files[i].len) memcpy(h + off[i], files[i].data, files[i].len);
+    h[off[i] + files[i].len] = 0;
+    if (files[i].path) memcpy(h + nbytes + poff[i], files[i].path, poff[i + 1] - poff[i]);
+  }
+  hipStream_t s = e->stream;
+  const uint32_t nf = (uint32_t)n_files;
+  const uint64_t n_blk = (nbytes + kStripBlock - 1) / kStripBlock;
+  bool ok = e->data.ensure(nbytes + 16) == hipSuccess && e->off.ensure(n_files + 1) == hipSuccess &&
+            e->paths.ensure(pbytes + 16) == hipSuccess && e->path_off.ensure(n_files + 1) == hipSuccess &&
+            e->bin8.ensure(n_files + 1) == hipSuccess && e->n_drop.ensure(1) == hipSuccess &&
+            e->blk_kept.ensure(n_blk + 1) == hipSuccess && e->blk_base.ensure(n_blk + 1) == hipSuccess;
+  if (ok)
+    ok = hipMemcpyAsync(e->data.p, h, nbytes, hipMemcpyHostToDevice, s) == hipSuccess &&
+         hipMemcpyAsync(e->paths.p, h + nbytes, pbytes, hipMemcpyHostToDevice, s) == hipSuccess &&
+         hipMemcpyAsync(e->off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
+         hipMemcpyAsync(e->path_off.p, poff.data(), poff.size() * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
+         hipStreamSynchronize(s) == hipSuccess;
+  (void)hipHostFree(h);
+  if (!ok) {
+    set_last_error("host-to-device staging failed");
+    return TSG_ERR_DEVICE;
+  }
+  const uint8_t* d_data = e->data.p;
+  const uint64_t* d_off = e->off.p;
+  uint64_t kept = nbytes;
+  std::vector<uint8_t> bin(n_files, 0);
+  if (nf) {
+    HIP_TRY(hipMemsetAsync(e->n_drop.p, 0, 8, s));
+    hipLaunchKernelGGL(k_binary, dim3((uint32_t)(((uint64_t)nf * 64 + 255) / 256)), dim3(256), 0, s, e->data.p,
+                       e->off.p, nf, e->bin8.p, e->n_drop.p);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_strip_count, dim3((uint32_t)n_blk), dim3(256), 0, s, e->data.p, nbytes, e->blk_kept.p);
+    HIP_TRY(hipGetLastError());
+    size_t tmp = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->blk_kept.p, e->blk_base.p, (int)n_blk, s));
+    HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(e->cub_tmp.p, tmp, e->blk_kept.p, e->blk_base.p, (int)n_blk, s));
+    uint64_t last[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&last[0], e->blk_base.p + n_blk - 1, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&last[1], e->blk_kept.p + n_blk - 1, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(bin.data(), e->bin8.p, n_files, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    kept = last[0] + last[1];
+    if (kept != nbytes) {  // some '\r' or a binary file: compact
+      const uint64_t n_chunks = (nbytes + 15) / 16;
+      HIP_TRY(e->strip_out.ensure(kept + 16));
+      HIP_TRY(e->strip_off.ensure(n_files + 1));
+      HIP_TRY(e->chunk_pos.ensure(n_chunks + 1));
+      hipLaunchKernelGGL(k_strip_compact, dim3((uint32_t)n_blk), dim3(256), 0, s, e->data.p, nbytes,
+                         e->blk_base.p, e->strip_out.p, e->chunk_pos.p);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_strip_offsets, dim3((nf + 1 + 255) / 256), dim3(256), 0, s, e->data.p, e->off.p, nf,
+                         e->chunk_pos.p, kept, e->strip_off.p);
+      HIP_TRY(hipGetLastError());
+      d_data = e->strip_out.p;
+      d_off = e->strip_off.p;
+    }
+  }
+  auto* res = new tsg_result();
+  int rc = run_pipeline(e, rs, d_data, d_off, e->paths.p, e->path_off.p, n_files, kept, res);
+  if (rc) {
+    delete res;
+    return rc;
+  }
+  auto& R = res->impl;
+  for (size_t i = 0; i < n_files && i < R.file_flags.size(); ++i)
+    if (bin[i]) R.file_flags[i] |= TSG_FILE_BINARY;
+  // findings are cut from the content Scan saw: strip the files that have any
+  std::vector<tsg_file> hf(files, files + n_files);
+  std::deque<std::string> stripped;
+  {
+    std::vector<uint8_t> has(n_files, 0);
+    for (auto& L : R.locs) has[L.file] = 1;
+    for (size_t i = 0; i < n_files; ++i) {
+      if (!has[i]) continue;
+      std::string t;
+      t.reserve(files[i].len);
+      for (uint64_t k = 0; k < files[i].len; ++k)
+        if (files[i].data[k] != '\r') t.push_back((char)files[i].data[k]);
+      stripped.push_back(std::move(t));
+      hf[i].data = (const uint8_t*)stripped.back().data();
+      hf[i].len = stripped.back().size();
+    }
+  }
+  if (!build_findings(&R, rs, hf.data(), n_files)) {
+    delete res;
+    return TSG_ERR_PANIC;
+  }
+  *out = res;
+  return TSG_OK;
+}
+
+int tsg_analyze(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, size_t n_files, tsg_result** out) {
+  try {
+    return analyze_impl(e, rs, files, n_files, out);
+  } catch (const std::exception& ex) {
+    set_last_error(std::string("internal error: ") + ex.what());
+    return TSG_ERR_INTERNAL;
+  }
 }
 
 int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, const uint64_t* d_offsets,

@@ -241,6 +241,15 @@ class Scanner:
         return self.scan_batch([args])[0]
 
     def scan_batch(self, batch: Sequence[ScanArgs]) -> List[Secret]:
+        return self._run(N.lib.tsg_scan, batch)
+
+    def analyze_batch(self, batch: Sequence[ScanArgs]) -> List[Optional[Secret]]:
+        """SecretAnalyzer.Analyze's per-file work on the GPU (tsg_analyze):
+        IsBinary gate, '\r' deletion, Scan.  `content` is the raw file; None
+        for binary files (secret.go:80-86)."""
+        return self._run(N.lib.tsg_analyze, batch)
+
+    def _run(self, fn, batch: Sequence[ScanArgs]):
         eng = get_engine(self.device)
         n = len(batch)
         files = (N.FileC * max(1, n))()
@@ -252,7 +261,7 @@ class Scanner:
             files[i].len = len(a.content)
             files[i].path = a.file_path.encode("utf-8", "surrogateescape")
         res = ctypes.c_void_p()
-        N.check(N.lib.tsg_scan(eng, self._rs.handle, files, n, ctypes.byref(res)))
+        N.check(fn(eng, self._rs.handle, files, n, ctypes.byref(res)))
         try:
             return self._convert(res, batch)
         finally:
@@ -266,6 +275,9 @@ class Scanner:
         flags = N.lib.tsg_result_file_flags(res)
         out = []
         for i, a in enumerate(batch):
+            if flags[i] & N.TSG_FILE_BINARY:
+                out.append(None)
+                continue
             if flags[i] & N.TSG_FILE_PATH_ALLOWED:
                 out.append(Secret(FilePath=a.file_path))
                 continue
