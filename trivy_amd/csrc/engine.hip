@@ -33,6 +33,7 @@
 #include <mutex>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "engine.h"
@@ -2243,6 +2244,9 @@ struct tsg_engine {
   DBuf<uint8_t> bin8, strip_out;
   DBuf<uint64_t> strip_off, blk_kept, blk_base, chunk_pos;
   DBuf<unsigned long long> n_drop;
+  uint8_t* h_stage = nullptr;  // pinned host staging of tsg_scan / tsg_analyze (grow-only)
+  size_t h_stage_n = 0;
+  double stage_ms[2] = {0, 0};  // last stage_host_batch: pack, H2D (host clock)
   std::vector<double> gate_tm;          // timings of the last tsg_gate_device call
 };
 
@@ -3340,6 +3344,9 @@ void tsg_engine_free(tsg_engine* e) {
   e->nl_blocks.release(); e->nl_pre.release(); e->tail.release(); e->region_file.release(); e->region_tmp.release();
   e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->special_files.release(); e->caps.release(); e->vprof.release(); e->fflags8.release();
   if (e->h_flags) (void)hipHostFree(e->h_flags);
+  if (e->h_stage) (void)hipHostFree(e->h_stage);
+  e->gate_out.release(); e->gate_rules.release(); e->bin8.release(); e->strip_out.release();
+  e->strip_off.release(); e->blk_kept.release(); e->blk_base.release(); e->chunk_pos.release(); e->n_drop.release();
   if (e->events)
     for (auto& ev : e->ev) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream);
@@ -3372,13 +3379,11 @@ int tsg_scan_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
   }
 }
 
-static int scan_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, size_t n_files,
-                     tsg_result** out) {
-  if (!e || !rs || !out || (n_files && !files)) return TSG_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(e->mu);
-  *out = nullptr;
-  HIP_TRY(hipSetDevice(e->device));
-  // pack contents (each followed by one NUL separator) and paths: pinned staging -> HBM
+// Host files -> device batch layout (contents each followed by one NUL, then
+// paths) in e->data / e->off / e->paths / e->path_off: packed into the
+// engine's pinned staging buffer by up to 16 threads (the copy, not PCIe,
+// bounds a single-threaded pack), then one H2D per array.
+static int stage_host_batch(tsg_engine* e, const tsg_file* files, size_t n_files, uint64_t* nbytes_out) {
   std::vector<uint64_t> off(n_files + 1, 0), poff(n_files + 1, 0);
   for (size_t i = 0; i < n_files; ++i) {
     if (files[i].len >= (1ull << 32)) {
@@ -3389,32 +3394,71 @@ static int scan_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files
     poff[i + 1] = poff[i] + (files[i].path ? strlen(files[i].path) : 0);
   }
   const uint64_t nbytes = off[n_files], pbytes = poff[n_files];
-  uint8_t* h = nullptr;
-  const size_t stage = nbytes + pbytes + 16;
-  HIP_TRY(hipHostMalloc((void**)&h, stage, hipHostMallocDefault));
-  for (size_t i = 0; i < n_files; ++i) {
-    if (files[i].len) memcpy(h + off[i], files[i].data, files[i].len);
-    h[off[i] + files[i].len] = 0;
-    if (files[i].path) memcpy(h + nbytes + poff[i], files[i].path, poff[i + 1] - poff[i]);
+  const size_t need = nbytes + pbytes + 16;
+  if (e->h_stage_n < need) {
+    if (e->h_stage) (void)hipHostFree(e->h_stage);
+    e->h_stage = nullptr;
+    e->h_stage_n = 0;
+    const size_t cap = need + need / 4;
+    HIP_TRY(hipHostMalloc((void**)&e->h_stage, cap, hipHostMallocDefault));
+    e->h_stage_n = cap;
   }
-  auto cleanup = [&]() { (void)hipHostFree(h); };
+  uint8_t* h = e->h_stage;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto pack = [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      if (files[i].len) memcpy(h + off[i], files[i].data, files[i].len);
+      h[off[i] + files[i].len] = 0;
+      if (files[i].path) memcpy(h + nbytes + poff[i], files[i].path, poff[i + 1] - poff[i]);
+    }
+  };
+  const unsigned nt = nbytes < (64u << 20) ? 1u : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  if (nt == 1) {
+    pack(0, n_files);
+  } else {  // split by bytes, not files
+    std::vector<std::thread> th;
+    size_t lo = 0;
+    for (unsigned t = 0; t < nt; ++t) {
+      const uint64_t target = nbytes * (t + 1) / nt;
+      size_t hi = t + 1 == nt ? n_files : (size_t)(std::lower_bound(off.begin(), off.end(), target) - off.begin());
+      hi = std::max(lo, std::min(hi, n_files));
+      th.emplace_back(pack, lo, hi);
+      lo = hi;
+    }
+    for (auto& t : th) t.join();
+  }
   if (e->data.ensure(nbytes + 16) != hipSuccess || e->off.ensure(n_files + 1) != hipSuccess ||
       e->paths.ensure(pbytes + 16) != hipSuccess || e->path_off.ensure(n_files + 1) != hipSuccess) {
-    cleanup();
     set_last_error("hipMalloc failed");
     return TSG_ERR_DEVICE;
   }
   hipStream_t s = e->stream;
-  bool ok = hipMemcpyAsync(e->data.p, h, nbytes, hipMemcpyHostToDevice, s) == hipSuccess &&
-            hipMemcpyAsync(e->paths.p, h + nbytes, pbytes, hipMemcpyHostToDevice, s) == hipSuccess &&
-            hipMemcpyAsync(e->off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
-            hipMemcpyAsync(e->path_off.p, poff.data(), poff.size() * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
-            hipStreamSynchronize(s) == hipSuccess;
-  cleanup();
+  const auto t1 = std::chrono::steady_clock::now();
+  const bool ok = hipMemcpyAsync(e->data.p, h, nbytes, hipMemcpyHostToDevice, s) == hipSuccess &&
+                  hipMemcpyAsync(e->paths.p, h + nbytes, pbytes, hipMemcpyHostToDevice, s) == hipSuccess &&
+                  hipMemcpyAsync(e->off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
+                  hipMemcpyAsync(e->path_off.p, poff.data(), poff.size() * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
+                  hipStreamSynchronize(s) == hipSuccess;
   if (!ok) {
     set_last_error("host-to-device copy failed");
     return TSG_ERR_DEVICE;
   }
+  const auto t2 = std::chrono::steady_clock::now();
+  e->stage_ms[0] = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  e->stage_ms[1] = std::chrono::duration<double, std::milli>(t2 - t1).count();
+  *nbytes_out = nbytes;
+  return TSG_OK;
+}
+
+static int scan_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, size_t n_files,
+                     tsg_result** out) {
+  if (!e || !rs || !out || (n_files && !files)) return TSG_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(e->mu);
+  *out = nullptr;
+  HIP_TRY(hipSetDevice(e->device));
+  uint64_t nbytes = 0;
+  int src = stage_host_batch(e, files, n_files, &nbytes);
+  if (src) return src;
   auto* res = new tsg_result();
   int rc = run_pipeline(e, rs, e->data.p, e->off.p, e->paths.p, e->path_off.p, n_files, nbytes, res);
   if (rc) {
@@ -3425,6 +3469,9 @@ static int scan_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files
     delete res;
     return TSG_ERR_PANIC;
   }
+  res->impl.timings.resize(20, 0.0);
+  res->impl.timings[18] = e->stage_ms[0];  // host pack into pinned staging
+  res->impl.timings[19] = e->stage_ms[1];  // H2D
   *out = res;
   return TSG_OK;
 }
@@ -3456,39 +3503,15 @@ static int analyze_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* fi
   std::lock_guard<std::mutex> lk(e->mu);
   *out = nullptr;
   HIP_TRY(hipSetDevice(e->device));
-  std::vector<uint64_t> off(n_files + 1, 0), poff(n_files + 1, 0);
-  for (size_t i = 0; i < n_files; ++i) {
-    if (files[i].len >= (1ull << 32)) {
-      set_last_error("files of 4 GiB or more are outside this engine's coverage");
-      return TSG_ERR_UNSUPPORTED;
-    }
-    off[i + 1] = off[i] + files[i].len + 1;
-    poff[i + 1] = poff[i] + (files[i].path ? strlen(files[i].path) : 0);
-  }
-  const uint64_t nbytes = off[n_files], pbytes = poff[n_files];
-  uint8_t* h = nullptr;
-  HIP_TRY(hipHostMalloc((void**)&h, nbytes + pbytes + 16, hipHostMallocDefault));
-  for (size_t i = 0; i < n_files; ++i) {
-    if (files[i].len) memcpy(h + off[i], files[i].data, files[i].len);
-    h[off[i] + files[i].len] = 0;
-    if (files[i].path) memcpy(h + nbytes + poff[i], files[i].path, poff[i + 1] - poff[i]);
-  }
+  uint64_t nbytes = 0;
+  int src = stage_host_batch(e, files, n_files, &nbytes);
+  if (src) return src;
   hipStream_t s = e->stream;
   const uint32_t nf = (uint32_t)n_files;
   const uint64_t n_blk = (nbytes + kStripBlock - 1) / kStripBlock;
-  bool ok = e->data.ensure(nbytes + 16) == hipSuccess && e->off.ensure(n_files + 1) == hipSuccess &&
-            e->paths.ensure(pbytes + 16) == hipSuccess && e->path_off.ensure(n_files + 1) == hipSuccess &&
-            e->bin8.ensure(n_files + 1) == hipSuccess && e->n_drop.ensure(1) == hipSuccess &&
-            e->blk_kept.ensure(n_blk + 1) == hipSuccess && e->blk_base.ensure(n_blk + 1) == hipSuccess;
-  if (ok)
-    ok = hipMemcpyAsync(e->data.p, h, nbytes, hipMemcpyHostToDevice, s) == hipSuccess &&
-         hipMemcpyAsync(e->paths.p, h + nbytes, pbytes, hipMemcpyHostToDevice, s) == hipSuccess &&
-         hipMemcpyAsync(e->off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
-         hipMemcpyAsync(e->path_off.p, poff.data(), poff.size() * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
-         hipStreamSynchronize(s) == hipSuccess;
-  (void)hipHostFree(h);
-  if (!ok) {
-    set_last_error("host-to-device staging failed");
+  if (e->bin8.ensure(n_files + 1) != hipSuccess || e->n_drop.ensure(1) != hipSuccess ||
+      e->blk_kept.ensure(n_blk + 1) != hipSuccess || e->blk_base.ensure(n_blk + 1) != hipSuccess) {
+    set_last_error("hipMalloc failed");
     return TSG_ERR_DEVICE;
   }
   const uint8_t* d_data = e->data.p;
@@ -3557,6 +3580,9 @@ static int analyze_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* fi
     delete res;
     return TSG_ERR_PANIC;
   }
+  res->impl.timings.resize(20, 0.0);
+  res->impl.timings[18] = e->stage_ms[0];  // host pack into pinned staging
+  res->impl.timings[19] = e->stage_ms[1];  // H2D
   *out = res;
   return TSG_OK;
 }
