@@ -470,7 +470,9 @@ def main():
             "counts": None if args.config == 1 else {k: int(v) for k, v in zip(
                 ["hits", "candidates", "jobs", "locs", "event_overflow", "events", "outputs"], stage[8:15])},
             "host_ms": {"call_wall": round(stage[15], 3), "post": round(stage[16], 3),
-                        **({"pack": round(stage[18], 3), "h2d": round(stage[19], 3)} if len(stage) > 19 else {})},
+                        **({"pack": round(stage[18], 3), "h2d": round(stage[19], 3)} if len(stage) > 19 else {}),
+                        **({"front": round(stage[20], 3), "pipeline": round(stage[21], 3),
+                            "findings": round(stage[22], 3)} if len(stage) > 22 else {})},
             "cpu_baseline": cpu,
             "parity": parity,
         }

@@ -3503,6 +3503,7 @@ static int analyze_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* fi
   std::lock_guard<std::mutex> lk(e->mu);
   *out = nullptr;
   HIP_TRY(hipSetDevice(e->device));
+  const auto w0 = std::chrono::steady_clock::now();
   uint64_t nbytes = 0;
   int src = stage_host_batch(e, files, n_files, &nbytes);
   if (src) return src;
@@ -3550,12 +3551,14 @@ static int analyze_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* fi
       d_off = e->strip_off.p;
     }
   }
+  const auto w1 = std::chrono::steady_clock::now();
   auto* res = new tsg_result();
   int rc = run_pipeline(e, rs, d_data, d_off, e->paths.p, e->path_off.p, n_files, kept, res);
   if (rc) {
     delete res;
     return rc;
   }
+  const auto w2 = std::chrono::steady_clock::now();
   auto& R = res->impl;
   for (size_t i = 0; i < n_files && i < R.file_flags.size(); ++i)
     if (bin[i]) R.file_flags[i] |= TSG_FILE_BINARY;
@@ -3567,10 +3570,18 @@ static int analyze_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* fi
     for (auto& L : R.locs) has[L.file] = 1;
     for (size_t i = 0; i < n_files; ++i) {
       if (!has[i]) continue;
+      const char* d = (const char*)files[i].data;
+      const char* end = d + files[i].len;
+      const char* cr = files[i].len ? (const char*)memchr(d, '\r', files[i].len) : nullptr;
+      if (!cr) continue;  // nothing to strip: findings read the caller's bytes
       std::string t;
       t.reserve(files[i].len);
-      for (uint64_t k = 0; k < files[i].len; ++k)
-        if (files[i].data[k] != '\r') t.push_back((char)files[i].data[k]);
+      while (cr) {  // copy the runs between '\r's
+        t.append(d, cr);
+        d = cr + 1;
+        cr = (const char*)memchr(d, '\r', end - d);
+      }
+      t.append(d, end);
       stripped.push_back(std::move(t));
       hf[i].data = (const uint8_t*)stripped.back().data();
       hf[i].len = stripped.back().size();
@@ -3580,9 +3591,16 @@ static int analyze_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* fi
     delete res;
     return TSG_ERR_PANIC;
   }
-  res->impl.timings.resize(20, 0.0);
+  res->impl.timings.resize(23, 0.0);
   res->impl.timings[18] = e->stage_ms[0];  // host pack into pinned staging
   res->impl.timings[19] = e->stage_ms[1];  // H2D
+  {
+    const auto w3 = std::chrono::steady_clock::now();
+    auto ms = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+    res->impl.timings[20] = ms(w0, w1);  // staging + front end (IsBinary, strip)
+    res->impl.timings[21] = ms(w1, w2);  // scan pipeline
+    res->impl.timings[22] = ms(w2, w3);  // findings
+  }
   *out = res;
   return TSG_OK;
 }

@@ -18,14 +18,17 @@ namespace {
 
 // Byte offset of the start of 0-based line `target`, scanning back from a
 // position inside line `cur` (cur >= target).
+// start of the line holding byte pos-1's successor: one past the last '\n' before pos
+size_t line_begin(const uint8_t* c, size_t pos) {
+  const void* q = pos ? memrchr(c, '\n', pos) : nullptr;
+  return q ? (size_t)((const uint8_t*)q - c) + 1 : 0;
+}
+
 size_t line_start_back(const uint8_t* c, size_t pos, uint32_t cur, uint32_t target) {
-  size_t p = pos;
-  // go to the start of line `cur`
-  while (p > 0 && c[p - 1] != '\n') --p;
+  size_t p = line_begin(c, pos);  // the start of line `cur`
   while (cur > target && p > 0) {
     // p is the start of line cur; previous line ends at p-1 ('\n')
-    --p;  // now at the '\n' terminating line cur-1
-    while (p > 0 && c[p - 1] != '\n') --p;
+    p = line_begin(c, p - 1);
     --cur;
   }
   return p;
@@ -57,15 +60,14 @@ bool build_findings(ResultImpl* R, const tsg_ruleset* rs, const tsg_file* files,
     }
     const uint8_t* c = reinterpret_cast<const uint8_t*>(censored.data());
     uint32_t total_lines = 1;  // len(bytes.Split(content, "\n"))
-    for (size_t i = 0; i < n; ++i) total_lines += c[i] == '\n';
+    for (const uint8_t* q = c; (q = (const uint8_t*)memchr(q, '\n', n - (q - c))) != nullptr; ++q) ++total_lines;
     std::vector<tsg_finding> out;
     for (auto* L : v) {
       const size_t start = L->start, end = L->end;
       // match window (scanner.go:484-502)
-      size_t ls = start;
-      while (ls > 0 && c[ls - 1] != '\n') --ls;
-      size_t le = start;
-      while (le < n && c[le] != '\n') ++le;
+      size_t ls = line_begin(c, start);
+      const void* nl = start < n ? memchr(c + start, '\n', n - start) : nullptr;
+      size_t le = nl ? (size_t)((const uint8_t*)nl - c) : n;
       if (le - ls > 100) {
         ls = start >= 30 ? start - 30 : 0;
         le = end + 20 > n ? n : end + 20;
@@ -81,8 +83,8 @@ bool build_findings(ResultImpl* R, const tsg_ruleset* rs, const tsg_file* files,
       size_t p = line_start_back(c, start, sl, cs);
       bool found_first = false;
       for (uint32_t ln = cs; ln < ce && p <= n; ++ln) {
-        size_t q = p;
-        while (q < n && c[q] != '\n') ++q;
+        const void* nq = p < n ? memchr(c + p, '\n', n - p) : nullptr;
+        size_t q = nq ? (size_t)((const uint8_t*)nq - c) : n;
         R->strs.emplace_back(censored.substr(p, q - p));
         const std::string& txt = R->strs.back();
         const bool cause = ln >= sl && ln <= el;
