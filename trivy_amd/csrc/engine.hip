@@ -2246,7 +2246,7 @@ struct tsg_engine {
   DBuf<unsigned long long> n_drop;
   uint8_t* h_stage = nullptr;  // pinned host staging of tsg_scan / tsg_analyze (grow-only)
   size_t h_stage_n = 0;
-  double stage_ms[2] = {0, 0};  // last stage_host_batch: pack, H2D (host clock)
+  double stage_ms[2] = {0, 0};  // last stage_host_batch: pack (+ overlapped H2D), H2D tail (host clock)
   std::vector<double> gate_tm;          // timings of the last tsg_gate_device call
 };
 
@@ -3404,41 +3404,48 @@ static int stage_host_batch(tsg_engine* e, const tsg_file* files, size_t n_files
     e->h_stage_n = cap;
   }
   uint8_t* h = e->h_stage;
-  const auto t0 = std::chrono::steady_clock::now();
-  auto pack = [&](size_t lo, size_t hi) {
-    for (size_t i = lo; i < hi; ++i) {
-      if (files[i].len) memcpy(h + off[i], files[i].data, files[i].len);
-      h[off[i] + files[i].len] = 0;
-      if (files[i].path) memcpy(h + nbytes + poff[i], files[i].path, poff[i + 1] - poff[i]);
-    }
-  };
-  const unsigned nt = nbytes < (64u << 20) ? 1u : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-  if (nt == 1) {
-    pack(0, n_files);
-  } else {  // split by bytes, not files
-    std::vector<std::thread> th;
-    size_t lo = 0;
-    for (unsigned t = 0; t < nt; ++t) {
-      const uint64_t target = nbytes * (t + 1) / nt;
-      size_t hi = t + 1 == nt ? n_files : (size_t)(std::lower_bound(off.begin(), off.end(), target) - off.begin());
-      hi = std::max(lo, std::min(hi, n_files));
-      th.emplace_back(pack, lo, hi);
-      lo = hi;
-    }
-    for (auto& t : th) t.join();
-  }
   if (e->data.ensure(nbytes + 16) != hipSuccess || e->off.ensure(n_files + 1) != hipSuccess ||
       e->paths.ensure(pbytes + 16) != hipSuccess || e->path_off.ensure(n_files + 1) != hipSuccess) {
     set_last_error("hipMalloc failed");
     return TSG_ERR_DEVICE;
   }
   hipStream_t s = e->stream;
+  const auto t0 = std::chrono::steady_clock::now();
+  // bytes [lo, hi) of the packed batch: the parts of the files (and their
+  // NUL separators) that fall inside
+  auto pack_range = [&](uint64_t lo, uint64_t hi) {
+    size_t i = (size_t)(std::upper_bound(off.begin(), off.end(), lo) - off.begin());
+    i = i ? i - 1 : 0;
+    for (; i < n_files && off[i] < hi; ++i) {
+      const uint64_t fs = off[i], fe = fs + files[i].len;  // separator at fe
+      const uint64_t a = std::max(fs, lo), b = std::min(fe, hi);
+      if (a < b) memcpy(h + a, files[i].data + (a - fs), b - a);
+      if (fe >= lo && fe < hi) h[fe] = 0;
+    }
+  };
+  const unsigned nt = nbytes < (64u << 20) ? 1u : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  // chunks: packing chunk k+1 overlaps the DMA of chunk k
+  constexpr uint64_t kStageChunk = 64ull << 20;
+  bool ok = true;
+  for (uint64_t lo = 0; lo < nbytes && ok; lo += kStageChunk) {
+    const uint64_t hi = std::min(nbytes, lo + kStageChunk);
+    if (nt == 1) {
+      pack_range(lo, hi);
+    } else {
+      std::vector<std::thread> th;
+      for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back(pack_range, lo + (hi - lo) * t / nt, lo + (hi - lo) * (t + 1) / nt);
+      for (auto& t : th) t.join();
+    }
+    ok = hipMemcpyAsync(e->data.p + lo, h + lo, hi - lo, hipMemcpyHostToDevice, s) == hipSuccess;
+  }
+  for (size_t i = 0; i < n_files; ++i)
+    if (files[i].path) memcpy(h + nbytes + poff[i], files[i].path, poff[i + 1] - poff[i]);
   const auto t1 = std::chrono::steady_clock::now();
-  const bool ok = hipMemcpyAsync(e->data.p, h, nbytes, hipMemcpyHostToDevice, s) == hipSuccess &&
-                  hipMemcpyAsync(e->paths.p, h + nbytes, pbytes, hipMemcpyHostToDevice, s) == hipSuccess &&
-                  hipMemcpyAsync(e->off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
-                  hipMemcpyAsync(e->path_off.p, poff.data(), poff.size() * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
-                  hipStreamSynchronize(s) == hipSuccess;
+  ok = ok && hipMemcpyAsync(e->paths.p, h + nbytes, pbytes, hipMemcpyHostToDevice, s) == hipSuccess &&
+       hipMemcpyAsync(e->off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
+       hipMemcpyAsync(e->path_off.p, poff.data(), poff.size() * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
+       hipStreamSynchronize(s) == hipSuccess;
   if (!ok) {
     set_last_error("host-to-device copy failed");
     return TSG_ERR_DEVICE;

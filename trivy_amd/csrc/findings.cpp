@@ -9,6 +9,9 @@
 // whole file per finding.
 #include <algorithm>
 #include <cstring>
+#include <string>
+#include <utility>
+#include <vector>
 
 #include "engine.h"
 
@@ -16,19 +19,75 @@ namespace tsg {
 
 namespace {
 
+// The FINAL censored buffer of scanner.go:425-429 without materialising it:
+// the caller's bytes plus the union of the kept locations, read as '*'.
+// Newline searches skip censored bytes, so lines are those of the censored
+// buffer (a censored multi-line match joins its lines, as in Go).
+struct CensoredView {
+  const uint8_t* o;
+  size_t n;
+  std::vector<std::pair<size_t, size_t>> iv;  // sorted, disjoint [a, b)
+
+  CensoredView(const uint8_t* data, size_t len, const std::vector<const tsg_loc*>& locs) : o(data), n(len) {
+    for (auto* L : locs)
+      if (L->end > L->start) iv.push_back({(size_t)L->start, (size_t)L->end});
+    std::sort(iv.begin(), iv.end());
+    size_t k = 0;
+    for (auto& r : iv) {
+      if (k && r.first <= iv[k - 1].second) iv[k - 1].second = std::max(iv[k - 1].second, r.second);
+      else iv[k++] = r;
+    }
+    iv.resize(k);
+  }
+  // the interval holding byte i, or nullptr
+  const std::pair<size_t, size_t>* holder(size_t i) const {
+    auto it = std::upper_bound(iv.begin(), iv.end(), std::make_pair(i, (size_t)-1));
+    if (it == iv.begin()) return nullptr;
+    --it;
+    return i < it->second ? &*it : nullptr;
+  }
+  // first '\n' at or after `from` (n if none)
+  size_t next_nl(size_t from) const {
+    while (from < n) {
+      const void* q = memchr(o + from, '\n', n - from);
+      if (!q) return n;
+      const size_t i = (size_t)((const uint8_t*)q - o);
+      const auto* h = holder(i);
+      if (!h) return i;
+      from = h->second;
+    }
+    return n;
+  }
+  // start of the line holding position pos: one past the last '\n' before pos
+  size_t line_begin(size_t pos) const {
+    while (pos) {
+      const void* q = memrchr(o, '\n', pos);
+      if (!q) return 0;
+      const size_t i = (size_t)((const uint8_t*)q - o);
+      const auto* h = holder(i);
+      if (!h) return i + 1;
+      pos = h->first;
+    }
+    return 0;
+  }
+  std::string substr(size_t p, size_t q) const {
+    std::string t(reinterpret_cast<const char*>(o) + p, q - p);
+    auto it = std::upper_bound(iv.begin(), iv.end(), std::make_pair(p, (size_t)-1));
+    if (it != iv.begin()) --it;
+    for (; it != iv.end() && it->first < q; ++it) {
+      const size_t a = std::max(it->first, p), b = std::min(it->second, q);
+      if (a < b) memset(&t[a - p], '*', b - a);
+    }
+    return t;
+  }
+};
+
 // Byte offset of the start of 0-based line `target`, scanning back from a
 // position inside line `cur` (cur >= target).
-// start of the line holding byte pos-1's successor: one past the last '\n' before pos
-size_t line_begin(const uint8_t* c, size_t pos) {
-  const void* q = pos ? memrchr(c, '\n', pos) : nullptr;
-  return q ? (size_t)((const uint8_t*)q - c) + 1 : 0;
-}
-
-size_t line_start_back(const uint8_t* c, size_t pos, uint32_t cur, uint32_t target) {
-  size_t p = line_begin(c, pos);  // the start of line `cur`
+size_t line_start_back(const CensoredView& c, size_t pos, uint32_t cur, uint32_t target) {
+  size_t p = c.line_begin(pos);  // the start of line `cur`
   while (cur > target && p > 0) {
-    // p is the start of line cur; previous line ends at p-1 ('\n')
-    p = line_begin(c, p - 1);
+    p = c.line_begin(p - 1);  // previous line ends at p-1 ('\n')
     --cur;
   }
   return p;
@@ -51,41 +110,35 @@ bool build_findings(ResultImpl* R, const tsg_ruleset* rs, const tsg_file* files,
       if (a->start != b->start) return a->start < b->start;
       return a->end < b->end;
     });
-    const uint8_t* src = files[f].data;
     const size_t n = files[f].len;
-    std::string censored(reinterpret_cast<const char*>(src), n);
-    for (auto* L : v) {
+    for (auto* L : v)
       if (L->end > n || L->start > L->end) return false;
-      memset(&censored[L->start], '*', L->end - L->start);
-    }
-    const uint8_t* c = reinterpret_cast<const uint8_t*>(censored.data());
-    uint32_t total_lines = 1;  // len(bytes.Split(content, "\n"))
-    for (const uint8_t* q = c; (q = (const uint8_t*)memchr(q, '\n', n - (q - c))) != nullptr; ++q) ++total_lines;
+    const CensoredView c(files[f].data, n, v);
     std::vector<tsg_finding> out;
     for (auto* L : v) {
       const size_t start = L->start, end = L->end;
       // match window (scanner.go:484-502)
-      size_t ls = line_begin(c, start);
-      const void* nl = start < n ? memchr(c + start, '\n', n - start) : nullptr;
-      size_t le = nl ? (size_t)((const uint8_t*)nl - c) : n;
+      size_t ls = c.line_begin(start);
+      size_t le = c.next_nl(start);
       if (le - ls > 100) {
         ls = start >= 30 ? start - 30 : 0;
         le = end + 20 > n ? n : end + 20;
       }
-      R->strs.emplace_back(censored.substr(ls, le - ls));
+      R->strs.emplace_back(c.substr(ls, le));
       const std::string& match = R->strs.back();
-      // code lines (scanner.go:505-534), 0-based line numbers
+      // code lines (scanner.go:505-534), 0-based line numbers; the window
+      // ends at el + 2 or after the buffer's last line (p > n), whichever
+      // comes first -- the min(.., len(lines)) of the reference
       const uint32_t sl = L->start_line - 1, el = L->end_line - 1;
       const uint32_t cs = sl >= 2 ? sl - 2 : 0;
-      const uint32_t ce = std::min<uint32_t>(el + 2, total_lines);
+      const uint32_t ce = el + 2;
       R->lines.emplace_back();
       auto& lines = R->lines.back();
       size_t p = line_start_back(c, start, sl, cs);
       bool found_first = false;
       for (uint32_t ln = cs; ln < ce && p <= n; ++ln) {
-        const void* nq = p < n ? memchr(c + p, '\n', n - p) : nullptr;
-        size_t q = nq ? (size_t)((const uint8_t*)nq - c) : n;
-        R->strs.emplace_back(censored.substr(p, q - p));
+        const size_t q = c.next_nl(p);
+        R->strs.emplace_back(c.substr(p, q));
         const std::string& txt = R->strs.back();
         const bool cause = ln >= sl && ln <= el;
         tsg_line tl{};
