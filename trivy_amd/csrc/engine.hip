@@ -1990,8 +1990,18 @@ __device__ inline uint32_t wave_nl_prefix(const uint8_t* data, const uint32_t* n
   uint32_t c = 0;
   constexpr uint32_t kPer = kNlBlock / 64;  // bytes per lane
   const uint64_t s = b0 + (uint64_t)lane * kPer;
-  const uint64_t e = s + kPer < x ? s + kPer : x;
-  for (uint64_t i = s; i < e; ++i) c += data[i] == '\n';
+  // 16-byte vectors wholly before x (SWAR count), bytes for the partial one;
+  // nothing at or past x is read
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; k += 16) {
+    const uint64_t p = s + k;
+    if (p + 16 <= x) {
+      const uint4 v = *(const uint4*)(data + p);
+      c += nl_count_dword(v.x) + nl_count_dword(v.y) + nl_count_dword(v.z) + nl_count_dword(v.w);
+    } else {
+      for (uint64_t i = p; i < x && i < p + 16; ++i) c += data[i] == '\n';
+    }
+  }
   for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
   return nl_pre[x / kNlBlock] + c;
 }
