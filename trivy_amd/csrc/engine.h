@@ -166,6 +166,7 @@ struct RuleHost {
 
 struct AcHost {
   std::vector<uint16_t> delta;  // generic: next state | 0x8000 output bit
+  std::vector<uint16_t> fail;   // Aho-Corasick failure link per state (same numbering)
   std::vector<uint8_t> fast;    // k_scan_fast image: nstates rows of kFastRowBytes, empty if not representable
   uint32_t fast_out_entry = 0;
   uint8_t cls[256];

@@ -94,8 +94,20 @@ struct DevLoc {
   uint32_t pad;
 };
 
+// k_scan_big's LDS blob (automata too large for one LDS table): the byte
+// class map, dense rows of the n_dense shallowest states, and for every
+// deeper ("cold") state only the classes on which it differs from its
+// failure state, plus the failure link -- delta(s, c) = its own entry, else
+// delta(fail(s), c), ending in a dense row.
+struct BigDev {
+  const uint8_t* blob;  // global copy
+  uint32_t blob_bytes, n_dense, n_cold;
+  uint32_t o_eoff, o_eval, o_fail;  // byte offsets: u32 [n_cold + 1], u32 (class << 16 | entry), u16 [n_cold]
+};
+
 struct ScanParams {
-  uint32_t report_mode;  // timing experiments only (TSG_REPORT_MODE): 1 = no file lookups in k_report
+  uint32_t report_mode;
+  BigDev big;  // timing experiments only (TSG_REPORT_MODE): 1 = no file lookups in k_report
   uint32_t gen_lds_rows;  // k_scan_generic<false>: automaton rows staged in LDS (the shallow ones)
   const uint8_t* data;
   const uint64_t* off;  // n_files + 1
@@ -294,6 +306,73 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_generic(ScanParams P) {
       const uint32_t nx = next(st, cls[b]);
       st = nx & 0x7FFFu;
       if (nx & 0x8000u) report(P, st, p, &last_kw);
+    }
+    atomicAdd(&P.nl_blocks[p0 / kNlBlock], nl);
+  }
+}
+
+// Scan with an automaton too large for an LDS table (configs[4]: 1000+
+// custom rules): everything in LDS anyway -- dense rows for the shallow
+// states (breadth-first numbering: where text keeps the automaton), sparse
+// rows + failure links for the rest (BigDev) -- so no step waits on global
+// memory.  One 128-byte chunk per lane per step (7 bytes of warm-up), bytes
+// straight from HBM in 16-byte vectors, 1024 threads per CU.
+constexpr uint32_t kBigThreads = 1024;
+constexpr uint32_t kBigLdsMax = 152 * 1024;
+
+__global__ __launch_bounds__(kBigThreads) void k_scan_big(ScanParams P) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  const BigDev& B = P.big;
+  for (uint32_t i = threadIdx.x; i < B.blob_bytes / 4; i += kBigThreads)
+    ((uint32_t*)smem)[i] = ((const uint32_t*)B.blob)[i];
+  __syncthreads();
+  const uint8_t* cls = smem;
+  const uint16_t* dense = (const uint16_t*)(smem + 256);
+  const uint32_t* eoff = (const uint32_t*)(smem + B.o_eoff);
+  const uint32_t* eval = (const uint32_t*)(smem + B.o_eval);
+  const uint16_t* fl = (const uint16_t*)(smem + B.o_fail);
+  const uint32_t K = P.rs.ac.nclasses, ND = B.n_dense;
+  auto next = [&](uint32_t st, uint32_t c) -> uint32_t {
+    while (st >= ND) {
+      const uint32_t j = st - ND;
+      for (uint32_t k = eoff[j]; k < eoff[j + 1]; ++k) {
+        const uint32_t v = eval[k];
+        if ((v >> 16) == c) return v & 0xFFFFu;
+      }
+      st = fl[j];
+    }
+    return dense[st * K + c];
+  };
+  const uint64_t nchunks = (P.nbytes + kChunk - 1) / kChunk;
+  uint64_t last_kw = ~0ull;
+  for (uint64_t ch = (uint64_t)blockIdx.x * kBigThreads + threadIdx.x; ch < nchunks;
+       ch += (uint64_t)gridDim.x * kBigThreads) {
+    const uint64_t p0 = ch * kChunk;
+    const uint64_t pend = p0 + kChunk < P.nbytes ? p0 + kChunk : P.nbytes;
+    uint32_t st = 0;
+    for (uint64_t p = p0 >= (uint64_t)(kAcMaxLit - 1) ? p0 - (kAcMaxLit - 1) : 0; p < p0; ++p)
+      st = next(st, cls[P.data[p]]) & 0x7FFFu;
+    uint32_t nl = 0;
+    for (uint64_t p = p0; p < pend; p += 16) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (p + 16 <= pend) {
+        v = *(const uint4*)(P.data + p);
+      } else {
+        uint8_t tmp[16] = {0};
+        for (uint64_t q = p; q < pend; ++q) tmp[q - p] = P.data[q];
+        memcpy(&v, tmp, 16);
+      }
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      const uint32_t m = pend - p < 16 ? (uint32_t)(pend - p) : 16u;
+#pragma unroll
+      for (uint32_t i = 0; i < 16; ++i) {
+        if (i >= m) break;
+        const uint32_t b = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+        nl += b == '\n';
+        const uint32_t nx = next(st, cls[b]);
+        st = nx & 0x7FFFu;
+        if (nx & 0x8000u) report(P, st, p + i, &last_kw);
+      }
     }
     atomicAdd(&P.nl_blocks[p0 / kNlBlock], nl);
   }
@@ -2170,6 +2249,8 @@ struct DBuf {
 
 struct DevImage {
   uint64_t rs_id = 0;
+  DBuf<uint8_t> big;  // k_scan_big blob (empty unless the automaton needs it)
+  BigDev big_view{};
   DBuf<gre::Inst> inst;
   DBuf<gre::ClassDesc> classes;
   DBuf<uint32_t> ranges;
@@ -2199,6 +2280,7 @@ struct DevImage {
   // offsets into u32
   uint32_t o_gpath = 0, n_gpath = 0, o_apoff = 0, o_ap = 0, o_full = 0, n_full = 0;
   void release() {
+    big.release();
     inst.release(); classes.release(); ranges.release(); progs.release(); rules.release();
     u32.release(); rule_path.release(); delta.release(); cls.release(); out_off.release();
     out_pat.release(); pats.release(); pat_bytes.release(); pat_rules.release(); fast.release();
@@ -2466,6 +2548,55 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   HIP_TRY(hipMemcpy(im.delta.p, ac.delta.data(), ac.delta.size() * 2, hipMemcpyHostToDevice));
   HIP_TRY(im.cls.ensure(256));
   HIP_TRY(hipMemcpy(im.cls.p, ac.cls, 256, hipMemcpyHostToDevice));
+  // k_scan_big blob: only for an automaton that neither k_scan_fast's image
+  // nor an LDS table holds (see BigDev); the most dense rows that fit
+  im.big_view = BigDev{};
+  if (ac.fast.empty() && (size_t)ac.nstates * ac.nclasses * 2 > (size_t)kLdsTableMax && ac.fail.size() == ac.nstates) {
+    const uint32_t S = ac.nstates, K = ac.nclasses;
+    std::vector<uint32_t> ecount(S + 1, 0);  // differing classes per state
+    std::vector<std::vector<uint32_t>> edges(S);
+    for (uint32_t st = 1; st < S; ++st) {
+      const uint32_t f = ac.fail[st];
+      for (uint32_t c = 0; c < K; ++c)
+        if (ac.delta[(size_t)st * K + c] != ac.delta[(size_t)f * K + c])
+          edges[st].push_back((c << 16) | ac.delta[(size_t)st * K + c]);
+    }
+    std::vector<uint64_t> suffix(S + 1, 0);  // edges of states >= s
+    for (uint32_t st = S; st-- > 0;) suffix[st] = suffix[st + 1] + edges[st].size();
+    auto a4 = [](uint64_t x) { return (x + 3) & ~3ull; };
+    auto bytes_for = [&](uint32_t nd) {
+      const uint64_t cold = S - nd;
+      return 256 + a4((uint64_t)nd * K * 2) + (cold + 1) * 4 + suffix[nd] * 4 + a4(cold * 2);
+    };
+    uint32_t lo = 1, hi = S;  // largest nd with bytes_for(nd) <= kBigLdsMax (bytes grow with nd)
+    if (bytes_for(1) <= kBigLdsMax) {
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) / 2;
+        if (bytes_for(mid) <= kBigLdsMax) lo = mid;
+        else hi = mid - 1;
+      }
+      const uint32_t nd = lo, cold = S - nd;
+      std::vector<uint8_t> blob(bytes_for(nd), 0);
+      memcpy(blob.data(), ac.cls, 256);
+      memcpy(blob.data() + 256, ac.delta.data(), (size_t)nd * K * 2);
+      const uint32_t o_eoff = (uint32_t)(256 + a4((uint64_t)nd * K * 2));
+      const uint32_t o_eval = o_eoff + (cold + 1) * 4;
+      const uint32_t o_fail = (uint32_t)(o_eval + suffix[nd] * 4);
+      uint32_t* eo = (uint32_t*)(blob.data() + o_eoff);
+      uint32_t* ev = (uint32_t*)(blob.data() + o_eval);
+      uint16_t* fl = (uint16_t*)(blob.data() + o_fail);
+      uint32_t k = 0;
+      for (uint32_t j = 0; j < cold; ++j) {
+        eo[j] = k;
+        for (uint32_t v : edges[nd + j]) ev[k++] = v;
+        fl[j] = ac.fail[nd + j];
+      }
+      eo[cold] = k;
+      HIP_TRY(im.big.ensure(blob.size()));
+      HIP_TRY(hipMemcpy(im.big.p, blob.data(), blob.size(), hipMemcpyHostToDevice));
+      im.big_view = BigDev{im.big.p, (uint32_t)blob.size(), nd, cold, o_eoff, o_eval, o_fail};
+    }
+  }
   HIP_TRY(im.out_off.ensure(ac.out_off.size()));
   HIP_TRY(hipMemcpy(im.out_off.p, ac.out_off.data(), ac.out_off.size() * 4, hipMemcpyHostToDevice));
   HIP_TRY(im.out_pat.ensure(ac.out_pat.size() + 1));
@@ -2834,6 +2965,13 @@ int launch_scan(tsg_engine* e, ScanParams P) {
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_fold_special, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_spans + 255) / 256, 2048))),
                        dim3(256), 0, s, P, n_spans);
+  } else if (P.big.blob && !getenv("TSG_NO_BIG")) {
+    const uint64_t nchunks = (P.nbytes + kChunk - 1) / kChunk;
+    const uint32_t blocks = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>((nchunks + kBigThreads - 1) / kBigThreads, (uint64_t)e->num_cus));
+    HIP_TRY(hipFuncSetAttribute((const void*)k_scan_big, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)P.big.blob_bytes));
+    hipLaunchKernelGGL(k_scan_big, dim3(blocks), dim3(kBigThreads), P.big.blob_bytes, s, P);
   } else {
     const size_t table_bytes = (size_t)ac.nstates * ac.nclasses * 2;
     const bool lds_table = table_bytes <= (size_t)kLdsTableMax;
@@ -2948,6 +3086,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   HIP_TRY(e->hits.ensure(hit_cap));
   hit_cap = e->hits.n;
   ScanParams P{};
+  P.big = e->img.big_view;
   P.data = d_data;
   P.off = d_off;
   P.nbytes = nbytes;
@@ -3666,6 +3805,7 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
   HIP_TRY(hipMemsetAsync(e->file_flags.p, 0, (nf + 1) * 4, s));
   HIP_TRY(e->hits.ensure(1));
   ScanParams P{};
+  P.big = e->img.big_view;
   P.data = d_data;
   P.off = d_offsets;
   P.nbytes = nbytes;

@@ -145,6 +145,9 @@ static bool build_ac_depth(tsg_ruleset* rs, int depth, std::string* err) {
     }
     go.swap(go2);
     outs.swap(outs2);
+    // failure links in the new numbering (k_scan_big's sparse cold rows)
+    ac.fail.assign(S, 0);
+    for (int n = 0; n < S; ++n) ac.fail[n] = (uint16_t)perm[fail[inv[n]]];
   }
   int first_out = S;
   for (int st = S - 1; st >= 0 && !outs[st].empty(); --st) first_out = st;
