@@ -45,6 +45,10 @@ WORKLOADS = {
        "mixed text corpus resident in HBM",
     2: "configs[2]: full builtin ruleset (prefilter + regex + line numbers + allow rules), mixed text corpus "
        "resident in HBM",
+    3: "configs[3]: image-layer set, builtin rules: one layer tar per GPU in host memory (ustar members = the "
+       "SURVEY.md §8(d) corpus files), native layer walk (whiteouts, skip rules) + SecretAnalyzer.Required + one "
+       "batched analyze (IsBinary, CR strip, scan, findings) per layer; PCIe-inclusive (pinned staging + H2D in "
+       "the step); file shards = layers per rank",
     4: "configs[4]: stress, builtin + generated gitleaks-style custom rules (explosion rules, keyword-less rules), "
        "mixed text corpus resident in HBM",
 }
@@ -99,6 +103,45 @@ def build_corpus(N, torch, seed, gb, density, device):
     del d_chunks
     return dict(n_files=n_files, total=content, packed=total, off=off, d_data=d_data, d_off=d_off, d_paths=d_paths,
                 d_poff=d_poff, plants=plants, sizes=sizes)
+
+
+def build_layer_tar(host, off, sizes, pbytes, poff):
+    """The corpus as one ustar layer: a 512-byte header per file (name, mode
+    0644, octal size, checksum, typeflag '0'), content padded to 512, two zero
+    blocks.  Headers are built vectorised in chunks; content copied per file."""
+    n = len(sizes)
+    sizes = sizes.astype(np.int64)
+    span = 512 + ((sizes + 511) // 512) * 512
+    toff = np.zeros(n + 1, dtype=np.int64)
+    toff[1:] = np.cumsum(span)
+    out = np.zeros(int(toff[-1]) + 1024, dtype=np.uint8)
+    plen = np.diff(poff.astype(np.int64))
+    assert plen.max() < 100
+    step = 1 << 15
+    for a in range(0, n, step):
+        b = min(n, a + step)
+        k = b - a
+        H = np.zeros((k, 512), dtype=np.uint8)
+        L = plen[a:b]
+        rows = np.repeat(np.arange(k), L)
+        cols = np.arange(int(L.sum())) - np.repeat(np.cumsum(L) - L, L)
+        H[rows, cols] = pbytes[int(poff[a]):int(poff[b])]
+        for fo, txt in ((100, b"0000644"), (108, b"0000000"), (116, b"0000000"), (136, b"00000000000"),
+                        (148, b"        "), (257, b"ustar\x0000"), (156, b"0")):
+            H[:, fo:fo + len(txt)] = np.frombuffer(txt, dtype=np.uint8)
+        sz = sizes[a:b]
+        for d in range(11):
+            H[:, 124 + d] = 48 + ((sz >> (3 * (10 - d))) & 7)
+        ck = H.astype(np.int64).sum(axis=1)
+        for d in range(6):
+            H[:, 148 + d] = 48 + ((ck >> (3 * (5 - d))) & 7)
+        H[:, 154] = 0
+        H[:, 155] = 32
+        out[(toff[a:b, None] + np.arange(512)).ravel()] = H.ravel()
+    for i in range(n):
+        o, z, t = int(off[i]), int(sizes[i]), int(toff[i]) + 512
+        out[t:t + z] = host[o:o + z]
+    return out
 
 
 def scan_device(N, eng, rs, c):
@@ -297,9 +340,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", type=int, default=2, choices=[0, 1, 2, 4],
+    ap.add_argument("--config", type=int, default=2, choices=[0, 1, 2, 3, 4],
                     help="BASELINE.json configs index: 2 full ruleset (default), 0 analyzer batch from host "
-                         "memory (PCIe-inclusive), 1 prefilter only, 4 stress rules")
+                         "memory (PCIe-inclusive), 1 prefilter only, 3 layer tar per GPU (PCIe-inclusive), 4 stress rules")
     ap.add_argument("--gb", type=float, default=None, help="corpus GB per GPU (configs[2]: 50, configs[1]: 20)")
     ap.add_argument("--stress-rules", type=int, default=1000)
     ap.add_argument("--density", type=float, default=1e-6)
@@ -310,7 +353,7 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     args = ap.parse_args()
     if args.gb is None:
-        args.gb = {0: 1.0, 1: 20.0}.get(args.config, 50.0)
+        args.gb = {0: 1.0, 1: 20.0, 3: 4.0}.get(args.config, 50.0)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -372,7 +415,37 @@ def main():
             host_files[i].path = path_objs[i]
         c["host_keep"] = (host, path_objs)
 
+    layer = None
+    if args.config == 3:
+        # configs[3]: this rank's shard of the layer set as one ustar layer in
+        # host memory; the step walks it natively and analyzes every required
+        # member in one call (tsg_layer_tar_walk + tsg_analyze_layer)
+        host = c["d_data"][: c["packed"]].cpu().numpy()
+        poff = c["d_poff"].cpu().numpy().astype(np.int64)
+        pbytes = c["d_paths"][: int(poff[-1])].cpu().numpy()
+        t_tar = time.perf_counter()
+        layer = build_layer_tar(host, c["off"], c["sizes"], pbytes, poff)
+        del host
+        c["layer_build_s"] = time.perf_counter() - t_tar
+        c["layer_bytes"] = len(layer)
+        c["kept"] = (ctypes.c_uint32 * c["n_files"])()
+        c["n_kept"] = ctypes.c_size_t()
+
+    def layer_step():
+        w = ctypes.c_void_p()
+        base = ctypes.c_void_p(layer.ctypes.data)
+        N.check(N.lib.tsg_layer_tar_walk(base, len(layer), None, 0, None, 0, ctypes.byref(w)))
+        r = ctypes.c_void_p()
+        try:
+            N.check(N.lib.tsg_analyze_layer(eng, rs, base, len(layer), w, b"", c["kept"], ctypes.byref(c["n_kept"]),
+                                            ctypes.byref(r)))
+        finally:
+            N.lib.tsg_tar_walk_free(w)
+        return r
+
     def one_step():
+        if args.config == 3:
+            return layer_step()
         if args.config == 0:
             r = ctypes.c_void_p()
             N.check(N.lib.tsg_analyze(eng, rs, host_files, c["n_files"], ctypes.byref(r)))
@@ -383,6 +456,9 @@ def main():
             return None
         return scan_device(N, eng, rs, c)
 
+    if args.config == 3:  # every member is required: result file i == corpus file i
+        N.lib.tsg_result_free(layer_step())
+        assert c["n_kept"].value == c["n_files"] and all(c["kept"][i] == i for i in range(0, c["n_files"], 997))
     for _ in range(args.warmup):
         r = one_step()
         if r is not None:
@@ -457,7 +533,9 @@ def main():
             "config": {"workload": WORKLOADS[args.config] + (f" ({args.stress_rules} generated rules)"
                                                               if args.config == 4 else ""),
                        "gb_per_gpu": round(c["total"] / 1e9, 3), "files_per_gpu": c["n_files"],
-                       "density": args.density, "parallelism": f"file shards x{world}, no collective"},
+                       "density": args.density, "parallelism": f"file shards x{world}, no collective",
+                       **({"layer_tar_bytes": c["layer_bytes"], "layer_build_s": round(c["layer_build_s"], 1)}
+                          if args.config == 3 else {})},
             "pct_hbm_peak": round(100.0 * value / (HBM_PEAK_GBPS * world), 2),
             "roofline": {"bound": "hbm", "kernel": scan_kernel, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),

@@ -211,6 +211,49 @@ int tsg_regex_match(const char* pattern, const uint8_t* text, size_t len, int* m
 int tsg_regex_find_all(const char* pattern, const uint8_t* text, size_t len, int64_t* pairs,
                        size_t cap, size_t* n_out);
 
+/* ---- container-image layers (walker.LayerTar.Walk, pkg/fanal/walker/tar.go:35-103) ----
+ * Walks a layer tar already in host memory without copying it: opaque-dir
+ * markers and whiteouts are collected (tar.go:51-61), SkipDirs/SkipFiles are
+ * doublestar globs (walk.go:28-53, CleanSkipPaths applied here), and every
+ * remaining directory and regular file is an entry in archive order whose
+ * content is tar[offset .. offset+size).  Regular-file entries go straight to
+ * tsg_analyze as tsg_file spans (path "/" + entry path: the image artifact
+ * calls AnalyzeFile with Dir "", secret.go:95-98).  A malformed archive
+ * returns -1 with "failed to extract the archive: ..." (tar.go:43). */
+typedef struct tsg_tar_entry {
+  const char* path; /* path.Clean'd, leading '/' trimmed (tar.go:47-49) */
+  size_t path_len;
+  uint64_t offset; /* content start in the caller's tar (0 for directories) */
+  uint64_t size;
+  uint32_t mode;
+  uint8_t is_dir;
+} tsg_tar_entry;
+typedef struct tsg_tar_walk tsg_tar_walk;
+
+int tsg_layer_tar_walk(const uint8_t* tar, size_t len, const char* const* skip_files, size_t n_skip_files,
+                       const char* const* skip_dirs, size_t n_skip_dirs, tsg_tar_walk** out);
+size_t tsg_tar_walk_entry_count(const tsg_tar_walk* w);
+const tsg_tar_entry* tsg_tar_walk_entries(const tsg_tar_walk* w);
+size_t tsg_tar_walk_opq_count(const tsg_tar_walk* w);
+const char* tsg_tar_walk_opq_dir(const tsg_tar_walk* w, size_t i);
+size_t tsg_tar_walk_wh_count(const tsg_tar_walk* w);
+const char* tsg_tar_walk_wh_file(const tsg_tar_walk* w, size_t i);
+void tsg_tar_walk_free(tsg_tar_walk* w);
+/* One walked layer through the secret analyzer in ONE tsg_analyze call:
+ * directories dropped (AnalyzerGroup.AnalyzeFile, analyzer.go:398-400),
+ * SecretAnalyzer.Required per regular file (secret.go:115-153: size, skip
+ * dirs/files/extensions, the config file's base name, global AllowPath with
+ * the ruleset's allow-path regexes on the host), content handed over as spans
+ * of `tar`, paths "/"-prefixed.  Result file k is walk entry kept[k]
+ * (kept: capacity tsg_tar_walk_entry_count; may be NULL). */
+int tsg_analyze_layer(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* tar, size_t len,
+                      const tsg_tar_walk* w, const char* config_path, uint32_t* kept, size_t* n_kept,
+                      tsg_result** out);
+/* Global AllowRules.AllowPath (scanner.go:200-207) on the host, per file. */
+int tsg_ruleset_allow_path(const tsg_ruleset* rs, const char* path, size_t len, int* allowed);
+/* doublestar.Match (bmatcuk/doublestar v4, walk.go:43): 1/0 in *matched; -1 on a bad pattern. */
+int tsg_glob_match(const char* pattern, const char* path, int* matched);
+
 /* ---- synthetic corpus (bench / test utility, not the scan path) ----------
  * SURVEY.md §8(d) text model with planted builtin-rule secrets.  The device
  * generator and the host twin produce identical bytes for a (seed, file). */

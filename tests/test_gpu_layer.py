@@ -1,0 +1,95 @@
+"""GPU parity of one container-image layer through the batched analyzer
+(trivy_amd.walker.analyze_layer): the native layer walk (walker/tar.go:35-117),
+AnalyzeFile's directory skip + SecretAnalyzer.Required (analyzer.go:396-411,
+secret.go:115-153) and ONE tsg_analyze call over spans of the layer buffer,
+against the oracle's tarfile-based walk followed by per-file
+SecretAnalyzer.Analyze with Dir "" (image.go:269), sorted by FilePath
+(AnalysisResult.Sort, analyzer.go:218-229)."""
+import io
+import os
+import random
+import tarfile
+
+import pytest
+
+from oracle import layertar_oracle as lo
+from oracle import secret_oracle as o
+
+from . import corpus_gen
+from .test_gpu_analyzer import _oracle_plain, _plain
+
+pytestmark = pytest.mark.gpu
+
+W = pytest.importorskip("trivy_amd.walker")
+from trivy_amd.analyzer import SecretAnalyzer  # noqa: E402
+
+
+def _layer(seed, n):
+    rng = random.Random(seed)
+    buf = io.BytesIO()
+    dirs = ["app", "app/src", "etc", "usr/share/doc/pkg", "node_modules/x", ".git", "proc", "root/.ssh",
+            "opt/" + "l" * 120]
+    with tarfile.open(fileobj=buf, mode="w", format=rng.choice([tarfile.GNU_FORMAT, tarfile.PAX_FORMAT])) as tf:
+        for d in dirs:
+            ti = tarfile.TarInfo(d)
+            ti.type = tarfile.DIRTYPE
+            tf.addfile(ti)
+        for i, (p, d) in enumerate(corpus_gen.make_corpus(seed, n)):
+            k = i % 9
+            if k == 0:
+                d = d.replace(b"\n", b"\r\n")
+            elif k == 1 and d:
+                d = d[:50] + b"\x00" + d[50:]  # binary head -> skipped
+            name = rng.choice(dirs) + "/" + p.replace("/", "_")
+            if k == 2:
+                name = rng.choice(dirs) + "/" + rng.choice(["go.sum", "yarn.lock", "logo.png", "a.pyc"])
+            if k == 3:
+                ti = tarfile.TarInfo(name + ".lnk")
+                ti.type = tarfile.SYMTYPE
+                ti.linkname = name
+                tf.addfile(ti)
+            ti = tarfile.TarInfo(name)
+            ti.size = len(d)
+            tf.addfile(ti, io.BytesIO(d))
+        wh = tarfile.TarInfo("etc/.wh.passwd")
+        tf.addfile(wh, io.BytesIO(b""))
+    return buf.getvalue()
+
+
+def _oracle_layer(data, skip_files=(), skip_dirs=()):
+    oa = o.SecretAnalyzer("")
+    out = []
+
+    def fn(path, size, is_dir, content):
+        if is_dir or not oa.required(path, size):
+            return
+        res = oa.analyze(path, content, "")
+        if res is not None:
+            out.extend(res)
+    opq, wh = lo.walk(data, fn, skip_files, skip_dirs)
+    out.sort(key=lambda r: r["FilePath"])
+    return out, opq, wh
+
+
+@pytest.mark.parametrize("seed,skip_dirs", [(41, ()), (42, tuple(W.DEFAULT_SKIP_DIRS)), (43, ("app/**",))])
+def test_analyze_layer_vs_oracle(seed, skip_dirs, tmp_path):
+    data = _layer(seed, 300)
+    a = SecretAnalyzer()
+    a.init("")
+    want, wopq, wwh = _oracle_layer(data, skip_dirs=skip_dirs)
+    got, opq, wh = W.analyze_layer(a, data, skip_dirs=skip_dirs)
+    assert (opq, wh) == (wopq, wwh) == ([], ["etc/passwd"])
+    assert _plain(got) == _oracle_plain(want)
+    assert len(want) > 20
+    # the same layer from a file (mmap'd, zero-copy spans)
+    f = tmp_path / "layer.tar"
+    f.write_bytes(data)
+    got2, _, _ = W.analyze_layer(a, str(f), skip_dirs=skip_dirs)
+    assert _plain(got2) == _plain(got)
+
+
+def test_analyze_layer_reference_tar():
+    a = SecretAnalyzer()
+    a.init("")
+    got, opq, wh = W.analyze_layer(a, os.path.join(os.path.dirname(__file__), "golden", "walker", "test.tar"))
+    assert (got, opq, wh) == ([], ["etc/"], ["foo/foo"])

@@ -76,6 +76,11 @@ class FindingC(ctypes.Structure):
                 ("start", ctypes.c_uint64), ("end", ctypes.c_uint64)]
 
 
+class TarEntryC(ctypes.Structure):
+    _fields_ = [("path", ctypes.c_void_p), ("path_len", ctypes.c_size_t), ("offset", ctypes.c_uint64),
+                ("size", ctypes.c_uint64), ("mode", ctypes.c_uint32), ("is_dir", ctypes.c_uint8)]
+
+
 _SIGS = {
     "tsg_version": (ctypes.c_char_p, []),
     "tsg_last_error": (ctypes.c_char_p, []),
@@ -139,6 +144,21 @@ _SIGS = {
     "tsg_regex_find_all": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t,
                                           ctypes.POINTER(ctypes.c_int64), ctypes.c_size_t,
                                           ctypes.POINTER(ctypes.c_size_t)]),
+    "tsg_layer_tar_walk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, c_char_pp, ctypes.c_size_t,
+                                          c_char_pp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+    "tsg_tar_walk_entry_count": (ctypes.c_size_t, [ctypes.c_void_p]),
+    "tsg_tar_walk_entries": (ctypes.POINTER(TarEntryC), [ctypes.c_void_p]),
+    "tsg_tar_walk_opq_count": (ctypes.c_size_t, [ctypes.c_void_p]),
+    "tsg_tar_walk_opq_dir": (ctypes.c_char_p, [ctypes.c_void_p, ctypes.c_size_t]),
+    "tsg_tar_walk_wh_count": (ctypes.c_size_t, [ctypes.c_void_p]),
+    "tsg_tar_walk_wh_file": (ctypes.c_char_p, [ctypes.c_void_p, ctypes.c_size_t]),
+    "tsg_tar_walk_free": (None, [ctypes.c_void_p]),
+    "tsg_analyze_layer": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                         ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32),
+                                         ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_void_p)]),
+    "tsg_ruleset_allow_path": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t,
+                                              ctypes.POINTER(ctypes.c_int)]),
+    "tsg_glob_match": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
 }
 
 for _name, (_res, _args) in _SIGS.items():

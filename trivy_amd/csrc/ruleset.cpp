@@ -664,6 +664,32 @@ static gre::ProgView view_of(const gre::Prog& p) {
                        p.start, (uint32_t)p.ncap};
 }
 
+extern "C++" namespace tsg {
+// Global AllowRules.AllowPath (scanner.go:200-207) on the host: MatchString of
+// every compiled global allow-path regex.  Per file, not per byte.
+bool host_allow_path(const tsg_ruleset* rs, const uint8_t* path, size_t len) {
+  for (int r : rs->global_allow_path) {
+    const gre::Prog& p = rs->regexes[r].c.prog;
+    thread_local HostVm* vm = nullptr;
+    thread_local size_t vm_n = 0;
+    if (!vm || vm_n < p.inst.size()) {
+      delete vm;
+      vm_n = p.inst.size() + 64;
+      vm = new HostVm(vm_n);
+    }
+    uint32_t ms, me;
+    if (gre::vm_search(view_of(p), path, (uint32_t)len, 0, (uint32_t)len, true, vm->sc, &ms, &me)) return true;
+  }
+  return false;
+}
+}  // namespace tsg
+
+int tsg_ruleset_allow_path(const tsg_ruleset* rs, const char* path, size_t len, int* allowed) {
+  if (!rs || (!path && len) || !allowed) return TSG_ERR_INVALID_ARG;
+  *allowed = tsg::host_allow_path(rs, (const uint8_t*)path, len) ? 1 : 0;
+  return TSG_OK;
+}
+
 int tsg_regex_match(const char* pattern, const uint8_t* text, size_t len, int* matched) {
   if (!pattern || !matched) return TSG_ERR_INVALID_ARG;
   gre::Compiled c;

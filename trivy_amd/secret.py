@@ -234,8 +234,11 @@ class Scanner:
 
     # Global.AllowPath (scanner.go:55-58, 200-207): per-file host check.
     def allow_path(self, path: str) -> bool:
+        """Global AllowPath (scanner.go:200-207) with the compiled ruleset's regexes."""
         p = path.encode("utf-8", "surrogateescape")
-        return any(a.path is not None and N.regex_match(a.path, p) for a in self.allow_rules)
+        m = ctypes.c_int()
+        N.check(N.lib.tsg_ruleset_allow_path(self._rs.handle, p, len(p), ctypes.byref(m)))
+        return bool(m.value)
 
     def scan(self, args: ScanArgs) -> Secret:
         return self.scan_batch([args])[0]

@@ -1,0 +1,178 @@
+"""Container-image layer walker: the mirror of walker.LayerTar
+(pkg/fanal/walker/tar.go:23-117, walk.go:28-53) over the native
+tsg_layer_tar_walk, plus `analyze_layer`, which hands every required regular
+file of a layer to the GPU analyzer in ONE tsg_analyze call (SURVEY.md §8f
+rank 2: batch submission instead of one Scan per file from --parallel
+goroutines).
+
+The layer is a host buffer (bytes, bytearray, mmap) or a path, which is
+mmap'd read-only; file contents are spans of it, never copied here.
+"""
+from __future__ import annotations
+
+import ctypes
+import mmap
+import os
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+from . import _native as N
+from .types import Secret
+
+Layer = Union[bytes, bytearray, memoryview, mmap.mmap, str, os.PathLike]
+
+# walker.defaultSkipDirs (walk.go:17-22) — applied by the fs/image artifacts,
+# not by LayerTar itself; exported for callers that want Trivy's defaults.
+DEFAULT_SKIP_DIRS = ["**/.git", "proc", "sys", "dev"]
+
+
+class WalkError(RuntimeError):
+    pass
+
+
+@dataclass(frozen=True)
+class FileInfo:
+    """The fs.FileInfo fields the analyzers read (hdr.FileInfo(), tar.go:85)."""
+    name: str
+    size: int
+    mode: int
+    is_dir: bool
+
+
+def glob_match(pattern: str, path: str) -> bool:
+    """doublestar.Match (walk.go:43), natively.  Raises on a bad pattern."""
+    m = ctypes.c_int()
+    N.check(N.lib.tsg_glob_match(pattern.encode(), path.encode(), ctypes.byref(m)))
+    return bool(m.value)
+
+
+def _open_layer(layer: Layer):
+    """(buffer, base address, length, closer) for a layer without copying it."""
+    if isinstance(layer, (str, os.PathLike)):
+        f = open(layer, "rb")
+        size = os.fstat(f.fileno()).st_size
+        if size == 0:
+            f.close()
+            return b"", 0, 0, lambda: None
+        mm = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
+
+        def close():
+            mm.close()
+            f.close()
+        buf = mm
+    else:
+        buf, close = layer, (lambda: None)
+    n = len(memoryview(buf).cast("B")) if not isinstance(buf, (bytes, bytearray, mmap.mmap)) else len(buf)
+    addr = int(np.frombuffer(buf, dtype=np.uint8).ctypes.data) if n else 0
+    return buf, addr, n, close
+
+
+def _cstrs(v: Sequence[str]):
+    arr = (ctypes.c_char_p * max(1, len(v)))(*[s.encode("utf-8", "surrogateescape") for s in v])
+    return arr, len(v)
+
+
+class _Walk:
+    """Native walk (tsg_layer_tar_walk): entries (path, offset, size, mode,
+    is_dir), opq dirs, whiteouts; the handle stays open for tsg_analyze_layer
+    until close()."""
+
+    def __init__(self, addr: int, n: int, skip_files: Sequence[str], skip_dirs: Sequence[str]):
+        sf, nsf = _cstrs(skip_files)
+        sd, nsd = _cstrs(skip_dirs)
+        self.handle = ctypes.c_void_p()
+        rc = N.lib.tsg_layer_tar_walk(addr or None, n, sf, nsf, sd, nsd, ctypes.byref(self.handle))
+        if rc != 0:
+            raise WalkError(N.lib.tsg_last_error().decode("utf-8", "replace"))
+        h = self.handle
+        k = N.lib.tsg_tar_walk_entry_count(h)
+        ents = N.lib.tsg_tar_walk_entries(h)
+        self.entries: List[Tuple[str, int, int, int, bool]] = []
+        for i in range(k):
+            e = ents[i]
+            p = ctypes.string_at(e.path, e.path_len).decode("utf-8", "surrogateescape")
+            self.entries.append((p, e.offset, e.size, e.mode, bool(e.is_dir)))
+        self.opq_dirs = [N.lib.tsg_tar_walk_opq_dir(h, i).decode("utf-8", "surrogateescape")
+                         for i in range(N.lib.tsg_tar_walk_opq_count(h))]
+        self.wh_files = [N.lib.tsg_tar_walk_wh_file(h, i).decode("utf-8", "surrogateescape")
+                         for i in range(N.lib.tsg_tar_walk_wh_count(h))]
+
+    def close(self):
+        if self.handle:
+            N.lib.tsg_tar_walk_free(self.handle)
+            self.handle = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class LayerTar:
+    """walker.LayerTar: NewLayerTar(Option{SkipFiles, SkipDirs}) (tar.go:28-33)."""
+
+    def __init__(self, skip_files: Sequence[str] = (), skip_dirs: Sequence[str] = ()):
+        self.skip_files = list(skip_files)
+        self.skip_dirs = list(skip_dirs)
+
+    def walk(self, layer: Layer,
+             analyze_fn: Callable[[str, FileInfo, Callable[[], bytes]], None]) -> Tuple[List[str], List[str]]:
+        """Walk (tar.go:35-90): analyze_fn(file_path, info, opener) for every
+        directory and regular file that survives the skip rules, in archive
+        order; returns (opqDirs, whFiles).  An analyze_fn error ends the walk
+        with "failed to process the file: failed to analyze file: ..."."""
+        buf, addr, n, close = _open_layer(layer)
+        view = memoryview(buf).cast("B") if n else None
+        try:
+            with _Walk(addr, n, self.skip_files, self.skip_dirs) as w:
+                pass
+            for path, off, size, mode, is_dir in w.entries:
+                info = FileInfo(path.rsplit("/", 1)[-1], size, mode, is_dir)
+                try:
+                    analyze_fn(path, info, lambda o=off, s=size: bytes(view[o:o + s]))
+                except Exception as e:  # noqa: BLE001 — mirrors the Go error wrap
+                    raise WalkError(f"failed to process the file: failed to analyze file: {e}") from e
+            return w.opq_dirs, w.wh_files
+        finally:
+            if n:
+                view.release()
+            del buf
+            close()
+
+
+def analyze_layer(analyzer, layer: Layer, skip_files: Sequence[str] = (),
+                  skip_dirs: Sequence[str] = ()) -> Tuple[List[Secret], List[str], List[str]]:
+    """One image layer through the secret analyzer, batched: the layer walk
+    (tar.go:35-90), then tsg_analyze_layer — AnalyzerGroup.AnalyzeFile's
+    directory skip and SecretAnalyzer.Required (analyzer.go:396-411,
+    secret.go:115-153) natively, and Analyze of every required file in one
+    tsg_analyze call over spans of the layer buffer, with Dir == "" (the image
+    artifact, image.go:269) so paths get the '/' prefix (secret.go:95-98).
+    Returns (secrets sorted by FilePath as AnalysisResult.Sort does,
+    analyzer.go:218-229, opqDirs, whFiles)."""
+    from .secret import ScanArgs, get_engine
+
+    sc = analyzer.scanner
+    buf, addr, n, close = _open_layer(layer)
+    try:
+        with _Walk(addr, n, skip_files, skip_dirs) as w:
+            kept = (ctypes.c_uint32 * max(1, len(w.entries)))()
+            nk = ctypes.c_size_t()
+            res = ctypes.c_void_p()
+            N.check(N.lib.tsg_analyze_layer(get_engine(sc.device), sc._rs.handle, addr or None, n, w.handle,
+                                            (analyzer.config_path or "").encode(), kept, ctypes.byref(nk),
+                                            ctypes.byref(res)))
+        try:
+            batch = [ScanArgs("/" + w.entries[kept[i]][0], b"") for i in range(nk.value)]
+            out = sc._convert(res, batch)
+        finally:
+            N.lib.tsg_result_free(res)
+        secrets = [r for r in out if r is not None and r.Findings]
+        secrets.sort(key=lambda s: s.FilePath)
+        return secrets, w.opq_dirs, w.wh_files
+    finally:
+        del buf
+        close()
