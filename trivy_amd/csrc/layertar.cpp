@@ -16,9 +16,11 @@
 // TypeRegA ('\0') read as TypeReg, or TypeDir for a name ending in '/',
 // octal or base-256 numeric fields, header checksum (unsigned or signed sum),
 // and end of archive at a zero block.
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "engine.h"
@@ -39,7 +41,23 @@ namespace {
 constexpr size_t kBlock = 512;
 
 // path.Clean (Go, lexical).
+// True when path.Clean would return p unchanged (the common case in layers):
+// no empty, "." or ".." element and no trailing '/'.
+bool already_clean(const std::string& p) {
+  if (p.empty() || p.back() == '/') return p == "/";
+  size_t i = p[0] == '/' ? 1 : 0;
+  while (i < p.size()) {
+    size_t j = p.find('/', i);
+    if (j == std::string::npos) j = p.size();
+    size_t n = j - i;
+    if (n == 0 || (n == 1 && p[i] == '.') || (n == 2 && p[i] == '.' && p[i + 1] == '.')) return false;
+    i = j + 1;
+  }
+  return true;
+}
+
 std::string go_path_clean(const std::string& p) {
+  if (already_clean(p)) return p;
   if (p.empty()) return ".";
   bool rooted = p[0] == '/';
   std::vector<std::string> parts;
@@ -223,6 +241,7 @@ bool doublestar_match(const std::string& pat, const std::string& s, bool* bad) {
 
 // walker.SkipPath (walk.go:39-53): a bad pattern ends the search (false).
 bool skip_path(const std::string& path, const std::vector<std::string>& pats) {
+  if (pats.empty()) return false;
   std::string p = trim_left_slash(path);
   for (auto& pat : pats) {
     bool bad = false;
@@ -250,6 +269,7 @@ std::vector<std::string> split_clean(const std::string& p) {
 // start with "../".  Both paths are clean and relative, so Rel is lexical:
 // ".." per unshared base component, then the target's remaining components.
 bool under_skipped_dir(const std::string& file, const std::vector<std::string>& dirs) {
+  if (dirs.empty()) return false;
   auto t = split_clean(file);
   for (auto& d : dirs) {
     auto b = split_clean(go_path_clean(d));
@@ -299,20 +319,27 @@ bool parse_numeric(const uint8_t* p, size_t n, int64_t* out) {
 bool checksum_ok(const uint8_t* h) {
   int64_t want;
   if (!parse_numeric(h + 148, 8, &want)) return false;
-  uint64_t u = 0;
-  int64_t s = 0;
-  for (size_t i = 0; i < kBlock; i++) {
-    uint8_t b = (i >= 148 && i < 156) ? ' ' : h[i];
-    u += b;
-    s += (int8_t)b;
+  // sums over the block with the checksum field read as spaces; plain loops
+  // the compiler vectorises (this runs once per member)
+  uint32_t u = 0;
+  int32_t s = 0;
+  for (size_t i = 0; i < kBlock; i++) u += h[i];
+  for (size_t i = 0; i < kBlock; i++) s += (int8_t)h[i];
+  for (size_t i = 148; i < 156; i++) {
+    u += ' ' - h[i];
+    s += ' ' - (int8_t)h[i];
   }
-  return want == (int64_t)u || want == s;
+  return want == (int64_t)u || want == (int64_t)s;
 }
 
 bool zero_block(const uint8_t* h) {
-  for (size_t i = 0; i < kBlock; i++)
-    if (h[i]) return false;
-  return true;
+  uint64_t acc = 0;
+  for (size_t i = 0; i < kBlock; i += 8) {
+    uint64_t v;
+    memcpy(&v, h + i, 8);
+    acc |= v;
+  }
+  return acc == 0;
 }
 
 // PAX records "%d key=value\n" (archive/tar parsePAX).
@@ -419,6 +446,8 @@ int tsg_layer_tar_walk(const uint8_t* tar, size_t len, const char* const* skip_f
       bool has_data = !(type == '1' || type == '2' || type == '3' || type == '4' || type == '5' || type == '6');
       if (has_data && (uint64_t)size > len - data) return err("unexpected EOF");
       off = has_data ? next : data;
+      if (off + kBlock <= len)  // the next header is a cache/TLB miss: start it before this entry's string work
+        for (size_t l = 0; l < kBlock; l += 64) __builtin_prefetch(tar + off + l);
 
       // tar.go:47-49: path.Clean, then strip leading '/'
       std::string fp = trim_left_slash(go_path_clean(name));
@@ -526,12 +555,31 @@ int tsg_analyze_layer(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* tar, 
     std::vector<tsg_file> files;
     std::vector<std::string> paths;
     std::vector<uint32_t> idx;
-    paths.reserve(w->entries.size());
-    for (size_t i = 0; i < w->entries.size(); i++) {
-      const tsg_tar_entry& en = w->entries[i];
-      if (en.is_dir) continue;  // AnalyzerGroup.AnalyzeFile (analyzer.go:398-400)
-      if (en.offset + en.size > len) return fail("tsg_analyze_layer: walk does not belong to this tar");
-      if (!secret_required(rs, w->paths[i], en.size, cb)) continue;
+    // Required per regular file, in parallel (the global allow-path regexes
+    // run on the host Pike VM; ~µs per path), then kept in walk order.
+    size_t ne = w->entries.size();
+    std::vector<uint8_t> req(ne, 0);
+    for (size_t i = 0; i < ne; i++)
+      if (!w->entries[i].is_dir && w->entries[i].offset + w->entries[i].size > len)
+        return fail("tsg_analyze_layer: walk does not belong to this tar");
+    auto work = [&](size_t a, size_t b) {
+      for (size_t i = a; i < b; i++) {
+        const tsg_tar_entry& en = w->entries[i];
+        // directories: AnalyzerGroup.AnalyzeFile (analyzer.go:398-400)
+        req[i] = !en.is_dir && secret_required(rs, w->paths[i], en.size, cb);
+      }
+    };
+    size_t nt = std::min<size_t>({16, std::max(1u, std::thread::hardware_concurrency()), ne / 4096 + 1});
+    if (nt <= 1) {
+      work(0, ne);
+    } else {
+      std::vector<std::thread> ts;
+      size_t per = (ne + nt - 1) / nt;
+      for (size_t t = 0; t < nt; t++) ts.emplace_back(work, std::min(ne, t * per), std::min(ne, (t + 1) * per));
+      for (auto& t : ts) t.join();
+    }
+    for (size_t i = 0; i < ne; i++) {
+      if (!req[i]) continue;
       paths.push_back("/" + w->paths[i]);  // Dir == "" (image.go:269) -> secret.go:95-98
       idx.push_back((uint32_t)i);
     }
