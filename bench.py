@@ -345,6 +345,7 @@ def main():
                          "memory (PCIe-inclusive), 1 prefilter only, 3 layer tar per GPU (PCIe-inclusive), 4 stress rules")
     ap.add_argument("--gb", type=float, default=None, help="corpus GB per GPU (configs[2]: 50, configs[1]: 20)")
     ap.add_argument("--stress-rules", type=int, default=1000)
+    ap.add_argument("--layers", type=int, default=4, help="configs[3]: layers per GPU")
     ap.add_argument("--density", type=float, default=1e-6)
     ap.add_argument("--seed", type=int, default=20261015 + 2)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -415,37 +416,61 @@ def main():
             host_files[i].path = path_objs[i]
         c["host_keep"] = (host, path_objs)
 
-    layer = None
+    layers = None
     if args.config == 3:
-        # configs[3]: this rank's shard of the layer set as one ustar layer in
-        # host memory; the step walks it natively and analyzes every required
-        # member in one call (tsg_layer_tar_walk + tsg_analyze_layer)
+        # configs[3]: this rank's shard of the layer set, as `--layers` ustar
+        # layers in host memory (the corpus files split in order); a step
+        # walks them natively on host threads, pipelined ahead of the engine,
+        # and analyzes each layer in one call (tsg_layer_tar_walk +
+        # tsg_analyze_layer), as trivy_amd.walker.analyze_layers does
+        from concurrent.futures import ThreadPoolExecutor
+
         host = c["d_data"][: c["packed"]].cpu().numpy()
         poff = c["d_poff"].cpu().numpy().astype(np.int64)
         pbytes = c["d_paths"][: int(poff[-1])].cpu().numpy()
         t_tar = time.perf_counter()
-        layer = build_layer_tar(host, c["off"], c["sizes"], pbytes, poff)
+        cuts = np.linspace(0, c["n_files"], args.layers + 1).astype(np.int64)
+        layers = []
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            layers.append((int(a), build_layer_tar(host, c["off"][a:b + 1], c["sizes"][a:b], pbytes,
+                                                   poff[a:b + 1])))
         del host
         c["layer_build_s"] = time.perf_counter() - t_tar
-        c["layer_bytes"] = len(layer)
-        c["kept"] = (ctypes.c_uint32 * c["n_files"])()
-        c["n_kept"] = ctypes.c_size_t()
+        c["layer_bytes"] = sum(len(x) for _, x in layers)
+        pool = ThreadPoolExecutor(max_workers=min(4, args.layers))
+        c["kept"] = [(ctypes.c_uint32 * (int(b - a) + 1))() for a, b in zip(cuts[:-1], cuts[1:])]
+        c["n_kept"] = [ctypes.c_size_t() for _ in layers]
+
+    def walk_one(layer):
+        w = ctypes.c_void_p()
+        N.check(N.lib.tsg_layer_tar_walk(ctypes.c_void_p(layer.ctypes.data), len(layer), None, 0, None, 0,
+                                         ctypes.byref(w)))
+        return w
 
     def layer_step():
-        w = ctypes.c_void_p()
-        base = ctypes.c_void_p(layer.ctypes.data)
-        N.check(N.lib.tsg_layer_tar_walk(base, len(layer), None, 0, None, 0, ctypes.byref(w)))
-        r = ctypes.c_void_p()
-        try:
-            N.check(N.lib.tsg_analyze_layer(eng, rs, base, len(layer), w, b"", c["kept"], ctypes.byref(c["n_kept"]),
-                                            ctypes.byref(r)))
-        finally:
-            N.lib.tsg_tar_walk_free(w)
-        return r
+        # one tsg_result per layer; the step returns the last (timings) and
+        # frees the others after reading their counts
+        futs = [pool.submit(walk_one, x) for _, x in layers]
+        results = []
+        for k, ((_, x), f) in enumerate(zip(layers, futs)):
+            w = f.result()
+            r = ctypes.c_void_p()
+            try:
+                N.check(N.lib.tsg_analyze_layer(eng, rs, ctypes.c_void_p(x.ctypes.data), len(x), w, b"",
+                                                c["kept"][k], ctypes.byref(c["n_kept"][k]), ctypes.byref(r)))
+            finally:
+                N.lib.tsg_tar_walk_free(w)
+            results.append(r)
+        return results
 
     def one_step():
         if args.config == 3:
-            return layer_step()
+            for r in c.pop("layer_results", []):  # the previous step's non-last layers
+                N.lib.tsg_result_free(r)
+            rs_ = layer_step()
+            c["layer_results"] = rs_[:-1]
+            c["layer_scan_ms"] = sum(result_timings(N, r)[17] for r in rs_)
+            return rs_[-1]
         if args.config == 0:
             r = ctypes.c_void_p()
             N.check(N.lib.tsg_analyze(eng, rs, host_files, c["n_files"], ctypes.byref(r)))
@@ -456,9 +481,11 @@ def main():
             return None
         return scan_device(N, eng, rs, c)
 
-    if args.config == 3:  # every member is required: result file i == corpus file i
-        N.lib.tsg_result_free(layer_step())
-        assert c["n_kept"].value == c["n_files"] and all(c["kept"][i] == i for i in range(0, c["n_files"], 997))
+    if args.config == 3:  # every member is required: result file i of layer k == corpus file cuts[k] + i
+        for k, r in enumerate(layer_step()):
+            N.lib.tsg_result_free(r)
+            nk = c["n_kept"][k].value
+            assert nk == int(cuts[k + 1] - cuts[k]) and all(c["kept"][k][i] == i for i in range(0, nk, 997))
     for _ in range(args.warmup):
         r = one_step()
         if r is not None:
@@ -482,7 +509,8 @@ def main():
             if last is not None:
                 N.lib.tsg_result_free(last)
             last = res
-        scan_ms.append(tm[17] if len(tm) > 17 and tm[17] > 0 else tm[7])
+        scan_ms.append(c["layer_scan_ms"] if args.config == 3 else
+                       tm[17] if len(tm) > 17 and tm[17] > 0 else tm[7])
         stage = tm
     torch.cuda.synchronize()
     barrier()
@@ -497,7 +525,16 @@ def main():
     else:
         total_all = float(c["total"])
 
-    if last is not None:
+    if last is not None and args.config == 3:  # merge the layers' locations into corpus file numbering
+        parts = []
+        for k, r in enumerate(c.pop("layer_results") + [last]):
+            lk, _ = read_result(N, r)
+            lk = lk.copy()
+            lk["file"] += np.uint32(cuts[k])
+            parts.append(lk)
+            N.lib.tsg_result_free(r)
+        locs = np.concatenate(parts)
+    elif last is not None:
         locs, _ = read_result(N, last)
         N.lib.tsg_result_free(last)
     ms_per_step = dt / args.steps * 1e3

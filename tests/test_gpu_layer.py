@@ -93,3 +93,16 @@ def test_analyze_layer_reference_tar():
     a.init("")
     got, opq, wh = W.analyze_layer(a, os.path.join(os.path.dirname(__file__), "golden", "walker", "test.tar"))
     assert (got, opq, wh) == ([], ["etc/"], ["foo/foo"])
+
+
+def test_analyze_layers_pipelined_matches_single():
+    a = SecretAnalyzer()
+    a.init("")
+    layers = [_layer(50 + k, 120) for k in range(5)]
+    got = W.analyze_layers(a, layers, skip_dirs=["proc"], walk_threads=3)
+    assert len(got) == 5
+    for data, (secs, opq, wh) in zip(layers, got):
+        one, opq1, wh1 = W.analyze_layer(a, data, skip_dirs=["proc"])
+        assert _plain(secs) == _plain(one) and (opq, wh) == (opq1, wh1)
+        want, _, _ = _oracle_layer(data, skip_dirs=["proc"])
+        assert _plain(secs) == _oracle_plain(want)

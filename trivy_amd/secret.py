@@ -277,12 +277,12 @@ class Scanner:
         self.last_timings_ms = [tm[i] for i in range(min(16, nt.value))]
         flags = N.lib.tsg_result_file_flags(res)
         out = []
-        for i, a in enumerate(batch):
+        for i in range(len(batch)):  # batch[i] only where a FilePath is emitted (lazy batches)
             if flags[i] & N.TSG_FILE_BINARY:
                 out.append(None)
                 continue
             if flags[i] & N.TSG_FILE_PATH_ALLOWED:
-                out.append(Secret(FilePath=a.file_path))
+                out.append(Secret(FilePath=batch[i].file_path))
                 continue
             fp = ctypes.POINTER(N.FindingC)()
             k = N.lib.tsg_result_findings(res, i, ctypes.byref(fp))
@@ -304,7 +304,7 @@ class Scanner:
                     RuleID=rule.id, Category=rule.category, Severity=rule.severity or "UNKNOWN",
                     Title=rule.title, StartLine=f.start_line, EndLine=f.end_line,
                     Code=Code(Lines=lines), Match=_s(f.match, f.match_len)))
-            out.append(Secret(FilePath=a.file_path, Findings=findings))
+            out.append(Secret(FilePath=batch[i].file_path, Findings=findings))
         return out
 
 

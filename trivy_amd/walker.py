@@ -75,9 +75,9 @@ def _cstrs(v: Sequence[str]):
 
 
 class _Walk:
-    """Native walk (tsg_layer_tar_walk): entries (path, offset, size, mode,
-    is_dir), opq dirs, whiteouts; the handle stays open for tsg_analyze_layer
-    until close()."""
+    """Native walk (tsg_layer_tar_walk).  Entry tuples (path, offset, size,
+    mode, is_dir) are materialised on first use only: the batched analyze
+    needs none of them, just the paths of files that carry findings."""
 
     def __init__(self, addr: int, n: int, skip_files: Sequence[str], skip_dirs: Sequence[str]):
         sf, nsf = _cstrs(skip_files)
@@ -87,28 +87,55 @@ class _Walk:
         if rc != 0:
             raise WalkError(N.lib.tsg_last_error().decode("utf-8", "replace"))
         h = self.handle
-        k = N.lib.tsg_tar_walk_entry_count(h)
-        ents = N.lib.tsg_tar_walk_entries(h)
-        self.entries: List[Tuple[str, int, int, int, bool]] = []
-        for i in range(k):
-            e = ents[i]
-            p = ctypes.string_at(e.path, e.path_len).decode("utf-8", "surrogateescape")
-            self.entries.append((p, e.offset, e.size, e.mode, bool(e.is_dir)))
+        self.count = N.lib.tsg_tar_walk_entry_count(h)
+        self._ents = N.lib.tsg_tar_walk_entries(h)
+        self._entries = None
         self.opq_dirs = [N.lib.tsg_tar_walk_opq_dir(h, i).decode("utf-8", "surrogateescape")
                          for i in range(N.lib.tsg_tar_walk_opq_count(h))]
         self.wh_files = [N.lib.tsg_tar_walk_wh_file(h, i).decode("utf-8", "surrogateescape")
                          for i in range(N.lib.tsg_tar_walk_wh_count(h))]
 
+    def path(self, i: int) -> str:
+        e = self._ents[i]
+        return ctypes.string_at(e.path, e.path_len).decode("utf-8", "surrogateescape")
+
+    @property
+    def entries(self) -> List[Tuple[str, int, int, int, bool]]:
+        if self._entries is None:
+            out = []
+            for i in range(self.count):
+                e = self._ents[i]
+                out.append((self.path(i), e.offset, e.size, e.mode, bool(e.is_dir)))
+            self._entries = out
+        return self._entries
+
     def close(self):
         if self.handle:
             N.lib.tsg_tar_walk_free(self.handle)
             self.handle = ctypes.c_void_p()
+            self._ents = None
 
     def __enter__(self):
         return self
 
     def __exit__(self, *exc):
         self.close()
+
+
+class _KeptBatch:
+    """The analyze batch of one layer, lazily: item k is ScanArgs("/" + path
+    of walk entry kept[k]), built only when a result needs its FilePath."""
+
+    def __init__(self, walk: _Walk, kept, n: int):
+        self.walk, self.kept, self.n = walk, kept, n
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, k):
+        from .secret import ScanArgs
+
+        return ScanArgs("/" + self.walk.path(self.kept[k]), b"")
 
 
 class LayerTar:
@@ -128,7 +155,7 @@ class LayerTar:
         view = memoryview(buf).cast("B") if n else None
         try:
             with _Walk(addr, n, self.skip_files, self.skip_dirs) as w:
-                pass
+                w.entries  # noqa: B018 — materialise before the handle closes
             for path, off, size, mode, is_dir in w.entries:
                 info = FileInfo(path.rsplit("/", 1)[-1], size, mode, is_dir)
                 try:
@@ -143,6 +170,25 @@ class LayerTar:
             close()
 
 
+def _analyze_walked(analyzer, addr: int, n: int, w: _Walk) -> List[Secret]:
+    from .secret import get_engine
+
+    sc = analyzer.scanner
+    kept = (ctypes.c_uint32 * max(1, w.count))()
+    nk = ctypes.c_size_t()
+    res = ctypes.c_void_p()
+    N.check(N.lib.tsg_analyze_layer(get_engine(sc.device), sc._rs.handle, addr or None, n, w.handle,
+                                    (analyzer.config_path or "").encode(), kept, ctypes.byref(nk),
+                                    ctypes.byref(res)))
+    try:
+        out = sc._convert(res, _KeptBatch(w, kept, nk.value))
+    finally:
+        N.lib.tsg_result_free(res)
+    secrets = [r for r in out if r is not None and r.Findings]
+    secrets.sort(key=lambda s: s.FilePath)
+    return secrets
+
+
 def analyze_layer(analyzer, layer: Layer, skip_files: Sequence[str] = (),
                   skip_dirs: Sequence[str] = ()) -> Tuple[List[Secret], List[str], List[str]]:
     """One image layer through the secret analyzer, batched: the layer walk
@@ -153,26 +199,34 @@ def analyze_layer(analyzer, layer: Layer, skip_files: Sequence[str] = (),
     artifact, image.go:269) so paths get the '/' prefix (secret.go:95-98).
     Returns (secrets sorted by FilePath as AnalysisResult.Sort does,
     analyzer.go:218-229, opqDirs, whFiles)."""
-    from .secret import ScanArgs, get_engine
+    return analyze_layers(analyzer, [layer], skip_files, skip_dirs, walk_threads=1)[0]
 
-    sc = analyzer.scanner
-    buf, addr, n, close = _open_layer(layer)
+
+def analyze_layers(analyzer, layers: Sequence[Layer], skip_files: Sequence[str] = (),
+                   skip_dirs: Sequence[str] = (), walk_threads: int = 4
+                   ) -> List[Tuple[List[Secret], List[str], List[str]]]:
+    """The layers of an image (image.go:242-331 inspects them concurrently),
+    pipelined: up to `walk_threads` native walks run ahead on host threads
+    (ctypes drops the GIL) while the engine analyzes the layers in order, so
+    the serial header-chain walk of layer k+1 hides under the analyze of
+    layer k.  One (secrets, opqDirs, whFiles) per layer, in input order."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    opened = [_open_layer(x) for x in layers]
     try:
-        with _Walk(addr, n, skip_files, skip_dirs) as w:
-            kept = (ctypes.c_uint32 * max(1, len(w.entries)))()
-            nk = ctypes.c_size_t()
-            res = ctypes.c_void_p()
-            N.check(N.lib.tsg_analyze_layer(get_engine(sc.device), sc._rs.handle, addr or None, n, w.handle,
-                                            (analyzer.config_path or "").encode(), kept, ctypes.byref(nk),
-                                            ctypes.byref(res)))
-        try:
-            batch = [ScanArgs("/" + w.entries[kept[i]][0], b"") for i in range(nk.value)]
-            out = sc._convert(res, batch)
-        finally:
-            N.lib.tsg_result_free(res)
-        secrets = [r for r in out if r is not None and r.Findings]
-        secrets.sort(key=lambda s: s.FilePath)
-        return secrets, w.opq_dirs, w.wh_files
+        with ThreadPoolExecutor(max_workers=max(1, walk_threads)) as pool:
+            futs = [pool.submit(_Walk, addr, n, skip_files, skip_dirs) for _, addr, n, _ in opened]
+            out = []
+            try:
+                for (_, addr, n, _), f in zip(opened, futs):
+                    with f.result() as w:
+                        out.append((_analyze_walked(analyzer, addr, n, w), w.opq_dirs, w.wh_files))
+            finally:
+                for f in futs:  # free walks left behind by an error
+                    if f.done() and f.exception() is None:
+                        f.result().close()
+            return out
     finally:
-        del buf
-        close()
+        for buf, _, _, close in opened:
+            del buf
+            close()
