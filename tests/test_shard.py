@@ -85,3 +85,52 @@ def test_sharded_engine_scan_matches_batch():
     sc = S.new_scanner(None)
     batch = [S.ScanArgs(p, d) for p, d in _corpus()]
     assert scan_sharded(sc.scan_batch, batch) == sc.scan_batch(batch)
+
+
+# --- layer sets (BASELINE configs[3]: image layers sharded across GPUs) ------
+
+def _layers():
+    from .test_gpu_layer import _layer
+    return [_layer(60 + k, 30 + 7 * k) for k in range(5)]
+
+
+def _oracle_layers(layers):
+    from .test_gpu_layer import _oracle_layer
+    return [_oracle_layer(x) for x in layers]
+
+
+def _layer_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        layers = _layers()
+        res = scan_sharded(_oracle_layers, layers, sizes=[len(x) for x in layers])
+        if rank == 0:
+            import json
+            with open(out_path, "w") as f:
+                json.dump(res, f, default=lambda o: o.__dict__)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_layer_set_merge_equals_single_process(tmp_path):
+    """Layers are the shard unit for an image: LPT over layer bytes, one
+    analyze_layers call per rank, host merge in layer order."""
+    import json
+    out = str(tmp_path / "layers.json")
+    mp.start_processes(_layer_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    merged = json.load(open(out))
+    want = json.loads(json.dumps(_oracle_layers(_layers()), default=lambda o: o.__dict__))
+    assert merged == want
+    assert sum(len(s) for s, _, _ in want) > 0
+
+
+@pytest.mark.gpu
+def test_sharded_layer_set_matches_pipelined():
+    from trivy_amd.analyzer import SecretAnalyzer
+    from trivy_amd.walker import analyze_layers
+    a = SecretAnalyzer()
+    a.init("")
+    layers = _layers()
+    fn = lambda ls: analyze_layers(a, ls)  # noqa: E731
+    assert scan_sharded(fn, layers, sizes=[len(x) for x in layers]) == fn(layers)

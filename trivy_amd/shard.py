@@ -14,6 +14,10 @@ order, the way the analyzer concatenates per-file `types.Secret`s
                              with all_gather_object (host objects only: tens of
                              bytes per finding) and returned in batch order
 
+For an image (BASELINE configs[3]) the shard unit is the layer: batch =
+the layer tars, sizes = their byte lengths, scan_fn = a closure over
+`trivy_amd.walker.analyze_layers` on this rank's engine.
+
 The merge is the only communication; with world size 1 (or no process group)
 it is a plain call.
 """
