@@ -666,6 +666,13 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
           const uint4 v = C[0].cur[k];
           const uint32_t d[4] = {v.x, v.y, v.z, v.w};
           fast_window<V, kMode, 2>(P, T, out_e, C[0], d, C[0].pos + 16 * k, live, lanes_lt, ev_seg, &ev_count);
+        } else if (kWin == 8) {
+          if (k % 4 == 0) {
+            const uint4 a = C[0].cur[k], b = C[0].cur[k + 1 < V ? k + 1 : k];
+            const uint4 c2 = C[0].cur[k + 2 < V ? k + 2 : k], d2 = C[0].cur[k + 3 < V ? k + 3 : k];
+            const uint32_t d[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c2.x, c2.y, c2.z, c2.w, d2.x, d2.y, d2.z, d2.w};
+            fast_window<V, kMode, 8>(P, T, out_e, C[0], d, C[0].pos + 16 * k, live, lanes_lt, ev_seg, &ev_count);
+          }
         } else if (kWin == 4) {
           if (k % 2 == 0) {
             const uint4 v = C[0].cur[k], w = C[0].cur[k + 1 < V ? k + 1 : k];
@@ -2953,6 +2960,7 @@ int launch_scan(tsg_engine* e, ScanParams P) {
 #undef TSG_MODE
     else if (chains == 1 && vecs == 8 && win == 2) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 2>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1 && vecs == 8 && win == 4) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 4>), dim3(blocks), dim3(nt), 0, s, P);
+    else if (chains == 1 && vecs == 8 && win == 8) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 8>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1 && vecs == 8) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1) hipLaunchKernelGGL((k_scan_fast<1, 4, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     else if (vecs == 4) hipLaunchKernelGGL((k_scan_fast<2, 4, 1024>), dim3(blocks), dim3(nt), 0, s, P);
