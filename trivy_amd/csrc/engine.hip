@@ -344,35 +344,62 @@ __global__ __launch_bounds__(kBigThreads) void k_scan_big(ScanParams P) {
     return dense[st * K + c];
   };
   const uint64_t nchunks = (P.nbytes + kChunk - 1) / kChunk;
+  const uint64_t nfull = P.nbytes / kChunk;  // chunks with all 128 bytes in the batch
+  const uint64_t stride = (uint64_t)gridDim.x * kBigThreads;
   uint64_t last_kw = ~0ull;
-  for (uint64_t ch = (uint64_t)blockIdx.x * kBigThreads + threadIdx.x; ch < nchunks;
-       ch += (uint64_t)gridDim.x * kBigThreads) {
-    const uint64_t p0 = ch * kChunk;
-    const uint64_t pend = p0 + kChunk < P.nbytes ? p0 + kChunk : P.nbytes;
-    uint32_t st = 0;
-    for (uint64_t p = p0 >= (uint64_t)(kAcMaxLit - 1) ? p0 - (kAcMaxLit - 1) : 0; p < p0; ++p)
-      st = next(st, cls[P.data[p]]) & 0x7FFFu;
-    uint32_t nl = 0;
-    for (uint64_t p = p0; p < pend; p += 16) {
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (p + 16 <= pend) {
-        v = *(const uint4*)(P.data + p);
-      } else {
-        uint8_t tmp[16] = {0};
-        for (uint64_t q = p; q < pend; ++q) tmp[q - p] = P.data[q];
-        memcpy(&v, tmp, 16);
-      }
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-      const uint32_t m = pend - p < 16 ? (uint32_t)(pend - p) : 16u;
+  // Full chunks: the chunk's 128 bytes and the 16 before it (warm-up) are
+  // loaded as nine independent 16-byte vectors, and the lane's NEXT chunk is
+  // loaded while this one walks, so HBM latency is paid once per lane rather
+  // than once per 16 bytes (the walk itself is LDS-bound).
+  constexpr int kVecs = kChunk / 16;
+  uint4 cur[kVecs + 1], nxt[kVecs + 1];
+  auto load_chunk = [&](uint64_t c, uint4 (&v)[kVecs + 1]) {
+    const uint64_t p0 = c * kChunk;
+    v[0] = p0 >= 16 ? *(const uint4*)(P.data + p0 - 16) : make_uint4(0, 0, 0, 0);
 #pragma unroll
-      for (uint32_t i = 0; i < 16; ++i) {
-        if (i >= m) break;
+    for (int k = 0; k < kVecs; ++k) v[k + 1] = *(const uint4*)(P.data + p0 + 16 * k);
+  };
+  uint64_t ch = (uint64_t)blockIdx.x * kBigThreads + threadIdx.x;
+  if (ch < nfull) load_chunk(ch, nxt);
+  for (; ch < nfull; ch += stride) {
+#pragma unroll
+    for (int k = 0; k <= kVecs; ++k) cur[k] = nxt[k];
+    if (ch + stride < nfull) load_chunk(ch + stride, nxt);
+    const uint64_t p0 = ch * kChunk;
+    uint32_t st = 0;
+    if (p0 >= (uint64_t)(kAcMaxLit - 1)) {  // warm-up: bytes p0-7 .. p0-1 (kAcMaxLit = 8)
+      const uint32_t w[4] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w};
+#pragma unroll
+      for (int i = 16 - (kAcMaxLit - 1); i < 16; ++i) st = next(st, cls[(w[i >> 2] >> (8 * (i & 3))) & 0xFFu]) & 0x7FFFu;
+    }
+    uint32_t nl = 0;
+#pragma unroll
+    for (int k = 0; k < kVecs; ++k) {
+      const uint32_t w[4] = {cur[k + 1].x, cur[k + 1].y, cur[k + 1].z, cur[k + 1].w};
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
         const uint32_t b = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
         nl += b == '\n';
         const uint32_t nx = next(st, cls[b]);
         st = nx & 0x7FFFu;
-        if (nx & 0x8000u) report(P, st, p + i, &last_kw);
+        if (nx & 0x8000u) report(P, st, p0 + 16 * k + i, &last_kw);
       }
+    }
+    atomicAdd(&P.nl_blocks[p0 / kNlBlock], nl);
+  }
+  // the partial last chunk (at most one in the batch), byte by byte
+  for (uint64_t c = nfull + (uint64_t)blockIdx.x * kBigThreads + threadIdx.x; c < nchunks; c += stride) {
+    const uint64_t p0 = c * kChunk;
+    uint32_t st = 0;
+    for (uint64_t p = p0 >= (uint64_t)(kAcMaxLit - 1) ? p0 - (kAcMaxLit - 1) : 0; p < p0; ++p)
+      st = next(st, cls[P.data[p]]) & 0x7FFFu;
+    uint32_t nl = 0;
+    for (uint64_t p = p0; p < P.nbytes; ++p) {
+      const uint32_t b = P.data[p];
+      nl += b == '\n';
+      const uint32_t nx = next(st, cls[b]);
+      st = nx & 0x7FFFu;
+      if (nx & 0x8000u) report(P, st, p, &last_kw);
     }
     atomicAdd(&P.nl_blocks[p0 / kNlBlock], nl);
   }
