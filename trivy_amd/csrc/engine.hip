@@ -131,6 +131,9 @@ struct ScanParams {
   uint64_t ev_overflow_cap;
   uint8_t* span_hi;               // per kNlBlock span: a byte >= 0x80 occurs (k_fold_special)
   uint32_t* special_files;        // files flagged kFileSpecial, ctrl->n_special of them
+  uint64_t* big_rec;              // k_scan_big deferred outputs: (p << 16 | state), lane-strided
+  uint32_t* big_nrec;             // records per lane
+  uint32_t big_rec_cap;           // records per lane before k_scan_big reports inline
 };
 
 // Flag a file as holding a fold-special sequence; the first flagger lists it
@@ -332,7 +335,11 @@ __global__ __launch_bounds__(kBigThreads) void k_scan_big(ScanParams P) {
   const uint32_t* eval = (const uint32_t*)(smem + B.o_eval);
   const uint16_t* fl = (const uint16_t*)(smem + B.o_fail);
   const uint32_t K = P.rs.ac.nclasses, ND = B.n_dense;
+  // timing ablations only (TSG_REPORT_MODE, wave-uniform): 8 = no inline
+  // reports, 16 = cold states answered by the root row (wrong results)
+  const bool no_report = P.report_mode & 8, dense_only = P.report_mode & 16;
   auto next = [&](uint32_t st, uint32_t c) -> uint32_t {
+    if (dense_only && st >= ND) st = 0;
     while (st >= ND) {
       const uint32_t j = st - ND;
       for (uint32_t k = eoff[j]; k < eoff[j + 1]; ++k) {
@@ -360,6 +367,17 @@ __global__ __launch_bounds__(kBigThreads) void k_scan_big(ScanParams P) {
     for (int k = 0; k < kVecs; ++k) v[k + 1] = *(const uint4*)(P.data + p0 + 16 * k);
   };
   uint64_t ch = (uint64_t)blockIdx.x * kBigThreads + threadIdx.x;
+  // outputs are deferred to k_big_report as lane-strided 8-byte records
+  // (resolving them inline cost 2/3 of the kernel: a call with spills, a file
+  // search and divergent output loops inside the LDS walk); a lane whose
+  // record space is full reports inline, so nothing is ever dropped
+  const uint64_t gl = (uint64_t)blockIdx.x * kBigThreads + threadIdx.x;
+  uint32_t nrec = 0;
+  auto output = [&](uint32_t st, uint64_t p) {
+    if (no_report) return;
+    if (nrec < P.big_rec_cap) P.big_rec[(uint64_t)nrec++ * stride + gl] = (p << 16) | st;
+    else report(P, st, p, &last_kw);
+  };
   if (ch < nfull) load_chunk(ch, nxt);
   for (; ch < nfull; ch += stride) {
 #pragma unroll
@@ -382,7 +400,7 @@ __global__ __launch_bounds__(kBigThreads) void k_scan_big(ScanParams P) {
         nl += b == '\n';
         const uint32_t nx = next(st, cls[b]);
         st = nx & 0x7FFFu;
-        if (nx & 0x8000u) report(P, st, p0 + 16 * k + i, &last_kw);
+        if (nx & 0x8000u) output(st, p0 + 16 * k + i);
       }
     }
     atomicAdd(&P.nl_blocks[p0 / kNlBlock], nl);
@@ -399,10 +417,56 @@ __global__ __launch_bounds__(kBigThreads) void k_scan_big(ScanParams P) {
       nl += b == '\n';
       const uint32_t nx = next(st, cls[b]);
       st = nx & 0x7FFFu;
-      if (nx & 0x8000u) report(P, st, p, &last_kw);
+      if (nx & 0x8000u) output(st, p);
     }
     atomicAdd(&P.nl_blocks[p0 / kNlBlock], nl);
   }
+  P.big_nrec[gl] = nrec;
+}
+
+// k_scan_big's deferred outputs: one thread per scan lane resolves its
+// records (report_t: file lookup, confirm, keyword gates, anchor hits).
+// Anchor hits of k_big_report staged in LDS and appended to P.hits with one
+// global atomic per block (a global atomic per hit on the one counter
+// serialised at L2: 2.3 M hits cost 27 ms on configs[4]); overflow past the
+// stage goes straight to global.
+constexpr uint32_t kBigHitStage = 4096;
+struct LdsHitSink {
+  uint64_t* buf;
+  uint32_t* cnt;
+  __device__ void push(const ScanParams& P, uint64_t rec) {
+    const uint32_t i = atomicAdd(cnt, 1u);
+    if (i < kBigHitStage) {
+      buf[i] = rec;
+    } else {
+      GlobalHitSink g;
+      g.push(P, rec);
+    }
+  }
+};
+
+__global__ __launch_bounds__(256) void k_big_report(ScanParams P, uint64_t nlanes) {
+  __shared__ uint64_t stage[kBigHitStage];
+  __shared__ uint32_t n_stage;
+  __shared__ unsigned long long base;
+  if (threadIdx.x == 0) n_stage = 0;
+  __syncthreads();
+  const uint64_t gl = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  LdsHitSink sink{stage, &n_stage};
+  if (gl < nlanes) {
+    const uint32_t n = P.big_nrec[gl];
+    uint64_t last_kw = ~0ull;
+    for (uint32_t k = 0; k < n; ++k) {
+      const uint64_t r = P.big_rec[(uint64_t)k * nlanes + gl];
+      report_t<false>(P, (uint32_t)(r & 0xFFFFu), r >> 16, &last_kw, sink);
+    }
+  }
+  __syncthreads();
+  const uint32_t m = n_stage < kBigHitStage ? n_stage : kBigHitStage;
+  if (threadIdx.x == 0) base = m ? atomicAdd(&P.ctrl->hits, (unsigned long long)m) : 0ull;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < m; i += 256)
+    if (base + i < P.hit_cap) P.hits[base + i] = stage[i];
 }
 
 // Fast scan: the HBM-bound hot loop — one pass of the keyword/anchor
@@ -2329,6 +2393,8 @@ struct tsg_engine {
   hipStream_t stream = nullptr;
   std::mutex mu;
   DevImage img;
+  DBuf<uint64_t> big_rec;  // k_scan_big deferred output records
+  DBuf<uint32_t> big_nrec;
   DBuf<uint8_t> data;
   DBuf<uint64_t> off;
   DBuf<uint8_t> paths;
@@ -3006,7 +3072,15 @@ int launch_scan(tsg_engine* e, ScanParams P) {
         1, std::min<uint64_t>((nchunks + kBigThreads - 1) / kBigThreads, (uint64_t)e->num_cus));
     HIP_TRY(hipFuncSetAttribute((const void*)k_scan_big, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)P.big.blob_bytes));
+    const uint64_t nlanes = (uint64_t)blocks * kBigThreads;
+    P.big_rec_cap = 64;  // 8-byte records per lane (~9 per lane per 10 GB on configs[4])
+    HIP_TRY(e->big_rec.ensure(nlanes * P.big_rec_cap));
+    HIP_TRY(e->big_nrec.ensure(nlanes));
+    P.big_rec = e->big_rec.p;
+    P.big_nrec = e->big_nrec.p;
     hipLaunchKernelGGL(k_scan_big, dim3(blocks), dim3(kBigThreads), P.big.blob_bytes, s, P);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_big_report, dim3((uint32_t)((nlanes + 255) / 256)), dim3(256), 0, s, P, nlanes);
   } else {
     const size_t table_bytes = (size_t)ac.nstates * ac.nclasses * 2;
     const bool lds_table = table_bytes <= (size_t)kLdsTableMax;
