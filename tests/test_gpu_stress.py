@@ -114,3 +114,21 @@ def test_stress_1000_rules_vs_oracle(stress_cfg):
         custom += sum(f["RuleID"].startswith("stress-") for f in want["Findings"])
         assert _canon(_plain(g)) == _canon(want), f"stress file {p}"
     assert custom > 200  # the generated rules really fire
+
+
+def test_stress_big_record_overflow_matches(stress_cfg, monkeypatch):
+    """k_scan_big's deferred-output slots full (TSG_BIG_REC_CAP=1): the
+    outputs past a lane's slots are resolved inline, and the findings equal
+    the deferred-only run (which test_stress_1000_rules_vs_oracle pins)."""
+    path, rules = stress_cfg
+    files = stress_rules.make_corpus(13, rules, 40)
+    sc_g = S.new_scanner(S.parse_config(path), device=0)
+    batch = [S.ScanArgs(p, d) for p, d in files]
+    want = sc_g.scan_batch(batch)
+    monkeypatch.setenv("TSG_BIG_REC_CAP", "1")
+    got = sc_g.scan_batch(batch)
+    monkeypatch.setenv("TSG_BIG_REC_CAP", "0")
+    got0 = sc_g.scan_batch(batch)
+    assert [_canon(_plain(g)) for g in got] == [_canon(_plain(w)) for w in want]
+    assert [_canon(_plain(g)) for g in got0] == [_canon(_plain(w)) for w in want]
+    assert sum(len(w.Findings) for w in want) > 50

@@ -3074,6 +3074,7 @@ int launch_scan(tsg_engine* e, ScanParams P) {
                                 (int)P.big.blob_bytes));
     const uint64_t nlanes = (uint64_t)blocks * kBigThreads;
     P.big_rec_cap = 64;  // 8-byte records per lane (~9 per lane per 10 GB on configs[4])
+    if (const char* c = getenv("TSG_BIG_REC_CAP")) P.big_rec_cap = (uint32_t)atoi(c);  // tests: force the inline fallback
     HIP_TRY(e->big_rec.ensure(nlanes * P.big_rec_cap));
     HIP_TRY(e->big_nrec.ensure(nlanes));
     P.big_rec = e->big_rec.p;
