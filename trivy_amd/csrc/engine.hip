@@ -1226,6 +1226,8 @@ struct GateParams {
   const int32_t* rule_path;       // per rule: path prog or -1
   const uint32_t* rule_apath_off;  // per rule: offset into rule_apath (n_rules+1)
   const uint32_t* rule_apath;
+  const uint32_t* path_rules;  // rules with a Path or allow paths, config order
+  uint32_t n_path_rules;
   uint32_t any_rule_paths;
   uint32_t* file_flags;
   uint32_t* path_mask;  // n_files * rule_words: bit set => rule skipped by path
@@ -1386,7 +1388,8 @@ __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
       }
       return memo_res;
     };
-    for (uint32_t r = 0; r < G.rs.n_rules; ++r) {
+    for (uint32_t q = 0; q < G.n_path_rules; ++q) {  // only rules a path can skip
+      const uint32_t r = G.path_rules[q];
       bool skip = false;
       if (G.rule_path[r] >= 0) skip = !path_match((uint32_t)G.rule_path[r]);
       for (uint32_t k = G.rule_apath_off[r]; k < G.rule_apath_off[r + 1] && !skip; ++k)
@@ -2376,7 +2379,7 @@ struct DevImage {
   uint64_t pac_always = 0;
   RuleSetDev view{};
   // offsets into u32
-  uint32_t o_gpath = 0, n_gpath = 0, o_apoff = 0, o_ap = 0, o_full = 0, n_full = 0;
+  uint32_t o_gpath = 0, n_gpath = 0, o_apoff = 0, o_ap = 0, o_full = 0, n_full = 0, o_prules = 0, n_prules = 0;
   void release() {
     big.release();
     inst.release(); classes.release(); ranges.release(); progs.release(); rules.release();
@@ -2541,7 +2544,7 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   std::vector<int32_t> rule_path;
   std::map<std::string, uint32_t> kwid;
   for (size_t k = 0; k < rs->keywords.size(); ++k) kwid[rs->keywords[k]] = (uint32_t)k;
-  std::vector<uint32_t> kw_ids, group_slots, allow_progs, apath_off, apath, full_rules;
+  std::vector<uint32_t> kw_ids, group_slots, allow_progs, apath_off, apath, full_rules, path_rules;
   std::vector<uint16_t> fdelta, ddelta;
   std::vector<uint8_t> fcls, dbytes;
   std::set<uint32_t> kw_needed_ids;
@@ -2607,6 +2610,7 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
     apath_off.push_back((uint32_t)apath.size());
     for (int x : r.allow_path) apath.push_back((uint32_t)x);
     if (r.mode == MODE_FULL) full_rules.push_back((uint32_t)ri);
+    if (r.path >= 0 || !r.allow_path.empty()) path_rules.push_back((uint32_t)ri);
   }
   apath_off.push_back((uint32_t)apath.size());
   auto append = [&](const std::vector<uint32_t>& v) {
@@ -2622,6 +2626,8 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   im.n_gpath = (uint32_t)gpath.size();
   im.o_apoff = append(apath_off);
   im.o_ap = append(apath);
+  im.o_prules = append(path_rules);
+  im.n_prules = (uint32_t)path_rules.size();
   im.o_full = append(full_rules);
   im.n_full = (uint32_t)full_rules.size();
   HIP_TRY(im.u32.ensure(u32.size() + 1));
@@ -3168,6 +3174,8 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     G.rule_path = im.rule_path.p;
     G.rule_apath_off = im.u32.p + im.o_apoff;
     G.rule_apath = im.u32.p + im.o_ap;
+    G.path_rules = im.u32.p + im.o_prules;
+    G.n_path_rules = im.n_prules;
     G.any_rule_paths = rs->any_path_rules;
     G.file_flags = e->file_flags.p;
     G.path_mask = e->path_mask.p;
