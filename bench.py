@@ -33,11 +33,8 @@ sys.path.insert(0, ROOT)
 
 PLANT_DTYPE = np.dtype([("file", "<u4"), ("tpl", "<u4"), ("start", "<u8"), ("end", "<u8"),
                         ("decoy", "<u4"), ("pad", "<u4")])
-# rule id of each corpus.hip template (kTpl order)
-TPL_RULES = ["aws-access-key-id", "aws-secret-access-key", "github-pat", "github-oauth", "gitlab-pat",
-             "hugging-face-access-token", "slack-access-token", "stripe-secret-token", "sendgrid-api-token",
-             "npm-access-token", "facebook-token", "twilio-api-key", "shopify-token", "age-secret-key",
-             "rubygems-api-token", "pulumi-api-token"]
+# plant kinds (corpus.hip PlantKind): 0 real, 1 one-char-short decoy, 2 EXAMPLE decoy, 3 K/ſ-spelled instance
+PLANT_REAL, PLANT_SHORT, PLANT_EXAMPLE, PLANT_FOLD = 0, 1, 2, 3
 WORKLOADS = {
     0: "configs[0]: builtin rules through the batched SecretAnalyzer (IsBinary, CR strip, scan, findings) on a "
        "1 GB source tree already read into host memory; PCIe-inclusive (pinned staging + H2D in the step)",
@@ -173,33 +170,57 @@ def read_result(N, res):
     return locs, [tm[i] for i in range(min(32, nt.value))]
 
 
-def parity_checks(N, S, c, locs, rules, seed, density, n_sample=300, oracle_cfg=None):
-    """Full-size properties + oracle spot checks on sample files."""
+def template_rules(N):
+    """Rule ID of each corpus.hip template (one per builtin rule)."""
+    return [N.lib.tsg_gen_template_rule(i).decode() for i in range(N.lib.tsg_gen_template_count())]
+
+
+def parity_checks(N, S, c, locs, rules, seed, density, n_sample=300, oracle_cfg=None, big_files=3,
+                  nonascii_files=24):
+    """Full-size properties + oracle spot checks on sample files.
+
+    Properties over the WHOLE batch: every real plant (an instance of one of
+    the 86 builtin rules) is reported at its exact location; no decoy (one
+    char short, or EXAMPLE inside the match) is.  Spot checks: the oracle's
+    Scan of sample files (plant files, random files, `big_files` files of
+    4-16 MiB and `nonascii_files` of the 0.1 % carrying é/K/ſ/İ, the K/ſ-spelled
+    rule instances first) must equal the engine's locations exactly."""
     from oracle import secret_oracle as O
 
+    tpl_rules = template_rules(N)
     rid = {r.id: i for i, r in enumerate(rules)}
     have = set(zip(locs["file"].tolist(), locs["rule"].tolist(), locs["start"].tolist(), locs["end"].tolist()))
     plants = c["plants"]
-    real = plants[plants["decoy"] == 0]
-    found = sum((int(p["file"]), rid[TPL_RULES[p["tpl"]]], int(p["start"]), int(p["end"])) in have for p in real)
-    decoys = plants[plants["decoy"] == 1]
-    decoy_hits = sum((int(p["file"]), rid[TPL_RULES[p["tpl"]]], int(p["start"]), int(p["end"])) in have
-                     or (int(p["file"]), rid[TPL_RULES[p["tpl"]]], int(p["start"]), int(p["end"]) - 1) in have
-                     for p in decoys)
-    # oracle spot checks: files holding plants + random files
+    key = lambda p, d=0: (int(p["file"]), rid[tpl_rules[p["tpl"]]], int(p["start"]), int(p["end"]) - d)
+    real = plants[plants["decoy"] == PLANT_REAL]
+    found = sum(key(p) in have for p in real)
+    decoys = plants[(plants["decoy"] == PLANT_SHORT) | (plants["decoy"] == PLANT_EXAMPLE)]
+    decoy_hits = sum(key(p) in have or key(p, 1) in have for p in decoys)
+    per_rule = {}
+    for p in real:
+        per_rule[tpl_rules[p["tpl"]]] = per_rule.get(tpl_rules[p["tpl"]], 0) + 1
+    # oracle spot checks
     rng = np.random.default_rng(seed + 7)
+    sizes = c["sizes"]
+    fold = plants[plants["decoy"] == PLANT_FOLD]
+    fold_files = [int(f) for f in np.unique(fold["file"]) if sizes[f] <= (8 << 20)]
+    nonascii = [f for f in range(c["n_files"]) if sizes[f] >= 600 and N.lib.tsg_gen_file_nonascii(seed, f)]
+    extra_na = [f for f in nonascii if f not in set(fold_files) and sizes[f] <= (8 << 20)]
+    na_pick = (fold_files + [int(x) for x in rng.permutation(extra_na)])[:nonascii_files]
+    big = np.nonzero((sizes >= (4 << 20)) & (sizes <= (16 << 20)))[0]
+    big_pick = [int(x) for x in rng.permutation(big)[:big_files]]
     cand = np.unique(np.concatenate([real["file"][: n_sample // 2].astype(np.int64),
                                      rng.integers(0, c["n_files"], n_sample // 2)]))
-    cand = [int(f) for f in cand if c["sizes"][f] <= (4 << 20)]
+    cand = sorted(set(int(f) for f in cand if sizes[f] <= (4 << 20)) | set(na_pick) | set(big_pick))
     by_file = {}
     for L in locs:
         by_file.setdefault(int(L["file"]), []).append(
             (rules[int(L["rule"])].id, int(L["start"]), int(L["end"]), int(L["start_line"]), int(L["end_line"])))
     oracle = O.Scanner(O.parse_config(oracle_cfg) if oracle_cfg else None)
-    mismatched = 0
-    spot_findings = 0
+    mismatched = []
+    spot_findings = spot_bytes = 0
     for f in cand:
-        n = int(c["sizes"][f])
+        n = int(sizes[f])
         buf = (ctypes.c_uint8 * max(1, n))()
         N.check(N.lib.tsg_gen_file(seed, f, n, density, buf))
         data = bytes(buf)[:n]
@@ -208,11 +229,16 @@ def parity_checks(N, S, c, locs, rules, seed, density, n_sample=300, oracle_cfg=
         w = sorted((x.RuleID, x.Start, x.End, x.StartLine, x.EndLine) for x in want["Findings"])
         g = sorted(by_file.get(f, []))
         spot_findings += len(w)
+        spot_bytes += n
         if w != g:
-            mismatched += 1
-    return dict(planted=int(len(real)), planted_found=int(found), decoys=int(len(decoys)),
-                decoys_found=int(decoy_hits), spot_files=len(cand), spot_findings=spot_findings,
-                spot_mismatched_files=mismatched, total_findings=int(len(locs)))
+            mismatched.append(f)
+    return dict(planted=int(len(real)), planted_found=int(found), planted_rules=len(per_rule),
+                decoys=int(len(decoys)), decoys_found=int(decoy_hits), fold_instances=int(len(fold)),
+                nonascii_files=len(nonascii), spot_files=len(cand), spot_bytes=spot_bytes,
+                spot_nonascii_files=len(na_pick), spot_big_files=len(big_pick),
+                spot_max_file_bytes=int(max(sizes[f] for f in cand)) if cand else 0,
+                spot_findings=spot_findings, spot_mismatched_files=len(mismatched),
+                spot_mismatched=mismatched[:10], total_findings=int(len(locs)))
 
 
 def gate_timings(N, eng):

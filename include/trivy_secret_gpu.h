@@ -99,7 +99,8 @@ typedef struct tsg_finding {
 
 /* Per-file flags in a result. */
 #define TSG_FILE_PATH_ALLOWED 1u /* Global.AllowPath matched: Secret{FilePath} without findings (scanner.go:375-379) */
-#define TSG_FILE_SPECIAL 2u      /* content holds U+0130/U+017F/U+212A: scanned on the exact full-scan path */
+#define TSG_FILE_SPECIAL 2u      /* content holds U+0130/U+017F/U+212A: keywords and anchor literals spelled
+                                    with them were re-checked around each occurrence (k_fold_windows) */
 #define TSG_FILE_BINARY 4u       /* tsg_analyze: utils.IsBinary (utils.go:77-95) -> skipped, Analyze returns nil */
 
 const char* tsg_version(void);
@@ -262,6 +263,16 @@ int tsg_gen_corpus_device(uint8_t* d_data, const uint64_t* d_offsets, const uint
                           uint64_t seed, double density, void* d_plants, uint64_t plant_cap,
                           unsigned long long* d_nplants);
 int tsg_gen_file(uint64_t seed, uint32_t file, uint64_t len, double density, uint8_t* out);
+/* As tsg_gen_file, plus the file's plant records (tsg_gen_plant_record_size
+ * bytes each: file, template, start, end, kind 0 real / 1 one-char-short
+ * decoy / 2 EXAMPLE decoy / 3 K-or-ſ-spelled instance) into plants[0..cap). */
+int tsg_gen_file_plants(uint64_t seed, uint32_t file, uint64_t len, double density, uint8_t* out, void* plants,
+                        size_t plant_cap, size_t* n_plants);
+/* 1 if file `file` of corpus `seed` is one of the 0.1 % carrying non-ASCII runes. */
+int tsg_gen_file_nonascii(uint64_t seed, uint32_t file);
+/* The planted-secret templates: one per builtin rule; the rule ID of template i. */
+size_t tsg_gen_template_count(void);
+const char* tsg_gen_template_rule(size_t i);
 size_t tsg_gen_plant_record_size(void);
 uint32_t tsg_gen_chunk_bytes(void);
 

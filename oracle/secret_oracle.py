@@ -34,8 +34,10 @@ from __future__ import annotations
 
 import dataclasses
 import os
+import re
 from typing import List, Optional
 
+import numpy as np
 import regex as _re
 import yaml
 
@@ -401,7 +403,7 @@ class GoRegexp:
 
     def find_all_index(self, data: bytes):
         _, off = _decode(data)
-        return [[off[m.start()], off[m.end()]] for m in self._iter(data)]
+        return [[int(off[m.start()]), int(off[m.end()])] for m in self._iter(data)]
 
     def find_all_submatch_index(self, data: bytes):
         _, off = _decode(data)
@@ -410,7 +412,7 @@ class GoRegexp:
             idx = []
             for g in range(len(self.names)):
                 a, b = m.span(g)
-                idx += [off[a], off[b]] if a >= 0 else [-1, -1]
+                idx += [int(off[a]), int(off[b])] if a >= 0 else [-1, -1]
             res.append(idx)
         return res
 
@@ -419,39 +421,49 @@ class GoRegexp:
         return self.rx.search(t) is not None
 
 
+_DECODE_CACHE = [None, None]  # (bytes object, result): Scan decodes one content once per rule
+
+
 def _decode(data: bytes):
     """Rune-decode like Go's utf8.DecodeRune (invalid byte -> one rune) and
     return (text, byte offset of each rune index incl. the end)."""
     if data.isascii():
         return data.decode("ascii"), range(len(data) + 1)
+    if _DECODE_CACHE[0] is data:
+        return _DECODE_CACHE[1]
     s = data.decode("utf-8", "surrogateescape")
-    off = [0] * (len(s) + 1)
-    b = 0
-    for k, ch in enumerate(s):
-        off[k] = b
-        cp = ord(ch)
-        if 0xDC80 <= cp <= 0xDCFF:
-            b += 1
-        elif cp < 0x80:
-            b += 1
-        elif cp < 0x800:
-            b += 2
-        elif cp < 0x10000:
-            b += 3
-        else:
-            b += 4
-    off[len(s)] = b
-    return s, off
+    # rune widths: escaped invalid bytes (U+DC80..U+DCFF) are 1 byte, else the UTF-8 length
+    cp = np.frombuffer(s.encode("utf-32-le", "surrogatepass"), dtype=np.uint32)
+    w = np.where(cp < 0x80, 1, np.where(cp < 0x800, 2, np.where(cp < 0x10000, 3, 4)))
+    w[(cp >= 0xDC80) & (cp <= 0xDCFF)] = 1
+    off = np.zeros(len(s) + 1, dtype=np.int64)
+    np.cumsum(w, out=off[1:])
+    res = (s, off)
+    _DECODE_CACHE[0], _DECODE_CACHE[1] = data, res
+    return res
 
 
 # --------------------------------------------------------------------------- #
 # bytes.ToLower (Go) for the keyword gate — scanner.go:175
 # --------------------------------------------------------------------------- #
 
+_INVALID = re.compile("[\udc80-\udcff]")
+
+
 def go_bytes_to_lower(b: bytes) -> bytes:
     if b.isascii():
         return b.lower()
     s = b.decode("utf-8", "surrogateescape")
+    if "\u03a3" in s:  # str.lower() applies Final_Sigma in context; Go maps each rune alone
+        return _go_bytes_to_lower_slow(s)
+    # invalid byte -> RuneError (re-encoded as EF BF BD); U+0130 -> 'i' (unicode.ToLower's
+    # simple mapping: the only rune whose str.lower() is not one rune); every other rune
+    # maps alone, as str.lower() does
+    s = _INVALID.sub("\ufffd", s).replace("\u0130", "i")
+    return s.lower().encode("utf-8")
+
+
+def _go_bytes_to_lower_slow(s: str) -> bytes:
     out = []
     for ch in s:
         cp = ord(ch)

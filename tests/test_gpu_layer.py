@@ -67,7 +67,10 @@ def _oracle_layer(data, skip_files=(), skip_dirs=()):
         if res is not None:
             out.extend(res)
     opq, wh = lo.walk(data, fn, skip_files, skip_dirs)
+    # AnalysisResult.Sort (analyzer.go:218-229): by FilePath, findings by (RuleID, StartLine)
     out.sort(key=lambda r: r["FilePath"])
+    for r in out:
+        r["Findings"].sort(key=lambda f: (f.RuleID, f.StartLine))
     return out, opq, wh
 
 
@@ -106,3 +109,22 @@ def test_analyze_layers_pipelined_matches_single():
         assert _plain(secs) == _plain(one) and (opq, wh) == (opq1, wh1)
         want, _, _ = _oracle_layer(data, skip_dirs=["proc"])
         assert _plain(secs) == _oracle_plain(want)
+
+
+def test_analyze_layer_finding_order():
+    """Two findings of one rule whose Match order (Scan's sort) is the reverse
+    of their line order: the layer result carries AnalysisResult.Sort's
+    (RuleID, StartLine) order, compared as lists (no re-sorting here)."""
+    content = b"x = 1\ntoken: ghp_" + b"Z" * 36 + b"\ny = 2\nauth: ghp_" + b"A" * 36 + b"\n"  # Match: "auth" < "token"
+    buf = io.BytesIO()
+    with tarfile.open(fileobj=buf, mode="w", format=tarfile.GNU_FORMAT) as tf:
+        ti = tarfile.TarInfo("app/config.env")
+        ti.size = len(content)
+        tf.addfile(ti, io.BytesIO(content))
+    data = buf.getvalue()
+    a = SecretAnalyzer()
+    a.init("")
+    got, _, _ = W.analyze_layer(a, data)
+    assert [(f.RuleID, f.StartLine) for f in got[0].Findings] == [("github-pat", 2), ("github-pat", 4)]
+    want, _, _ = _oracle_layer(data)
+    assert _plain(got) == _oracle_plain(want)

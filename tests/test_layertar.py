@@ -148,6 +148,42 @@ def test_malformed_layers_fail_loudly():
         _native(bytes(bad))
 
 
+def test_zero_block_rules():
+    """archive/tar readHeader: one zero block then EOF ends the walk, two zero
+    blocks end it, a zero block followed by a header is ErrHeader ("invalid
+    tar header"), a zero block followed by a partial block is unexpected EOF."""
+    one = make_layer(8, n=3)
+    body = one.rstrip(b"\0")
+    body += b"\0" * ((-len(body)) % 512)
+    z = b"\0" * 512
+    assert _native(body + z)[0] == _native(one)[0]
+    assert _native(body + z + z)[0] == _native(one)[0]
+    with pytest.raises(W.WalkError, match="invalid tar header"):
+        _native(body + z + make_layer(9, n=2))
+    with pytest.raises(W.WalkError, match="unexpected EOF"):
+        _native(body + z + b"x" * 100)
+
+
+def test_fuzzed_layers_never_crash():
+    """Random truncations and byte flips of generated layers: the walk either
+    succeeds or reports "failed to extract the archive" (never aborts)."""
+    rng = random.Random(99)
+    ok = bad = 0
+    for k in range(300):
+        data = bytearray(make_layer(100 + k % 7, n=6, fmt=rng.choice([tarfile.GNU_FORMAT, tarfile.PAX_FORMAT])))
+        for _ in range(rng.randint(1, 6)):
+            data[rng.randrange(len(data))] = rng.randrange(256)
+        if rng.random() < 0.3:
+            data = data[: rng.randrange(len(data) + 1)]
+        try:
+            _native(bytes(data))
+            ok += 1
+        except W.WalkError as e:
+            assert "failed to extract the archive" in str(e)
+            bad += 1
+    assert ok and bad
+
+
 # --- doublestar.Match (walk.go:43) --------------------------------------------
 
 GLOBS = [

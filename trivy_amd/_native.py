@@ -137,6 +137,12 @@ _SIGS = {
                                              ctypes.c_double, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     "tsg_gen_file": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double,
                                     ctypes.c_void_p]),
+    "tsg_gen_file_plants": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.POINTER(ctypes.c_size_t)]),
+    "tsg_gen_file_nonascii": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32]),
+    "tsg_gen_template_count": (ctypes.c_size_t, []),
+    "tsg_gen_template_rule": (ctypes.c_char_p, [ctypes.c_size_t]),
     "tsg_gen_plant_record_size": (ctypes.c_size_t, []),
     "tsg_gen_chunk_bytes": (ctypes.c_uint32, []),
     "tsg_regex_match": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t,

@@ -8,7 +8,8 @@
 //                 keyword (MatchKeywords gate bits, scanner.go:169-181), every rule's
 //                 anchor literal (hit records) and the fold-special sequences
 //   k_expand      anchor hits -> (rule, position) candidates for gated files
-//   k_full_jobs   rules without an anchor / files with special bytes -> full-scan jobs
+//   k_fold_windows  keywords / anchor literals spelled with İ, K, ſ around each such rune
+//   k_full_jobs   rules without an anchor -> full-scan jobs
 //   radix sort    candidates by (rule, position)
 //   k_verify      one lane per (file, rule) job: Go leftmost-first Pike VM restricted to
 //                 the anchor windows, FindAll iteration, allow rules, secret groups
@@ -81,7 +82,7 @@ struct Ctrl {
   unsigned int pad;
   unsigned long long ev_overflow;
   unsigned long long outputs;  // patterns k_report resolved (diagnostics)
-  unsigned long long n_special;  // files flagged kFileSpecial (ScanParams::special_files)
+  unsigned long long n_fold;     // fold-special rune occurrences recorded (ScanParams::fold_pos)
   unsigned long long n_caps;     // matches whose secret-group spans k_captures resolves
 };
 
@@ -130,21 +131,28 @@ struct ScanParams {
   struct FastEvent* ev_overflow;  // events beyond a wave's segment
   uint64_t ev_overflow_cap;
   uint8_t* span_hi;               // per kNlBlock span: a byte >= 0x80 occurs (k_fold_special)
-  uint32_t* special_files;        // files flagged kFileSpecial, ctrl->n_special of them
+  uint64_t* fold_pos;             // fold-special runes: position << 2 | kind (FoldKind), ctrl->n_fold of them
+  uint64_t fold_cap;
   uint64_t* big_rec;              // k_scan_big deferred outputs: (p << 16 | state), lane-strided
   uint32_t* big_nrec;             // records per lane
   uint32_t big_rec_cap;           // records per lane before k_scan_big reports inline
 };
 
-// Flag a file as holding a fold-special sequence; the first flagger lists it
-// for k_special_gate (so that kernel visits flagged files only).
+// Fold-special runes (the only non-ASCII runes that Go's case rules tie to
+// ASCII letters): U+0130 İ lowers to 'i' and U+212A K to 'k' in bytes.ToLower
+// (the MatchKeywords gate, scanner.go:175); U+212A K and U+017F ſ match 'k' /
+// 's' under (?i) simple folding (regexp/syntax).  Every occurrence is
+// recorded (position of its lead byte + kind); k_fold_windows then examines
+// only the bytes around each one (keywords / anchor literals spelled with it).
+enum FoldKind : uint32_t { FOLD_I = 0, FOLD_S = 1, FOLD_K = 2 };
+
 __device__ inline void mark_special(const ScanParams& P, uint32_t fi) {
-  if (P.file_flags[fi] & kFileSpecial) return;
-  const uint32_t old = atomicOr(&P.file_flags[fi], kFileSpecial);
-  if (!(old & kFileSpecial)) {
-    const unsigned long long k = atomicAdd(&P.ctrl->n_special, 1ull);
-    if (k < P.n_files) P.special_files[k] = fi;
-  }
+  if (!(P.file_flags[fi] & kFileSpecial)) atomicOr(&P.file_flags[fi], kFileSpecial);
+}
+
+__device__ inline void note_fold(const ScanParams& P, uint64_t pos, uint32_t kind) {
+  const unsigned long long k = atomicAdd(&P.ctrl->n_fold, 1ull);
+  if (k < P.fold_cap) P.fold_pos[k] = (pos << 2) | kind;
 }
 
 
@@ -213,7 +221,11 @@ __device__ inline void report_t(const ScanParams& P, uint32_t st, uint64_t p, ui
       for (uint32_t k = ac.depth; k < pd.len && ok; ++k) ok = lower_ascii(P.data[start + k]) == pb[k];
       if (!ok) continue;
     }
-    if (pd.special) mark_special(P, fi);
+    if (pd.special) {
+      mark_special(P, fi);
+      const uint8_t b0 = ac.pat_bytes[pd.bytes_off];
+      note_fold(P, start, b0 == 0xC4 ? FOLD_I : b0 == 0xC5 ? FOLD_S : FOLD_K);
+    }
     if (pd.kw != kNoKw) {
       const uint64_t key = ((uint64_t)fi << 32) | pd.kw;  // per-lane dedupe of repeated keywords
       if (*last_kw != key) {
@@ -1126,7 +1138,7 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
 
 // Fold-special sequences (C4B0 U+0130, C5BF U+017F, E284AA U+212A) in the
 // spans k_scan_fast saw a byte >= 0x80 in: one wave per span, 64 bytes per
-// lane, flag the file so it takes the exact full-scan path (k_special_gate).
+// lane, flag the file and record each occurrence for k_fold_windows.
 __global__ __launch_bounds__(256) void k_fold_special(ScanParams P, uint64_t n_spans) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -1142,8 +1154,11 @@ __global__ __launch_bounds__(256) void k_fold_special(ScanParams P, uint64_t n_s
       uint32_t b1 = a >= 1 && a - 1 < P.nbytes ? P.data[a - 1] : 0, b2 = a >= 2 && a - 2 < P.nbytes ? P.data[a - 2] : 0;
       for (uint64_t q = a; q < b; ++q) {
         const uint32_t c = P.data[q];
-        if ((c == 0xB0 && b1 == 0xC4) || (c == 0xBF && b1 == 0xC5) || (c == 0xAA && b1 == 0x84 && b2 == 0xE2))
+        const bool fi = c == 0xB0 && b1 == 0xC4, fs = c == 0xBF && b1 == 0xC5, fk = c == 0xAA && b1 == 0x84 && b2 == 0xE2;
+        if (fi || fs || fk) {
           mark_special(P, file_of_pos(P, q));
+          note_fold(P, fk ? q - 2 : q - 1, fi ? FOLD_I : fs ? FOLD_S : FOLD_K);
+        }
         b2 = b1;
         b1 = c;
       }
@@ -1151,65 +1166,91 @@ __global__ __launch_bounds__(256) void k_fold_special(ScanParams P, uint64_t n_s
   }
 }
 
-// Exact MatchKeywords for files holding U+0130 (C4 B0) or U+212A (E2 84 AA):
-// bytes.ToLower maps them to 'i' / 'k' (scanner.go:175), the only non-ASCII
-// runes whose lowercase is ASCII; every other byte >= 0x80 can never be part
-// of an (ASCII) keyword.  One wave per flagged file, one segment per lane,
-// 32 raw bytes of warm-up (>= 7 lowered runes) snapped to a rune start.
-// Keyword bits are idempotent, so overlapping segments are harmless.
-__global__ __launch_bounds__(256) void k_special_gate(ScanParams P) {
+// Fold windows: around each fold-special rune occurrence q (k_fold_special,
+// report_t), every work item (a pattern) is tried at every start h whose
+// occurrence would contain q, so no file is ever rescanned whole:
+//  * gate items (keywords holding 'i' or 'k'): MatchKeywords lowers the whole
+//    file (bytes.ToLower, scanner.go:175) and İ -> 'i', K -> 'k' are the only
+//    non-ASCII runes that lower to ASCII; a keyword spelled with one sets the
+//    file's keyword bit (ASCII spellings were set by the scan already)
+//  * hit items (anchor literals with a case-free 'k' or 's'): the literal
+//    spelled with K / ſ ((?i) simple folding) is an anchor hit the ASCII scan
+//    cannot see; it is appended with kFoldHit so that k_expand applies the
+//    rule's keyword gate itself (ToLower(ſ) is ſ: such a match does not
+//    imply the gate).  Every other match of the file still holds an ASCII
+//    literal hit; gre's anchor offsets and prefix alphabets already count
+//    K / ſ bytes, so those windows stay exact.
+// An occurrence is taken only at its FIRST fold rune (each once).
+constexpr uint64_t kFoldHit = 1ull << 63;
+constexpr uint32_t kFoldItemGate = 1u << 31, kFoldItemHit = 1u << 30;
+
+struct FoldItems {
+  const uint32_t* items;  // pattern id | kFoldItemGate | kFoldItemHit
+  uint32_t n;
+  uint32_t with_hits;     // 0 for the prefilter-only pass (no anchor hits)
+};
+
+// Does pattern (lowered L, case requirement R or null, m bytes) occur at h,
+// spelled with fold runes?  gate: bytes.ToLower view (İ, K); else the (?i)
+// view (K, ſ on case-free positions).  *first = its first fold rune.
+__device__ inline bool fold_match(const uint8_t* d, uint64_t nbytes, uint64_t h, const uint8_t* L, const uint8_t* R,
+                                  uint32_t m, bool gate, uint64_t* first) {
+  uint64_t t = h;
+  *first = ~0ull;
+  for (uint32_t i = 0; i < m; ++i) {
+    if (t >= nbytes) return false;
+    const uint32_t c = d[t];
+    const uint8_t l = L[i];
+    if (c >= 0x80) {
+      uint32_t w = 0;
+      if (c == 0xE2 && t + 2 < nbytes && d[t + 1] == 0x84 && d[t + 2] == 0xAA && l == 'k' && (gate || !R || !R[i])) w = 3;
+      else if (!gate && c == 0xC5 && t + 1 < nbytes && d[t + 1] == 0xBF && l == 's' && (!R || !R[i])) w = 2;
+      else if (gate && c == 0xC4 && t + 1 < nbytes && d[t + 1] == 0xB0 && l == 'i') w = 2;
+      if (!w) return false;
+      if (*first == ~0ull) *first = t;
+      t += w;
+      continue;
+    }
+    if (lower_ascii((uint8_t)c) != l) return false;
+    if (!gate && R && R[i] && c != R[i]) return false;
+    ++t;
+  }
+  return *first != ~0ull;
+}
+
+__global__ __launch_bounds__(256) void k_fold_windows(ScanParams P, FoldItems F, uint64_t n_fold) {
   const AcDev& ac = P.rs.ac;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint64_t wave0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-  for (uint64_t f = wave0; f < P.n_files; f += nwaves) {
-    if (!(P.file_flags[f] & kFileSpecial)) continue;
-    const uint64_t fs = P.off[f], fe = P.off[f + 1] - 1;
-    const uint64_t len = fe - fs;
-    const uint64_t seg = (len + 63) / 64;
-    uint64_t a = fs + lane * seg, b = a + seg < fe ? a + seg : fe;
-    if (a >= b) continue;
-    uint64_t p = a >= fs + 32 ? a - 32 : fs;
-    while (p > fs && (P.data[p] & 0xC0) == 0x80) --p;  // snap to a rune start
-    uint32_t st = 0;
-    while (p < b) {
-      uint32_t c = P.data[p];
-      uint32_t w = 1;
-      if (c == 0xC4 && p + 1 < fe && P.data[p + 1] == 0xB0) {
-        c = 'i';
-        w = 2;
-      } else if (c == 0xE2 && p + 2 < fe && P.data[p + 1] == 0x84 && P.data[p + 2] == 0xAA) {
-        c = 'k';
-        w = 3;
-      } else if (c >= 0x80) {
-        c = 0;  // breaker: never inside an ASCII keyword
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= n_fold * F.n) return;
+  const uint64_t rec = P.fold_pos[tid / F.n];
+  const uint32_t it = F.items[tid % F.n];
+  const uint64_t q = rec >> 2;
+  const uint32_t kind = (uint32_t)(rec & 3);
+  const uint32_t pid = it & 0xFFFFu;
+  const bool want_gate = (it & kFoldItemGate) && kind != FOLD_S;
+  const bool want_hit = (it & kFoldItemHit) && F.with_hits && kind != FOLD_I;
+  if (!want_gate && !want_hit) return;
+  const PatDev pd = ac.pats[pid];
+  const uint8_t* L = ac.pat_bytes + pd.bytes_off;
+  const uint8_t* R = pd.confirm ? ac.pat_bytes + pd.req_off : nullptr;
+  const uint32_t m = pd.len;
+  if (!m) return;
+  const uint64_t span = 3ull * (m - 1);
+  uint32_t fi = 0xFFFFFFFFu;
+  for (uint64_t h = q > span ? q - span : 0; h <= q; ++h) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const bool gate = g == 0;
+      if (gate ? !want_gate : !want_hit) continue;
+      uint64_t first;
+      if (!fold_match(P.data, P.nbytes, h, L, R, m, gate, &first) || first != q) continue;
+      if (gate) {
+        if (fi == 0xFFFFFFFFu) fi = file_of_pos(P, q);
+        atomicOr(&P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)], 1u << (pd.kw & 31));
+      } else {
+        const unsigned long long idx = atomicAdd(&P.ctrl->hits, 1ull);
+        if (idx < P.hit_cap) P.hits[idx] = kFoldHit | (h << 16) | pid;
       }
-      const uint32_t nx = ac.delta[st * ac.nclasses + ac.cls[c]];
-      st = nx & 0x7FFFu;
-      if (nx & 0x8000u) {
-        for (uint32_t o = ac.out_off[st]; o < ac.out_off[st + 1]; ++o) {
-          const PatDev pd = ac.pats[ac.out_pat[o]];
-          if (pd.kw == kNoKw) continue;
-          if (pd.trunc) {  // confirm the rest of a long keyword on the lowered stream
-            const uint8_t* pb = ac.pat_bytes + pd.bytes_off;
-            uint64_t q = p + w;
-            bool ok = true;
-            for (uint32_t k = ac.depth; k < pd.len && ok; ++k) {
-              if (q >= fe) { ok = false; break; }
-              uint32_t ch = P.data[q];
-              uint32_t cw = 1;
-              if (ch == 0xC4 && q + 1 < fe && P.data[q + 1] == 0xB0) { ch = 'i'; cw = 2; }
-              else if (ch == 0xE2 && q + 2 < fe && P.data[q + 1] == 0x84 && P.data[q + 2] == 0xAA) { ch = 'k'; cw = 3; }
-              else if (ch >= 0x80) { ok = false; break; }
-              ok = lower_ascii((uint8_t)ch) == pb[k];
-              q += cw;
-            }
-            if (!ok) continue;
-          }
-          atomicOr(&P.file_kw[(size_t)f * P.rs.kw_words + (pd.kw >> 5)], 1u << (pd.kw & 31));
-        }
-      }
-      p += w;
     }
   }
 }
@@ -1460,13 +1501,14 @@ __global__ __launch_bounds__(256) void k_expand(ExpandParams E) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= E.n_hits) return;
   const uint64_t h = E.hits[i];
-  const uint64_t gpos = h >> 16;
+  const bool fold = (h & kFoldHit) != 0;  // literal spelled with K / ſ (k_fold_windows)
+  const uint64_t gpos = (h & ~kFoldHit) >> 16;
   const uint32_t pid = (uint32_t)(h & 0xFFFF);
   const uint64_t rg = gpos / kNlBlock;
   const uint32_t fhi = rg + 1 < E.n_regions ? min(E.region_file[rg + 1] + 1, E.n_files) : E.n_files;
   const uint32_t fi = find_file(E.off, E.region_file[rg], fhi, gpos);
   const uint32_t fl = E.file_flags[fi];
-  if (fl & (kFileAllowed | kFileSpecial)) return;
+  if (fl & kFileAllowed) return;
   const PatDev pd = E.rs.ac.pats[pid];
   const uint32_t* kw = E.file_kw + (size_t)fi * E.rs.kw_words;
   const uint64_t fend = E.off[fi + 1] - 1;
@@ -1474,9 +1516,9 @@ __global__ __launch_bounds__(256) void k_expand(ExpandParams E) {
     const uint32_t r = E.rs.ac.pat_rules[pd.rule_off + k];
     if (E.path_mask && ((E.path_mask[(size_t)fi * E.rule_words + (r >> 5)] >> (r & 31)) & 1)) continue;
     const RuleDev& rd = E.rs.rules[r];
-    // the file holds no fold-special byte here (those take k_full_jobs), so an
-    // implied gate needs no keyword bit
-    if (!rd.gate_implied && !rule_gate(E.rs, rd, kw)) continue;
+    // an ASCII literal hit that holds a keyword proves the gate (gate_implied);
+    // a K/ſ spelling does not (ToLower(ſ) == ſ)
+    if ((fold || !rd.gate_implied) && !rule_gate(E.rs, rd, kw)) continue;
     if (!follow_accepts_dev(E.rs, rd, E.data, gpos, fend)) continue;
     emit_cand(E, r, gpos, fi);
   }
@@ -1489,16 +1531,6 @@ __global__ __launch_bounds__(256) void k_full_jobs(ExpandParams E) {
   if (fl & kFileAllowed) return;
   const uint32_t* kw = E.file_kw + (size_t)fi * E.rs.kw_words;
   const uint64_t fstart = E.off[fi];
-  if (fl & kFileSpecial) {
-    for (uint32_t r = 0; r < E.rs.n_rules; ++r) {
-      const RuleDev& rd = E.rs.rules[r];
-      if (rd.mode == MODE_NEVER) continue;
-      if (E.path_mask && ((E.path_mask[(size_t)fi * E.rule_words + (r >> 5)] >> (r & 31)) & 1)) continue;
-      if (!rule_gate(E.rs, rd, kw)) continue;
-      emit_cand(E, r, fstart, fi | kFullFlag);
-    }
-    return;
-  }
   for (uint32_t k = 0; k < E.n_full_rules; ++k) {
     const uint32_t r = E.full_rules[k];
     if (E.path_mask && ((E.path_mask[(size_t)fi * E.rule_words + (r >> 5)] >> (r & 31)) & 1)) continue;
@@ -2380,6 +2412,7 @@ struct DevImage {
   RuleSetDev view{};
   // offsets into u32
   uint32_t o_gpath = 0, n_gpath = 0, o_apoff = 0, o_ap = 0, o_full = 0, n_full = 0, o_prules = 0, n_prules = 0;
+  uint32_t o_fold = 0, n_fold_items = 0;  // k_fold_windows work items
   void release() {
     big.release();
     inst.release(); classes.release(); ranges.release(); progs.release(); rules.release();
@@ -2419,7 +2452,8 @@ struct tsg_engine {
   DBuf<FastEvent> ev_buf, ev_overflow;
   DBuf<uint64_t> vprof;
   DBuf<uint8_t> span_hi;
-  DBuf<uint32_t> special_files;
+  DBuf<uint64_t> fold_pos;    // fold-special rune occurrences (k_fold_windows)
+  uint64_t fold_need = 0;     // fold-position capacity learnt from a lost scan
   DBuf<uint4> caps;
   DBuf<uint32_t> ev_counts;
   uint64_t ev_ovf_need = 0;  // overflow-event capacity learnt from a lost scan
@@ -2630,6 +2664,23 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   im.n_prules = (uint32_t)path_rules.size();
   im.o_full = append(full_rules);
   im.n_full = (uint32_t)full_rules.size();
+  {
+    // k_fold_windows items: keywords a fold rune can spell (İ -> i, K -> k in
+    // bytes.ToLower) and anchor literals with a case-free k / s ((?i) K, ſ)
+    std::vector<uint32_t> fold;
+    for (size_t pi = 0; pi < rs->patterns.size(); ++pi) {
+      const PatternHost& p = rs->patterns[pi];
+      if (p.special) continue;
+      const bool gate = p.kw >= 0 && p.lower.find_first_of("ik") != std::string::npos;
+      bool hit = false;
+      if (!p.rules.empty())
+        for (size_t j = 0; j < p.lower.size(); ++j)
+          hit |= (p.lower[j] == 'k' || p.lower[j] == 's') && (!p.confirm || p.req[j] == 0);
+      if (gate || hit) fold.push_back((uint32_t)pi | (gate ? kFoldItemGate : 0u) | (hit ? kFoldItemHit : 0u));
+    }
+    im.o_fold = append(fold);
+    im.n_fold_items = (uint32_t)fold.size();
+  }
   HIP_TRY(im.u32.ensure(u32.size() + 1));
   if (!u32.empty()) HIP_TRY(hipMemcpy(im.u32.p, u32.data(), u32.size() * 4, hipMemcpyHostToDevice));
   HIP_TRY(im.rules.ensure(rules.size() + 1));
@@ -2970,7 +3021,7 @@ int read_ctrl(tsg_engine* e, Ctrl* h) {
 
 // Launch the AC pass: k_scan_fast when the automaton fits its LDS image,
 // else the generic kernel (transition table in LDS or, if too large, global).
-int launch_scan(tsg_engine* e, ScanParams P) {
+int launch_scan(tsg_engine* e, ScanParams& P) {
   hipStream_t s = e->stream;
   P.n_regions = P.nbytes / kNlBlock + 1;
   HIP_TRY(e->region_file.ensure(P.n_regions + 1));
@@ -3115,16 +3166,19 @@ int launch_scan(tsg_engine* e, ScanParams P) {
   return TSG_OK;
 }
 
-// Run the device pipeline on a batch already in HBM.  Fills r->impl.locs and flags.
-// Exact keyword gates of the files mark_special listed: one wave per file.
-int launch_special_gate(tsg_engine* e, const ScanParams& P, uint64_t n_special) {
-  if (!n_special) return TSG_OK;
-  const uint64_t waves = std::min<uint64_t>(std::min<uint64_t>(n_special, P.n_files), 16384);
-  hipLaunchKernelGGL(k_special_gate, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, e->stream, P);
+// Keywords / anchor literals spelled with fold-special runes, around each of
+// the n_fold occurrences the scan recorded (k_fold_windows).
+int launch_fold_windows(tsg_engine* e, const ScanParams& P, uint64_t n_fold, bool with_hits) {
+  const DevImage& im = e->img;
+  if (!n_fold || !im.n_fold_items) return TSG_OK;
+  const FoldItems F{im.u32.p + im.o_fold, im.n_fold_items, with_hits ? 1u : 0u};
+  const uint64_t threads = n_fold * F.n;
+  hipLaunchKernelGGL(k_fold_windows, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, e->stream, P, F, n_fold);
   HIP_TRY(hipGetLastError());
   return TSG_OK;
 }
 
+// Run the device pipeline on a batch already in HBM.  Fills r->impl.locs and flags.
 int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, const uint64_t* d_off,
                  const uint8_t* d_paths, const uint64_t* d_path_off, size_t n_files, uint64_t nbytes,
                  tsg_result* res) {
@@ -3215,14 +3269,16 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   P.hits = e->hits.p;
   P.hit_cap = hit_cap;
   P.ctrl = e->ctrl.p;
-  HIP_TRY(e->special_files.ensure(nf + 1));
-  P.special_files = e->special_files.p;
+  HIP_TRY(e->fold_pos.ensure(std::max<uint64_t>(1 << 16, e->fold_need)));
+  P.fold_pos = e->fold_pos.p;
+  P.fold_cap = e->fold_pos.n;
   if (const char* m = getenv("TSG_REPORT_MODE")) P.report_mode = (uint32_t)atoi(m);
   const uint64_t n_nlb = nbytes / kNlBlock + 2;
   HIP_TRY(e->nl_blocks.ensure(n_nlb));
   HIP_TRY(e->nl_pre.ensure(n_nlb));
   P.nl_blocks = e->nl_blocks.p;
-  for (int attempt = 0; attempt < 2 && nbytes; ++attempt) {
+  bool scanned = nbytes == 0;
+  for (int attempt = 0; attempt < 3 && !scanned; ++attempt) {
     HIP_TRY(hipMemsetAsync(e->nl_blocks.p, 0, n_nlb * 4, s));
     HIP_TRY(hipEventRecord(e->ev[8], s));
     if ((rc = launch_scan(e, P))) return rc;
@@ -3230,16 +3286,37 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     Ctrl c;
     if ((rc = read_ctrl(e, &c))) return rc;
     const bool ev_lost = rs->ac.fast.size() && c.ev_overflow > e->ev_overflow.n;
-    if (c.hits <= hit_cap && !ev_lost) {
-      if ((rc = launch_special_gate(e, P, c.n_special))) return rc;
-      break;
+    const bool fold_lost = c.n_fold > P.fold_cap;
+    if (c.hits <= hit_cap && !ev_lost && !fold_lost) {
+      if (!c.n_fold) {
+        scanned = true;
+        break;
+      }
+      if ((rc = launch_fold_windows(e, P, c.n_fold, true))) return rc;
+      if ((rc = read_ctrl(e, &c))) return rc;
+      if (c.hits <= hit_cap) {
+        scanned = true;
+        break;
+      }
     }
     // overflow: grow and rescan (keyword bits are idempotent)
     if (ev_lost) e->ev_ovf_need = c.ev_overflow + (c.ev_overflow >> 2);
-    HIP_TRY(e->hits.ensure(c.hits));
-    hit_cap = P.hit_cap = e->hits.n;
-    P.hits = e->hits.p;
-    HIP_TRY(hipMemsetAsync(e->ctrl.p, 0, offsetof(Ctrl, n_special), s));  // keep the special-file list
+    if (fold_lost) {
+      e->fold_need = c.n_fold + (c.n_fold >> 2);
+      HIP_TRY(e->fold_pos.ensure(e->fold_need));
+      P.fold_pos = e->fold_pos.p;
+      P.fold_cap = e->fold_pos.n;
+    }
+    if (c.hits > hit_cap) {
+      HIP_TRY(e->hits.ensure(c.hits + (c.hits >> 2)));
+      hit_cap = P.hit_cap = e->hits.n;
+      P.hits = e->hits.p;
+    }
+    HIP_TRY(hipMemsetAsync(e->ctrl.p, 0, offsetof(Ctrl, n_caps), s));
+  }
+  if (!scanned) {
+    set_last_error("internal: scan buffers still overflowed after regrowing them twice");
+    return TSG_ERR_INTERNAL;
   }
   HIP_TRY(hipEventRecord(e->ev[2], s));
   Ctrl c;
@@ -3609,7 +3686,7 @@ void tsg_engine_free(tsg_engine* e) {
   e->job_start.release(); e->nsel.release(); e->cub_tmp.release(); e->locs.release(); e->locs2.release();
   e->scratch.release(); e->ctrl.release(); e->excl_jobs.release(); e->excl_out.release();
   e->nl_blocks.release(); e->nl_pre.release(); e->tail.release(); e->region_file.release(); e->region_tmp.release();
-  e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->special_files.release(); e->caps.release(); e->vprof.release(); e->fflags8.release();
+  e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->fold_pos.release(); e->caps.release(); e->vprof.release(); e->fflags8.release();
   if (e->h_flags) (void)hipHostFree(e->h_flags);
   if (e->h_stage) (void)hipHostFree(e->h_stage);
   e->gate_out.release(); e->gate_rules.release(); e->bin8.release(); e->strip_out.release();
@@ -3934,23 +4011,37 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
   P.hits = e->hits.p;
   P.hit_cap = 0;  // prefilter only: hits are counted, not stored
   P.ctrl = e->ctrl.p;
-  HIP_TRY(e->special_files.ensure(nf + 1));
-  P.special_files = e->special_files.p;
+  HIP_TRY(e->fold_pos.ensure(std::max<uint64_t>(1 << 16, e->fold_need)));
+  P.fold_pos = e->fold_pos.p;
+  P.fold_cap = e->fold_pos.n;
   const uint64_t n_nlb = nbytes / kNlBlock + 2;
   HIP_TRY(e->nl_blocks.ensure(n_nlb));
   HIP_TRY(hipMemsetAsync(e->nl_blocks.p, 0, n_nlb * 4, s));
   P.nl_blocks = e->nl_blocks.p;
   HIP_TRY(hipEventRecord(e->ev[8], s));
-  for (int attempt = 0; attempt < 2 && nbytes; ++attempt) {
+  bool scanned = nbytes == 0;
+  for (int attempt = 0; attempt < 3 && !scanned; ++attempt) {
     if ((rc = launch_scan(e, P))) return rc;
     Ctrl c;
     if ((rc = read_ctrl(e, &c))) return rc;
-    if (!rs->ac.fast.size() || c.ev_overflow <= e->ev_overflow.n) {
-      if ((rc = launch_special_gate(e, P, c.n_special))) return rc;
+    const bool ev_lost = rs->ac.fast.size() && c.ev_overflow > e->ev_overflow.n;
+    if (!ev_lost && c.n_fold <= P.fold_cap) {
+      if ((rc = launch_fold_windows(e, P, c.n_fold, false))) return rc;
+      scanned = true;
       break;
     }
-    e->ev_ovf_need = c.ev_overflow + (c.ev_overflow >> 2);  // events were lost: grow and rescan
-    HIP_TRY(hipMemsetAsync(e->ctrl.p, 0, offsetof(Ctrl, n_special), s));  // keep the special-file list
+    if (ev_lost) e->ev_ovf_need = c.ev_overflow + (c.ev_overflow >> 2);  // events were lost: grow and rescan
+    if (c.n_fold > P.fold_cap) {
+      e->fold_need = c.n_fold + (c.n_fold >> 2);
+      HIP_TRY(e->fold_pos.ensure(e->fold_need));
+      P.fold_pos = e->fold_pos.p;
+      P.fold_cap = e->fold_pos.n;
+    }
+    HIP_TRY(hipMemsetAsync(e->ctrl.p, 0, offsetof(Ctrl, n_caps), s));
+  }
+  if (!scanned) {
+    set_last_error("internal: scan buffers still overflowed after regrowing them twice");
+    return TSG_ERR_INTERNAL;
   }
   if (e->events) HIP_TRY(hipEventRecord(e->ev[9], s));
   if (h_gates_out && nf && gate_words_per_file) {

@@ -20,6 +20,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -403,7 +404,15 @@ int tsg_layer_tar_walk(const uint8_t* tar, size_t len, const char* const* skip_f
         return err("unexpected EOF");
       }
       const uint8_t* h = tar + off;
-      if (zero_block(h)) break;  // end-of-archive marker
+      if (zero_block(h)) {
+        // archive/tar readHeader: a zero block must be followed by EOF or a
+        // second zero block; a zero block then a header is ErrHeader
+        const size_t nx = off + kBlock;
+        if (nx == len) break;                                  // io.EOF after one block
+        if (nx + kBlock > len) return err("unexpected EOF");   // partial second block
+        if (zero_block(tar + nx)) break;                       // normal end of archive
+        return err("archive/tar: invalid tar header");
+      }
       if (!checksum_ok(h)) return err("archive/tar: invalid tar header");
       int64_t size;
       if (!parse_numeric(h + 124, 12, &size) || size < 0) return err("archive/tar: invalid tar header");
@@ -573,9 +582,20 @@ int tsg_analyze_layer(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* tar, 
     if (nt <= 1) {
       work(0, ne);
     } else {
+      // a thread that cannot be started leaves its range to this thread; the
+      // started ones are always joined (no std::terminate on unwinding)
       std::vector<std::thread> ts;
       size_t per = (ne + nt - 1) / nt;
-      for (size_t t = 0; t < nt; t++) ts.emplace_back(work, std::min(ne, t * per), std::min(ne, (t + 1) * per));
+      size_t done_to = 0;
+      for (size_t t = 0; t < nt; t++) {
+        try {
+          ts.emplace_back(work, std::min(ne, t * per), std::min(ne, (t + 1) * per));
+          done_to = std::min(ne, (t + 1) * per);
+        } catch (const std::system_error&) {
+          break;
+        }
+      }
+      if (done_to < ne) work(done_to, ne);
       for (auto& t : ts) t.join();
     }
     for (size_t i = 0; i < ne; i++) {

@@ -7,6 +7,7 @@
 #include <cstring>
 #include <deque>
 #include <map>
+#include <memory>
 #include <mutex>
 
 #include "engine.h"
@@ -670,12 +671,13 @@ extern "C++" namespace tsg {
 bool host_allow_path(const tsg_ruleset* rs, const uint8_t* path, size_t len) {
   for (int r : rs->global_allow_path) {
     const gre::Prog& p = rs->regexes[r].c.prog;
-    thread_local HostVm* vm = nullptr;
+    // per-thread VM scratch, freed when the thread exits (tsg_analyze_layer's
+    // Required workers are short-lived threads)
+    thread_local std::unique_ptr<HostVm> vm;
     thread_local size_t vm_n = 0;
     if (!vm || vm_n < p.inst.size()) {
-      delete vm;
       vm_n = p.inst.size() + 64;
-      vm = new HostVm(vm_n);
+      vm.reset(new HostVm(vm_n));
     }
     uint32_t ms, me;
     if (gre::vm_search(view_of(p), path, (uint32_t)len, 0, (uint32_t)len, true, vm->sc, &ms, &me)) return true;

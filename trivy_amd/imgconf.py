@@ -7,10 +7,14 @@ The rendering restates encoding/json for the go-containerregistry
 ``v1.ConfigFile`` shape (a dependency absent from the reference tree): the
 top-level fields in struct order with their omitempty rules, ``created``
 always present (a zero ``v1.Time`` marshals as "0001-01-01T00:00:00Z"),
-``rootfs`` always present; nested objects are taken in the order the caller
-gives (Go struct order for ``config``) with empty values omitted, as every
-``v1.Config`` field is omitempty.  Parity is pinned by the reference's own
-test (tests/golden/imgconf_cases.json).
+``rootfs`` always present; ``config`` in ``v1.Config`` struct order (every
+field omitempty; keys the struct does not know follow in the caller's order),
+its map fields (Labels, Volumes, ExposedPorts) with keys sorted as
+encoding/json sorts map keys, and each ``history`` entry in ``v1.History``
+order (author, created, created_by, comment, empty_layer) with ``created``
+always present.  Parity is pinned by the reference's own test
+(tests/golden/imgconf_cases.json); the config/history ordering beyond it is
+restatement-derived (go-containerregistry v1 types, not in the reference tree).
 """
 from __future__ import annotations
 
@@ -21,6 +25,35 @@ from . import secret as S
 from .types import Secret
 
 _ZERO_TIME = "0001-01-01T00:00:00Z"
+# go-containerregistry pkg/v1 Config field order (all omitempty)
+_CONFIG_ORDER = ["AttachStderr", "AttachStdin", "AttachStdout", "Cmd", "Healthcheck", "Domainname", "Entrypoint",
+                 "Env", "Hostname", "Image", "Labels", "OnBuild", "OpenStdin", "StdinOnce", "Tty", "User", "Volumes",
+                 "WorkingDir", "ExposedPorts", "ArgsEscaped", "NetworkDisabled", "MacAddress", "StopSignal", "Shell"]
+_CONFIG_MAPS = {"Labels", "Volumes", "ExposedPorts"}
+_HISTORY_ORDER = ["author", "created", "created_by", "comment", "empty_layer"]
+
+
+def _go_config(c: dict) -> dict:
+    """v1.Config in struct order, empty fields omitted, map keys sorted."""
+    out = {}
+    for k in _CONFIG_ORDER + [k for k in c if k not in _CONFIG_ORDER]:
+        v = c.get(k)
+        if _empty(v):
+            continue
+        out[k] = {m: v[m] for m in sorted(v)} if k in _CONFIG_MAPS and isinstance(v, dict) else v
+    return out
+
+
+def _go_history(h: dict) -> dict:
+    """v1.History: `created` is a struct (never omitted), the rest omitempty."""
+    out = {}
+    for k in _HISTORY_ORDER:
+        v = h.get(k)
+        if k == "created":
+            out[k] = v or _ZERO_TIME
+        elif not _empty(v):
+            out[k] = v
+    return out
 
 
 def _empty(v: Any) -> bool:
@@ -70,12 +103,13 @@ def marshal_config_file(cfg: dict) -> bytes:
         if not _empty(cfg.get(k)):
             doc[k] = cfg[k]
     doc["created"] = cfg.get("created") or _ZERO_TIME
-    for k in ("docker_version", "history"):
-        if not _empty(cfg.get(k)):
-            doc[k] = cfg[k]
+    if not _empty(cfg.get("docker_version")):
+        doc["docker_version"] = cfg["docker_version"]
+    if not _empty(cfg.get("history")):
+        doc["history"] = [_go_history(h) for h in cfg["history"]]
     doc["os"] = cfg.get("os", "")
     doc["rootfs"] = {"type": rootfs.get("type", ""), "diff_ids": rootfs.get("diff_ids")}
-    doc["config"] = {k: v for k, v in (cfg.get("config") or {}).items() if not _empty(v)}
+    doc["config"] = _go_config(cfg.get("config") or {})
     for k in ("os.version", "variant", "os.features"):
         if not _empty(cfg.get(k)):
             doc[k] = cfg[k]

@@ -185,7 +185,11 @@ def _analyze_walked(analyzer, addr: int, n: int, w: _Walk) -> List[Secret]:
     finally:
         N.lib.tsg_result_free(res)
     secrets = [r for r in out if r is not None and r.Findings]
+    # AnalysisResult.Sort (analyzer.go:218-229): secrets by FilePath, then each
+    # secret's findings by (RuleID, StartLine) -- Scan left them by (RuleID, Match)
     secrets.sort(key=lambda s: s.FilePath)
+    for sec in secrets:
+        sec.Findings.sort(key=lambda f: (f.RuleID, f.StartLine))
     return secrets
 
 
