@@ -1190,11 +1190,12 @@ struct FoldItems {
   uint32_t with_hits;     // 0 for the prefilter-only pass (no anchor hits)
 };
 
-// Does pattern (lowered L, case requirement R or null, m bytes) occur at h,
-// spelled with fold runes?  gate: bytes.ToLower view (İ, K); else the (?i)
-// view (K, ſ on case-free positions).  *first = its first fold rune.
+// Does pattern (lowered L, case requirement R or null, m bytes) occur at h?
+// gate: the bytes.ToLower view (İ -> i, K -> k); else the (?i) view (K, ſ on
+// case-free k / s).  *first = its first fold rune (~0 when spelled in ASCII),
+// *end = the byte after it.
 __device__ inline bool fold_match(const uint8_t* d, uint64_t nbytes, uint64_t h, const uint8_t* L, const uint8_t* R,
-                                  uint32_t m, bool gate, uint64_t* first) {
+                                  uint32_t m, bool gate, uint64_t* first, uint64_t* end) {
   uint64_t t = h;
   *first = ~0ull;
   for (uint32_t i = 0; i < m; ++i) {
@@ -1215,7 +1216,16 @@ __device__ inline bool fold_match(const uint8_t* d, uint64_t nbytes, uint64_t h,
     if (!gate && R && R[i] && c != R[i]) return false;
     ++t;
   }
-  return *first != ~0ull;
+  *end = t;
+  return true;
+}
+
+// Width of the fold-special rune at t (İ, ſ: 2, K: 3), 0 if none.
+__device__ inline uint32_t fold_rune_at(const uint8_t* d, uint64_t nbytes, uint64_t t) {
+  const uint32_t c = d[t];
+  if (c == 0xE2) return t + 2 < nbytes && d[t + 1] == 0x84 && d[t + 2] == 0xAA ? 3 : 0;
+  if (c == 0xC4 || c == 0xC5) return t + 1 < nbytes && d[t + 1] == (c == 0xC4 ? 0xB0 : 0xBF) ? 2 : 0;
+  return 0;
 }
 
 __global__ __launch_bounds__(256) void k_fold_windows(ScanParams P, FoldItems F, uint64_t n_fold) {
@@ -1227,30 +1237,45 @@ __global__ __launch_bounds__(256) void k_fold_windows(ScanParams P, FoldItems F,
   const uint64_t q = rec >> 2;
   const uint32_t kind = (uint32_t)(rec & 3);
   const uint32_t pid = it & 0xFFFFu;
-  const bool want_gate = (it & kFoldItemGate) && kind != FOLD_S;
-  const bool want_hit = (it & kFoldItemHit) && F.with_hits && kind != FOLD_I;
-  if (!want_gate && !want_hit) return;
   const PatDev pd = ac.pats[pid];
+  const bool want_gate = (it & kFoldItemGate) && kind != FOLD_S;
+  // a literal spelled with K / ſ, or an ASCII literal whose scan-automaton
+  // extension (classes the rule requires next, follow_ext) meets the rune:
+  // the extended pattern cannot fire there, so the hit is made here
+  const bool want_hit = (it & kFoldItemHit) && F.with_hits && (kind != FOLD_I || pd.ext);
+  if (!want_gate && !want_hit) return;
   const uint8_t* L = ac.pat_bytes + pd.bytes_off;
   const uint8_t* R = pd.confirm ? ac.pat_bytes + pd.req_off : nullptr;
   const uint32_t m = pd.len;
   if (!m) return;
-  const uint64_t span = 3ull * (m - 1);
+  const uint64_t span = max(3ull * (m - 1), (uint64_t)m + 3ull * pd.ext);
   uint32_t fi = 0xFFFFFFFFu;
   for (uint64_t h = q > span ? q - span : 0; h <= q; ++h) {
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      const bool gate = g == 0;
-      if (gate ? !want_gate : !want_hit) continue;
-      uint64_t first;
-      if (!fold_match(P.data, P.nbytes, h, L, R, m, gate, &first) || first != q) continue;
-      if (gate) {
-        if (fi == 0xFFFFFFFFu) fi = file_of_pos(P, q);
-        atomicOr(&P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)], 1u << (pd.kw & 31));
-      } else {
-        const unsigned long long idx = atomicAdd(&P.ctrl->hits, 1ull);
-        if (idx < P.hit_cap) P.hits[idx] = kFoldHit | (h << 16) | pid;
+    uint64_t first, end;
+    if (want_gate && fold_match(P.data, P.nbytes, h, L, R, m, true, &first, &end) && first == q) {
+      if (fi == 0xFFFFFFFFu) fi = file_of_pos(P, q);
+      atomicOr(&P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)], 1u << (pd.kw & 31));
+    }
+    if (!want_hit || !fold_match(P.data, P.nbytes, h, L, R, m, false, &first, &end)) continue;
+    uint64_t rec_hit = ~0ull;
+    if (first != ~0ull) {
+      if (first == q && kind != FOLD_I) rec_hit = kFoldHit | (h << 16) | pid;  // k_expand gates it exactly
+    } else if (pd.ext) {
+      // ASCII literal: the first fold rune within its ext following characters
+      uint64_t t = end;
+      for (uint32_t j = 0; j < pd.ext && t < P.nbytes; ++j) {
+        const uint32_t w = fold_rune_at(P.data, P.nbytes, t);
+        if (w) {
+          if (t == q) rec_hit = (h << 16) | pid;  // an ordinary anchor hit (gate implied as usual)
+          break;
+        }
+        if (P.data[t] >= 0x80) break;
+        ++t;
       }
+    }
+    if (rec_hit != ~0ull) {
+      const unsigned long long idx = atomicAdd(&P.ctrl->hits, 1ull);
+      if (idx < P.hit_cap) P.hits[idx] = rec_hit;
     }
   }
 }
@@ -1647,6 +1672,17 @@ struct IvIter {
   }
 };
 
+// Exactly one permitted start: an anchored leftmost-first match at s.
+struct OneStart {
+  uint32_t s;
+  __device__ bool skip_to(uint32_t pos, uint32_t* np) {
+    if (pos > s) return false;
+    *np = s;
+    return true;
+  }
+  __device__ bool allowed(uint32_t pos) { return pos == s; }
+};
+
 struct LimitStarts {
   uint32_t limit;
   __device__ bool skip_to(uint32_t pos, uint32_t* np) {
@@ -1728,13 +1764,6 @@ typedef __attribute__((address_space(1))) const uint16_t gu16;
 template <typename T>
 __device__ inline T* as_global(const void* p) { return reinterpret_cast<T*>(reinterpret_cast<uintptr_t>(p)); }
 
-constexpr uint32_t kVerifyDfaLds = 48 * 1024;  // bytes of LDS for the block's verify DFA
-__shared__ __align__(16) uint16_t g_vdfa[kVerifyDfaLds / 2];  // k_verify's staged DFA table
-__shared__ __align__(16) uint8_t g_vcls[128];                 // and its class map
-
-// kLds: the rule's table / class map are the block's staged copy (g_vdfa,
-// g_vcls); else d.T / d.cls in global memory.
-template <bool kLds>
 __device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, uint32_t n, uint32_t s, uint32_t* me) {
   gu16* Tg = as_global<gu16>(d.T);
   gu8* cg = as_global<gu8>(d.cls);
@@ -1758,8 +1787,8 @@ __device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, uint
     for (int i = 0; i < 16; ++i) {
       if ((uint32_t)i >= m || !st) break;
       if (c[i] >= 0x80) return 2;  // runes / case folding: the Pike VM decides
-      const uint32_t k = kLds ? (uint32_t)g_vcls[c[i]] : (uint32_t)cg[c[i]];
-      const uint32_t e = kLds ? (uint32_t)g_vdfa[st * K + k] : (uint32_t)Tg[st * K + k];
+      const uint32_t k = cg[c[i]];
+      const uint32_t e = Tg[st * K + k];
       if (q0 + i + 1 == n) {
         if (e & 0x8000u) last = n;
         st = 0;
@@ -1780,25 +1809,25 @@ __device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, uint
 // spans of a match [ms, me) the DFA or VM already found.  Visited bits, job
 // stack and the tracked capture slots live in the lane's LDS arena; only the
 // SecretGroupName slots are tracked (captures never steer the search).
-// Returns false when the match does not fit the arena (the caller then runs
-// the Pike capture VM) — never a different answer.
+// Returns false when the match does not fit the arena (`words` LDS words; the
+// caller then defers it to a larger arena, or runs the Pike capture VM) —
+// never a different answer.
 constexpr uint32_t kVerifyThreads = 64;
-#ifndef TSG_BS_WORDS
-#define TSG_BS_WORDS 560
-#endif
-constexpr uint32_t kBsWords = TSG_BS_WORDS;  // LDS words per lane: 140 KiB per block
+constexpr uint32_t kBsWords = 560;        // k_verify: LDS words per lane (140 KiB per block)
+constexpr uint32_t kBigCapLanes = 4;      // k_captures_big: lanes per block
+constexpr uint32_t kBigBsWords = 9216;    // and their arenas (36 KiB: P x W <= 294 K (pc, pos) bits)
 
 __device__ bool bitstate_captures(const gre::ProgView& p, const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me,
-                                  const uint32_t* gnum, uint32_t ng, uint32_t* area, int32_t* gcap) {
+                                  const uint32_t* gnum, uint32_t ng, uint32_t* area, uint32_t words, int32_t* gcap) {
   const uint32_t P = p.ninst;
   const uint32_t end = me + 16 < n ? me + 16 : n;  // positions the search may visit: [ms, end]
   const uint32_t W = end - ms + 1;
   const uint32_t vis_words = (P * W + 31) / 32;
   // arena: visited bits | job stack | the 8 tracked capture slots (gcap, the last 8 words)
-  if (2 * ng > 8 || P >= 0x4000 || W >= 0xFFFF || vis_words + 8 + 32 > kBsWords) return false;
+  if (2 * ng > 8 || P >= 0x4000 || W >= 0xFFFF || vis_words + 8 + 32 > words) return false;
   uint32_t* vis = area;
   uint32_t* stk = area + vis_words;
-  const uint32_t stk_cap = kBsWords - 8 - vis_words;
+  const uint32_t stk_cap = words - 8 - vis_words;
   for (uint32_t i = 0; i < vis_words; ++i) vis[i] = 0;
   for (uint32_t k = 0; k < 2 * ng; ++k) gcap[k] = -1;
   auto local = [&](uint32_t slot) -> int {  // tracked index of capture slot, or -1
@@ -1865,19 +1894,25 @@ __device__ bool bitstate_captures(const gre::ProgView& p, const uint8_t* text, u
 }
 
 // Secret-group spans of one kept match (getMatchSubgroupsLocations,
-// scanner.go:150-163): bit-state backtracker in the lane's LDS arena, the
-// capture VM when the match does not fit it.
+// scanner.go:150-163): bit-state backtracker in the lane's LDS arena; a match
+// too long for it is deferred to k_captures_big (`defer`), whose arenas are
+// 16x larger, and only past those does the capture VM run.
 __device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t rule, uint32_t fi,
                             const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me, gre::VmScratch& sc,
-                            uint32_t* bs_area) {
+                            uint32_t* bs_area, uint32_t words, bool defer) {
   const gre::ProgView& pv = V.rs.progs[rd.prog];
   const uint32_t* gnum = V.rs.group_slots + rd.group_off;
-  int32_t* gcap = (int32_t*)(bs_area + kBsWords - 8);  // tracked slots (the arena's last 8 words)
+  int32_t* gcap = (int32_t*)(bs_area + words - 8);  // tracked slots (the arena's last 8 words)
   const uint64_t tb0 = V.dbg ? clock64() : 0;
-  const bool bs_ok = bitstate_captures(pv, text, n, ms, me, gnum, rd.group_n, bs_area, gcap);
+  const bool bs_ok = bitstate_captures(pv, text, n, ms, me, gnum, rd.group_n, bs_area, words, gcap);
   if (V.dbg) {
     atomicAdd((unsigned long long*)&V.dbg[2], bs_ok ? 1ull : 0ull);
     atomicAdd((unsigned long long*)&V.dbg[3], (unsigned long long)(clock64() - tb0));
+  }
+  if (!bs_ok && defer) {
+    const unsigned long long idx = atomicAdd(&V.ctrl->n_caps, 1ull);
+    if (idx < V.cap_cap) V.caps[idx] = make_uint4(fi, rule, ms, me);
+    return;
   }
   if (bs_ok) {
     for (uint32_t g = 0; g < rd.group_n; ++g) {
@@ -1910,9 +1945,7 @@ __device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t r
 }
 
 // A match k_verify found: allow rules, then the whole-match location or, for
-// rules with a secret group, a capture job for k_captures (the bit-state
-// arenas need ~140 KiB of LDS per wave, which would cap k_verify at one wave
-// per CU; split off, the match search runs at full occupancy).
+// rules with a secret group, its group spans.
 __device__ void emit_match(const VerifyParams& V, const RuleDev& rd, uint32_t rule, uint32_t fi,
                            const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me, gre::VmScratch& sc,
                            uint32_t* bs_area) {
@@ -1926,17 +1959,14 @@ __device__ void emit_match(const VerifyParams& V, const RuleDev& rd, uint32_t ru
     if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, ms, me, 0, 0, 0, 0};
     return;
   }
-  if (bs_area) {  // combined shape: resolve the groups here
-    emit_groups(V, rd, rule, fi, text, n, ms, me, sc, bs_area);
-    return;
-  }
-  unsigned long long idx = atomicAdd(&V.ctrl->n_caps, 1ull);
-  if (idx < V.cap_cap) V.caps[idx] = make_uint4(fi, rule, ms, me);
+  emit_groups(V, rd, rule, fi, text, n, ms, me, sc, bs_area, kBsWords, true);
 }
 
-__global__ __launch_bounds__(kVerifyThreads) void k_captures(VerifyParams V, uint32_t n_caps) {
-  __shared__ uint32_t bs_lds[kVerifyThreads * kBsWords];
-  uint32_t* bs_area = bs_lds + threadIdx.x * kBsWords;
+// Secret groups of the matches too long for k_verify's arenas (private keys,
+// long tokens): kBigCapLanes lanes per block, 36 KiB of LDS each.
+__global__ __launch_bounds__(kBigCapLanes) void k_captures_big(VerifyParams V, uint32_t n_caps) {
+  __shared__ uint32_t bs_lds[kBigCapLanes * kBigBsWords];
+  uint32_t* bs_area = bs_lds + threadIdx.x * kBigBsWords;
   const uint32_t nthreads = gridDim.x * blockDim.x;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   gre::VmScratch sc = make_scratch(V.scratch + (uint64_t)t * V.scratch_stride, V.rs);
@@ -1945,7 +1975,7 @@ __global__ __launch_bounds__(kVerifyThreads) void k_captures(VerifyParams V, uin
     const RuleDev rd = V.rs.rules[c.y];
     const uint64_t fstart = V.off[c.x];
     const uint32_t n = (uint32_t)(V.off[c.x + 1] - 1 - fstart);
-    emit_groups(V, rd, c.y, c.x, V.data + fstart, n, c.z, c.w, sc, bs_area);
+    emit_groups(V, rd, c.y, c.x, V.data + fstart, n, c.z, c.w, sc, bs_area, kBigBsWords, false);
   }
 }
 
@@ -1973,36 +2003,15 @@ __global__ __launch_bounds__(256) void k_warm(WarmRanges R, uint32_t* sink) {
   if (acc == 0x5EED1234u) sink[0] = acc;  // keeps the loads alive
 }
 
-constexpr uint32_t kVerifyBlock = 256;
-
-// kInline: one wave per block with the bit-state arenas in LDS, groups
-// resolved in place (default); else (TSG_VERIFY_SPLIT) the search runs at
-// full occupancy and defers group captures to k_captures.
-template <bool kInline>
-__global__ __launch_bounds__(kInline ? kVerifyThreads : kVerifyBlock) void k_verify(VerifyParams V) {
-  uint32_t* bs_area = nullptr;
-  if constexpr (kInline) {
-    __shared__ uint32_t bs_lds[kVerifyThreads * kBsWords];
-    bs_area = bs_lds + threadIdx.x * kBsWords;
-  }
+// One wave per block with the bit-state arenas in LDS: secret groups are
+// resolved in place (measured: 0.67 ms at 50 GB vs 0.48 + 0.21 ms with a
+// full-occupancy search and the groups in a kernel of their own).
+__global__ __launch_bounds__(kVerifyThreads) void k_verify(VerifyParams V) {
+  __shared__ uint32_t bs_lds[kVerifyThreads * kBsWords];
+  uint32_t* bs_area = bs_lds + threadIdx.x * kBsWords;
   const uint32_t nthreads = gridDim.x * blockDim.x;
   gre::VmScratch sc = make_scratch(V.scratch + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * V.scratch_stride, V.rs);
-  // block-uniform loop: jobs are sorted by rule, so the block's first job's
-  // rule is (nearly) every lane's; its verify DFA goes to LDS when it fits,
-  // turning each dependent step's L2 round trip into an LDS read
-  for (uint32_t base = blockIdx.x * blockDim.x; base < V.n_jobs; base += nthreads) {
-    const uint32_t r0 = (uint32_t)(V.keys[V.job_start[base]] >> kPosBits);
-    const RuleDev& rd0 = V.rs.rules[r0];
-    const bool stage = !kInline && rd0.dfa_off != kNoFollow && rd0.dfa_size * 2 <= kVerifyDfaLds;
-    __syncthreads();  // previous iteration's readers are done
-    if constexpr (!kInline) if (stage) {
-      const uint16_t* src = V.rs.dfa_delta + rd0.dfa_off;
-      for (uint32_t i = threadIdx.x; i < rd0.dfa_size; i += blockDim.x) g_vdfa[i] = src[i];
-      if (threadIdx.x < 128) g_vcls[threadIdx.x] = V.rs.dfa_bytes[rd0.dfa_cls_off + threadIdx.x];
-    }
-    __syncthreads();
-    const uint32_t j = base + threadIdx.x;
-    if (j >= V.n_jobs) continue;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < V.n_jobs; j += nthreads) {
     const uint64_t t0 = V.prof ? clock64() : 0;
     const uint64_t c0 = V.job_start[j];
     const uint64_t c1 = (j + 1 < V.n_jobs) ? V.job_start[j + 1] : V.n_cands;
@@ -2023,7 +2032,6 @@ __global__ __launch_bounds__(kInline ? kVerifyThreads : kVerifyBlock) void k_ver
     for (uint64_t c = c0; c < c1 && !full; ++c) full = (V.vals[c] & kFullFlag) != 0;
     if (full) pg.nc |= 1u << 31;
     const RuleDev rd = V.rs.rules[rule];
-    const bool in_lds = stage && rule == r0;
     const gre::ProgView& pv = V.rs.progs[rd.prog];
     const uint64_t fstart = V.off[fi];
     const uint8_t* text = V.data + fstart;
@@ -2068,10 +2076,9 @@ __global__ __launch_bounds__(kInline ? kVerifyThreads : kVerifyBlock) void k_ver
                           rd.dfa_start1, rd.dfa_smatch};
         const uint32_t fm0 = rd.dfa_first[0], fm1 = rd.dfa_first[1], fm2 = rd.dfa_first[2], fm3 = rd.dfa_first[3];
         // FindAll over the permitted starts with the verify DFA: the first
-        // start (>= pos) that matches is Go's leftmost match; a byte >= 0x80
-        // hands the rest of the job to the Pike VM below
-        bool vm = false;
-        while (it.have && !vm) {
+        // start (>= pos) that matches is Go's leftmost match; a start the DFA
+        // cannot decide (byte >= 0x80) is decided by the Pike VM
+        while (it.have) {
           bool found = false;
           uint32_t s0 = it.cs > pos ? it.cs : pos;
           for (uint32_t sp = s0; sp <= it.ce && sp < n; ++sp) {
@@ -2082,9 +2089,7 @@ __global__ __launch_bounds__(kInline ? kVerifyThreads : kVerifyBlock) void k_ver
               if (c0 < 0x80 && !((fw >> (c0 & 31)) & 1)) continue;
             }
             const uint64_t td0 = V.dbg ? clock64() : 0;
-            int r;
-            if constexpr (kInline) r = dfa_anchored_dev<false>(dref, text, n, sp, &me);
-            else r = in_lds ? dfa_anchored_dev<true>(dref, text, n, sp, &me) : dfa_anchored_dev<false>(dref, text, n, sp, &me);
+            int r = dfa_anchored_dev(dref, text, n, sp, &me);
             if (V.dbg) {
               atomicAdd((unsigned long long*)&V.dbg[0], 1ull);
               atomicAdd((unsigned long long*)&V.dbg[1], (unsigned long long)(clock64() - td0));
@@ -2094,8 +2099,12 @@ __global__ __launch_bounds__(kInline ? kVerifyThreads : kVerifyBlock) void k_ver
               if (rule < 64) atomicAdd((unsigned long long*)&V.dbg[13], 0ull);
             }
             if (r == 2) {
-              vm = true;
-              break;
+              // a byte >= 0x80 before the DFA decided: the Pike VM decides this
+              // start alone (anchored at sp, same leftmost-first end), and the
+              // DFA goes on with the next starts -- one rune no longer sends
+              // every later window of the job to the VM
+              OneStart one{sp};
+              r = vm_search_starts(pv, text, n, sp, one, sc, &ms, &me) ? 1 : 0;
             }
             if (r == 1) {
               emit_match(V, rd, rule, fi, text, n, sp, me, sc, bs_area);
@@ -2104,11 +2113,10 @@ __global__ __launch_bounds__(kInline ? kVerifyThreads : kVerifyBlock) void k_ver
               break;
             }
           }
-          if (vm) break;
           if (!found) it.advance();
           else while (it.have && it.ce < pos) it.advance();
         }
-        if (!vm) continue;
+        continue;
       }
       while (it.have) {
         const uint64_t ts0 = V.dbg ? clock64() : 0;
@@ -2633,7 +2641,7 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
       d.group_n = (uint32_t)group_slots.size() - d.group_off;
     }
     d.gate_implied = r.gate_implied;  // ruleset.cpp: every anchor literal contains a keyword
-    if (!d.gate_implied)
+    if (!d.gate_implied || r.fold_gate)  // exact keyword bits: non-implied gates, K/ſ-spelled hits
       for (auto& kw : r.keywords)
         if (!kw.empty()) kw_needed_ids.insert(kwid[kw]);
     d.allow_off = (uint32_t)allow_progs.size();
@@ -2672,7 +2680,7 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
       const PatternHost& p = rs->patterns[pi];
       if (p.special) continue;
       const bool gate = p.kw >= 0 && p.lower.find_first_of("ik") != std::string::npos;
-      bool hit = false;
+      bool hit = !p.rules.empty() && !rs->ac.fast.empty() && rs->ac.fast_ext[pi] > 0;
       if (!p.rules.empty())
         for (size_t j = 0; j < p.lower.size(); ++j)
           hit |= (p.lower[j] == 'k' || p.lower[j] == 's') && (!p.confirm || p.req[j] == 0);
@@ -3363,6 +3371,10 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     if ((rc = read_ctrl(e, &c))) return rc;
     n_cands = c.cands;
     if (n_cands <= E.cand_cap) break;
+    if (attempt == 2) {
+      set_last_error("internal: candidate buffers still overflowed after regrowing them");
+      return TSG_ERR_INTERNAL;
+    }
     cand_cap = n_cands;
   }
   HIP_TRY(hipEventRecord(e->ev[3], s));
@@ -3399,7 +3411,8 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   uint64_t loc_cap = std::max<uint64_t>(1 << 16, n_jobs);
   uint64_t caps_cap = std::max<uint64_t>(1 << 14, n_jobs / 4);
   uint64_t n_locs = 0;
-  for (int attempt = 0; attempt < 4 && n_jobs; ++attempt) {
+  bool verified = n_jobs == 0;
+  for (int attempt = 0; attempt < 4 && !verified; ++attempt) {
     HIP_TRY(e->locs.ensure(loc_cap));
     HIP_TRY(e->caps.ensure(caps_cap));
     HIP_TRY(hipMemsetAsync(&e->ctrl.p->locs, 0, 8, s));
@@ -3447,13 +3460,9 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
       hipLaunchKernelGGL(k_warm, dim3(8 * kWarmParts), dim3(256), 0, s, W, (uint32_t*)e->nsel.p);
       HIP_TRY(hipGetLastError());
     }
-    // default: one kernel (measured 0.67 ms vs 0.48 + 0.21 ms split at 50 GB);
-    // TSG_VERIFY_SPLIT=1 runs the full-occupancy search + k_captures instead
-    static const bool inl = getenv("TSG_VERIFY_SPLIT") == nullptr;
-    const uint32_t vb = inl ? kVerifyThreads : kVerifyBlock;
-    uint32_t blocks = std::min<uint32_t>((n_jobs + vb - 1) / vb, e->vm_threads / vb);
-    if (inl) hipLaunchKernelGGL(k_verify<true>, dim3(std::max(1u, blocks)), dim3(vb), 0, s, V);
-    else hipLaunchKernelGGL(k_verify<false>, dim3(std::max(1u, blocks)), dim3(vb), 0, s, V);
+    const uint32_t blocks = std::min<uint32_t>((n_jobs + kVerifyThreads - 1) / kVerifyThreads,
+                                               e->vm_threads / kVerifyThreads);
+    hipLaunchKernelGGL(k_verify, dim3(std::max(1u, blocks)), dim3(kVerifyThreads), 0, s, V);
     HIP_TRY(hipGetLastError());
     if ((rc = read_ctrl(e, &c))) return rc;
     if (c.n_caps > e->caps.n) {  // capture list overflow: grow and re-run the search
@@ -3461,10 +3470,11 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
       continue;
     }
     if (c.n_caps) {
-      // one wave per block: each block's LDS holds its lanes' bit-state arenas
-      const uint32_t cb = std::min<uint32_t>((uint32_t)((c.n_caps + kVerifyThreads - 1) / kVerifyThreads),
-                                             e->vm_threads / kVerifyThreads);
-      hipLaunchKernelGGL(k_captures, dim3(std::max(1u, cb)), dim3(kVerifyThreads), 0, s, V, (uint32_t)c.n_caps);
+      // matches too long for k_verify's arenas: kBigCapLanes lanes per block
+      const uint32_t cb = std::min<uint32_t>((uint32_t)((c.n_caps + kBigCapLanes - 1) / kBigCapLanes),
+                                             e->vm_threads / kBigCapLanes);
+      hipLaunchKernelGGL(k_captures_big, dim3(std::max(1u, cb)), dim3(kBigCapLanes), 0, s, V, (uint32_t)c.n_caps);
+      HIP_TRY(hipGetLastError());
     }
     if (prof) {
       std::vector<uint64_t> hp(2ull * n_jobs + 16);
@@ -3495,8 +3505,15 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(hipGetLastError());
     if ((rc = read_ctrl(e, &c))) return rc;
     n_locs = c.locs;
-    if (n_locs <= e->locs.n) break;
+    if (n_locs <= e->locs.n) {
+      verified = true;
+      break;
+    }
     loc_cap = n_locs;
+  }
+  if (!verified) {
+    set_last_error("internal: location buffers still overflowed after regrowing them");
+    return TSG_ERR_INTERNAL;
   }
   if (c.err) {
     set_last_error("internal: capture re-run disagreed with the whole-match run");
@@ -3537,6 +3554,10 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
         HIP_TRY(hipGetLastError());
         if ((rc = read_ctrl(e, &c))) return rc;
         if (c.excl <= e->excl_out.n) break;
+        if (attempt == 2) {
+          set_last_error("internal: exclude-block buffers still overflowed after regrowing them");
+          return TSG_ERR_INTERNAL;
+        }
         cap = c.excl;
       }
       ranges.resize(c.excl);

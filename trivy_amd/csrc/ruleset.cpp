@@ -466,6 +466,10 @@ int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_r
         }
         r.gate_implied = all;
       }
+      if (r.mode == MODE_ANCHORED)
+        for (auto& l : c.anchor.lits)
+          for (size_t j = 0; j < l.lower.size(); ++j)
+            r.fold_gate |= (l.lower[j] == 'k' || l.lower[j] == 's') && l.req[j] == 0;
     }
     for (auto& kw : r.keywords) {
       if (!kwid.count(kw) && !kw.empty()) {
@@ -515,7 +519,7 @@ int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_r
   {
     std::vector<uint8_t> kw_needed(rs->keywords.size(), 0);
     for (auto& r : rs->rules)
-      if (!r.gate_implied)
+      if (!r.gate_implied || r.fold_gate)  // the same set engine.hip marks kw_needed
         for (auto& kw : r.keywords)
           for (size_t k = 0; k < rs->keywords.size(); ++k)
             if (!kw.empty() && rs->keywords[k] == kw) kw_needed[k] = 1;
