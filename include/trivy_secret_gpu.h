@@ -29,7 +29,7 @@ extern "C" {
 #define TSG_ERR_REGEX 2       /* "regexp compile error" (scanner.go:77) */
 #define TSG_ERR_DEVICE 3      /* HIP runtime failure */
 #define TSG_ERR_NO_DEVICE 4   /* no MI355X visible: the product path does not fall back to CPU */
-#define TSG_ERR_UNSUPPORTED 5 /* rule feature outside this engine's coverage (e.g. \p{..}) */
+#define TSG_ERR_UNSUPPORTED 5 /* rule feature outside this engine's coverage (e.g. a non-ASCII keyword) */
 #define TSG_ERR_INTERNAL 6
 #define TSG_ERR_PANIC 7       /* input on which the Go reference panics (secret group did not participate) */
 

@@ -41,6 +41,8 @@ import numpy as np
 import regex as _re
 import yaml
 
+from oracle import go_unicode as _go_unicode
+
 # --------------------------------------------------------------------------- #
 # Go RE2 syntax -> python `regex` translation
 # --------------------------------------------------------------------------- #
@@ -165,19 +167,29 @@ class _Translator:
             if nxt in ("*", "+", "?") or (nxt == "{" and _re.match(r"\{(\d+)(,(\d*))?\}", self.p[self.i:])):
                 raise GoSyntaxError("invalid nested repetition operator")
 
-    def wrap(self, s, flags):
+    def wrap(self, s, flags, cls=False):
         if not flags["i"]:
             return s
-        # Go's simple folding keeps U+0130/U+0131 out of the i/I orbit;
-        # python's (?i) folds them in, so exclude them explicitly.
+        # Go's simple folding keeps U+0130/U+0131 out of the i/I orbit (each
+        # is its own orbit); the `regex` module relates them to i / I, so they
+        # never reach its (?i): a class decides them case-sensitively, a
+        # folded literal (never one of them, see fold_lit) not at all.
+        if cls:
+            return "(?:(?=[\\u0130\\u0131])%s|(?![\\u0130\\u0131])(?i:%s))" % (s, s)
         return "(?:(?![\\u0130\\u0131])(?i:%s))" % s
+
+    def fold_lit(self, ch, flags):
+        """A literal rune under the current flags (U+0130/U+0131 fold to themselves only)."""
+        if ch in "\u0130\u0131":
+            return _esc_char(ch)
+        return self.wrap(_esc_char(ch), flags)
 
     def atom(self, flags):
         c = self.peek()
         if c == "(":
             return self.group(flags)
         if c == "[":
-            return self.wrap(self.char_class(flags), flags)
+            return self.char_class(flags)
         if c == ".":
             self.i += 1
             return "(?s:.)" if flags["s"] else "[^\\n]"
@@ -192,7 +204,7 @@ class _Translator:
         if c == "\\":
             return self.escape(flags)
         self.i += 1
-        return self.wrap(_esc_char(c), flags)
+        return self.fold_lit(c, flags)
 
     def group(self, flags):
         self.i += 1  # (
@@ -234,12 +246,12 @@ class _Translator:
             raise GoSyntaxError("trailing backslash")
         self.i += 1
         perl = {"d": "0-9", "w": _WORD, "s": _SPACE}
-        if c in perl:
-            return perl[c] if in_class else "[%s]" % perl[c]
+        if c in perl:  # Go folds the group under (?i): (?i)\\w holds U+017F and U+212A
+            return perl[c] if in_class else self.wrap("[%s]" % perl[c], flags, cls=True)
         if c in "DWS":
             if in_class:
                 raise GoSyntaxError("negated perl class inside class unsupported by oracle")
-            return "[^%s]" % perl[c.lower()]
+            return self.wrap("[^%s]" % perl[c.lower()], flags, cls=True)
         if not in_class:
             if c == "b":
                 return "(?:(?<=[%s])(?![%s])|(?<![%s])(?=[%s]))" % ((_WORD,) * 4)
@@ -257,21 +269,39 @@ class _Translator:
                 # repetition binds to the last rune only.
                 if not lit:
                     return None
-                self.pending = "".join(self.wrap(_esc_char(ch), flags) for ch in lit[:-1])
-                return self.wrap(_esc_char(lit[-1]), flags)
+                self.pending = "".join(self.fold_lit(ch, flags) for ch in lit[:-1])
+                return self.fold_lit(lit[-1], flags)
         if c in "pP":
+            # parse.go parseUnicodeClass: the set is explicit (Go's tables and
+            # fold closure, oracle/go_unicode.py), so it needs no (?i) wrap
+            start = self.i - 2
             if self.peek() == "{":
-                end = self.p.index("}", self.i)
+                end = self.p.find("}", self.i)
+                if end < 0:
+                    raise GoSyntaxError("invalid character class range: `%s`" % self.p[start:])
                 name = self.p[self.i + 1:end]
                 self.i = end + 1
             else:
                 name = self.peek()
-                self.i += 1
+                self.i += len(name)
             neg = c == "P"
             if name.startswith("^"):
                 name, neg = name[1:], not neg
-            s = "\\%s{%s}" % ("P" if neg else "p", name)
-            return s if in_class else s
+            rs = _go_unicode.go_class(name, neg, flags["i"])
+            if rs is None:
+                raise GoSyntaxError("invalid character class range: `%s`" % self.p[start:self.i])
+            # the text's invalid bytes are U+DC80..U+DCFF here (see _decode) and
+            # U+FFFD in Go; no valid UTF-8 decodes to a surrogate
+            cut = []
+            for lo, hi in rs:
+                if lo < 0xD800:
+                    cut.append((lo, min(hi, 0xD7FF)))
+                if hi > 0xDFFF:
+                    cut.append((max(lo, 0xE000), hi))
+            if any(lo <= 0xFFFD <= hi for lo, hi in rs):
+                cut.append((0xDC80, 0xDCFF))
+            body = "".join("\\U%08x-\\U%08x" % (lo, hi) for lo, hi in cut)
+            return ("p", body) if in_class else ("[%s]" % body if body else "(?!)")
         simple = {"a": 7, "f": 12, "t": 9, "n": 10, "r": 13, "v": 11}
         if c in simple:
             ch = chr(simple[c])
@@ -295,15 +325,19 @@ class _Translator:
             ch = c
         else:
             raise GoSyntaxError("invalid escape \\" + c)
-        return _esc_char(ch) if in_class else self.wrap(_esc_char(ch), flags)
+        return _esc_char(ch) if in_class else self.fold_lit(ch, flags)
 
     def char_class(self, flags):
+        """A bracket class, (?i)-wrapped here: the \\p members (already Go's
+        folded sets) stay outside the wrap, whose U+0130/U+0131 exclusion is
+        for folded literals only."""
         self.i += 1
         neg = False
         if self.peek() == "^":
             neg = True
             self.i += 1
         items = []
+        pitems = []
         first = True
         while True:
             c = self.peek()
@@ -326,7 +360,10 @@ class _Translator:
             if lo is None:
                 continue
             if isinstance(lo, tuple):  # a perl class expansion
-                items.append(lo[0])
+                if isinstance(lo[0], tuple):  # \\p{..}: an explicit set
+                    pitems.append(lo[0][1])
+                else:
+                    items.append(lo[0])
                 continue
             if self.peek() == "-" and self.peek(1) not in ("]", ""):
                 self.i += 1
@@ -338,7 +375,15 @@ class _Translator:
                 items.append("%s-%s" % (_esc_char(lo), _esc_char(hi)))
             else:
                 items.append(_esc_char(lo))
-        return "[%s%s]" % ("^" if neg else "", "".join(items))
+        if not pitems:
+            return self.wrap("[%s%s]" % ("^" if neg else "", "".join(items)), flags, cls=True)
+        pset = "".join(pitems)
+        if not items:
+            return "[%s%s]" % ("^" if neg else "", pset) if pset else ("(?s:.)" if neg else "(?!)")
+        if neg:  # neither a \\p member nor a (folded) literal member
+            return "(?:%s%s)" % ("(?![%s])" % pset if pset else "",
+                                 self.wrap("[^%s]" % "".join(items), flags, cls=True))
+        return "(?:%s%s)" % ("[%s]|" % pset if pset else "", self.wrap("[%s]" % "".join(items), flags, cls=True))
 
     def _class_char(self, flags):
         c = self.peek()

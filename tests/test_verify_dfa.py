@@ -83,3 +83,74 @@ def test_verify_dfa_priorities(pat, text):
     if ns.value == 0:
         pytest.skip("no DFA for this pattern (VM path)")
     assert _dfa_find_all(rs, 0, text) == N.regex_find_all(pat, text)
+
+
+def _rune_starts(t: bytes):
+    """Byte offsets where utf8.DecodeRune starts a rune (invalid byte = width 1)."""
+    s = t.decode("utf-8", "surrogateescape")
+    out, b = [], 0
+    for ch in s:
+        out.append(b)
+        cp = ord(ch)
+        b += 1 if (0xDC80 <= cp <= 0xDCFF or cp < 0x80) else 2 if cp < 0x800 else 3 if cp < 0x10000 else 4
+    return out
+
+
+def _dfa_find_all_runes(rs, i, t):
+    """FindAllIndex from the DFA over rune starts; None if some start is left to the VM."""
+    res, me, ns = ctypes.c_int(), ctypes.c_size_t(), ctypes.c_uint32()
+    starts = _rune_starts(t)
+    out, pos = [], 0
+    while True:
+        hit = None
+        for s in starts:
+            if s < pos:
+                continue
+            N.check(N.lib.tsg_ruleset_dfa_check(rs, i, t, len(t), s, ctypes.byref(res), ctypes.byref(me), ctypes.byref(ns)))
+            if res.value == 2:
+                return None
+            if res.value == 1:
+                hit = (s, me.value)
+                break
+        if hit is None:
+            return out
+        out.append(list(hit))
+        pos = hit[1]
+
+
+def test_verify_dfa_rune_symbols_equal_vm():
+    """Non-ASCII text: the DFA's rune symbols (K, ſ, İ, U+FFFD, other runes)
+    give the VM's matches, for every builtin rule whose classes treat other
+    non-ASCII runes alike (the device leaves the rest to the VM)."""
+    rng = random.Random(17)
+    tpl = corpus_gen.secret_instances(rng)
+    fold = {"k": "K", "K": "K", "s": "ſ", "S": "ſ", "i": "İ"}
+    texts = []
+    for _ in range(120):
+        parts = []
+        for _ in range(3):
+            x = tpl[rng.randrange(len(tpl))]()
+            x = "".join(fold[c] if c in fold and rng.random() < 0.3 else c for c in x)
+            parts.append(x)
+        t = rng.choice([" é ", "\n", "'ſ'", " ÿ "]).join(parts).encode()
+        if rng.random() < 0.3:
+            p = rng.randrange(len(t) + 1)
+            t = t[:p] + bytes([rng.randint(0x80, 0xFF)]) + t[p:]
+        texts.append(t)
+    sc = S.new_scanner(None)
+    rs = sc._rs.handle
+    res, me, ns = ctypes.c_int(), ctypes.c_size_t(), ctypes.c_uint32()
+    decided = total = 0
+    for i, r in enumerate(sc.rules):
+        N.check(N.lib.tsg_ruleset_dfa_check(rs, i, b"x", 1, 0, ctypes.byref(res), ctypes.byref(me), ctypes.byref(ns)))
+        if ns.value == 0:
+            continue
+        for t in texts:
+            got = _dfa_find_all_runes(rs, i, t)
+            if got is None:
+                continue
+            want = N.regex_find_all(r.regex, t)
+            assert got == want, (r.id, t[:160])
+            decided += 1
+            total += len(want)
+    assert decided > 5000 and total > 100

@@ -28,6 +28,7 @@ constexpr uint32_t kFollowDepth = 96;        // bytes a candidate filter reads p
 constexpr uint32_t kNoFollow = 0xFFFFFFFFu;
 constexpr uint32_t kDfaMaxStates = 4096;     // verify-DFA budget per rule (else the Pike VM)
 constexpr uint32_t kDfaStateMask = 0x3FFF;  // verify-DFA entry: bit15 end-match, bit14 match state
+constexpr uint32_t kDfaRuneSyms = 5;        // verify-DFA rune symbols: K, ſ, İ, U+FFFD, other non-ASCII
 
 enum RuleMode : uint8_t { MODE_NEVER = 0, MODE_ANCHORED = 1, MODE_FULL = 2 };
 
@@ -54,6 +55,7 @@ struct RuleDev {
   uint32_t dfa_first[4];        // ASCII bytes on which a start state does not die (k_verify start skip)
   uint32_t dfa_size;            // u16 entries of its table (k_verify stages it in LDS when it fits)
   uint32_t dfa_smatch;          // bit 0/1: start0/start1 is a match state
+  uint32_t dfa_sym;             // first rune-symbol column | 0x80000000 when other non-ASCII runes are one symbol
 };
 
 struct PatDev {
@@ -92,7 +94,9 @@ struct AcDev {
   uint32_t rep_bytes, o_out_off, o_out_pat, o_pats, o_pat_bytes;
 };
 
-constexpr uint32_t kLitRec = 36;  // prefilter literal record: len, lower[16], req[16], pad
+constexpr uint32_t kLitRec = 36;  // prefilter literal record: len, lower[16], req[16], exact, pad
+constexpr uint32_t kLitExactByte = 33;  // 1 in every record of a literal-exact program (gre::Compiled)
+constexpr uint32_t kLitFoldByte = 34;   // 1 in every record of a program with a case-free k / s literal byte
 
 struct RuleSetDev {
   const uint16_t* follow_delta;  // all rules' candidate-filter tables (follow.cpp)
@@ -139,6 +143,8 @@ std::vector<uint64_t> follow_ext(const gre::Compiled& c, const gre::Lit& lit, in
 struct DfaHost {
   bool valid = false;
   uint32_t ncls = 0, nstates = 0;
+  uint32_t sym_base = 0;  // first rune symbol column (after the ASCII classes)
+  bool na_ok = false;     // "other non-ASCII rune" is one symbol for this program
   uint32_t start[2] = {0, 0};
   uint32_t first[4] = {0, 0, 0, 0};  // ASCII first bytes that keep some start state alive
   uint8_t cls[128] = {};

@@ -84,6 +84,7 @@ struct Ctrl {
   unsigned long long outputs;  // patterns k_report resolved (diagnostics)
   unsigned long long n_fold;     // fold-special rune occurrences recorded (ScanParams::fold_pos)
   unsigned long long n_caps;     // matches whose secret-group spans k_captures resolves
+  unsigned long long n_caps_big; // ... and those too long for its arenas (k_captures_big)
 };
 
 struct DevLoc {
@@ -177,6 +178,14 @@ __device__ inline uint32_t find_file(const uint64_t* off, uint32_t lo, uint32_t 
 }
 
 __device__ inline uint8_t lower_ascii(uint8_t b) { return (b >= 'A' && b <= 'Z') ? b + 32 : b; }
+
+// Global / LDS address spaces spelled out: through generic pointers the
+// compiler emits flat loads that wait on both counters.
+typedef __attribute__((address_space(1))) const uint8_t gu8;
+typedef __attribute__((address_space(1))) const uint16_t gu16;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <typename T>
+__device__ inline T* as_global(const void* p) { return reinterpret_cast<T*>(reinterpret_cast<uintptr_t>(p)); }
 
 // Report every pattern ending at global position p (AC state st has outputs).
 // Files are NUL-separated, so the pattern lies inside file fi.
@@ -1343,35 +1352,94 @@ __device__ inline bool match_string(const gre::ProgView& pv, const uint8_t* s, u
   return gre::vm_search(pv, s, n, 0, n, true, sc, &ms, &me);
 }
 
-// Literal prefilter for MatchString on short strings (paths, match texts):
-// a pattern with an anchor factor can only match a string that contains one
-// of its literals (case rules as in the scan).  Strings with bytes >= 0x80
-// skip the filter (fold-special runes).
-__device__ inline bool may_match(const RuleSetDev& rs, uint32_t prog, const uint8_t* s, uint32_t n) {
+// Literal prefilter for MatchString on match texts inside the batch: a
+// pattern with an anchor factor can only match a string that contains one of
+// its literals (case rules as in the scan).  Strings with bytes >= 0x80 skip
+// the filter when a literal holds a case-free k or s (U+212A / U+017F match
+// those); otherwise such bytes simply match nothing.  SWAR over aligned 16-byte blocks (one
+// dwordx4 load each; the batch is padded past its end): per 4-byte word and
+// literal, a zero-byte test on (lowered pair) ^ (literal's first two bytes),
+// with `| 0x20` as the lowering (a superset for every byte: c == L implies
+// c | 0x20 == L | 0x20); only the rare surviving positions re-read the literal
+// from memory.  Returns kMayNo, kMayHit (a literal occurs) or kMayMaybe
+// (a byte >= 0x80 was seen).
+constexpr uint32_t kMayLits = 4;  // literals whose first bytes stay in registers
+enum MayResult : uint32_t { kMayNo = 0, kMayHit = 1, kMayMaybe = 2 };
+
+__device__ inline uint32_t zero_bytes(uint32_t x) {  // 0x80 in every byte of x that is 0 (and maybe above one)
+  return (x - 0x01010101u) & ~x & 0x80808080u;
+}
+
+__device__ inline uint32_t may_match(const RuleSetDev& rs, uint32_t prog, const uint8_t* s, uint32_t n) {
   const uint32_t l0 = rs.prog_lit_off[prog], l1 = rs.prog_lit_off[prog + 1];
-  if (l0 == l1) return true;
-  for (uint32_t i = 0; i < n; ++i)
-    if (s[i] >= 0x80) return true;
-  for (uint32_t l = l0; l < l1; ++l) {
+  if (l0 == l1) return kMayMaybe;
+  const uint32_t nl = l1 - l0 < kMayLits ? l1 - l0 : kMayLits;
+  uint32_t f1[kMayLits], f2[kMayLits];  // (lowered | 0x20) first / second byte, broadcast
+  bool one[kMayLits];
+  const bool fold = rs.prog_lits[(size_t)l0 * kLitRec + kLitFoldByte] != 0;
+#pragma unroll
+  for (uint32_t l = 0; l < kMayLits; ++l) {
+    const uint8_t* rec = rs.prog_lits + (size_t)(l0 + (l < nl ? l : 0)) * kLitRec;
+    one[l] = rec[0] < 2;
+    f1[l] = (uint32_t)(rec[1] | 0x20) * 0x01010101u;
+    f2[l] = (uint32_t)(rec[one[l] ? 1 : 2] | 0x20) * 0x01010101u;
+  }
+  auto full_check = [&](uint32_t l, int64_t i) {
     const uint8_t* rec = rs.prog_lits + (size_t)l * kLitRec;
     const uint32_t len = rec[0];
-    const uint8_t* lo = rec + 1;
-    const uint8_t* rq = rec + 1 + 16;
-    for (uint32_t i = 0; i + len <= n; ++i) {
-      uint32_t k = 0;
-      for (; k < len; ++k) {
-        const uint8_t c = s[i + k];
-        if (lower_ascii(c) != lo[k] || (rq[k] && c != rq[k])) break;
+    if (i < 0 || (uint64_t)i + len > n) return false;
+    for (uint32_t k = 0; k < len; ++k) {
+      const uint8_t c = s[i + k];
+      if (lower_ascii(c) != rec[1 + k] || (rec[17 + k] && c != rec[17 + k])) return false;
+    }
+    return true;
+  };
+  const uintptr_t base = reinterpret_cast<uintptr_t>(s);
+  const uintptr_t a0 = base & ~(uintptr_t)15;
+  uint32_t prev = 0;  // the previous word (lowered; bytes outside [0, n) are 0)
+  for (uintptr_t a = a0; a < base + n; a += 16) {
+    const u32x4 v = *as_global<__attribute__((address_space(1))) const u32x4>(reinterpret_cast<const void*>(a));
+    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (uint32_t wi = 0; wi < 4; ++wi) {
+      const int64_t q = (int64_t)(a + 4 * wi) - (int64_t)base;  // offset of the word's byte 0 in s
+      uint32_t w = wv[wi];
+      if (q < 0 || q + 4 > (int64_t)n) {  // keep bytes [max(0,-q), min(4, n-q))
+        const int64_t lo = q < 0 ? -q : 0, hi = (int64_t)n - q;
+        uint32_t keep = 0;
+        for (int64_t k = lo; k < 4 && k < hi; ++k) keep |= 0xFFu << (8 * k);
+        w &= keep;
       }
-      if (k == len) return true;
+      if (fold && (w & 0x80808080u)) return kMayMaybe;  // (c | 0x20 >= 0xA0 never equals a literal byte)
+      // bytes outside the string read 0x20 here: a candidate there fails full_check's bounds
+      const uint32_t lwx = w | 0x20202020u;
+      const uint32_t pw = (lwx << 8) | (prev >> 24);  // byte k: the byte before position q + k
+#pragma unroll
+      for (uint32_t l = 0; l < kMayLits; ++l) {
+        if (l >= nl) break;
+        uint32_t m = one[l] ? zero_bytes(lwx ^ f1[l]) : (zero_bytes(pw ^ f1[l]) & zero_bytes(lwx ^ f2[l]));
+        while (m) {
+          const uint32_t k = (uint32_t)__builtin_ctz(m) >> 3;
+          m &= m - 1;
+          if (full_check(l0 + l, q + k - (one[l] ? 0 : 1))) return kMayHit;
+        }
+      }
+      prev = lwx;
     }
   }
-  return false;
+  for (uint32_t l = l0 + nl; l < l1; ++l)  // literals past the register set (rare)
+    for (uint32_t i = 0; i < n; ++i)
+      if (full_check(l, i)) return kMayHit;
+  return kMayNo;
 }
 
 __device__ inline bool match_string_pf(const RuleSetDev& rs, uint32_t prog, const uint8_t* s, uint32_t n,
                                        gre::VmScratch& sc) {
-  return may_match(rs, prog, s, n) && match_string(rs.progs[prog], s, n, sc);
+  const uint32_t mm = may_match(rs, prog, s, n);
+  if (mm == kMayNo) return false;
+  // a literal-exact program (e.g. the builtin "(?i)example") matches iff a literal occurs
+  if (mm == kMayHit && rs.prog_lits[(size_t)rs.prog_lit_off[prog] * kLitRec + kLitExactByte]) return true;
+  return match_string(rs.progs[prog], s, n, sc);
 }
 
 // Path gates (Global.AllowPath / Rule.MatchPath / Rule.AllowPath,
@@ -1605,11 +1673,12 @@ struct VerifyParams {
   Ctrl* ctrl;
   uint8_t* scratch;
   uint64_t scratch_stride;
-  uint64_t* prof;  // diagnostics (TSG_PROFILE_VERIFY): per job {cycles, rule<<32 | candidates}
-  uint64_t* dbg;   // diagnostics: [0] dfa starts [1] dfa cycles [2] bitstate ok [3] bitstate cycles
-                   // [4] vm captures [5] vm capture cycles [6] vm searches [7] vm search cycles [8] allow cycles
-  uint4* caps;     // deferred capture jobs {file, rule, ms, me} (k_captures)
+  uint64_t* prof;  // diagnostics (TSG_PROFILE_VERIFY): per job {duration | end (100 MHz), rule << 32 | full}
+  uint32_t* tck;   // diagnostics: per job, 100 MHz ticks spent in DFA walks / in emit_match
+  uint4* caps;     // capture jobs {file, rule, ms, me} for k_captures
   uint64_t cap_cap;
+  uint4* caps_big; // those too long for its arenas, for k_captures_big
+  uint64_t cap_big_cap;
 };
 
 // Candidate start windows of one (file, rule) job, in increasing order
@@ -1754,48 +1823,58 @@ __device__ bool vm_search_starts(const gre::ProgView& p, const uint8_t* text, ui
 struct DfaRef {
   const uint16_t* T;
   const uint8_t* cls;
-  uint32_t K, start0, start1, smatch;
+  uint32_t K, start0, start1, smatch, sym;
 };
 
-// Global / LDS address spaces spelled out: through generic pointers the
-// compiler emits flat loads that wait on both counters.
-typedef __attribute__((address_space(1))) const uint8_t gu8;
-typedef __attribute__((address_space(1))) const uint16_t gu16;
-template <typename T>
-__device__ inline T* as_global(const void* p) { return reinterpret_cast<T*>(reinterpret_cast<uintptr_t>(p)); }
 
-__device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, uint32_t n, uint32_t s, uint32_t* me) {
+// kLds: d.T / d.cls are the block's LDS copy (k_verify stages the wave's rule).
+template <bool kLds>
+__device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, uint32_t n, uint32_t s, uint32_t* me,
+                                       uint32_t* steps) {
+  typedef __attribute__((address_space(3))) const uint16_t lu16;
+  typedef __attribute__((address_space(3))) const uint8_t lu8;
   gu16* Tg = as_global<gu16>(d.T);
   gu8* cg = as_global<gu8>(d.cls);
-  gu8* tx = as_global<gu8>(text);
-  const uint32_t K = d.K;
+  lu16* Tl = (lu16*)d.T;  // addrspacecast: only meaningful (and only read) when kLds
+  lu8* cl = (lu8*)d.cls;
   uint32_t st = s == 0 ? d.start1 : d.start0;
   int64_t last = ((d.smatch >> (s == 0 ? 1 : 0)) & 1) ? (int64_t)s : -1;
-  // 16 bytes at a time: the byte loads issue together (unconditionally when
-  // the chunk lies inside the file), only the transition loads are chained
-  for (uint32_t q0 = s; q0 < n && st; q0 += 16) {
-    uint32_t c[16];
-    if (q0 + 16 <= n) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) c[i] = tx[q0 + i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) c[i] = q0 + i < n ? (uint32_t)tx[q0 + i] : 0u;
-    }
-    const uint32_t m = n - q0 < 16 ? n - q0 : 16;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if ((uint32_t)i >= m || !st) break;
-      if (c[i] >= 0x80) return 2;  // runes / case folding: the Pike VM decides
-      const uint32_t k = cg[c[i]];
-      const uint32_t e = Tg[st * K + k];
-      if (q0 + i + 1 == n) {
+  const uint32_t K = d.K;
+  // the text in aligned 16-byte blocks, one dwordx4 load each (a byte load per
+  // step cost a TLB lookup per lane per byte; the batch is padded past its
+  // end, so a block holding a content byte never leaves the allocation)
+  const uintptr_t base = reinterpret_cast<uintptr_t>(text);
+  uint32_t q = s;
+  while (q < n && st) {
+    const uintptr_t addr = (base + q) & ~(uintptr_t)15;
+    const u32x4 v = *as_global<__attribute__((address_space(1))) const u32x4>(reinterpret_cast<const void*>(addr));
+    uint32_t i = (uint32_t)((base + q) & 15);
+    while (i < 16 && q < n && st) {
+      const uint32_t wd = i < 8 ? (i < 4 ? v.x : v.y) : (i < 12 ? v.z : v.w);  // no dynamically indexed array
+      const uint32_t c = (wd >> (8 * (i & 3))) & 0xFFu;
+      uint32_t k, w = 1;
+      if (c < 0x80) {
+        k = kLds ? cl[c] : cg[c];
+      } else {
+        // a decoded rune: K, ſ, İ, U+FFFD or any other non-ASCII rune (dfa.cpp
+        // symbols after the ASCII classes); the VM decides only when this
+        // program tells other non-ASCII runes apart
+        const int r = gre::decode_rune(text, n, q, &w);
+        const uint32_t j = r == 0x212A ? 0u : r == 0x17F ? 1u : r == 0x130 ? 2u : r == 0xFFFD ? 3u : 4u;
+        if (j == 4 && !(d.sym >> 31)) return 2;
+        k = (d.sym & 0x7FFFFFFFu) + j;
+      }
+      const uint32_t e = kLds ? Tl[st * K + k] : Tg[st * K + k];
+      ++*steps;
+      if (q + w == n) {
         if (e & 0x8000u) last = n;
         st = 0;
         break;
       }
       st = e & kDfaStateMask;
-      if (e & 0x4000u) last = q0 + i + 1;
+      q += w;
+      i += w;
+      if (e & 0x4000u) last = q;
     }
   }
   if (last < 0) return 0;
@@ -1894,24 +1973,21 @@ __device__ bool bitstate_captures(const gre::ProgView& p, const uint8_t* text, u
 }
 
 // Secret-group spans of one kept match (getMatchSubgroupsLocations,
-// scanner.go:150-163): bit-state backtracker in the lane's LDS arena; a match
-// too long for it is deferred to k_captures_big (`defer`), whose arenas are
-// 16x larger, and only past those does the capture VM run.
+// scanner.go:150-163) with the bit-state backtracker in the lane's LDS arena
+// of `words` words; a match too long for it goes on to the next stage's list
+// (`next`, k_captures -> k_captures_big), and only past the last arena does
+// the capture VM run.
 __device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t rule, uint32_t fi,
                             const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me, gre::VmScratch& sc,
-                            uint32_t* bs_area, uint32_t words, bool defer) {
+                            uint32_t* bs_area, uint32_t words, uint4* next, uint64_t next_cap,
+                            unsigned long long* next_n) {
   const gre::ProgView& pv = V.rs.progs[rd.prog];
   const uint32_t* gnum = V.rs.group_slots + rd.group_off;
   int32_t* gcap = (int32_t*)(bs_area + words - 8);  // tracked slots (the arena's last 8 words)
-  const uint64_t tb0 = V.dbg ? clock64() : 0;
   const bool bs_ok = bitstate_captures(pv, text, n, ms, me, gnum, rd.group_n, bs_area, words, gcap);
-  if (V.dbg) {
-    atomicAdd((unsigned long long*)&V.dbg[2], bs_ok ? 1ull : 0ull);
-    atomicAdd((unsigned long long*)&V.dbg[3], (unsigned long long)(clock64() - tb0));
-  }
-  if (!bs_ok && defer) {
-    const unsigned long long idx = atomicAdd(&V.ctrl->n_caps, 1ull);
-    if (idx < V.cap_cap) V.caps[idx] = make_uint4(fi, rule, ms, me);
+  if (!bs_ok && next) {
+    const unsigned long long idx = atomicAdd(next_n, 1ull);
+    if (idx < next_cap) next[idx] = make_uint4(fi, rule, ms, me);
     return;
   }
   if (bs_ok) {
@@ -1926,12 +2002,7 @@ __device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t r
     return;
   }
   int32_t out[kMaxCap];  // ncap <= kMaxCap is enforced by the rule compiler
-  const uint64_t tv0 = V.dbg ? clock64() : 0;
   bool ok = gre::vm_captures(pv, text, n, ms, sc, out);
-  if (V.dbg) {
-    atomicAdd((unsigned long long*)&V.dbg[4], 1ull);
-    atomicAdd((unsigned long long*)&V.dbg[5], (unsigned long long)(clock64() - tv0));
-  }
   if (!ok || (uint32_t)out[1] != me) atomicOr(&V.ctrl->err, 1u);
   for (uint32_t g = 0; g < rd.group_n; ++g) {
     const uint32_t slot = gnum[g];
@@ -1945,37 +2016,51 @@ __device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t r
 }
 
 // A match k_verify found: allow rules, then the whole-match location or, for
-// rules with a secret group, its group spans.
-__device__ void emit_match(const VerifyParams& V, const RuleDev& rd, uint32_t rule, uint32_t fi,
-                           const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me, gre::VmScratch& sc,
-                           uint32_t* bs_area) {
+// rules with a secret group, a capture job for k_captures (whose bit-state
+// arenas take LDS that would cap the search at one wave per CU).
+__device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, uint32_t fi, const uint8_t* text,
+                                        uint32_t n, uint32_t ms, uint32_t me, gre::VmScratch& sc,
+                                        uint32_t* tck = nullptr) {
+  const uint64_t t0 = tck ? __builtin_amdgcn_s_memrealtime() : 0;
+  const RuleDev& rd = V.rs.rules[rule];
   // AllowLocation (scanner.go:145-148): global then rule allow regexes on the whole match
-  for (uint32_t k = 0; k < V.rs.n_global_allow; ++k)
-    if (match_string_pf(V.rs, V.rs.global_allow[k], text + ms, me - ms, sc)) return;
-  for (uint32_t k = 0; k < rd.allow_n; ++k)
-    if (match_string_pf(V.rs, V.rs.allow_progs[rd.allow_off + k], text + ms, me - ms, sc)) return;
+  for (uint32_t k = 0; k < V.rs.n_global_allow; ++k) {
+    const bool al = match_string_pf(V.rs, V.rs.global_allow[k], text + ms, me - ms, sc);
+    if (tck) tck[2] += (uint32_t)(__builtin_amdgcn_s_memrealtime() - t0);
+    if (al) return;
+  }
+  const uint32_t allow_off = rd.allow_off, allow_n = rd.allow_n;
+  for (uint32_t k = 0; k < allow_n; ++k)
+    if (match_string_pf(V.rs, V.rs.allow_progs[allow_off + k], text + ms, me - ms, sc)) return;
   if (!rd.use_groups) {
     unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
     if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, ms, me, 0, 0, 0, 0};
     return;
   }
-  emit_groups(V, rd, rule, fi, text, n, ms, me, sc, bs_area, kBsWords, true);
+  unsigned long long idx = atomicAdd(&V.ctrl->n_caps, 1ull);
+  if (idx < V.cap_cap) V.caps[idx] = make_uint4(fi, rule, ms, me);
 }
 
-// Secret groups of the matches too long for k_verify's arenas (private keys,
-// long tokens): kBigCapLanes lanes per block, 36 KiB of LDS each.
-__global__ __launch_bounds__(kBigCapLanes) void k_captures_big(VerifyParams V, uint32_t n_caps) {
-  __shared__ uint32_t bs_lds[kBigCapLanes * kBigBsWords];
-  uint32_t* bs_area = bs_lds + threadIdx.x * kBigBsWords;
+// Capture stages: a fixed grid walks the list the previous stage filled,
+// its length read on the device (no host round trip between the stages).
+template <uint32_t kLanes, uint32_t kWords, bool kLast>
+__global__ __launch_bounds__(kLanes) void k_captures(VerifyParams V) {
+  __shared__ uint32_t bs_lds[kLanes * kWords];
+  uint32_t* bs_area = bs_lds + threadIdx.x * kWords;
   const uint32_t nthreads = gridDim.x * blockDim.x;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   gre::VmScratch sc = make_scratch(V.scratch + (uint64_t)t * V.scratch_stride, V.rs);
-  for (uint32_t i = t; i < n_caps; i += nthreads) {
-    const uint4 c = V.caps[i];
+  const uint4* list = kLast ? V.caps_big : V.caps;
+  const unsigned long long cnt = kLast ? V.ctrl->n_caps_big : V.ctrl->n_caps;
+  const uint64_t cap = kLast ? V.cap_big_cap : V.cap_cap;
+  const uint64_t n_caps = cnt < cap ? cnt : cap;
+  for (uint64_t i = t; i < n_caps; i += nthreads) {
+    const uint4 c = list[i];
     const RuleDev rd = V.rs.rules[c.y];
     const uint64_t fstart = V.off[c.x];
     const uint32_t n = (uint32_t)(V.off[c.x + 1] - 1 - fstart);
-    emit_groups(V, rd, c.y, c.x, V.data + fstart, n, c.z, c.w, sc, bs_area, kBigBsWords, false);
+    emit_groups(V, rd, c.y, c.x, V.data + fstart, n, c.z, c.w, sc, bs_area, kWords, kLast ? nullptr : V.caps_big,
+                V.cap_big_cap, &V.ctrl->n_caps_big);
   }
 }
 
@@ -2003,133 +2088,162 @@ __global__ __launch_bounds__(256) void k_warm(WarmRanges R, uint32_t* sink) {
   if (acc == 0x5EED1234u) sink[0] = acc;  // keeps the loads alive
 }
 
-// One wave per block with the bit-state arenas in LDS: secret groups are
-// resolved in place (measured: 0.67 ms at 50 GB vs 0.48 + 0.21 ms with a
-// full-occupancy search and the groups in a kernel of their own).
-__global__ __launch_bounds__(kVerifyThreads) void k_verify(VerifyParams V) {
-  __shared__ uint32_t bs_lds[kVerifyThreads * kBsWords];
-  uint32_t* bs_area = bs_lds + threadIdx.x * kBsWords;
+// The match search: no LDS, so occupancy hides the dependent global reads of
+// the DFA / VM walks; secret-group captures are left to k_captures.  Each job
+// kind runs in a function of its own: the Pike VM takes its start oracle by
+// reference, which would otherwise put the DFA path's IvIter (read on every
+// start) in scratch memory -- 35 K lanes of scratch thrash L2 and made each
+// dependent DFA step an HBM round trip (k_verify 1.96 ms at 50 GB).
+constexpr uint32_t kVerifyBlock = 64;  // one wave per block: jobs spread over every CU (UTCL1 reach per CU)
+
+// regexp.go allMatches over the whole file (rules without an anchor)
+__device__ __noinline__ void verify_full_job(const VerifyParams& V, uint32_t rule, uint32_t fi, const uint8_t* text,
+                                             uint32_t n, gre::VmScratch& sc) {
+  const gre::ProgView& pv = V.rs.progs[V.rs.rules[rule].prog];
+  uint32_t pos = 0, ms, me;
+  int64_t prev_end = -1;
+  while (pos <= n) {
+    LimitStarts ls{n};
+    if (!vm_search_starts(pv, text, n, pos, ls, sc, &ms, &me)) break;
+    bool accept = true;
+    if (me == pos) {
+      if ((int64_t)ms == prev_end) accept = false;
+      uint32_t w;
+      gre::decode_rune(text, n, pos, &w);
+      pos = w > 0 ? pos + w : n + 1;
+    } else {
+      pos = me;
+    }
+    prev_end = me;
+    if (accept) emit_match(V, rule, fi, text, n, ms, me, sc);
+  }
+}
+
+__device__ inline void iv_init(IvIter& it, const VerifyParams& V, uint32_t rule, uint64_t c0, uint64_t c1,
+                               uint64_t fstart, const uint8_t* text, uint32_t n) {
+  const RuleDev& rd = V.rs.rules[rule];
+  it.keys = V.keys;
+  it.ci = c0;
+  it.c1 = c1;
+  it.fstart = fstart;
+  it.text = text;
+  it.n = n;
+  it.a = rd.off_min;
+  it.b = rd.off_max;
+  it.alpha = rd.alpha;
+  it.have_prev = false;
+  it.h_prev = it.p_prev = 0;
+  it.advance();
+}
+
+// FindAll over the anchor windows with the verify DFA: the first permitted
+// start (>= pos) that matches is Go's leftmost match; a start the DFA cannot
+// decide (byte >= 0x80) is decided by the Pike VM alone, anchored there.
+template <bool kLds>
+__device__ __noinline__ uint32_t verify_dfa_job(const VerifyParams& V, uint32_t rule, uint32_t fi, uint64_t c0,
+                                                uint64_t c1, uint64_t fstart, const uint8_t* text, uint32_t n,
+                                                gre::VmScratch& sc, const uint16_t* lds_T, const uint8_t* lds_cls,
+                                                uint32_t* tck) {
+  uint32_t steps = 0;  // DFA transitions taken (diagnostics)
+  uint32_t tck_dfa = 0, tck_emit = 0;
+  const RuleDev& rd = V.rs.rules[rule];
+  const DfaRef dref{kLds ? lds_T : V.rs.dfa_delta + rd.dfa_off, kLds ? lds_cls : V.rs.dfa_bytes + rd.dfa_cls_off,
+                    rd.dfa_ncls, rd.dfa_start0, rd.dfa_start1, rd.dfa_smatch, rd.dfa_sym};
+  const uint32_t fm0 = rd.dfa_first[0], fm1 = rd.dfa_first[1], fm2 = rd.dfa_first[2], fm3 = rd.dfa_first[3];
+  const uint32_t prog = rd.prog;
+  IvIter it;
+  iv_init(it, V, rule, c0, c1, fstart, text, n);
+  uint32_t pos = 0, ms, me;
+  while (it.have) {
+    bool found = false;
+    const uint32_t s0 = it.cs > pos ? it.cs : pos;
+    for (uint32_t sp = s0; sp <= it.ce && sp < n; ++sp) {
+      if (!gre::is_rune_start(text, n, sp)) continue;
+      const uint32_t b0 = as_global<gu8>(text)[sp];  // first-byte skip (no dependent table loads)
+      const uint32_t fw = b0 < 32 ? fm0 : b0 < 64 ? fm1 : b0 < 96 ? fm2 : fm3;
+      if (b0 < 0x80 && !((fw >> (b0 & 31)) & 1)) continue;
+      const uint64_t ta = tck ? __builtin_amdgcn_s_memrealtime() : 0;
+      int r = dfa_anchored_dev<kLds>(dref, text, n, sp, &me, &steps);
+      if (tck) tck_dfa += (uint32_t)(__builtin_amdgcn_s_memrealtime() - ta);
+      if (r == 2) {
+        OneStart one{sp};
+        r = vm_search_starts(V.rs.progs[prog], text, n, sp, one, sc, &ms, &me) ? 1 : 0;
+      }
+      if (r == 1) {
+        const uint64_t tb = tck ? __builtin_amdgcn_s_memrealtime() : 0;
+        emit_match(V, rule, fi, text, n, sp, me, sc, tck);
+        if (tck) tck_emit += (uint32_t)(__builtin_amdgcn_s_memrealtime() - tb);
+        pos = me;
+        found = true;
+        break;
+      }
+    }
+    if (!found) it.advance();
+    else while (it.have && it.ce < pos) it.advance();
+  }
+  if (tck) { tck[0] = tck_dfa; tck[1] = tck_emit; }
+  return steps;
+}
+
+// The same FindAll with the Pike VM (rules without a verify DFA)
+__device__ __noinline__ void verify_vm_job(const VerifyParams& V, uint32_t rule, uint32_t fi, uint64_t c0, uint64_t c1,
+                                           uint64_t fstart, const uint8_t* text, uint32_t n, gre::VmScratch& sc) {
+  const gre::ProgView& pv = V.rs.progs[V.rs.rules[rule].prog];
+  IvIter it;
+  iv_init(it, V, rule, c0, c1, fstart, text, n);
+  uint32_t pos = 0, ms, me;
+  while (it.have) {
+    if (!vm_search_starts(pv, text, n, pos, it, sc, &ms, &me)) break;
+    emit_match(V, rule, fi, text, n, ms, me, sc);
+    if (me == ms) break;  // cannot happen for anchored rules (non-empty literal)
+    pos = me;
+  }
+}
+
+// The block (one wave) stages the verify DFA of its first job's rule in LDS:
+// jobs are sorted by rule, so nearly every lane walks that table, and an LDS
+// step costs no L2 round trip and no TLB lookup (the random text pages the
+// lanes touch evict the table's translations from the small per-CU TLB).
+constexpr uint32_t kVerifyDfaLds = 64 * 1024;
+
+__global__ __launch_bounds__(kVerifyBlock) void k_verify(VerifyParams V) {
+  __shared__ __align__(16) uint16_t dfa_lds[kVerifyDfaLds / 2];
+  __shared__ __align__(16) uint8_t cls_lds[128];
   const uint32_t nthreads = gridDim.x * blockDim.x;
   gre::VmScratch sc = make_scratch(V.scratch + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * V.scratch_stride, V.rs);
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < V.n_jobs; j += nthreads) {
-    const uint64_t t0 = V.prof ? clock64() : 0;
+  for (uint32_t jb = blockIdx.x * blockDim.x; jb < V.n_jobs; jb += nthreads) {  // block-uniform
+    const uint32_t r0 = (uint32_t)(V.keys[V.job_start[jb]] >> kPosBits);
+    const RuleDev& rd0 = V.rs.rules[r0];
+    const bool staged = rd0.dfa_off != kNoFollow && rd0.dfa_size * 2 <= kVerifyDfaLds;
+    __syncthreads();  // the previous group's walks are done with the table
+    if (staged) {
+      const uint32_t* src = (const uint32_t*)(V.rs.dfa_delta + rd0.dfa_off);  // dfa_off is even (build pads)
+      for (uint32_t i = threadIdx.x; i < (rd0.dfa_size + 1) / 2; i += blockDim.x) ((uint32_t*)dfa_lds)[i] = src[i];
+      for (uint32_t i = threadIdx.x; i < 128; i += blockDim.x) cls_lds[i] = V.rs.dfa_bytes[rd0.dfa_cls_off + i];
+    }
+    __syncthreads();
+    const uint32_t j = jb + threadIdx.x;
+    if (j >= V.n_jobs) continue;
+    const uint64_t t0 = V.prof ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz wall clock
     const uint64_t c0 = V.job_start[j];
     const uint64_t c1 = (j + 1 < V.n_jobs) ? V.job_start[j + 1] : V.n_cands;
     const uint32_t rule = (uint32_t)(V.keys[c0] >> kPosBits);
-    struct ProfGuard {
-      const VerifyParams& V;
-      uint32_t j, rule;
-      uint64_t t0, nc;
-      __device__ ~ProfGuard() {
-        if (V.prof) {
-          V.prof[2 * j] = clock64() - t0;
-          V.prof[2 * j + 1] = ((uint64_t)rule << 32) | nc;
-        }
-      }
-    } pg{V, j, rule, t0, 0};  // nc: DFA starts tried (diagnostics), bit 31 = full-file job
     const uint32_t fi = V.vals[c0] & ~kFullFlag;
     bool full = false;
     for (uint64_t c = c0; c < c1 && !full; ++c) full = (V.vals[c] & kFullFlag) != 0;
-    if (full) pg.nc |= 1u << 31;
-    const RuleDev rd = V.rs.rules[rule];
-    const gre::ProgView& pv = V.rs.progs[rd.prog];
     const uint64_t fstart = V.off[fi];
     const uint8_t* text = V.data + fstart;
     const uint32_t n = (uint32_t)(V.off[fi + 1] - 1 - fstart);  // NUL separator excluded
-    uint32_t ms, me;
-    if (full) {
-      // regexp.go allMatches over the whole file
-      uint32_t pos = 0;
-      int64_t prev_end = -1;
-      while (pos <= n) {
-        LimitStarts ls{n};
-        if (!vm_search_starts(pv, text, n, pos, ls, sc, &ms, &me)) break;
-        bool accept = true;
-        if (me == pos) {
-          if ((int64_t)ms == prev_end) accept = false;
-          uint32_t w;
-          gre::decode_rune(text, n, pos, &w);
-          pos = w > 0 ? pos + w : n + 1;
-        } else {
-          pos = me;
-        }
-        prev_end = me;
-        if (accept) emit_match(V, rd, rule, fi, text, n, ms, me, sc, bs_area);
-      }
-    } else {
-      IvIter it;
-      it.keys = V.keys;
-      it.ci = c0;
-      it.c1 = c1;
-      it.fstart = fstart;
-      it.text = text;
-      it.n = n;
-      it.a = rd.off_min;
-      it.b = rd.off_max;
-      it.alpha = V.rs.rules[rule].alpha;
-      it.have_prev = false;
-      it.h_prev = it.p_prev = 0;
-      it.advance();
-      uint32_t pos = 0;
-      if (rd.dfa_off != kNoFollow) {
-        const DfaRef dref{V.rs.dfa_delta + rd.dfa_off, V.rs.dfa_bytes + rd.dfa_cls_off, rd.dfa_ncls, rd.dfa_start0,
-                          rd.dfa_start1, rd.dfa_smatch};
-        const uint32_t fm0 = rd.dfa_first[0], fm1 = rd.dfa_first[1], fm2 = rd.dfa_first[2], fm3 = rd.dfa_first[3];
-        // FindAll over the permitted starts with the verify DFA: the first
-        // start (>= pos) that matches is Go's leftmost match; a start the DFA
-        // cannot decide (byte >= 0x80) is decided by the Pike VM
-        while (it.have) {
-          bool found = false;
-          uint32_t s0 = it.cs > pos ? it.cs : pos;
-          for (uint32_t sp = s0; sp <= it.ce && sp < n; ++sp) {
-            if (!gre::is_rune_start(text, n, sp)) continue;
-            {
-              const uint32_t c0 = as_global<gu8>(text)[sp];  // first-byte skip (no dependent table loads)
-              const uint32_t fw = c0 < 32 ? fm0 : c0 < 64 ? fm1 : c0 < 96 ? fm2 : fm3;
-              if (c0 < 0x80 && !((fw >> (c0 & 31)) & 1)) continue;
-            }
-            const uint64_t td0 = V.dbg ? clock64() : 0;
-            int r = dfa_anchored_dev(dref, text, n, sp, &me);
-            if (V.dbg) {
-              atomicAdd((unsigned long long*)&V.dbg[0], 1ull);
-              atomicAdd((unsigned long long*)&V.dbg[1], (unsigned long long)(clock64() - td0));
-              atomicAdd((unsigned long long*)&V.dbg[9 + (r == 1 ? 1 : r == 2 ? 2 : 0)], 1ull);
-              if (r == 1) atomicAdd((unsigned long long*)&V.dbg[12], (unsigned long long)(me - sp));
-              ++pg.nc;
-              if (rule < 64) atomicAdd((unsigned long long*)&V.dbg[13], 0ull);
-            }
-            if (r == 2) {
-              // a byte >= 0x80 before the DFA decided: the Pike VM decides this
-              // start alone (anchored at sp, same leftmost-first end), and the
-              // DFA goes on with the next starts -- one rune no longer sends
-              // every later window of the job to the VM
-              OneStart one{sp};
-              r = vm_search_starts(pv, text, n, sp, one, sc, &ms, &me) ? 1 : 0;
-            }
-            if (r == 1) {
-              emit_match(V, rd, rule, fi, text, n, sp, me, sc, bs_area);
-              pos = me;
-              found = true;
-              break;
-            }
-          }
-          if (!found) it.advance();
-          else while (it.have && it.ce < pos) it.advance();
-        }
-        continue;
-      }
-      while (it.have) {
-        const uint64_t ts0 = V.dbg ? clock64() : 0;
-        const bool got = vm_search_starts(pv, text, n, pos, it, sc, &ms, &me);
-        if (V.dbg) {
-          atomicAdd((unsigned long long*)&V.dbg[6], 1ull);
-          atomicAdd((unsigned long long*)&V.dbg[7], (unsigned long long)(clock64() - ts0));
-        }
-        if (!got) break;
-        emit_match(V, rd, rule, fi, text, n, ms, me, sc, bs_area);
-        if (me == ms) break;  // cannot happen for anchored rules (non-empty literal)
-        pos = me;
-      }
+    uint32_t steps = 0;
+    if (full) verify_full_job(V, rule, fi, text, n, sc);
+    else if (staged && rule == r0) steps = verify_dfa_job<true>(V, rule, fi, c0, c1, fstart, text, n, sc, dfa_lds, cls_lds, V.tck ? V.tck + 4 * j : nullptr);
+    else if (V.rs.rules[rule].dfa_off != kNoFollow)
+      steps = verify_dfa_job<false>(V, rule, fi, c0, c1, fstart, text, n, sc, nullptr, nullptr, V.tck ? V.tck + 4 * j : nullptr);
+    else verify_vm_job(V, rule, fi, c0, c1, fstart, text, n, sc);
+    if (V.prof) {  // diagnostics (TSG_PROFILE_VERIFY): duration | end, rule | full
+      const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+      V.prof[2 * j] = (t1 - t0) | ((t1 & 0xFFFFFFFFull) << 32);
+      V.prof[2 * j + 1] = ((uint64_t)rule << 32) | (steps << 1) | (full ? 1u : 0u);
     }
   }
 }
@@ -2462,7 +2576,7 @@ struct tsg_engine {
   DBuf<uint8_t> span_hi;
   DBuf<uint64_t> fold_pos;    // fold-special rune occurrences (k_fold_windows)
   uint64_t fold_need = 0;     // fold-position capacity learnt from a lost scan
-  DBuf<uint4> caps;
+  DBuf<uint4> caps, caps_big;
   DBuf<uint32_t> ev_counts;
   uint64_t ev_ovf_need = 0;  // overflow-event capacity learnt from a lost scan
   bool fast_timed = false;   // ev[10..11] bracket the last k_scan_fast launch
@@ -2563,11 +2677,18 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   for (auto& rx : rs->regexes) {
     const gre::Anchor& a = rx.c.anchor;
     if (a.valid && a.lits.size() <= 32) {
+      // only a case-free k / s can be matched by a non-ASCII rune (U+212A, U+017F)
+      bool fold_lits = false;
+      for (auto& l : a.lits)
+        for (size_t j = 0; j < l.lower.size(); ++j)
+          fold_lits |= (l.lower[j] == 'k' || l.lower[j] == 's') && l.req[j] == 0;
       for (auto& l : a.lits) {
         uint8_t rec[kLitRec] = {0};
         rec[0] = (uint8_t)l.lower.size();
         memcpy(rec + 1, l.lower.data(), l.lower.size());
         memcpy(rec + 17, l.req.data(), l.req.size());
+        rec[kLitExactByte] = rx.c.literal_exact ? 1 : 0;
+        rec[kLitFoldByte] = fold_lits ? 1 : 0;
         lits.insert(lits.end(), rec, rec + kLitRec);
       }
     }
@@ -2596,6 +2717,7 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
     d.follow_off = kNoFollow;
     d.dfa_off = kNoFollow;
     if (r.dfa.valid) {
+      if (ddelta.size() & 1) ddelta.push_back(0);  // even offsets: k_verify stages tables as dwords
       d.dfa_off = (uint32_t)ddelta.size();
       d.dfa_ncls = r.dfa.ncls;
       d.dfa_cls_off = (uint32_t)dbytes.size();
@@ -2607,6 +2729,7 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
       for (int q = 0; q < 4; ++q) d.dfa_first[q] = r.dfa.first[q];
       d.dfa_size = (uint32_t)r.dfa.delta.size();
       d.dfa_smatch = (r.dfa.match[r.dfa.start[0]] ? 1u : 0u) | (r.dfa.match[r.dfa.start[1]] ? 2u : 0u);
+      d.dfa_sym = r.dfa.sym_base | (r.dfa.na_ok ? 0x80000000u : 0u);
       ddelta.insert(ddelta.end(), r.dfa.delta.begin(), r.dfa.delta.end());
     }
     if (r.follow.valid) {
@@ -3409,14 +3532,15 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   HIP_TRY(hipEventRecord(e->ev[4], s));
   // ---- 5. verify
   uint64_t loc_cap = std::max<uint64_t>(1 << 16, n_jobs);
-  uint64_t caps_cap = std::max<uint64_t>(1 << 14, n_jobs / 4);
+  uint64_t caps_cap = std::max<uint64_t>(1 << 14, n_jobs / 2), caps_big_cap = std::max<uint64_t>(1 << 12, n_jobs / 16);
   uint64_t n_locs = 0;
   bool verified = n_jobs == 0;
   for (int attempt = 0; attempt < 4 && !verified; ++attempt) {
     HIP_TRY(e->locs.ensure(loc_cap));
     HIP_TRY(e->caps.ensure(caps_cap));
+    HIP_TRY(e->caps_big.ensure(caps_big_cap));
     HIP_TRY(hipMemsetAsync(&e->ctrl.p->locs, 0, 8, s));
-    HIP_TRY(hipMemsetAsync(&e->ctrl.p->n_caps, 0, 8, s));
+    HIP_TRY(hipMemsetAsync(&e->ctrl.p->n_caps, 0, 16, s));  // n_caps, n_caps_big
     VerifyParams V{};
     V.data = d_data;
     V.off = d_off;
@@ -3433,13 +3557,13 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     V.scratch_stride = e->scratch_stride;
     V.caps = e->caps.p;
     V.cap_cap = e->caps.n;
+    V.caps_big = e->caps_big.p;
+    V.cap_big_cap = e->caps_big.n;
     const bool prof = getenv("TSG_PROFILE_VERIFY") != nullptr;
-    if (prof) {
-      HIP_TRY(e->vprof.ensure(2ull * n_jobs + 16));
-      HIP_TRY(hipMemsetAsync(e->vprof.p + 2ull * n_jobs, 0, 16 * 8, s));
-    }
+    if (prof) HIP_TRY(e->vprof.ensure(4ull * n_jobs + 16));
+    if (prof) HIP_TRY(hipMemsetAsync(e->vprof.p, 0, (4ull * n_jobs + 16) * 8, s));
     V.prof = prof ? e->vprof.p : nullptr;
-    V.dbg = prof ? e->vprof.p + 2ull * n_jobs : nullptr;
+    V.tck = prof ? (uint32_t*)(e->vprof.p + 2ull * n_jobs) : nullptr;
     // rule tables back into L2, then the match search (no LDS: full occupancy)
     if (attempt == 0) {
       WarmRanges W{};
@@ -3460,56 +3584,59 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
       hipLaunchKernelGGL(k_warm, dim3(8 * kWarmParts), dim3(256), 0, s, W, (uint32_t*)e->nsel.p);
       HIP_TRY(hipGetLastError());
     }
-    const uint32_t blocks = std::min<uint32_t>((n_jobs + kVerifyThreads - 1) / kVerifyThreads,
-                                               e->vm_threads / kVerifyThreads);
-    hipLaunchKernelGGL(k_verify, dim3(std::max(1u, blocks)), dim3(kVerifyThreads), 0, s, V);
+    const uint32_t blocks = std::min<uint32_t>((n_jobs + kVerifyBlock - 1) / kVerifyBlock, e->vm_threads / kVerifyBlock);
+    hipLaunchKernelGGL(k_verify, dim3(std::max(1u, blocks)), dim3(kVerifyBlock), 0, s, V);
+    // capture stages over the device-side lists (one wave per CU with 140 KiB
+    // of arenas, then kBigCapLanes lanes per CU with 36 KiB each)
+    hipLaunchKernelGGL((k_captures<kVerifyThreads, kBsWords, false>), dim3(e->num_cus), dim3(kVerifyThreads), 0, s, V);
+    hipLaunchKernelGGL((k_captures<kBigCapLanes, kBigBsWords, true>), dim3(e->num_cus), dim3(kBigCapLanes), 0, s, V);
     HIP_TRY(hipGetLastError());
-    if ((rc = read_ctrl(e, &c))) return rc;
-    if (c.n_caps > e->caps.n) {  // capture list overflow: grow and re-run the search
-      caps_cap = c.n_caps;
-      continue;
-    }
-    if (c.n_caps) {
-      // matches too long for k_verify's arenas: kBigCapLanes lanes per block
-      const uint32_t cb = std::min<uint32_t>((uint32_t)((c.n_caps + kBigCapLanes - 1) / kBigCapLanes),
-                                             e->vm_threads / kBigCapLanes);
-      hipLaunchKernelGGL(k_captures_big, dim3(std::max(1u, cb)), dim3(kBigCapLanes), 0, s, V, (uint32_t)c.n_caps);
-      HIP_TRY(hipGetLastError());
-    }
-    if (prof) {
-      std::vector<uint64_t> hp(2ull * n_jobs + 16);
+    if (prof) {  // the jobs that end last (their waves set k_verify's length), per-rule totals
+      std::vector<uint64_t> hp(4ull * n_jobs);
+      std::vector<uint32_t> hjs(n_jobs);
       HIP_TRY(hipMemcpyAsync(hp.data(), e->vprof.p, hp.size() * 8, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipMemcpyAsync(hjs.data(), e->job_start.p, n_jobs * 4, hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
+      auto dur = [&](uint32_t q) { return hp[2 * q] & 0xFFFFFFFFull; };
+      auto end = [&](uint32_t q) { return hp[2 * q] >> 32; };
+      uint64_t tmin = ~0ull;
+      for (uint32_t q = 0; q < n_jobs; ++q) tmin = std::min<uint64_t>(tmin, end(q) - dur(q));
       std::vector<uint32_t> idx(n_jobs);
       for (uint32_t q = 0; q < n_jobs; ++q) idx[q] = q;
-      std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return hp[2 * a] > hp[2 * b]; });
+      std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return end(a) > end(b); });
+      fprintf(stderr, "[verify] kernel span %.3f ms\n", (end(idx[0]) - tmin) / 1e5);
+      for (uint32_t q = 0; q < std::min<uint32_t>(16, n_jobs); ++q) {
+        const uint32_t jq = idx[q];
+        const uint64_t c0 = hjs[jq], c1 = jq + 1 < n_jobs ? hjs[jq + 1] : n_cands;
+        const uint32_t* tk = (const uint32_t*)(hp.data() + 2ull * n_jobs) + 4 * jq;
+        fprintf(stderr,
+                "[verify] job %u dur %.3f ms end %.3f ms rule %s full %llu dfa steps %llu cands %llu dfa %.3f emit %.3f "
+                "(global allow %.3f)\n",
+                jq, dur(jq) / 1e5, (end(jq) - tmin) / 1e5, rs->rules[hp[2 * jq + 1] >> 32].id.c_str(),
+                (unsigned long long)(hp[2 * jq + 1] & 1), (unsigned long long)((hp[2 * jq + 1] & 0xFFFFFFFFull) >> 1),
+                (unsigned long long)(c1 - c0), tk[0] / 1e5, tk[1] / 1e5, tk[2] / 1e5);
+      }
       std::map<uint32_t, std::pair<uint64_t, uint64_t>> per_rule;
       for (uint32_t q = 0; q < n_jobs; ++q) {
         auto& pr = per_rule[(uint32_t)(hp[2 * q + 1] >> 32)];
-        pr.first += hp[2 * q];
-        pr.second = std::max(pr.second, hp[2 * q]);
+        pr.first += dur(q);
+        pr.second = std::max<uint64_t>(pr.second, dur(q));
       }
-      for (uint32_t q = 0; q < std::min<uint32_t>(10, n_jobs); ++q)
-        fprintf(stderr, "[verify] job %u cycles %llu rule %s starts %llx\n", idx[q], (unsigned long long)hp[2 * idx[q]],
-                rs->rules[hp[2 * idx[q] + 1] >> 32].id.c_str(), (unsigned long long)(hp[2 * idx[q] + 1] & 0xFFFFFFFF));
       for (auto& kv : per_rule)
-        fprintf(stderr, "[verify] rule %s total %llu max %llu\n", rs->rules[kv.first].id.c_str(),
-                (unsigned long long)kv.second.first, (unsigned long long)kv.second.second);
-      const uint64_t* d = hp.data() + 2ull * n_jobs;
-      fprintf(stderr, "[verify] dfa starts %llu cycles %llu | bitstate ok %llu cycles %llu | vm captures %llu cycles %llu | vm searches %llu cycles %llu\n",
-              (unsigned long long)d[0], (unsigned long long)d[1], (unsigned long long)d[2], (unsigned long long)d[3],
-              (unsigned long long)d[4], (unsigned long long)d[5], (unsigned long long)d[6], (unsigned long long)d[7]);
-      fprintf(stderr, "[verify] dfa results none %llu match %llu vm %llu match bytes %llu\n", (unsigned long long)d[9],
-              (unsigned long long)d[10], (unsigned long long)d[11], (unsigned long long)d[12]);
+        fprintf(stderr, "[verify] rule %s total %.3f ms max %.3f ms\n", rs->rules[kv.first].id.c_str(),
+                kv.second.first / 1e5, kv.second.second / 1e5);
     }
     HIP_TRY(hipGetLastError());
     if ((rc = read_ctrl(e, &c))) return rc;
     n_locs = c.locs;
-    if (n_locs <= e->locs.n) {
+    if (n_locs <= e->locs.n && c.n_caps <= e->caps.n && c.n_caps_big <= e->caps_big.n) {
       verified = true;
       break;
     }
-    loc_cap = n_locs;
+    // a list overflowed: grow it and re-run the search and the capture stages
+    loc_cap = std::max<uint64_t>(loc_cap, n_locs);
+    caps_cap = std::max<uint64_t>(caps_cap, c.n_caps);
+    caps_big_cap = std::max<uint64_t>(caps_big_cap, c.n_caps_big);
   }
   if (!verified) {
     set_last_error("internal: location buffers still overflowed after regrowing them");
@@ -3707,7 +3834,7 @@ void tsg_engine_free(tsg_engine* e) {
   e->job_start.release(); e->nsel.release(); e->cub_tmp.release(); e->locs.release(); e->locs2.release();
   e->scratch.release(); e->ctrl.release(); e->excl_jobs.release(); e->excl_out.release();
   e->nl_blocks.release(); e->nl_pre.release(); e->tail.release(); e->region_file.release(); e->region_tmp.release();
-  e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->fold_pos.release(); e->caps.release(); e->vprof.release(); e->fflags8.release();
+  e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->fold_pos.release(); e->caps.release(); e->caps_big.release(); e->vprof.release(); e->fflags8.release();
   if (e->h_flags) (void)hipHostFree(e->h_flags);
   if (e->h_stage) (void)hipHostFree(e->h_stage);
   e->gate_out.release(); e->gate_rules.release(); e->bin8.release(); e->strip_out.release();

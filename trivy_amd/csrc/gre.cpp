@@ -10,6 +10,7 @@
 #include <functional>
 
 #include "gre_fold_table.h"
+#include "gre_unicode_tables.h"
 
 namespace gre {
 
@@ -134,6 +135,25 @@ bool posix_class(const std::string& name, std::vector<uint32_t>* out) {
       *out = e.r;
       return true;
     }
+  }
+  return false;
+}
+
+// unicodeTable (regexp/syntax parse.go): "Any", then unicode.Categories, then
+// unicode.Scripts (tables: gre_unicode_tables.h, Unicode 15.0 as in Go 1.22).
+bool unicode_table(const std::string& name, std::vector<uint32_t>* out) {
+  out->clear();
+  if (name == "Any") {
+    *out = {0, kMaxRune};
+    return true;
+  }
+  for (uint32_t t = 0; t < kUniTableCount; ++t) {
+    if (name != kUniTables[t].name) continue;
+    for (uint32_t k = 0; k < kUniTables[t].n; ++k) {
+      out->push_back(kUniRanges[kUniTables[t].off + k][0]);
+      out->push_back(kUniRanges[kUniTables[t].off + k][1]);
+    }
+    return true;
   }
   return false;
 }
@@ -419,6 +439,39 @@ class Parser {
     return neg ? negate_class(tmp) : tmp;
   }
 
+  // \p{Name}, \pN, \P{Name}, \p{^Name} (parse.go parseUnicodeClass), i_ just
+  // past the 'p' / 'P'.  Under (?i) the table's simple-fold closure joins it
+  // before any negation (Go's unicode.FoldCategory / FoldScript additions).
+  std::vector<uint32_t> unicode_class(bool neg, const Flags& f) {
+    const size_t start = i_ - 2;  // the backslash
+    std::string name;
+    if (peek() != '{' || eof()) {
+      const size_t b = i_;
+      if (!eof()) next_rune();
+      name = p_.substr(b, i_ - b);
+    } else {
+      const size_t end = p_.find('}', i_);
+      if (end == std::string::npos)
+        throw SyntaxError{"invalid character class range: `" + p_.substr(start) + "`"};
+      name = p_.substr(i_ + 1, end - i_ - 1);
+      i_ = end + 1;
+    }
+    const std::string seq = p_.substr(start, i_ - start);
+    if (!name.empty() && name[0] == '^') {
+      neg = !neg;
+      name = name.substr(1);
+    }
+    std::vector<uint32_t> tab;
+    if (!unicode_table(name, &tab)) throw SyntaxError{"invalid character class range: `" + seq + "`"};
+    if (f.i) {
+      std::vector<uint32_t> folded;
+      for (size_t k = 0; k + 1 < tab.size(); k += 2) append_folded_range(folded, tab[k], tab[k + 1]);
+      tab.swap(folded);
+    }
+    clean_class(tab);
+    return neg ? negate_class(tab) : tab;
+  }
+
   // Simple escapes shared by class and non-class context; returns rune.
   uint32_t simple_escape(char c) {
     switch (c) {
@@ -482,7 +535,8 @@ class Parser {
         return;
       }
       case 'p': case 'P':
-        throw SyntaxError{"invalid character class range: Unicode classes (\\p) are not supported by this engine"};
+        items.push_back(class_node(unicode_class(c == 'P', f)));
+        return;
       case 'Q': {
         size_t end = p_.find("\\E", i_);
         size_t stop = end == std::string::npos ? p_.size() : end;
@@ -507,8 +561,11 @@ class Parser {
         out.insert(out.end(), g.begin(), g.end());
         return false;
       }
-      if (c == 'p' || c == 'P')
-        throw SyntaxError{"invalid character class range: Unicode classes (\\p) are not supported by this engine"};
+      if (c == 'p' || c == 'P') {
+        auto g = unicode_class(c == 'P', f);
+        out.insert(out.end(), g.begin(), g.end());
+        return false;
+      }
       *r = simple_escape(c);
       return true;
     }
@@ -1098,6 +1155,13 @@ A analyze(const Node* n) {
   return a;
 }
 
+bool has_assert(const Node* n) {
+  if (n->op == NO_ASSERT) return true;
+  for (auto* s : n->sub)
+    if (has_assert(s)) return true;
+  return false;
+}
+
 }  // namespace
 
 bool compile(const std::string& pattern, Compiled* out, std::string* err) {
@@ -1127,6 +1191,13 @@ bool compile(const std::string& pattern, Compiled* out, std::string* err) {
     out->min_len = a.minlen;
     out->max_len = a.maxlen;
     if (out->anchor.valid && a.nullable) out->anchor.valid = false;  // defensive
+    out->literal_exact = false;
+    if (out->anchor.valid && a.exact && !has_assert(root) && out->anchor.off_min == 0 && out->anchor.off_max == 0 &&
+        out->anchor.lits.size() == a.ex.size()) {
+      bool same = true;
+      for (auto& l : a.ex) same &= std::find(out->anchor.lits.begin(), out->anchor.lits.end(), l) != out->anchor.lits.end();
+      out->literal_exact = same;
+    }
     return true;
   } catch (const SyntaxError& e) {
     *err = "error parsing regexp: " + e.msg;

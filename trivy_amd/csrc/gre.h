@@ -58,6 +58,9 @@ struct Compiled {
   Anchor anchor;
   bool can_match_empty = false;
   uint32_t min_len = 0, max_len = 0;  // bytes
+  // The language is exactly the anchor's literal set (no assertions, no other
+  // constraint): on ASCII text, MatchString == "some anchor literal occurs".
+  bool literal_exact = false;
 };
 
 // Compile a Go regexp.  On syntax error returns false and sets *err to a

@@ -117,12 +117,14 @@ __host__ __device__ inline int prev_ctx_rune(const uint8_t* s, uint32_t i) {
 __host__ __device__ inline bool class_match(const ProgView& p, uint32_t ci, int r) {
   const ClassDesc& c = p.classes[ci];
   if (r < 128) return (c.ascii[r >> 5] >> (r & 31)) & 1;
-  const uint32_t* rg = p.ranges + c.range_off;
-  for (uint32_t k = 0; k < c.nranges; ++k) {
-    if ((uint32_t)r < rg[2 * k]) return false;
-    if ((uint32_t)r <= rg[2 * k + 1]) return true;
+  const uint32_t* rg = p.ranges + c.range_off;  // sorted, disjoint [lo, hi] pairs
+  uint32_t lo = 0, hi = c.nranges;
+  while (lo < hi) {  // first range whose hi >= r (Unicode tables run to hundreds of ranges)
+    const uint32_t m = (lo + hi) / 2;
+    if ((uint32_t)r > rg[2 * m + 1]) lo = m + 1;
+    else hi = m;
   }
-  return false;
+  return lo < c.nranges && (uint32_t)r >= rg[2 * lo];
 }
 
 __host__ __device__ inline bool inst_consumes(const Inst& in, const ProgView& p, int r) {
