@@ -14,7 +14,13 @@ HDRS      = $(wildcard $(SRC_DIR)/*.h) include/trivy_secret_gpu.h
 
 OBJS = $(patsubst $(SRC_DIR)/%.cpp,$(BUILD)/%.o,$(HOST_SRCS)) $(patsubst $(SRC_DIR)/%.hip,$(BUILD)/%.o,$(HIP_SRCS))
 
-all: $(LIB)
+# bench-only CPU baseline (bench.py cpu_baseline): not part of the product library
+BENCH_LIB = bench_cpu/libtsg_cpu_scan.so
+
+all: $(LIB) $(BENCH_LIB)
+
+$(BENCH_LIB): bench_cpu/cpu_scan.cpp $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $< -lpthread
 
 $(BUILD)/%.o: $(SRC_DIR)/%.cpp $(HDRS)
 	@mkdir -p $(BUILD)
@@ -28,6 +34,6 @@ $(LIB): $(OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJS) -lamdhip64
 
 clean:
-	rm -rf $(BUILD) $(LIB)
+	rm -rf $(BUILD) $(LIB) $(BENCH_LIB)
 
 .PHONY: all clean

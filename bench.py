@@ -14,8 +14,9 @@ builtin + 1000 generated gitleaks-style custom rules (tests/stress_rules.py;
 the automaton no longer fits k_scan_fast's LDS image).
 
 Prints ONE JSON line (rank 0).  Roofline is reported for the dominant kernel
-(k_scan, the HBM pass).  cpu_baseline times the CPU oracle (a Python port of
-the Go scanner; Go is not installed) on a bounded sample of the same corpus.
+(k_scan, the HBM pass).  cpu_baseline times bench_cpu/cpu_scan.cpp (the Go
+scanner's Scan restated in C++ on the repo's host Go-regexp VM, multi-threaded;
+Go is not installed) on a bounded sample of the same corpus.
 """
 from __future__ import annotations
 
@@ -285,80 +286,68 @@ def traffic_bytes(content_bytes):
     return round(t["hbm_read_bytes_per_launch"] * content_bytes / t["algorithmic_bytes_per_launch"])
 
 
-def cpu_baseline(N, c, seed, density, seconds, cores):
-    """Time the CPU oracle (Python port of Scan, one process per core) on a
-    bounded sample of the same corpus; generation is excluded from the clock."""
-    import multiprocessing as mp
-
-    from oracle import secret_oracle as O
-
-    # calibrate single-core rate on ~2 MB
-    sc = O.Scanner(None)
-    sample = []
-    total = 0
-    f = 0
-    while total < 2_000_000 and f < c["n_files"]:
-        n = int(c["sizes"][f])
-        if n <= (8 << 20):
-            buf = (ctypes.c_uint8 * max(1, n))()
-            N.lib.tsg_gen_file(seed, f, n, density, buf)
-            sample.append(("src/f%d.txt" % f, bytes(buf)[:n]))
-            total += n
-        f += 1
-    t0 = time.perf_counter()
-    for p, d in sample:
-        sc.scan(p, d)
-    rate1 = total / max(1e-6, time.perf_counter() - t0)
-    # size the sample for `seconds` of wall time on `cores` processes
-    want = int(rate1 * seconds * cores)
-    files = []
-    acc = 0
-    f = 0
-    while acc < want and f < c["n_files"]:
-        n = int(c["sizes"][f])
-        if n <= (8 << 20):
-            files.append((f, n, "src/f%d.txt" % f))
-            acc += n
-        f += 1
-    # pre-generate per worker shards, then time only the scanning
-    shards = [files[i::cores] for i in range(cores)]
-    ctx = mp.get_context("spawn")
-    with ctx.Pool(cores, initializer=_pool_init, initargs=(seed, density)) as pool:
-        pool.map(_pool_warm, range(cores))
-        out = pool.map(_pool_scan, shards)
-    dt = max(o[1] for o in out)  # slowest worker's scan time (generation excluded)
-    nbytes = sum(o[0] for o in out)
-    return dict(value=nbytes / dt / 1e9, unit="GB/s", cores=cores, kind="port",
-                sample=f"{len(files)} files / {nbytes/1e6:.1f} MB of the same corpus (first files in index order), "
-                       f"oracle/secret_oracle.py (Python restatement of Scanner.Scan over builtin rules, "
-                       f"Go regexp semantics via the `regex` module), {cores} processes, {dt:.1f}s wall; "
-                       f"Go reference not runnable (no Go toolchain)")
+def physical_cores():
+    """Physical cores of this host (unique (package, core) pairs in /proc/cpuinfo)."""
+    pairs, phys, core = set(), None, None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                phys = line.split(":")[1].strip()
+            elif line.startswith("core id"):
+                core = line.split(":")[1].strip()
+            elif not line.strip() and core is not None:
+                pairs.add((phys, core))
+                core = None
+    except OSError:
+        pass
+    return len(pairs) or None
 
 
-_POOL = {}
+def cpu_baseline(N, c, locs, rs, seconds, threads):
+    """Time bench_cpu/libtsg_cpu_scan.so — Scanner.Scan restated in C++ on
+    the repo's host Go-regexp VM, `threads` threads — on a bounded sample of the
+    same corpus: the first files in index order, copied from HBM (copy excluded
+    from the clock).  Per-file finding counts are checked against the GPU run."""
+    lib = ctypes.CDLL(os.path.join(ROOT, "bench_cpu", "libtsg_cpu_scan.so"))
+    lib.tsgb_cpu_scan.restype = ctypes.c_int
+    lib.tsgb_cpu_scan.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                  ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                  ctypes.POINTER(ctypes.c_double)]
+    off = c["off"]
+    poff = c["d_poff"].cpu().numpy()
+    gpu_counts = np.bincount(locs["file"].astype(np.int64), minlength=c["n_files"]) if len(locs) else \
+        np.zeros(c["n_files"], np.int64)
 
+    def run(k):
+        host = c["d_data"][: int(off[k])].cpu().numpy()
+        pb = c["d_paths"][: int(poff[k])].cpu().numpy().tobytes()
+        paths = [pb[int(poff[i]):int(poff[i + 1])] for i in range(k)]
+        arr = (ctypes.c_char_p * k)(*paths)
+        per = np.zeros(k, dtype=np.uint32)
+        tot, sec = ctypes.c_uint64(), ctypes.c_double()
+        N.check(lib.tsgb_cpu_scan(rs, host.ctypes.data, off.ctypes.data, k, ctypes.cast(arr, ctypes.c_void_p),
+                                  threads, per.ctypes.data, ctypes.byref(tot), ctypes.byref(sec)))
+        nbytes = int(off[k]) - k  # content bytes (NUL separators excluded)
+        return nbytes, sec.value, per
 
-def _pool_init(seed, density):
-    from oracle import secret_oracle as O
-    from trivy_amd import _native as N
-    _POOL.update(seed=seed, density=density, O=O, N=N, sc=O.Scanner(None), cache={})
-
-
-def _pool_warm(_):
-    return 0
-
-
-def _pool_scan(files):
-    N, sc = _POOL["N"], _POOL["sc"]
-    datas = []
-    for f, n, path in files:
-        buf = (ctypes.c_uint8 * max(1, n))()
-        N.lib.tsg_gen_file(_POOL["seed"], f, n, _POOL["density"], buf)
-        datas.append((path, bytes(buf)[:n]))
-    t0 = time.perf_counter()
-    for path, d in datas:
-        sc.scan(path, d)
-    return sum(len(d) for _, d in datas), time.perf_counter() - t0
+    # calibrate on ~64 MB, then size the sample for `seconds` of wall time
+    k0 = int(np.searchsorted(off, 64 << 20))
+    k0 = max(1, min(k0, c["n_files"]))
+    b0, t0, _ = run(k0)
+    want = min(int(b0 / max(t0, 1e-6) * seconds), 16 << 30, int(off[-1]))
+    k = max(k0, min(c["n_files"], int(np.searchsorted(off, want))))
+    nbytes, dt, per = run(k)
+    agree = int((per.astype(np.int64) == gpu_counts[:k]).sum())
+    phys = physical_cores()
+    return dict(value=nbytes / dt / 1e9, unit="GB/s", cores=threads, kind="cpp-restatement",
+                physical_cores=phys,
+                sample=f"{k} files / {nbytes / 1e6:.1f} MB of the same corpus (first files in index order, copied "
+                       f"from HBM), {dt:.1f}s wall on {threads} threads (this box's CPU share"
+                       + (f" of {phys} physical cores" if phys else "") + "); "
+                       "bench_cpu/cpu_scan.cpp: Scanner.Scan restated in C++ on the repo's host Go-regexp VM "
+                       "(not Go: no Go toolchain in the image); per-file finding counts equal the GPU's on "
+                       f"{agree}/{k} files",
+                files_agree=agree, files=k)
 
 
 def main():
@@ -576,8 +565,8 @@ def main():
                                    n_sample=300 if args.config == 2 else 24, oracle_cfg=cfg_path if cfg else None)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.config in (0, 2):
-        cores = args.cpu_cores or min(16, os.cpu_count() or 1)
-        cpu = cpu_baseline(N, c, seed, args.density, args.cpu_seconds, cores)
+        cores = args.cpu_cores or min(16, len(os.sched_getaffinity(0)))
+        cpu = cpu_baseline(N, c, locs, rs, args.cpu_seconds, cores)
     if rank == 0:
         out = {
             "metric": "secret-scan GB/s (whole node), builtin rules, 1/2/4/8 MI355X; % HBM peak",
