@@ -33,7 +33,26 @@ $(BUILD)/%.o: $(SRC_DIR)/%.hip $(HDRS)
 $(LIB): $(OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJS) -lamdhip64
 
-clean:
-	rm -rf $(BUILD) $(LIB) $(BENCH_LIB)
+# ablation build for tools/*.sh A/B runs (TSG_LIB_VARIANT=exp selects it in
+# trivy_amd/_native.py): dead kernel shapes + getenv switches, some of which
+# give wrong results by design.  Never the product library.
+EXP_LIB  = trivy_amd/libtrivy_secret_gpu_exp.so
+EXP_OBJS = $(patsubst $(SRC_DIR)/%.cpp,build_exp/%.o,$(HOST_SRCS)) $(patsubst $(SRC_DIR)/%.hip,build_exp/%.o,$(HIP_SRCS))
 
-.PHONY: all clean
+exp: $(EXP_LIB)
+
+build_exp/%.o: $(SRC_DIR)/%.cpp $(HDRS)
+	@mkdir -p build_exp
+	$(HIPCC) $(HIPFLAGS) -DTSG_EXPERIMENTS -c $< -o $@
+
+build_exp/%.o: $(SRC_DIR)/%.hip $(HDRS)
+	@mkdir -p build_exp
+	$(HIPCC) $(HIPFLAGS) -DTSG_EXPERIMENTS -c $< -o $@
+
+$(EXP_LIB): $(EXP_OBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(EXP_OBJS) -lamdhip64
+
+clean:
+	rm -rf $(BUILD) build_exp $(LIB) $(BENCH_LIB) $(EXP_LIB)
+
+.PHONY: all clean exp

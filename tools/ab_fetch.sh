@@ -1,4 +1,6 @@
 #!/bin/bash
+# needs the ablation build: `make exp` here, then TSG_LIB_VARIANT=exp (exported below)
+export TSG_LIB_VARIANT=exp
 # Per k_scan_fast shape: kernel time (trace) and HBM read bytes (FETCH_SIZE pass) on an 8 GB corpus.
 set -o pipefail
 export TMPDIR=/tmp

@@ -1,4 +1,6 @@
 #!/bin/bash
+# needs the ablation build: `make exp` here, then TSG_LIB_VARIANT=exp (exported below)
+export TSG_LIB_VARIANT=exp
 # A/B the k_scan_fast shapes (TSG_FAST_VARIANT=chains x vectors) on the GPU box:
 # parity tests once, then per variant a bench line (with parity properties)
 # under a rocprofv3 kernel trace, printing per-kernel average times.

@@ -1,4 +1,6 @@
 #!/bin/bash
+# needs the ablation build: `make exp` here, then TSG_LIB_VARIANT=exp (exported below)
+export TSG_LIB_VARIANT=exp
 # Ablation of k_scan_big (configs[4]) by TSG_REPORT_MODE: 0 normal, 8 no inline
 # reports, 16 cold states answered by the root row, 24 both.  Kernel time from
 # rocprofv3; modes != 0 give wrong findings (timing only, no parity).

@@ -1,4 +1,6 @@
 #!/bin/bash
+# needs the ablation build: `make exp` here, then TSG_LIB_VARIANT=exp (exported below)
+export TSG_LIB_VARIANT=exp
 # Timing-only ablation of k_scan_fast (TSG_SCAN_MODE bits: 1 = no events, 2 = no newline count,
 # 4 = loads from the first MiB only (L2-resident), so HBM is out of the picture).
 set -o pipefail

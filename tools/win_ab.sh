@@ -1,4 +1,6 @@
 #!/bin/bash
+# needs the ablation build: `make exp` here, then TSG_LIB_VARIANT=exp (exported below)
+export TSG_LIB_VARIANT=exp
 # A/B of k_scan_fast's event-check window (TSG_EVENT_WIN = 8-byte groups per
 # wave-level check), kernel time from rocprofv3 + bench parity properties.
 set -o pipefail

@@ -11,7 +11,12 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtrivy_secret_gpu.so")
+# TSG_LIB_VARIANT selects a diagnostic build of the same sources: "exp" = the
+# ablation build (`make exp`, tools/*.sh only), "asan" = host ASan/UBSan
+# (`make -f tools/asan.mk`, tests/test_asan.py on the CPU only)
+_VARIANT = os.environ.get("TSG_LIB_VARIANT", "")
+LIB_PATH = os.path.join(
+    _HERE, f"libtrivy_secret_gpu_{_VARIANT}.so" if _VARIANT in ("exp", "asan") else "libtrivy_secret_gpu.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

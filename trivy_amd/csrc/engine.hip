@@ -815,6 +815,7 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
   if (lane == 0) P.ev_counts[wave] = ev_count < P.ev_cap_per_wave ? ev_count : P.ev_cap_per_wave;
 }
 
+#ifdef TSG_EXPERIMENTS  // A/B shapes measured slower; not in the product library
 // Deep-prefetch shape of k_scan_fast (one chain per lane): the lane's span
 // streams through a ring of R = D + 1 register sets of V 16-byte vectors, and
 // step s issues the loads of step s + D before walking set s mod R — so every
@@ -997,6 +998,8 @@ __global__ __launch_bounds__(1024) void k_scan_ring(ScanParams P) {
   }
   if (lane == 0) P.ev_counts[wave] = ev_count < P.ev_cap_per_wave ? ev_count : P.ev_cap_per_wave;
 }
+
+#endif  // TSG_EXPERIMENTS
 
 // Resolve k_scan_fast's events.  Each event is replayed on an LDS copy of the
 // scan image with the output tables (out_off/out_pat/pats/pat_bytes) behind
@@ -3144,6 +3147,17 @@ void censored_lines(std::vector<DevLoc>& locs) {
   }
 }
 
+// Ablation / diagnostic switches: read only in a
+// -DTSG_EXPERIMENTS build; the product library ignores the environment.
+inline const char* experiment_env(const char* name) {
+#ifdef TSG_EXPERIMENTS
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+
 int read_ctrl(tsg_engine* e, Ctrl* h) {
   HIP_TRY(hipMemcpyAsync(h, e->ctrl.p, sizeof(Ctrl), hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -3178,9 +3192,14 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
   const AcDev& ac = P.rs.ac;
   if (ac.fast_lds) {
     // final partial region: zero-padded copy (with 8 bytes of warm-up context)
-    // variant: chains per lane x 16-byte vectors per chain step (A/B via TSG_FAST_VARIANT)
-    int chains = kFastChains, vecs = kFastVecs;
-    bool ring = false;  // TSG_FAST_VARIANT=ring: the two-chain register ring (A/B; spills today)
+    // product shape: one chain per lane, 8 x 16-byte vectors per chain step,
+    // one event check per kFastEventWin groups.  The other shapes, ablation
+    // modes and event windows (all measured slower; modes give
+    // wrong results) exist only in a -DTSG_EXPERIMENTS build.
+    int chains = kFastChains;
+    [[maybe_unused]] int vecs = kFastVecs;
+    bool ring = false;
+#ifdef TSG_EXPERIMENTS
     int deep_v = 0, deep_d = 0;  // TSG_FAST_VARIANT=d<V>x<D>: k_scan_deep
     int mode = 0;                // TSG_SCAN_MODE: timing experiments only (see fast_group)
     if (const char* m = getenv("TSG_SCAN_MODE")) mode = atoi(m);
@@ -3196,6 +3215,7 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
       chains = kFastChains;
       vecs = kFastVecs;
     }
+#endif
     const uint64_t unit = ring ? (uint64_t)kNlBlock : (uint64_t)chains * kNlBlock;
     P.tail_base = (P.nbytes / unit) * unit;
     const uint64_t lead = P.tail_base >= 8 ? 8 : P.tail_base;
@@ -3209,9 +3229,7 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     const uint64_t n_spans = (P.nbytes + kNlBlock - 1) / kNlBlock;
     HIP_TRY(e->span_hi.ensure(n_spans + 1));
     P.span_hi = e->span_hi.p;
-    // shape: 1x8 = 1024 threads, one block per CU (120 VGPRs); 1x4 = 768
-    // threads, two blocks per CU (two LDS images, 24 waves); 2x4 = 1024, one
-    // every shape: 1024 threads, one block per CU (the image takes most of the LDS)
+    // 1024 threads, one block per CU (the image takes most of the LDS)
     const uint32_t nt = 1024;
     const uint32_t per_cu = 1;
     const uint32_t blocks = (uint32_t)std::max<uint64_t>(
@@ -3229,6 +3247,7 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     HIP_TRY(hipMemsetAsync(&P.ctrl->ev_overflow, 0, 8, s));
     // (the image lives in the kernel's static kFastImgMax array: no dynamic LDS)
     if (e->events) HIP_TRY(hipEventRecord(e->ev[10], s));
+#ifdef TSG_EXPERIMENTS
     if (ring) hipLaunchKernelGGL(k_scan_ring, dim3(blocks), dim3(nt), 0, s, P);
 #define TSG_DEEP(VV, DD, M)                                                                 \
   else if (deep_v == VV && deep_d == DD && mode == M)                                      \
@@ -3240,12 +3259,15 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     TSG_MODE(1) TSG_MODE(2) TSG_MODE(3) TSG_MODE(4) TSG_MODE(5) TSG_MODE(6) TSG_MODE(7)
 #undef TSG_MODE
     else if (chains == 1 && vecs == 8 && win == 2) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 2>), dim3(blocks), dim3(nt), 0, s, P);
-    else if (chains == 1 && vecs == 8 && win == 4) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 4>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1 && vecs == 8 && win == 8) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 8>), dim3(blocks), dim3(nt), 0, s, P);
+    else if (chains == 1 && vecs == 8 && win == 4) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 4>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1 && vecs == 8) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1) hipLaunchKernelGGL((k_scan_fast<1, 4, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     else if (vecs == 4) hipLaunchKernelGGL((k_scan_fast<2, 4, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     else hipLaunchKernelGGL((k_scan_fast<2, 2, 1024>), dim3(blocks), dim3(nt), 0, s, P);
+#else
+    hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, kFastEventWin>), dim3(blocks), dim3(nt), 0, s, P);
+#endif
     HIP_TRY(hipGetLastError());
     if (e->events) HIP_TRY(hipEventRecord(e->ev[11], s));
     e->fast_timed = e->events;
@@ -3254,7 +3276,7 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_fold_special, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_spans + 255) / 256, 2048))),
                        dim3(256), 0, s, P, n_spans);
-  } else if (P.big.blob && !getenv("TSG_NO_BIG")) {
+  } else if (P.big.blob && !experiment_env("TSG_NO_BIG")) {
     const uint64_t nchunks = (P.nbytes + kChunk - 1) / kChunk;
     const uint32_t blocks = (uint32_t)std::max<uint64_t>(
         1, std::min<uint64_t>((nchunks + kBigThreads - 1) / kBigThreads, (uint64_t)e->num_cus));
@@ -3262,7 +3284,8 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
                                 (int)P.big.blob_bytes));
     const uint64_t nlanes = (uint64_t)blocks * kBigThreads;
     P.big_rec_cap = 64;  // 8-byte records per lane (~9 per lane per 10 GB on configs[4])
-    if (const char* c = getenv("TSG_BIG_REC_CAP")) P.big_rec_cap = (uint32_t)atoi(c);  // tests: force the inline fallback
+    // test hook (same results, exercises the inline fallback): tests/test_gpu_stress.py
+    if (const char* c = getenv("TSG_BIG_REC_CAP")) P.big_rec_cap = (uint32_t)std::max(0, atoi(c));
     HIP_TRY(e->big_rec.ensure(nlanes * P.big_rec_cap));
     HIP_TRY(e->big_nrec.ensure(nlanes));
     P.big_rec = e->big_rec.p;
@@ -3280,7 +3303,7 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     // the LDS halves the blocks per CU.  TSG_GEN_LDS_KB re-enables it for A/B.
     P.gen_lds_rows = lds_table ? ac.nstates : 0;
     if (!lds_table)
-      if (const char* kb = getenv("TSG_GEN_LDS_KB"))
+      if (const char* kb = experiment_env("TSG_GEN_LDS_KB"))
         P.gen_lds_rows = (uint32_t)std::min<size_t>(ac.nstates, ((size_t)atoi(kb) << 10) / (2u * ac.nclasses));
     const size_t lds = 256 + kTileLds + (size_t)P.gen_lds_rows * ac.nclasses * 2;
     const uint64_t nsteps = (P.nbytes + kBlockBytes - 1) / kBlockBytes;
@@ -3403,7 +3426,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   HIP_TRY(e->fold_pos.ensure(std::max<uint64_t>(1 << 16, e->fold_need)));
   P.fold_pos = e->fold_pos.p;
   P.fold_cap = e->fold_pos.n;
-  if (const char* m = getenv("TSG_REPORT_MODE")) P.report_mode = (uint32_t)atoi(m);
+  if (const char* m = experiment_env("TSG_REPORT_MODE")) P.report_mode = (uint32_t)atoi(m);
   const uint64_t n_nlb = nbytes / kNlBlock + 2;
   HIP_TRY(e->nl_blocks.ensure(n_nlb));
   HIP_TRY(e->nl_pre.ensure(n_nlb));
@@ -3559,7 +3582,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     V.cap_cap = e->caps.n;
     V.caps_big = e->caps_big.p;
     V.cap_big_cap = e->caps_big.n;
-    const bool prof = getenv("TSG_PROFILE_VERIFY") != nullptr;
+    const bool prof = experiment_env("TSG_PROFILE_VERIFY") != nullptr;
     if (prof) HIP_TRY(e->vprof.ensure(4ull * n_jobs + 16));
     if (prof) HIP_TRY(hipMemsetAsync(e->vprof.p, 0, (4ull * n_jobs + 16) * 8, s));
     V.prof = prof ? e->vprof.p : nullptr;

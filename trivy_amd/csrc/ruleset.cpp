@@ -150,8 +150,6 @@ static bool build_ac_depth(tsg_ruleset* rs, int depth, std::string* err) {
     ac.fail.assign(S, 0);
     for (int n = 0; n < S; ++n) ac.fail[n] = (uint16_t)perm[fail[inv[n]]];
   }
-  int first_out = S;
-  for (int st = S - 1; st >= 0 && !outs[st].empty(); --st) first_out = st;
   ac.nstates = (uint32_t)S;
   ac.nclasses = (uint32_t)ncls;
   ac.delta.assign((size_t)S * ncls, 0);
