@@ -53,7 +53,7 @@ struct Vm {
 
 gre::ProgView view(const gre::Prog& p) {
   return gre::ProgView{p.inst.data(), p.classes.data(), p.ranges.data(), (uint32_t)p.inst.size(), p.start,
-                       (uint32_t)p.ncap};
+                       (uint32_t)p.ncap, p.nvis};
 }
 
 // Go's Prog.Prefix: the case-sensitive literal every match starts with.

@@ -137,6 +137,11 @@ int tsg_ruleset_scan_image(const tsg_ruleset* rs, uint8_t* buf, size_t cap, size
 /* Instruction count and capture slots of rule i's compiled regex. */
 int tsg_ruleset_rule_prog(const tsg_ruleset* rs, size_t i, uint32_t* n_inst, uint32_t* n_cap);
 
+/* Secret-group span rule of rule i: when *valid, the group of every ASCII
+ * match [ms, me) is [ms + *pre, me - *suf), *len filling a side that is -1
+ * (k_verify then skips the capture search); *valid = 0: the search decides. */
+int tsg_ruleset_group_span(const tsg_ruleset* rs, size_t i, int* valid, int* pre, int* len, int* suf);
+
 /* Candidate filter of rule i, run on host text from anchor position h:
  * *accept = 0 only when no match of the rule can contain an anchor hit at h
  * (k_expand drops such hits); *n_states = its DFA size (0 = no filter). */

@@ -56,6 +56,11 @@ struct RuleDev {
   uint32_t dfa_size;            // u16 entries of its table (k_verify stages it in LDS when it fits)
   uint32_t dfa_smatch;          // bit 0/1: start0/start1 is a match state
   uint32_t dfa_sym;             // first rune-symbol column | 0x80000000 when other non-ASCII runes are one symbol
+  // secret group from the match span alone (gre::group_span; one group, ASCII
+  // matches): group = [ms + grp_pre, me - grp_suf), grp_len filling a missing
+  // side; grp_fast = 0 -> the capture search (k_captures)
+  uint32_t grp_fast;
+  int32_t grp_pre, grp_len, grp_suf;
 };
 
 struct PatDev {

@@ -1901,8 +1901,10 @@ constexpr uint32_t kBigBsWords = 9216;    // and their arenas (36 KiB: P x W <= 
 
 __device__ bool bitstate_captures(const gre::ProgView& p, const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me,
                                   const uint32_t* gnum, uint32_t ng, uint32_t* area, uint32_t words, int32_t* gcap) {
-  const uint32_t P = p.ninst;
-  const uint32_t end = me + 16 < n ? me + 16 : n;  // positions the search may visit: [ms, end]
+  // visited rows for the join points only (Inst::vis); a path that consumes
+  // past me can never end at me, so positions stay in [ms, me]
+  const uint32_t P = p.nvis;
+  const uint32_t end = me;
   const uint32_t W = end - ms + 1;
   const uint32_t vis_words = (P * W + 31) / 32;
   // arena: visited bits | job stack | the 8 tracked capture slots (gcap, the last 8 words)
@@ -1930,12 +1932,13 @@ __device__ bool bitstate_captures(const gre::ProgView& p, const uint8_t* text, u
     uint32_t pos = ms + v;
     uint32_t pc = kind == 1 ? p.inst[pc0].arg : pc0;  // ALT: the second branch
     for (;;) {
-      if (pc == 0) break;
-      if (pos > end) return false;
-      const uint32_t bit = pc * W + (pos - ms);
-      if (vis[bit >> 5] & (1u << (bit & 31))) break;
-      vis[bit >> 5] |= 1u << (bit & 31);
+      if (pc == 0 || pos > end) break;
       const gre::Inst in = p.inst[pc];
+      if (in.vis != gre::kNoVis) {
+        const uint32_t bit = in.vis * W + (pos - ms);
+        if (vis[bit >> 5] & (1u << (bit & 31))) break;
+        vis[bit >> 5] |= 1u << (bit & 31);
+      }
       if (in.op == gre::I_ALT) {
         if (sp >= stk_cap) return false;
         stk[sp++] = (1u << 30) | (pc << 16) | (pos - ms);
@@ -2039,6 +2042,20 @@ __device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, ui
     unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
     if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, ms, me, 0, 0, 0, 0};
     return;
+  }
+  if (rd.grp_fast) {  // the group's span follows from [ms, me) on ASCII text (gre::group_span)
+    bool ascii = true;
+    for (uint32_t q = ms; q < me && ascii; ++q) ascii = as_global<gu8>(text)[q] < 0x80;
+    if (ascii) {
+      const int64_t gs = rd.grp_pre >= 0 ? (int64_t)ms + rd.grp_pre : (int64_t)me - rd.grp_suf - rd.grp_len;
+      const int64_t ge = rd.grp_suf >= 0 ? (int64_t)me - rd.grp_suf : gs + rd.grp_len;
+      if (gs >= (int64_t)ms && gs <= ge && ge <= (int64_t)me) {
+        unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
+        if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, (uint64_t)gs, (uint64_t)ge, 0, 0, 0, 0};
+        return;
+      }
+      // (unreachable for a real match of the rule; the capture search decides)
+    }
   }
   unsigned long long idx = atomicAdd(&V.ctrl->n_caps, 1ull);
   if (idx < V.cap_cap) V.caps[idx] = make_uint4(fi, rule, ms, me);
@@ -2672,7 +2689,7 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   for (size_t k = 0; k < rs->regexes.size(); ++k) {
     const gre::Prog& p = rs->regexes[k].c.prog;
     views.push_back(gre::ProgView{im.inst.p + offs[k].i, im.classes.p + offs[k].c, im.ranges.p,
-                                  (uint32_t)p.inst.size(), p.start, (uint32_t)p.ncap});
+                                  (uint32_t)p.inst.size(), p.start, (uint32_t)p.ncap, p.nvis});
   }
   // per-program anchor literals for the MatchString prefilter
   std::vector<uint32_t> lit_off{0};
@@ -2765,6 +2782,13 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
         for (size_t g = 0; g < c.prog.cap_names.size(); ++g)
           if (c.prog.cap_names[g] == r.group_name) group_slots.push_back((uint32_t)g);
       d.group_n = (uint32_t)group_slots.size() - d.group_off;
+      if (d.use_groups && d.group_n == 1) {
+        const gre::GroupSpan gs = gre::group_span(c.prog, group_slots[d.group_off] / 2);
+        d.grp_fast = gs.valid ? 1u : 0u;
+        d.grp_pre = gs.pre;
+        d.grp_len = gs.len;
+        d.grp_suf = gs.suf;
+      }
     }
     d.gate_implied = r.gate_implied;  // ruleset.cpp: every anchor literal contains a keyword
     if (!d.gate_implied || r.fold_gate)  // exact keyword bits: non-implied gates, K/ſ-spelled hits

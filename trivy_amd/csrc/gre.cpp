@@ -1164,6 +1164,183 @@ bool has_assert(const Node* n) {
 
 }  // namespace
 
+
+// Capture-group span from the whole match alone (see gre.h GroupSpan).  The
+// program is a graph (consuming insts weigh 1 rune, the rest 0); a distance is
+// "fixed" when every path has the same rune count, found by propagation in
+// which a second, different distance (or a consuming cycle) turns a node into
+// "many".  The group's CAP pair must be unique and must dominate every MATCH.
+GroupSpan group_span(const Prog& p, uint32_t slot) {
+  GroupSpan g;
+  const int n = (int)p.inst.size();
+  int open = -1, close = -1;
+  for (int pc = 0; pc < n; ++pc) {
+    const Inst& in = p.inst[pc];
+    if (in.op != I_CAP) continue;
+    if (in.arg == 2 * slot) {
+      if (open >= 0) return g;
+      open = pc;
+    } else if (in.arg == 2 * slot + 1) {
+      if (close >= 0) return g;
+      close = pc;
+    }
+  }
+  if (open < 0 || close < 0) return g;
+  auto succ = [&](int pc, int* out) -> int {  // successor count, out[0..1]
+    const Inst& in = p.inst[pc];
+    switch (in.op) {
+      case I_FAIL:
+      case I_MATCH: return 0;
+      case I_ALT: out[0] = (int)in.out; out[1] = (int)in.arg; return 2;
+      default: out[0] = (int)in.out; return 1;
+    }
+  };
+  auto weight = [&](int pc) {
+    const uint8_t op = p.inst[pc].op;
+    return (op == I_RUNE || op == I_RUNE1 || op == I_ANY || op == I_ANYNL) ? 1 : 0;
+  };
+  // MATCH reachable from start when node `cut` is removed?
+  auto reaches_match = [&](int cut) {
+    std::vector<uint8_t> seen(n, 0);
+    std::vector<int> st{(int)p.start};
+    while (!st.empty()) {
+      const int pc = st.back();
+      st.pop_back();
+      if (pc == cut || pc <= 0 || pc >= n || seen[pc]) continue;
+      seen[pc] = 1;
+      if (p.inst[pc].op == I_MATCH) return true;
+      int o[2];
+      for (int k = succ(pc, o); k-- > 0;) st.push_back(o[k]);
+    }
+    return false;
+  };
+  if (reaches_match(open) || reaches_match(close)) return g;  // the group may not participate
+  constexpr int kUnset = -1, kMany = -2;
+  // forward: runes from the match start to each node's entry
+  std::vector<int> fw(n, kUnset);
+  {
+    std::vector<int> wl{(int)p.start};
+    fw[p.start] = 0;
+    while (!wl.empty()) {
+      const int pc = wl.back();
+      wl.pop_back();
+      int o[2];
+      const int k = succ(pc, o);
+      for (int q = 0; q < k; ++q) {
+        const int t = o[q];
+        if (t <= 0 || t >= n) continue;
+        const int d = fw[pc] == kMany ? kMany : fw[pc] + weight(pc);
+        if (fw[t] == kUnset) fw[t] = d;
+        else if (fw[t] != d && fw[t] != kMany) fw[t] = kMany;
+        else continue;
+        wl.push_back(t);
+      }
+    }
+  }
+  // backward: runes from each node's entry to the match end
+  std::vector<std::vector<int>> pred(n);
+  for (int pc = 1; pc < n; ++pc) {
+    int o[2];
+    for (int k = succ(pc, o); k-- > 0;)
+      if (o[k] > 0 && o[k] < n) pred[o[k]].push_back(pc);
+  }
+  std::vector<int> bw(n, kUnset);
+  {
+    std::vector<int> wl;
+    for (int pc = 1; pc < n; ++pc)
+      if (p.inst[pc].op == I_MATCH) {
+        bw[pc] = 0;
+        wl.push_back(pc);
+      }
+    while (!wl.empty()) {
+      const int pc = wl.back();
+      wl.pop_back();
+      for (int t : pred[pc]) {
+        const int d = bw[pc] == kMany ? kMany : bw[pc] + weight(t);
+        if (bw[t] == kUnset) bw[t] = d;
+        else if (bw[t] != d && bw[t] != kMany) bw[t] = kMany;
+        else continue;
+        wl.push_back(t);
+      }
+    }
+  }
+  // group length: runes from `open` to `close` on every path between them
+  int glen = kUnset;
+  {
+    std::vector<int> d(n, kUnset);
+    std::vector<int> wl{open};
+    d[open] = 0;
+    while (!wl.empty()) {
+      const int pc = wl.back();
+      wl.pop_back();
+      if (pc == close) continue;
+      int o[2];
+      const int k = succ(pc, o);
+      for (int q = 0; q < k; ++q) {
+        const int t = o[q];
+        if (t <= 0 || t >= n) continue;
+        const int nd = d[pc] == kMany ? kMany : d[pc] + weight(pc);
+        if (d[t] == kUnset) d[t] = nd;
+        else if (d[t] != nd && d[t] != kMany) d[t] = kMany;
+        else continue;
+        wl.push_back(t);
+      }
+    }
+    glen = d[close];
+  }
+  // a CAP on a cycle would show up as "many" below only if the cycle consumes;
+  // an empty cycle through it is rejected outright
+  auto on_cycle = [&](int node) {
+    std::vector<uint8_t> seen(n, 0);
+    std::vector<int> st;
+    int o[2];
+    for (int k = succ(node, o); k-- > 0;) st.push_back(o[k]);
+    while (!st.empty()) {
+      const int pc = st.back();
+      st.pop_back();
+      if (pc <= 0 || pc >= n || seen[pc]) continue;
+      if (pc == node) return true;
+      seen[pc] = 1;
+      for (int k = succ(pc, o); k-- > 0;) st.push_back(o[k]);
+    }
+    return false;
+  };
+  if (on_cycle(open) || on_cycle(close)) return g;
+  g.pre = fw[open] >= 0 ? fw[open] : -1;
+  g.suf = bw[close] >= 0 ? bw[close] : -1;
+  g.len = glen >= 0 ? glen : -1;
+  g.valid = (g.pre >= 0 || (g.suf >= 0 && g.len >= 0)) && (g.suf >= 0 || (g.pre >= 0 && g.len >= 0));
+  return g;
+}
+
+// Inst::vis rows: the start plus every instruction with >= 2 predecessors
+// among the instructions reachable from the start.
+static void assign_vis_rows(Prog* p) {
+  const size_t n = p->inst.size();
+  std::vector<uint32_t> indeg(n, 0);
+  std::vector<uint8_t> seen(n, 0);
+  std::vector<uint32_t> st{p->start};
+  while (!st.empty()) {
+    const uint32_t pc = st.back();
+    st.pop_back();
+    if (pc == 0 || pc >= n || seen[pc]) continue;
+    seen[pc] = 1;
+    const Inst& in = p->inst[pc];
+    if (in.op == I_FAIL || in.op == I_MATCH) continue;
+    const uint32_t o[2] = {in.out, in.arg};
+    for (int k = 0; k < (in.op == I_ALT ? 2 : 1); ++k)
+      if (o[k] && o[k] < n) {
+        ++indeg[o[k]];
+        st.push_back(o[k]);
+      }
+  }
+  p->nvis = 0;
+  for (size_t pc = 0; pc < n; ++pc) {
+    const bool row = seen[pc] && (pc == p->start || indeg[pc] >= 2);
+    p->inst[pc].vis = row ? (uint16_t)p->nvis++ : kNoVis;
+  }
+}
+
 bool compile(const std::string& pattern, Compiled* out, std::string* err) {
   try {
     Parser ps(pattern);
@@ -1181,6 +1358,7 @@ bool compile(const std::string& pattern, Compiled* out, std::string* err) {
     }
     out->prog.ncap = 2 * (ps.ncap() + 1);
     out->prog.cap_names = ps.names();
+    assign_vis_rows(&out->prog);
     if (out->prog.inst.size() >= 65535) {
       *err = "expression too large";
       return false;

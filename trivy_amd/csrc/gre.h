@@ -67,6 +67,21 @@ struct Compiled {
 // message in the style of Go's regexp/syntax errors.
 bool compile(const std::string& pattern, Compiled* out, std::string* err);
 
+// Where capture group `slot` sits inside ANY match of the program, from the
+// match span alone: on a match [ms, me) whose bytes are all ASCII (one byte
+// per rune) the group is [ms + pre, me - suf), with len filling in a missing
+// side.  Valid only when the group's CAP pair is unique, on no cycle, and on
+// every path to MATCH (it always participates), and each side is fixed: every
+// program path gives the same rune count (-1 = not fixed).  Lets k_verify skip
+// the capture search for the `(?P<key>..){0,25}..(?P<secret>[..]{N})['"]`
+// family of builtin rules (builtin-rules.go), whose group ends one rune before
+// the match end.
+struct GroupSpan {
+  bool valid = false;
+  int pre = -1, len = -1, suf = -1;
+};
+GroupSpan group_span(const Prog& p, uint32_t slot);
+
 // Unicode simple-fold orbit lookup (next member, or r itself when trivial).
 uint32_t simple_fold(uint32_t r);
 

@@ -35,10 +35,17 @@ enum : uint8_t {
 struct Inst {
   uint8_t op;
   uint8_t empty;
-  uint16_t pad;
+  uint16_t vis;  // bit-state visited-row index (join points only), kNoVis elsewhere
   uint32_t out;
   uint32_t arg;
 };
+
+// Only join points (instructions with two or more reachable predecessors,
+// plus the start) get a visited row in the capture backtracker: every cycle
+// passes through one, and an instruction with a single predecessor is reached
+// at most as often as that predecessor (bounded), so memoising the join points
+// keeps the search polynomial with a fraction of the (pc, pos) bits.
+constexpr uint16_t kNoVis = 0xFFFF;
 
 struct ClassDesc {
   uint32_t ascii[4];   // membership bitmap for runes < 128
@@ -52,6 +59,7 @@ struct Prog {
   std::vector<uint32_t> ranges;
   uint32_t start = 0;
   int ncap = 2;                         // 2 * (number of groups + 1)
+  uint32_t nvis = 0;                    // instructions with a visited row (Inst::vis)
   std::vector<std::string> cap_names;   // index = group number; [0] = ""
 };
 
@@ -63,6 +71,7 @@ struct ProgView {
   uint32_t ninst;
   uint32_t start;
   uint32_t ncap;
+  uint32_t nvis;
 };
 
 }  // namespace gre

@@ -621,6 +621,26 @@ int tsg_ruleset_rule_prog(const tsg_ruleset* rs, size_t i, uint32_t* n_inst, uin
   return TSG_OK;
 }
 
+// Secret-group span rule of rule i (gre::group_span; what k_verify uses to
+// skip the capture search): *valid = 0 when the capture search decides.
+int tsg_ruleset_group_span(const tsg_ruleset* rs, size_t i, int* valid, int* pre, int* len, int* suf) {
+  if (!rs || i >= rs->rules.size() || !valid) return TSG_ERR_INVALID_ARG;
+  const RuleHost& r = rs->rules[i];
+  gre::GroupSpan g;
+  if (r.regex >= 0 && !r.group_name.empty()) {
+    const gre::Prog& p = rs->regexes[r.regex].c.prog;
+    int slot = -1, count = 0;
+    for (size_t k = 0; k < p.cap_names.size(); ++k)
+      if (p.cap_names[k] == r.group_name) slot = (int)k, ++count;
+    if (count == 1) g = gre::group_span(p, (uint32_t)slot);
+  }
+  *valid = g.valid ? 1 : 0;
+  if (pre) *pre = g.pre;
+  if (len) *len = g.len;
+  if (suf) *suf = g.suf;
+  return TSG_OK;
+}
+
 // Verify DFA of rule i on host text: 1 = match [s, *me), 0 = none, 2 = not
 // decidable by the DFA (no DFA, byte >= 0x80, s at the end) -> Pike VM.
 int tsg_ruleset_dfa_check(const tsg_ruleset* rs, size_t i, const uint8_t* text, size_t len, size_t s,
@@ -664,7 +684,7 @@ struct HostVm {
 
 static gre::ProgView view_of(const gre::Prog& p) {
   return gre::ProgView{p.inst.data(), p.classes.data(), p.ranges.data(), (uint32_t)p.inst.size(),
-                       p.start, (uint32_t)p.ncap};
+                       p.start, (uint32_t)p.ncap, p.nvis};
 }
 
 extern "C++" namespace tsg {
