@@ -173,6 +173,7 @@ struct RuleHost {
   FollowDfa follow;  // MODE_ANCHORED only
   DfaHost dfa;       // MODE_ANCHORED only
   bool gate_implied = false;  // every anchor literal contains one of the keywords
+  gre::GroupSpan grp;         // secret-group span rule (valid: k_verify skips the capture search)
   bool fold_gate = false;     // an anchor literal has a case-free k / s: K/ſ spellings of it
                               // (k_fold_windows) are gated exactly, so its keyword bits are kept
 };

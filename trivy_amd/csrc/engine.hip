@@ -2782,12 +2782,11 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
         for (size_t g = 0; g < c.prog.cap_names.size(); ++g)
           if (c.prog.cap_names[g] == r.group_name) group_slots.push_back((uint32_t)g);
       d.group_n = (uint32_t)group_slots.size() - d.group_off;
-      if (d.use_groups && d.group_n == 1) {
-        const gre::GroupSpan gs = gre::group_span(c.prog, group_slots[d.group_off] / 2);
-        d.grp_fast = gs.valid ? 1u : 0u;
-        d.grp_pre = gs.pre;
-        d.grp_len = gs.len;
-        d.grp_suf = gs.suf;
+      if (d.use_groups && r.grp.valid) {  // ruleset.cpp: gre::group_span of the one named group
+        d.grp_fast = 1;
+        d.grp_pre = r.grp.pre;
+        d.grp_len = r.grp.len;
+        d.grp_suf = r.grp.suf;
       }
     }
     d.gate_implied = r.gate_implied;  // ruleset.cpp: every anchor literal contains a keyword

@@ -444,6 +444,14 @@ int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_r
         e = "rule " + r.id + ": too many capture groups for the secret-group extractor";
         return fail(TSG_ERR_UNSUPPORTED);
       }
+      // secret group from the match span alone (k_verify emit_match): one
+      // group of that name whose position gre::group_span pins
+      if (has_group && !r.group_name.empty()) {
+        int slot = -1, count = 0;
+        for (size_t k = 0; k < c.prog.cap_names.size(); ++k)
+          if (c.prog.cap_names[k] == r.group_name) slot = (int)k, ++count;
+        if (count == 1) r.grp = gre::group_span(c.prog, (uint32_t)slot);
+      }
       // no group of that name => getMatchSubgroupsLocations yields nothing
       if (!has_group) r.mode = MODE_NEVER;
       else r.mode = c.anchor.valid ? MODE_ANCHORED : MODE_FULL;
@@ -625,15 +633,7 @@ int tsg_ruleset_rule_prog(const tsg_ruleset* rs, size_t i, uint32_t* n_inst, uin
 // skip the capture search): *valid = 0 when the capture search decides.
 int tsg_ruleset_group_span(const tsg_ruleset* rs, size_t i, int* valid, int* pre, int* len, int* suf) {
   if (!rs || i >= rs->rules.size() || !valid) return TSG_ERR_INVALID_ARG;
-  const RuleHost& r = rs->rules[i];
-  gre::GroupSpan g;
-  if (r.regex >= 0 && !r.group_name.empty()) {
-    const gre::Prog& p = rs->regexes[r.regex].c.prog;
-    int slot = -1, count = 0;
-    for (size_t k = 0; k < p.cap_names.size(); ++k)
-      if (p.cap_names[k] == r.group_name) slot = (int)k, ++count;
-    if (count == 1) g = gre::group_span(p, (uint32_t)slot);
-  }
+  const gre::GroupSpan& g = rs->rules[i].grp;  // exactly what upload_ruleset hands the device
   *valid = g.valid ? 1 : 0;
   if (pre) *pre = g.pre;
   if (len) *len = g.len;
