@@ -83,6 +83,7 @@ struct Ctrl {
   unsigned long long ev_overflow;
   unsigned long long outputs;  // patterns k_report resolved (diagnostics)
   unsigned long long n_fold;     // fold-special rune occurrences recorded (ScanParams::fold_pos)
+  unsigned long long events;     // k_scan_fast events in the wave segments (diagnostics, summed by k_report)
   unsigned long long n_caps;     // matches whose secret-group spans k_captures resolves
   unsigned long long n_caps_big; // ... and those too long for its arenas (k_captures_big)
 };
@@ -1058,6 +1059,7 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
     if (w < n_waves) {
       seg = P.events + (uint64_t)w * P.ev_cap_per_wave;
       n = P.ev_counts[w];
+      if (threadIdx.x == 0 && n) atomicAdd(&P.ctrl->events, (unsigned long long)n);
     } else {  // overflow bucket
       seg = P.ev_overflow;
       n = P.ctrl->ev_overflow < P.ev_overflow_cap ? P.ctrl->ev_overflow : P.ev_overflow_cap;
@@ -1240,10 +1242,8 @@ __device__ inline uint32_t fold_rune_at(const uint8_t* d, uint64_t nbytes, uint6
   return 0;
 }
 
-__global__ __launch_bounds__(256) void k_fold_windows(ScanParams P, FoldItems F, uint64_t n_fold) {
+__device__ __noinline__ void fold_window(const ScanParams& P, const FoldItems& F, uint64_t tid) {
   const AcDev& ac = P.rs.ac;
-  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= n_fold * F.n) return;
   const uint64_t rec = P.fold_pos[tid / F.n];
   const uint32_t it = F.items[tid % F.n];
   const uint64_t q = rec >> 2;
@@ -1290,6 +1290,16 @@ __global__ __launch_bounds__(256) void k_fold_windows(ScanParams P, FoldItems F,
       if (idx < P.hit_cap) P.hits[idx] = rec_hit;
     }
   }
+}
+
+// One thread per (recorded fold-special rune, fold item); the rune count is
+// read on the device (the scan's count, capped), so no host round trip sits
+// between the scan and this pass.
+__global__ __launch_bounds__(256) void k_fold_windows(ScanParams P, FoldItems F) {
+  const uint64_t nf = P.ctrl->n_fold < P.fold_cap ? P.ctrl->n_fold : P.fold_cap;
+  const uint64_t total = nf * F.n;
+  for (uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; tid < total; tid += (uint64_t)gridDim.x * blockDim.x)
+    fold_window(P, F, tid);
 }
 
 // ---------------------------------------------------------------- gating --
@@ -1670,7 +1680,7 @@ struct VerifyParams {
   const uint32_t* vals;
   uint64_t n_cands;
   const uint32_t* job_start;
-  uint32_t n_jobs;
+  const uint32_t* n_jobs_dev;  // job count, written by the job-segmentation select (no host read)
   DevLoc* locs;
   uint64_t loc_cap;
   Ctrl* ctrl;
@@ -1682,6 +1692,7 @@ struct VerifyParams {
   uint64_t cap_cap;
   uint4* caps_big; // those too long for its arenas, for k_captures_big
   uint64_t cap_big_cap;
+  const uint8_t* span_hi;  // k_scan_fast's per-span ">= 0x80 occurs" flags (nullptr: not computed)
 };
 
 // Candidate start windows of one (file, rule) job, in increasing order
@@ -2044,8 +2055,16 @@ __device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, ui
     return;
   }
   if (rd.grp_fast) {  // the group's span follows from [ms, me) on ASCII text (gre::group_span)
+    // ASCII: the scan's per-4 KiB-span flags, byte by byte only in a flagged span
     bool ascii = true;
-    for (uint32_t q = ms; q < me && ascii; ++q) ascii = as_global<gu8>(text)[q] < 0x80;
+    if (V.span_hi) {
+      const uint64_t a = (uint64_t)(text - V.data) + ms, b = (uint64_t)(text - V.data) + me;
+      for (uint64_t sp = a / kNlBlock; sp <= (b - 1) / kNlBlock && ascii; ++sp) ascii = V.span_hi[sp] == 0;
+    }
+    if (!ascii || !V.span_hi) {
+      ascii = true;
+      for (uint32_t q = ms; q < me && ascii; ++q) ascii = as_global<gu8>(text)[q] < 0x80;
+    }
     if (ascii) {
       const int64_t gs = rd.grp_pre >= 0 ? (int64_t)ms + rd.grp_pre : (int64_t)me - rd.grp_suf - rd.grp_len;
       const int64_t ge = rd.grp_suf >= 0 ? (int64_t)me - rd.grp_suf : gs + rd.grp_len;
@@ -2074,7 +2093,9 @@ __global__ __launch_bounds__(kLanes) void k_captures(VerifyParams V) {
   const unsigned long long cnt = kLast ? V.ctrl->n_caps_big : V.ctrl->n_caps;
   const uint64_t cap = kLast ? V.cap_big_cap : V.cap_cap;
   const uint64_t n_caps = cnt < cap ? cnt : cap;
-  for (uint64_t i = t; i < n_caps; i += nthreads) {
+  // job i -> block i % grid, lane i / grid: a short list spreads over every CU
+  // (few divergent lanes per wave) instead of filling the first waves
+  for (uint64_t i = blockIdx.x + (uint64_t)threadIdx.x * gridDim.x; i < n_caps; i += nthreads) {
     const uint4 c = list[i];
     const RuleDev rd = V.rs.rules[c.y];
     const uint64_t fstart = V.off[c.x];
@@ -2231,7 +2252,8 @@ __global__ __launch_bounds__(kVerifyBlock) void k_verify(VerifyParams V) {
   __shared__ __align__(16) uint8_t cls_lds[128];
   const uint32_t nthreads = gridDim.x * blockDim.x;
   gre::VmScratch sc = make_scratch(V.scratch + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * V.scratch_stride, V.rs);
-  for (uint32_t jb = blockIdx.x * blockDim.x; jb < V.n_jobs; jb += nthreads) {  // block-uniform
+  const uint32_t n_jobs = *V.n_jobs_dev;
+  for (uint32_t jb = blockIdx.x * blockDim.x; jb < n_jobs; jb += nthreads) {  // block-uniform
     const uint32_t r0 = (uint32_t)(V.keys[V.job_start[jb]] >> kPosBits);
     const RuleDev& rd0 = V.rs.rules[r0];
     const bool staged = rd0.dfa_off != kNoFollow && rd0.dfa_size * 2 <= kVerifyDfaLds;
@@ -2243,10 +2265,10 @@ __global__ __launch_bounds__(kVerifyBlock) void k_verify(VerifyParams V) {
     }
     __syncthreads();
     const uint32_t j = jb + threadIdx.x;
-    if (j >= V.n_jobs) continue;
+    if (j >= n_jobs) continue;
     const uint64_t t0 = V.prof ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz wall clock
     const uint64_t c0 = V.job_start[j];
-    const uint64_t c1 = (j + 1 < V.n_jobs) ? V.job_start[j + 1] : V.n_cands;
+    const uint64_t c1 = (j + 1 < n_jobs) ? V.job_start[j + 1] : V.n_cands;
     const uint32_t rule = (uint32_t)(V.keys[c0] >> kPosBits);
     const uint32_t fi = V.vals[c0] & ~kFullFlag;
     bool full = false;
@@ -3345,12 +3367,11 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
 
 // Keywords / anchor literals spelled with fold-special runes, around each of
 // the n_fold occurrences the scan recorded (k_fold_windows).
-int launch_fold_windows(tsg_engine* e, const ScanParams& P, uint64_t n_fold, bool with_hits) {
+int launch_fold_windows(tsg_engine* e, const ScanParams& P, bool with_hits) {
   const DevImage& im = e->img;
-  if (!n_fold || !im.n_fold_items) return TSG_OK;
+  if (!im.n_fold_items) return TSG_OK;
   const FoldItems F{im.u32.p + im.o_fold, im.n_fold_items, with_hits ? 1u : 0u};
-  const uint64_t threads = n_fold * F.n;
-  hipLaunchKernelGGL(k_fold_windows, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, e->stream, P, F, n_fold);
+  hipLaunchKernelGGL(k_fold_windows, dim3(std::max(1u, e->num_cus) * 2), dim3(256), 0, e->stream, P, F);
   HIP_TRY(hipGetLastError());
   return TSG_OK;
 }
@@ -3460,21 +3481,16 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(hipEventRecord(e->ev[8], s));
     if ((rc = launch_scan(e, P))) return rc;
     HIP_TRY(hipEventRecord(e->ev[9], s));
+    // the fold-window pass reads the scan's rune count on the device; one
+    // read of the counters afterwards checks every buffer of both passes
+    if ((rc = launch_fold_windows(e, P, true))) return rc;
     Ctrl c;
     if ((rc = read_ctrl(e, &c))) return rc;
     const bool ev_lost = rs->ac.fast.size() && c.ev_overflow > e->ev_overflow.n;
     const bool fold_lost = c.n_fold > P.fold_cap;
     if (c.hits <= hit_cap && !ev_lost && !fold_lost) {
-      if (!c.n_fold) {
-        scanned = true;
-        break;
-      }
-      if ((rc = launch_fold_windows(e, P, c.n_fold, true))) return rc;
-      if ((rc = read_ctrl(e, &c))) return rc;
-      if (c.hits <= hit_cap) {
-        scanned = true;
-        break;
-      }
+      scanned = true;
+      break;
     }
     // overflow: grow and rescan (keyword bits are idempotent)
     if (ev_lost) e->ev_ovf_need = c.ev_overflow + (c.ev_overflow >> 2);
@@ -3501,12 +3517,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   const uint64_t n_hits = c.hits;
   const uint64_t scan_overflow = c.ev_overflow;
   const uint64_t n_outputs = c.outputs;
-  uint64_t n_events = scan_overflow;
-  if (rs->ac.fast.size() && e->ev_counts.n) {
-    std::vector<uint32_t> evc(e->ev_counts.n);
-    HIP_TRY(hipMemcpy(evc.data(), e->ev_counts.p, evc.size() * 4, hipMemcpyDeviceToHost));
-    for (uint32_t x : evc) n_events += x;
-  }
+  const uint64_t n_events = scan_overflow + c.events;
   // ---- 3. candidates
   uint64_t cand_cap = std::max<uint64_t>(1 << 16, n_hits * 2 + nf / 4);
   ExpandParams E{};
@@ -3572,15 +3583,16 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
     HIP_TRY(hipcub::DeviceSelect::Flagged(e->cub_tmp.p, tmp2, cnt, e->flags8.p, e->job_start.p, e->nsel.p,
                                           (int)n_cands, s));
-    HIP_TRY(hipMemcpyAsync(&n_jobs, e->nsel.p, 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
   }
+  // the job count stays on the device: k_verify reads it, and its grid and
+  // the location lists are sized from n_cands (>= jobs); the host reads the
+  // count with the verify counters
   HIP_TRY(hipEventRecord(e->ev[4], s));
   // ---- 5. verify
-  uint64_t loc_cap = std::max<uint64_t>(1 << 16, n_jobs);
-  uint64_t caps_cap = std::max<uint64_t>(1 << 14, n_jobs / 2), caps_big_cap = std::max<uint64_t>(1 << 12, n_jobs / 16);
+  uint64_t loc_cap = std::max<uint64_t>(1 << 16, n_cands);
+  uint64_t caps_cap = std::max<uint64_t>(1 << 14, n_cands / 2), caps_big_cap = std::max<uint64_t>(1 << 12, n_cands / 16);
   uint64_t n_locs = 0;
-  bool verified = n_jobs == 0;
+  bool verified = n_cands == 0;
   for (int attempt = 0; attempt < 4 && !verified; ++attempt) {
     HIP_TRY(e->locs.ensure(loc_cap));
     HIP_TRY(e->caps.ensure(caps_cap));
@@ -3595,7 +3607,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     V.vals = e->vals2.p;
     V.n_cands = n_cands;
     V.job_start = e->job_start.p;
-    V.n_jobs = n_jobs;
+    V.n_jobs_dev = e->nsel.p;
     V.locs = e->locs.p;
     V.loc_cap = e->locs.n;
     V.ctrl = e->ctrl.p;
@@ -3605,7 +3617,12 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     V.cap_cap = e->caps.n;
     V.caps_big = e->caps_big.p;
     V.cap_big_cap = e->caps_big.n;
+    V.span_hi = rs->ac.fast.size() && nbytes ? e->span_hi.p : nullptr;
     const bool prof = experiment_env("TSG_PROFILE_VERIFY") != nullptr;
+    if (prof) {  // diagnostics only: the job count on the host
+      HIP_TRY(hipMemcpyAsync(&n_jobs, e->nsel.p, 4, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+    }
     if (prof) HIP_TRY(e->vprof.ensure(4ull * n_jobs + 16));
     if (prof) HIP_TRY(hipMemsetAsync(e->vprof.p, 0, (4ull * n_jobs + 16) * 8, s));
     V.prof = prof ? e->vprof.p : nullptr;
@@ -3630,7 +3647,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
       hipLaunchKernelGGL(k_warm, dim3(8 * kWarmParts), dim3(256), 0, s, W, (uint32_t*)e->nsel.p);
       HIP_TRY(hipGetLastError());
     }
-    const uint32_t blocks = std::min<uint32_t>((n_jobs + kVerifyBlock - 1) / kVerifyBlock, e->vm_threads / kVerifyBlock);
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((n_cands + kVerifyBlock - 1) / kVerifyBlock, e->vm_threads / kVerifyBlock);
     hipLaunchKernelGGL(k_verify, dim3(std::max(1u, blocks)), dim3(kVerifyBlock), 0, s, V);
     // capture stages over the device-side lists (one wave per CU with 140 KiB
     // of arenas, then kBigCapLanes lanes per CU with 36 KiB each)
@@ -3673,6 +3690,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
                 kv.second.first / 1e5, kv.second.second / 1e5);
     }
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(&n_jobs, e->nsel.p, 4, hipMemcpyDeviceToHost, s));  // (read by read_ctrl's sync)
     if ((rc = read_ctrl(e, &c))) return rc;
     n_locs = c.locs;
     if (n_locs <= e->locs.n && c.n_caps <= e->caps.n && c.n_caps_big <= e->caps_big.n) {
@@ -4220,7 +4238,7 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
     if ((rc = read_ctrl(e, &c))) return rc;
     const bool ev_lost = rs->ac.fast.size() && c.ev_overflow > e->ev_overflow.n;
     if (!ev_lost && c.n_fold <= P.fold_cap) {
-      if ((rc = launch_fold_windows(e, P, c.n_fold, false))) return rc;
+      if ((rc = launch_fold_windows(e, P, false))) return rc;
       scanned = true;
       break;
     }
