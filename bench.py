@@ -176,8 +176,29 @@ def template_rules(N):
     return [N.lib.tsg_gen_template_rule(i).decode() for i in range(N.lib.tsg_gen_template_count())]
 
 
+def result_findings(N, res, f, rules):
+    """Findings of file f from a result (device-built Match / Code), in order."""
+    fp = ctypes.POINTER(N.FindingC)()
+    k = N.lib.tsg_result_findings(res, f, ctypes.byref(fp))
+    out = []
+    for j in range(k):
+        x = fp[j]
+        lines = tuple((x.lines[q].number, ctypes.string_at(x.lines[q].content, x.lines[q].content_len),
+                       bool(x.lines[q].is_cause), bool(x.lines[q].first_cause), bool(x.lines[q].last_cause))
+                      for q in range(x.n_lines))
+        out.append((rules[x.rule].id, x.start_line, x.end_line, ctypes.string_at(x.match, x.match_len), lines))
+    return out
+
+
+def oracle_findings(want):
+    enc = lambda t: t.encode("utf-8", "surrogateescape")
+    return [(x.RuleID, x.StartLine, x.EndLine, enc(x.Match),
+             tuple((ln.Number, enc(ln.Content), ln.IsCause, ln.FirstCause, ln.LastCause) for ln in x.Code["Lines"]))
+            for x in want["Findings"]]
+
+
 def parity_checks(N, S, c, locs, rules, seed, density, n_sample=300, oracle_cfg=None, big_files=3,
-                  nonascii_files=24):
+                  nonascii_files=24, res=None):
     """Full-size properties + oracle spot checks on sample files.
 
     Properties over the WHOLE batch: every real plant (an instance of one of
@@ -231,7 +252,13 @@ def parity_checks(N, S, c, locs, rules, seed, density, n_sample=300, oracle_cfg=
         g = sorted(by_file.get(f, []))
         spot_findings += len(w)
         spot_bytes += n
-        if w != g:
+        # the device-built findings in Scan order (Match and Code lines included);
+        # (RuleID, Match) ties are order-free in the reference's sort
+        full_ok = res is None or sorted(result_findings(N, res, f, rules)) == sorted(oracle_findings(want))
+        if res is not None:
+            got_ids = [x[0] for x in result_findings(N, res, f, rules)]
+            full_ok = full_ok and got_ids == sorted(got_ids)
+        if w != g or not full_ok:
             mismatched.append(f)
     return dict(planted=int(len(real)), planted_found=int(found), planted_rules=len(per_rule),
                 decoys=int(len(decoys)), decoys_found=int(decoy_hits), fold_instances=int(len(fold)),
@@ -551,7 +578,6 @@ def main():
         locs = np.concatenate(parts)
     elif last is not None:
         locs, _ = read_result(N, last)
-        N.lib.tsg_result_free(last)
     ms_per_step = dt / args.steps * 1e3
     value = total_all * args.steps / dt / 1e9
     scan_kernel_ms = float(np.mean(scan_ms))
@@ -562,11 +588,14 @@ def main():
             parity = gate_checks(N, c, sc.rules, gates, gate_words, seed, args.density)
         else:
             parity = parity_checks(N, S, c, locs, sc.rules, seed, args.density,
-                                   n_sample=300 if args.config == 2 else 24, oracle_cfg=cfg_path if cfg else None)
+                                   n_sample=300 if args.config == 2 else 24, oracle_cfg=cfg_path if cfg else None,
+                                   res=last if args.config in (0, 2, 4) else None)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.config in (0, 2):
         cores = args.cpu_cores or min(16, len(os.sched_getaffinity(0)))
         cpu = cpu_baseline(N, c, locs, rs, args.cpu_seconds, cores)
+    if last is not None and args.config != 3:
+        N.lib.tsg_result_free(last)
     if rank == 0:
         out = {
             "metric": "secret-scan GB/s (whole node), builtin rules, 1/2/4/8 MI355X; % HBM peak",

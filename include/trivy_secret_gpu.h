@@ -172,8 +172,10 @@ int tsg_scan(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, size_t
  *   content of file i = d_data[d_offsets[i] .. d_offsets[i+1] - 1), d_data[d_offsets[i+1] - 1] == 0,
  *   path of file i    = d_paths[d_path_offsets[i] .. d_path_offsets[i+1]).
  * (The separator resets the keyword automaton so no literal spans two files;
- * NUL bytes inside content are fine.)  Produces locs with line numbers;
- * findings need host content and are not built (tsg_result_findings returns 0). */
+ * NUL bytes inside content are fine.)  Produces locs with line numbers and
+ * the full findings: censoring, Match and Code (scanner.go:425-537) are cut
+ * from the batch on the device, and only the records and their strings come
+ * back (tsg_result_findings). */
 int tsg_scan_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
                     const uint64_t* d_offsets, const uint8_t* d_paths,
                     const uint64_t* d_path_offsets, size_t n_files, tsg_result** out);

@@ -47,6 +47,22 @@ def test_scanner_golden(case):
     assert _plain(got) == case["want"]
 
 
+def test_scanner_golden_device_resident():
+    """Every golden case through tsg_scan_device (batch already in HBM,
+    findings -- Match and Code -- built on the device), one batch per config,
+    compared in order."""
+    by_cfg = {}
+    for c in _CASES:
+        by_cfg.setdefault(c["config"], []).append(c)
+    for cfg, cases in by_cfg.items():
+        sc = S.new_scanner(S.parse_config(os.path.join(GOLDEN, cfg)))
+        batch = [S.ScanArgs(c["file_path"], open(os.path.join(GOLDEN, c["input"]), "rb").read().replace(b"\r", b""))
+                 for c in cases]
+        got = sc.scan_batch_device(batch)
+        for c, g in zip(cases, got):
+            assert _plain(g) == c["want"], c["name"]
+
+
 @pytest.mark.parametrize("case", _ACASES["analyze"], ids=[c["name"] for c in _ACASES["analyze"]])
 def test_analyzer_golden(case):
     a = SecretAnalyzer()

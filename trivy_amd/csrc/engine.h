@@ -3,7 +3,9 @@
 #include <cstdint>
 #include <deque>
 #include <map>
+#include <memory>
 #include <mutex>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -61,6 +63,7 @@ struct RuleDev {
   // side; grp_fast = 0 -> the capture search (k_captures)
   uint32_t grp_fast;
   int32_t grp_pre, grp_len, grp_suf;
+  uint32_t id_rank;  // position of the rule ID in sorted (ID, index) order: findings sort (scanner.go:441-446)
 };
 
 struct PatDev {
@@ -239,19 +242,51 @@ const tsg_ruleset* gate_ruleset(const tsg_ruleset* rs, std::string* err);
 namespace tsg {
 constexpr uint32_t kMaxCap = 64;  // capture slots of a SecretGroupName rule's regex
 
+// Device-built findings (engine.hip k_censor / k_find_spans / k_find_copy),
+// records shared by the device and the host copy of a result.
+constexpr uint32_t kCodeLines = 5;  // Code window: lines [StartLine - 2, EndLine + 2), EndLine == StartLine
+
+struct FindRec {
+  uint32_t file, rule, line, n_lines;  // line = StartLine = EndLine (1-based, censored buffer)
+  uint64_t start, end;                 // the kept location
+  uint64_t m_src, m_off;               // match window: file-relative source start / arena offset
+  uint32_t m_len, loc;                 // its length / index of the location (its line records)
+  uint32_t rank, pad;                  // RuleDev::id_rank of the rule
+};
+
+struct CodeRec {
+  uint64_t src, off;   // file-relative source start / arena offset
+  uint32_t len, number;
+  uint32_t flags, pad;  // 1 IsCause, 2 FirstCause, 4 LastCause
+};
+
+// Page-locked host blocks for the findings' string arena, recycled across
+// results (a result keeps its block; freeing the result returns it).
+struct PinnedPool {
+  std::mutex mu;
+  std::vector<std::pair<void*, size_t>> free_blocks;
+  ~PinnedPool();
+};
+struct PinnedBlock {
+  void* p = nullptr;
+  size_t n = 0;
+  std::shared_ptr<PinnedPool> pool;
+  ~PinnedBlock();
+};
+std::shared_ptr<PinnedBlock> pinned_get(const std::shared_ptr<PinnedPool>& pool, size_t bytes);
+
 struct ResultImpl {
   std::vector<tsg_loc> locs;
   std::vector<uint8_t> file_flags;
-  std::vector<std::vector<tsg_finding>> findings;  // per file, Scan order
-  std::deque<std::vector<tsg_line>> lines;          // stable backing store for findings
-  std::deque<std::string> strs;                     // stable backing store for strings
+  // findings in Scan order per file (sorted by file, then RuleID, then Match)
+  std::vector<FindRec> frec;
+  std::vector<CodeRec> code;  // kCodeLines per location, indexed by FindRec::loc
+  std::shared_ptr<PinnedBlock> arena;
+  mutable std::mutex fmu;     // tsg_result_findings materialises a file's views once
+  mutable std::unordered_map<uint32_t, std::pair<std::vector<tsg_finding>, std::vector<tsg_line>>> fcache;
   std::vector<double> timings;
   bool have_findings = false;
 };
-
-// censorLocation + toFinding + findLocation + sort (scanner.go:425-537) on the
-// caller's host content.
-bool build_findings(ResultImpl* r, const tsg_ruleset* rs, const tsg_file* files, size_t n_files);
 }  // namespace tsg
 
 struct tsg_result {

@@ -84,6 +84,7 @@ struct Ctrl {
   unsigned long long outputs;  // patterns k_report resolved (diagnostics)
   unsigned long long n_fold;     // fold-special rune occurrences recorded (ScanParams::fold_pos)
   unsigned long long events;     // k_scan_fast events in the wave segments (diagnostics, summed by k_report)
+  unsigned long long find_bytes; // string arena bytes of the findings (k_find_copy)
   unsigned long long n_caps;     // matches whose secret-group spans k_captures resolves
   unsigned long long n_caps_big; // ... and those too long for its arenas (k_captures_big)
 };
@@ -2402,6 +2403,322 @@ __global__ __launch_bounds__(256) void k_lines(const uint8_t* data, const uint64
   }
 }
 
+// ------------------------------------------------------------- findings --
+// toFinding / findLocation over the FINAL censored buffer (scanner.go:425-537)
+// on the device: the censored buffer is the batch plus, per file, the merged
+// kept locations read as '*' (never materialised), so a '\n' inside one is no
+// line break.  Per kept location (ordered by (file, start)):
+//   k_censor      one lane per file group: merged censor intervals + the
+//                 censored StartLine (= EndLine) from k_lines' raw counts
+//   k_find_spans  one wave per location: Match window (the line, or 30 / 20
+//                 bytes around the secret when the line exceeds 100 bytes)
+//                 and up to 5 Code lines (secretHighlightRadius 2), found with
+//                 wave-wide 1 KiB newline searches that skip 4 KiB blocks
+//                 without '\n' (nl_blocks); byte counts for the arena
+//   k_find_copy   one wave per location: the spans into the string arena,
+//                 censored bytes written as '*'
+// The records are then ordered by (file, RuleID rank) on the device; the host
+// only breaks (file, RuleID) ties by Match (scanner.go:441-446).
+struct FindParams {
+  const uint8_t* data;
+  uint64_t data_end;  // bytes of the batch buffer (reads stay below it)
+  const uint64_t* off;
+  const uint32_t* nl_blocks;
+  const RuleDev* rules;
+  DevLoc* locs;        // sorted by (file, start); lines rewritten by k_censor
+  uint64_t n_locs;
+  uint64_t* iv;        // merged censor intervals, 2 u64 per slot, at the group's slots
+  uint2* grp;          // per location: (first slot of its file group, intervals in it)
+  FindRec* rec;
+  CodeRec* code;       // kCodeLines per location
+  uint64_t* len;       // per location: arena bytes
+  uint64_t* arena_off; // exclusive prefix of len
+  uint8_t* arena;
+  uint64_t arena_cap;
+  uint64_t* sort_key;
+  uint32_t* sort_idx;
+  Ctrl* ctrl;
+};
+
+// One lane per location; the head of each file group does the group.
+__global__ __launch_bounds__(256) void k_censor(FindParams F) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= F.n_locs || (i > 0 && F.locs[i - 1].file == F.locs[i].file)) return;
+  const uint32_t file = F.locs[i].file;
+  uint64_t j = i;
+  while (j < F.n_locs && F.locs[j].file == file) ++j;
+  // merged intervals [a, b) with the raw newline prefix counts P(a), P(b)
+  uint32_t m = 0;
+  uint64_t a = 0, b = 0;
+  uint32_t pa = 0, pb = 0;
+  for (uint64_t k = i; k < j; ++k) {
+    const DevLoc L = F.locs[k];
+    if (L.flags) continue;
+    if (m && L.start <= b) {
+      if (L.end > b) {
+        b = L.end;
+        pb = L.end_line;
+      }
+      F.iv[2 * (i + m - 1) + 1] = b;
+      F.sort_idx[i + m - 1] = pb;  // (scratch: P(b) of the interval)
+    } else {
+      a = L.start, b = L.end, pa = L.start_line, pb = L.end_line;
+      F.iv[2 * (i + m)] = a;
+      F.iv[2 * (i + m) + 1] = b;
+      F.sort_key[i + m] = pa;      // (scratch: P(a))
+      F.sort_idx[i + m] = pb;
+      ++m;
+    }
+  }
+  uint32_t q = 0, before = 0;  // newlines censored in intervals wholly before the current location
+  for (uint64_t k = i; k < j; ++k) {
+    F.grp[k] = make_uint2((uint32_t)i, m);
+    DevLoc& L = F.locs[k];
+    if (L.flags) continue;
+    while (q < m && F.iv[2 * (i + q) + 1] <= L.start) {
+      before += F.sort_idx[i + q] - (uint32_t)F.sort_key[i + q];
+      ++q;
+    }
+    uint32_t hidden = before;
+    if (q < m && F.iv[2 * (i + q)] < L.start) hidden += L.start_line - (uint32_t)F.sort_key[i + q];
+    const uint32_t line = L.start_line - hidden + 1;
+    L.start_line = line;
+    L.end_line = line;
+  }
+}
+
+// The censor interval holding file-relative byte x, or -1 (binary search).
+__device__ inline int64_t censor_holder(const uint64_t* iv, uint32_t g0, uint32_t m, uint64_t x) {
+  uint32_t lo = 0, hi = m;  // first interval with a > x
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (iv[2 * (g0 + mid)] <= x) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo == 0) return -1;
+  return x < iv[2 * (g0 + lo - 1) + 1] ? (int64_t)(g0 + lo - 1) : -1;
+}
+
+// 16 bytes at p (zero past `end`): whole-vector load when it fits the buffer.
+__device__ inline uint4 ld16_guard(const uint8_t* data, uint64_t p, uint64_t end) {
+  if (p + 16 <= end) return *(const uint4*)(data + p);
+  uint32_t w[4] = {0, 0, 0, 0};
+  for (uint32_t k = 0; k < 16 && p + k < end; ++k) w[k >> 2] |= (uint32_t)data[p + k] << (8 * (k & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// bit k set <=> byte k of the 16 is '\n'
+__device__ inline uint32_t nl_mask16(uint4 v) {
+  const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t t = d[k] ^ 0x0A0A0A0Au;
+    const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);  // 0x80 per '\n' byte
+    m |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * k);
+  }
+  return m;
+}
+
+// First raw '\n' in [A, E) (absolute), or E: one 1 KiB chunk per wave step,
+// 4 KiB blocks without a newline skipped.  Wave-uniform arguments.
+__device__ uint64_t wave_nl_fwd(const FindParams& F, uint64_t A, uint64_t E, uint32_t lane) {
+  while (A < E) {
+    const uint64_t blk = A / kNlBlock;
+    if (F.nl_blocks[blk] == 0) {
+      A = (blk + 1) * kNlBlock;
+      continue;
+    }
+    const uint64_t base = A & ~(uint64_t)15;
+    const uint64_t p = base + 16ull * lane;
+    uint32_t m = p < E ? nl_mask16(ld16_guard(F.data, p, F.data_end)) : 0u;
+    if (p < A) m &= ~0u << (uint32_t)(A - p);
+    if (p + 16 > E) m &= (E > p) ? ((1u << (uint32_t)(E - p)) - 1u) : 0u;
+    const uint64_t hit = __ballot(m != 0);
+    if (hit) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(hit);
+      const uint32_t ml = __shfl(m, l);
+      return base + 16ull * l + (uint32_t)__builtin_ctz(ml);
+    }
+    A = base + 1024;
+  }
+  return E;
+}
+
+// Last raw '\n' in [S, B) (absolute), or -1.
+__device__ int64_t wave_nl_bwd(const FindParams& F, uint64_t S, uint64_t B, uint32_t lane) {
+  while (B > S) {
+    const uint64_t blk = (B - 1) / kNlBlock;
+    if (F.nl_blocks[blk] == 0) {
+      const uint64_t b0 = blk * kNlBlock;
+      B = b0 > S ? b0 : S;
+      continue;
+    }
+    const uint64_t top = ((B - 1) & ~(uint64_t)15) + 16;  // chunk [top - 1024, top)
+    const int64_t base = (int64_t)top - 1024;
+    const int64_t p = base + 16ll * lane;
+    uint32_t m = 0;  // (p is 16-aligned: a lane with p < 0 lies wholly before S)
+    if (p >= 0 && p + 16 > (int64_t)S) {
+      m = nl_mask16(ld16_guard(F.data, (uint64_t)p, F.data_end));
+      if (p < (int64_t)S) m &= ~0u << (uint32_t)((int64_t)S - p);
+    }
+    if (p + 16 > (int64_t)B) m &= (int64_t)B > p ? ((1u << (uint32_t)((int64_t)B - p)) - 1u) : 0u;
+    const uint64_t hit = __ballot(m != 0);
+    if (hit) {
+      const uint32_t l = 63u - (uint32_t)__builtin_clzll(hit);
+      const uint32_t ml = __shfl(m, l);
+      return base + 16ll * l + (31 - __builtin_clz(ml));
+    }
+    B = base > (int64_t)S ? (uint64_t)base : S;
+  }
+  return -1;
+}
+
+// Censored-buffer line breaks of file [fs, fs + n) with intervals (g0, m):
+// first '\n' at or after `from` (n if none) / start of the line holding pos.
+__device__ uint64_t cens_next_nl(const FindParams& F, uint64_t fs, uint64_t n, uint32_t g0, uint32_t m, uint64_t from,
+                                 uint32_t lane) {
+  while (from < n) {
+    const uint64_t i = wave_nl_fwd(F, fs + from, fs + n, lane) - fs;
+    if (i >= n) return n;
+    const int64_t h = censor_holder(F.iv, g0, m, i);
+    if (h < 0) return i;
+    from = F.iv[2 * h + 1];
+  }
+  return n;
+}
+
+__device__ uint64_t cens_line_begin(const FindParams& F, uint64_t fs, uint32_t g0, uint32_t m, uint64_t pos,
+                                    uint32_t lane) {
+  while (pos) {
+    const int64_t a = wave_nl_bwd(F, fs, fs + pos, lane);
+    if (a < 0) return 0;
+    const uint64_t i = (uint64_t)a - fs;
+    const int64_t h = censor_holder(F.iv, g0, m, i);
+    if (h < 0) return i + 1;
+    pos = F.iv[2 * h];
+  }
+  return 0;
+}
+
+// One wave per location: the Match window and Code line spans.
+__global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
+  const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  if (w >= F.n_locs) return;
+  const DevLoc L = F.locs[w];
+  FindRec r{};
+  r.file = L.file;
+  r.rule = L.rule;
+  r.start = L.start;
+  r.end = L.end;
+  r.loc = (uint32_t)w;
+  uint64_t total = 0;
+  const uint64_t fs = F.off[L.file];
+  const uint64_t n = F.off[L.file + 1] - 1 - fs;
+  if (!L.flags && L.start <= L.end && L.end <= n) {
+    const uint2 g = F.grp[w];
+    // match window (scanner.go:484-502)
+    uint64_t ls = cens_line_begin(F, fs, g.x, g.y, L.start, lane);
+    uint64_t le = cens_next_nl(F, fs, n, g.x, g.y, L.start, lane);
+    if (le - ls > 100) {
+      ls = L.start >= 30 ? L.start - 30 : 0;
+      le = L.end + 20 > n ? n : L.end + 20;
+    }
+    r.m_src = ls;
+    r.m_len = (uint32_t)(le - ls);
+    total = le - ls;
+    // code lines (scanner.go:505-534), 0-based numbers [sl - 2, el + 2)
+    const uint32_t sl = L.start_line - 1, el = L.end_line - 1;
+    const uint32_t cs = sl >= 2 ? sl - 2 : 0, ce = el + 2;
+    uint64_t p = cens_line_begin(F, fs, g.x, g.y, L.start, lane);
+    for (uint32_t cur = sl; cur > cs && p > 0; --cur) p = cens_line_begin(F, fs, g.x, g.y, p - 1, lane);
+    uint32_t k = 0;
+    bool found_first = false;
+    for (uint32_t ln = cs; ln < ce && p <= n && k < kCodeLines; ++ln, ++k) {
+      const uint64_t q = cens_next_nl(F, fs, n, g.x, g.y, p, lane);
+      const bool cause = ln >= sl && ln <= el;
+      if (lane == 0) {
+        CodeRec c{};
+        c.src = p;
+        c.len = (uint32_t)(q - p);
+        c.number = ln + 1;
+        c.flags = (cause ? 1u : 0u) | (cause && !found_first ? 2u : 0u) | (cause && ln == el ? 4u : 0u);
+        F.code[w * kCodeLines + k] = c;
+      }
+      found_first = found_first || cause;
+      total += q - p;
+      p = q + 1;
+    }
+    r.n_lines = k;
+    r.line = L.start_line;
+  }
+  if (lane == 0) {
+    F.rec[w] = r;
+    F.len[w] = total;
+  }
+}
+
+// One wave per location: copy the spans into the arena ('*' over censored bytes).
+__device__ inline void wave_copy_censored(const FindParams& F, uint64_t fs, uint32_t g0, uint32_t m, uint64_t src,
+                                          uint64_t len, uint64_t dst, uint32_t lane) {
+  if (dst + len > F.arena_cap) return;  // the host re-runs with a larger arena
+  uint32_t lo = 0, hi = m;  // first interval ending after src (intervals are disjoint and sorted)
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (F.iv[2 * (g0 + mid) + 1] <= src) lo = mid + 1;
+    else hi = mid;
+  }
+  uint32_t j = lo;
+  for (uint64_t o = 0; o < len; o += 64) {
+    const uint64_t x = src + o + lane;  // this lane's byte
+    while (j < m && F.iv[2 * (g0 + j) + 1] <= src + o) ++j;  // wave-uniform advance to the chunk
+    if (o + lane < len) {
+      bool cens = false;
+      for (uint32_t t = j; t < m && F.iv[2 * (g0 + t)] <= x; ++t)
+        if (x < F.iv[2 * (g0 + t) + 1]) {
+          cens = true;
+          break;
+        }
+      F.arena[dst + o + lane] = cens ? (uint8_t)'*' : F.data[fs + x];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_find_copy(FindParams F) {
+  const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  if (w >= F.n_locs) return;
+  FindRec r = F.rec[w];
+  const uint64_t fs = F.off[r.file];
+  const uint2 g = F.grp[w];
+  uint64_t dst = F.arena_off[w];
+  r.m_off = dst;
+  wave_copy_censored(F, fs, g.x, g.y, r.m_src, r.m_len, dst, lane);
+  dst += r.m_len;
+  for (uint32_t k = 0; k < r.n_lines; ++k) {
+    CodeRec c = F.code[w * kCodeLines + k];
+    wave_copy_censored(F, fs, g.x, g.y, c.src, c.len, dst, lane);
+    if (lane == 0) F.code[w * kCodeLines + k].off = dst;
+    dst += c.len;
+  }
+  if (lane == 0) {
+    F.rec[w].m_off = r.m_off;
+    // final order: (file, RuleID rank) -- ties (file, RuleID) keep (file, start)
+    // order here and are ordered by Match on the host
+    const uint32_t rank = F.rules[r.rule].id_rank;
+    F.rec[w].rank = rank;
+    F.sort_key[w] = ((uint64_t)r.file << 32) | rank;
+    F.sort_idx[w] = (uint32_t)w;
+    if (w + 1 == F.n_locs) F.ctrl->find_bytes = dst;
+  }
+}
+
+__global__ void k_find_gather(const FindRec* in, const uint32_t* idx, uint64_t n, FindRec* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = in[idx[i]];
+}
+
 // ---- SecretAnalyzer front end (tsg_analyze) --------------------------------
 // utils.IsBinary (utils.go:77-95) per byte of the head.
 __device__ inline bool is_binary_byte(uint32_t b) {
@@ -2641,6 +2958,14 @@ struct tsg_engine {
   size_t h_stage_n = 0;
   double stage_ms[2] = {0, 0};  // last stage_host_batch: pack (+ overlapped H2D), H2D tail (host clock)
   std::vector<double> gate_tm;          // timings of the last tsg_gate_device call
+  // device findings (build_findings_dev)
+  DBuf<uint64_t> f_iv, f_len, f_off;
+  DBuf<uint2> f_grp;
+  DBuf<FindRec> f_rec, f_rec2;
+  DBuf<CodeRec> f_code;
+  DBuf<uint8_t> f_arena;
+  uint64_t f_arena_need = 0;  // arena size learnt from an overflowing call
+  std::shared_ptr<PinnedPool> pinned = std::make_shared<PinnedPool>();
 };
 
 namespace {
@@ -2753,9 +3078,14 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   std::vector<uint16_t> fdelta, ddelta;
   std::vector<uint8_t> fcls, dbytes;
   std::set<uint32_t> kw_needed_ids;
+  std::vector<std::string> ids;  // sorted distinct rule IDs: the findings' RuleID order
+  for (auto& r : rs->rules) ids.push_back(r.id);
+  std::sort(ids.begin(), ids.end());
+  ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
   for (size_t ri = 0; ri < rs->rules.size(); ++ri) {
     const RuleHost& r = rs->rules[ri];
     RuleDev d{};
+    d.id_rank = (uint32_t)(std::lower_bound(ids.begin(), ids.end(), r.id) - ids.begin());
     d.follow_off = kNoFollow;
     d.dfa_off = kNoFollow;
     if (r.dfa.valid) {
@@ -3152,45 +3482,6 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   return TSG_OK;
 }
 
-// findLocation (scanner.go:481-503) counts '\n' in the FINAL censored buffer
-// (scanner.go:433-435): newlines inside any kept location have become '*'.
-// So StartLine = 1 + P(start) - (newlines censored before start), and
-// EndLine == StartLine because [start,end) itself is censored.  P(x) are the
-// raw prefix counts k_lines produced at every location boundary.
-// `locs` arrive ordered by (file, start) (k_loc_keys + radix sort on the device).
-void censored_lines(std::vector<DevLoc>& locs) {
-  size_t i = 0;
-  std::vector<uint64_t> ia, ib;
-  std::vector<uint32_t> ipa, ipb;
-  while (i < locs.size()) {
-    size_t j = i;
-    while (j < locs.size() && locs[j].file == locs[i].file) ++j;
-    // merged censored intervals of this file: (a, b, P(a), P(b))
-    ia.clear(); ib.clear(); ipa.clear(); ipb.clear();
-    for (size_t k = i; k < j; ++k) {
-      const DevLoc& L = locs[k];
-      if (L.flags) continue;
-      if (!ia.empty() && L.start <= ib.back()) {
-        if (L.end > ib.back()) { ib.back() = L.end; ipb.back() = L.end_line; }
-      } else {
-        ia.push_back(L.start); ib.push_back(L.end); ipa.push_back(L.start_line); ipb.push_back(L.end_line);
-      }
-    }
-    size_t m = 0;
-    uint32_t before = 0;  // newlines censored in intervals entirely before the current one
-    for (size_t k = i; k < j; ++k) {
-      DevLoc& L = locs[k];
-      if (L.flags) continue;
-      while (m < ia.size() && ib[m] <= L.start) { before += ipb[m] - ipa[m]; ++m; }
-      uint32_t hidden = before;
-      if (m < ia.size() && ia[m] < L.start) hidden += L.start_line - ipa[m];
-      const uint32_t line = L.start_line - hidden + 1;
-      L.start_line = line;
-      L.end_line = line;
-    }
-    i = j;
-  }
-}
 
 // Ablation / diagnostic switches: read only in a
 // -DTSG_EXPERIMENTS build; the product library ignores the environment.
@@ -3374,6 +3665,107 @@ int launch_fold_windows(tsg_engine* e, const ScanParams& P, bool with_hits) {
   hipLaunchKernelGGL(k_fold_windows, dim3(std::max(1u, e->num_cus) * 2), dim3(256), 0, e->stream, P, F);
   HIP_TRY(hipGetLastError());
   return TSG_OK;
+}
+
+// Findings of the sorted kept locations (e->locs2): k_censor, k_find_spans,
+// the arena prefix, k_find_copy, the (file, RuleID rank) order; the records
+// and the string arena come back with the caller's final synchronisation.
+int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_off, uint64_t nbytes, uint64_t n_locs,
+                       tsg_result* res) {
+  hipStream_t s = e->stream;
+  HIP_TRY(e->f_iv.ensure(2 * n_locs));
+  HIP_TRY(e->f_grp.ensure(n_locs));
+  HIP_TRY(e->f_rec.ensure(n_locs));
+  HIP_TRY(e->f_rec2.ensure(n_locs));
+  HIP_TRY(e->f_code.ensure(kCodeLines * n_locs));
+  HIP_TRY(e->f_len.ensure(n_locs));
+  HIP_TRY(e->f_off.ensure(n_locs));
+  HIP_TRY(e->f_arena.ensure(std::max<uint64_t>(1 << 20, e->f_arena_need)));
+  FindParams F{};
+  F.data = d_data;
+  F.data_end = nbytes;
+  F.off = d_off;
+  F.nl_blocks = e->nl_blocks.p;
+  F.rules = e->img.view.rules;
+  F.locs = e->locs2.p;
+  F.n_locs = n_locs;
+  F.iv = e->f_iv.p;
+  F.grp = e->f_grp.p;
+  F.rec = e->f_rec.p;
+  F.code = e->f_code.p;
+  F.len = e->f_len.p;
+  F.arena_off = e->f_off.p;
+  F.sort_key = e->keys.p;
+  F.sort_idx = e->vals.p;
+  F.ctrl = e->ctrl.p;
+  const uint32_t lane_blocks = (uint32_t)((n_locs + 255) / 256), wave_blocks = (uint32_t)((n_locs * 64 + 255) / 256);
+  hipLaunchKernelGGL(k_censor, dim3(lane_blocks), dim3(256), 0, s, F);
+  hipLaunchKernelGGL(k_find_spans, dim3(wave_blocks), dim3(256), 0, s, F);
+  HIP_TRY(hipGetLastError());
+  size_t tmp = 0;
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->f_len.p, e->f_off.p, (int)n_locs, s));
+  HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(e->cub_tmp.p, tmp, e->f_len.p, e->f_off.p, (int)n_locs, s));
+  Ctrl c;
+  for (int attempt = 0;; ++attempt) {
+    F.arena = e->f_arena.p;
+    F.arena_cap = e->f_arena.n;
+    hipLaunchKernelGGL(k_find_copy, dim3(wave_blocks), dim3(256), 0, s, F);
+    HIP_TRY(hipGetLastError());
+    size_t tmp2 = 0;
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
+                                               (int)n_locs, 0, 64, s));
+    HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
+                                               (int)n_locs, 0, 64, s));
+    hipLaunchKernelGGL(k_find_gather, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->vals2.p, n_locs,
+                       e->f_rec2.p);
+    HIP_TRY(hipGetLastError());
+    if (int rc = read_ctrl(e, &c)) return rc;
+    if (c.find_bytes <= e->f_arena.n) break;
+    if (attempt == 1) {
+      set_last_error("internal: findings arena still overflowed after regrowing it");
+      return TSG_ERR_INTERNAL;
+    }
+    e->f_arena_need = c.find_bytes + (c.find_bytes >> 3);
+    HIP_TRY(e->f_arena.ensure(e->f_arena_need));
+  }
+  auto& R = res->impl;
+  R.frec.resize(n_locs);
+  R.code.resize((size_t)kCodeLines * n_locs);
+  R.arena = pinned_get(e->pinned, std::max<uint64_t>(1, c.find_bytes));
+  if (!R.arena) {
+    set_last_error("hipHostMalloc failed for the findings arena");
+    return TSG_ERR_DEVICE;
+  }
+  HIP_TRY(hipMemcpyAsync(R.frec.data(), e->f_rec2.p, n_locs * sizeof(FindRec), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(R.code.data(), e->f_code.p, R.code.size() * sizeof(CodeRec), hipMemcpyDeviceToHost, s));
+  if (c.find_bytes)
+    HIP_TRY(hipMemcpyAsync(R.arena->p, e->f_arena.p, c.find_bytes, hipMemcpyDeviceToHost, s));
+  return TSG_OK;
+}
+
+// Scan's final sort (scanner.go:441-446) is by (RuleID, Match); the device
+// ordered the records by (file, RuleID rank) keeping (file, start) order, so
+// only runs with an equal (file, RuleID) are ordered here, by Match and then
+// (rule, start, end) -- the order the reference's matches arrive in.
+void order_finding_ties(ResultImpl& R) {
+  const uint8_t* A = R.arena ? (const uint8_t*)R.arena->p : nullptr;
+  size_t i = 0;
+  while (i < R.frec.size()) {
+    size_t j = i + 1;
+    while (j < R.frec.size() && R.frec[j].file == R.frec[i].file && R.frec[j].rank == R.frec[i].rank) ++j;
+    if (j - i > 1)
+      std::stable_sort(R.frec.begin() + i, R.frec.begin() + j, [&](const FindRec& x, const FindRec& y) {
+        const int c = memcmp(A + x.m_off, A + y.m_off, std::min(x.m_len, y.m_len));
+        if (c != 0) return c < 0;
+        if (x.m_len != y.m_len) return x.m_len < y.m_len;
+        if (x.rule != y.rule) return x.rule < y.rule;
+        if (x.start != y.start) return x.start < y.start;
+        return x.end < y.end;
+      });
+    i = j;
+  }
 }
 
 // Run the device pipeline on a batch already in HBM.  Fills r->impl.locs and flags.
@@ -3802,6 +4194,8 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     hipLaunchKernelGGL(k_loc_gather, dim3((uint32_t)((n_locs + 255) / 256)), dim3(256), 0, s, e->locs.p,
                        e->vals2.p, n_locs, e->locs2.p);
     HIP_TRY(hipGetLastError());
+    // ---- 8. findings (censored lines, Match, Code, order) on the device
+    if ((rc = build_findings_dev(e, d_data, d_off, nbytes, n_locs, res))) return rc;
     hl.resize(n_locs);
     HIP_TRY(hipMemcpyAsync(hl.data(), e->locs2.p, n_locs * sizeof(DevLoc), hipMemcpyDeviceToHost, s));
   }
@@ -3847,7 +4241,6 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   }
   auto& R = res->impl;
   R.file_flags.assign(e->h_flags, e->h_flags + nf);
-  censored_lines(hl);
   R.locs.clear();
   for (auto& L : hl) {
     if (L.flags & 1) {
@@ -3856,6 +4249,8 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     }
     R.locs.push_back(tsg_loc{L.file, L.rule, L.start, L.end, L.start_line, L.end_line});
   }
+  order_finding_ties(R);
+  R.have_findings = true;
   const auto wall2 = std::chrono::steady_clock::now();
   tm[15] = std::chrono::duration<double, std::milli>(wall2 - wall0).count();  // whole call, host clock
   tm[16] = std::chrono::duration<double, std::milli>(wall2 - wall1).count();  // host post-processing
@@ -3863,6 +4258,42 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
 }
 
 }  // namespace
+
+namespace tsg {
+PinnedPool::~PinnedPool() {
+  for (auto& b : free_blocks) (void)hipHostFree(b.first);
+}
+PinnedBlock::~PinnedBlock() {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(pool->mu);
+  if (pool->free_blocks.size() < 4) pool->free_blocks.push_back({p, n});
+  else (void)hipHostFree(p);
+}
+std::shared_ptr<PinnedBlock> pinned_get(const std::shared_ptr<PinnedPool>& pool, size_t bytes) {
+  auto b = std::make_shared<PinnedBlock>();
+  b->pool = pool;
+  {
+    std::lock_guard<std::mutex> lk(pool->mu);
+    size_t best = (size_t)-1;
+    for (size_t i = 0; i < pool->free_blocks.size(); ++i)
+      if (pool->free_blocks[i].second >= bytes && (best == (size_t)-1 || pool->free_blocks[i].second < pool->free_blocks[best].second))
+        best = i;
+    if (best != (size_t)-1) {
+      b->p = pool->free_blocks[best].first;
+      b->n = pool->free_blocks[best].second;
+      pool->free_blocks.erase(pool->free_blocks.begin() + best);
+      return b;
+    }
+  }
+  const size_t n = std::max<size_t>(1 << 20, bytes + bytes / 4);
+  if (hipHostMalloc(&b->p, n, hipHostMallocDefault) != hipSuccess) {
+    b->p = nullptr;
+    return nullptr;
+  }
+  b->n = n;
+  return b;
+}
+}  // namespace tsg
 
 extern "C" {
 
@@ -4028,10 +4459,6 @@ static int scan_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files
     delete res;
     return rc;
   }
-  if (!build_findings(&res->impl, rs, files, n_files)) {
-    delete res;
-    return TSG_ERR_PANIC;
-  }
   res->impl.timings.resize(20, 0.0);
   res->impl.timings[18] = e->stage_ms[0];  // host pack into pinned staging
   res->impl.timings[19] = e->stage_ms[1];  // H2D
@@ -4125,35 +4552,8 @@ static int analyze_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* fi
   auto& R = res->impl;
   for (size_t i = 0; i < n_files && i < R.file_flags.size(); ++i)
     if (bin[i]) R.file_flags[i] |= TSG_FILE_BINARY;
-  // findings are cut from the content Scan saw: strip the files that have any
-  std::vector<tsg_file> hf(files, files + n_files);
-  std::deque<std::string> stripped;
-  {
-    std::vector<uint8_t> has(n_files, 0);
-    for (auto& L : R.locs) has[L.file] = 1;
-    for (size_t i = 0; i < n_files; ++i) {
-      if (!has[i]) continue;
-      const char* d = (const char*)files[i].data;
-      const char* end = d + files[i].len;
-      const char* cr = files[i].len ? (const char*)memchr(d, '\r', files[i].len) : nullptr;
-      if (!cr) continue;  // nothing to strip: findings read the caller's bytes
-      std::string t;
-      t.reserve(files[i].len);
-      while (cr) {  // copy the runs between '\r's
-        t.append(d, cr);
-        d = cr + 1;
-        cr = (const char*)memchr(d, '\r', end - d);
-      }
-      t.append(d, end);
-      stripped.push_back(std::move(t));
-      hf[i].data = (const uint8_t*)stripped.back().data();
-      hf[i].len = stripped.back().size();
-    }
-  }
-  if (!build_findings(&R, rs, hf.data(), n_files)) {
-    delete res;
-    return TSG_ERR_PANIC;
-  }
+  // findings were built on the device from the CR-stripped batch Scan saw
+
   res->impl.timings.resize(23, 0.0);
   res->impl.timings[18] = e->stage_ms[0];  // host pack into pinned staging
   res->impl.timings[19] = e->stage_ms[1];  // H2D
@@ -4309,12 +4709,55 @@ const tsg_loc* tsg_result_locs(const tsg_result* r) { return r ? r->impl.locs.da
 size_t tsg_result_file_count(const tsg_result* r) { return r ? r->impl.file_flags.size() : 0; }
 const uint8_t* tsg_result_file_flags(const tsg_result* r) { return r ? r->impl.file_flags.data() : nullptr; }
 size_t tsg_result_findings(const tsg_result* r, size_t file, const tsg_finding** out) {
-  if (!r || !out || !r->impl.have_findings || file >= r->impl.findings.size()) {
-    if (out) *out = nullptr;
-    return 0;
+  if (out) *out = nullptr;
+  if (!r || !out || !r->impl.have_findings) return 0;
+  const auto& R = r->impl;
+  auto lo = std::lower_bound(R.frec.begin(), R.frec.end(), (uint32_t)file,
+                             [](const FindRec& a, uint32_t f) { return a.file < f; });
+  if (lo == R.frec.end() || lo->file != file) return 0;
+  auto hi = lo;
+  while (hi != R.frec.end() && hi->file == file) ++hi;
+  std::lock_guard<std::mutex> lk(R.fmu);
+  auto it = R.fcache.find((uint32_t)file);
+  if (it == R.fcache.end()) {  // views into the result's string arena, built once per file
+    auto& slot = R.fcache[(uint32_t)file];
+    const char* A = (const char*)R.arena->p;
+    size_t nl = 0;
+    for (auto q = lo; q != hi; ++q) nl += q->n_lines;
+    slot.second.reserve(nl);
+    for (auto q = lo; q != hi; ++q) {
+      tsg_finding fd{};
+      fd.file = q->file;
+      fd.rule = q->rule;
+      fd.start_line = q->line;
+      fd.end_line = q->line;
+      fd.match = A + q->m_off;
+      fd.match_len = q->m_len;
+      fd.start = q->start;
+      fd.end = q->end;
+      fd.n_lines = q->n_lines;
+      for (uint32_t k = 0; k < q->n_lines; ++k) {
+        const CodeRec& c = R.code[(size_t)q->loc * kCodeLines + k];
+        tsg_line tl{};
+        tl.number = c.number;
+        tl.content = A + c.off;
+        tl.content_len = c.len;
+        tl.is_cause = (c.flags & 1) != 0;
+        tl.first_cause = (c.flags & 2) != 0;
+        tl.last_cause = (c.flags & 4) != 0;
+        slot.second.push_back(tl);
+      }
+      slot.first.push_back(fd);
+    }
+    size_t k = 0;  // line pointers after the vector stopped growing
+    for (auto& fd : slot.first) {
+      fd.lines = fd.n_lines ? slot.second.data() + k : nullptr;
+      k += fd.n_lines;
+    }
+    it = R.fcache.find((uint32_t)file);
   }
-  *out = r->impl.findings[file].data();
-  return r->impl.findings[file].size();
+  *out = it->second.first.data();
+  return it->second.first.size();
 }
 int tsg_result_timings(const tsg_result* r, double* ms, size_t n, size_t* n_out) {
   if (!r) return TSG_ERR_INVALID_ARG;

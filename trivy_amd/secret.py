@@ -246,6 +246,41 @@ class Scanner:
     def scan_batch(self, batch: Sequence[ScanArgs]) -> List[Secret]:
         return self._run(N.lib.tsg_scan, batch)
 
+    def scan_batch_device(self, batch: Sequence[ScanArgs]) -> List[Secret]:
+        """Scan through tsg_scan_device: the batch is packed into HBM first
+        (content + one NUL separator per file, the layout include/
+        trivy_secret_gpu.h documents) and the findings -- Match and Code
+        included -- are built on the device."""
+        import numpy as np
+        import torch
+
+        dev = torch.device("cuda", default_device() if self.device is None else self.device)
+        n = len(batch)
+        sizes = np.array([len(a.content) + 1 for a in batch], dtype=np.uint64)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(sizes, out=off[1:])
+        host = np.zeros(int(off[-1]) + 16, dtype=np.uint8)
+        for i, a in enumerate(batch):
+            host[int(off[i]):int(off[i]) + len(a.content)] = np.frombuffer(bytes(a.content), dtype=np.uint8)
+        paths = [a.file_path.encode("utf-8", "surrogateescape") for a in batch]
+        poff = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum([len(x) for x in paths], out=poff[1:])
+        pbuf = np.frombuffer(b"".join(paths) + b"\0" * 16, dtype=np.uint8)
+        d_data = torch.from_numpy(host).to(dev)
+        d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+        d_paths = torch.from_numpy(pbuf.copy()).to(dev)
+        d_poff = torch.from_numpy(poff.view(np.int64)).to(dev)
+        torch.cuda.synchronize(dev)
+        eng = get_engine(self.device)
+        res = ctypes.c_void_p()
+        N.check(N.lib.tsg_scan_device(eng, self._rs.handle, ctypes.c_void_p(d_data.data_ptr()),
+                                      ctypes.c_void_p(d_off.data_ptr()), ctypes.c_void_p(d_paths.data_ptr()),
+                                      ctypes.c_void_p(d_poff.data_ptr()), n, ctypes.byref(res)))
+        try:
+            return self._convert(res, batch)
+        finally:
+            N.lib.tsg_result_free(res)
+
     def analyze_batch(self, batch: Sequence[ScanArgs]) -> List[Optional[Secret]]:
         """SecretAnalyzer.Analyze's per-file work on the GPU (tsg_analyze):
         IsBinary gate, '\r' deletion, Scan.  `content` is the raw file; None
