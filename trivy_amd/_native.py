@@ -204,3 +204,30 @@ def regex_match(pattern: str, text: bytes) -> bool:
     m = ctypes.c_int()
     check(lib.tsg_regex_match(pattern.encode(), text, len(text), ctypes.byref(m)))
     return bool(m.value)
+
+
+class DeviceBuffer:
+    """A copy of a host numpy array in device memory, through the HIP runtime
+    libtrivy_secret_gpu.so links (libamdhip64.so.7, already mapped), for the
+    device-resident entry points (tsg_scan_device).  Test / tooling helper."""
+    _hip = None
+
+    def __init__(self, arr):
+        if DeviceBuffer._hip is None:
+            h = ctypes.CDLL("libamdhip64.so.7")
+            h.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+            h.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+            h.hipFree.argtypes = [ctypes.c_void_p]
+            DeviceBuffer._hip = h
+        self.ptr = ctypes.c_void_p()
+        n = max(1, arr.nbytes)
+        if DeviceBuffer._hip.hipMalloc(ctypes.byref(self.ptr), n) != 0:
+            raise EngineError(TSG_ERR_DEVICE, "hipMalloc failed")
+        if arr.nbytes and DeviceBuffer._hip.hipMemcpy(self.ptr, arr.ctypes.data, arr.nbytes, 1) != 0:  # H2D
+            self.free()
+            raise EngineError(TSG_ERR_DEVICE, "hipMemcpy failed")
+
+    def free(self):
+        if self.ptr:
+            DeviceBuffer._hip.hipFree(self.ptr)
+            self.ptr = ctypes.c_void_p()

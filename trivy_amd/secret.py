@@ -250,36 +250,33 @@ class Scanner:
         """Scan through tsg_scan_device: the batch is packed into HBM first
         (content + one NUL separator per file, the layout include/
         trivy_secret_gpu.h documents) and the findings -- Match and Code
-        included -- are built on the device."""
+        included -- are built on the device.  Device memory comes from the HIP
+        runtime the engine itself links (no second runtime in the process)."""
         import numpy as np
-        import torch
 
-        dev = torch.device("cuda", default_device() if self.device is None else self.device)
+        get_engine(self.device)  # selects and initialises the device first
         n = len(batch)
-        sizes = np.array([len(a.content) + 1 for a in batch], dtype=np.uint64)
         off = np.zeros(n + 1, dtype=np.uint64)
-        np.cumsum(sizes, out=off[1:])
+        np.cumsum(np.array([len(a.content) + 1 for a in batch], dtype=np.uint64), out=off[1:])
         host = np.zeros(int(off[-1]) + 16, dtype=np.uint8)
         for i, a in enumerate(batch):
             host[int(off[i]):int(off[i]) + len(a.content)] = np.frombuffer(bytes(a.content), dtype=np.uint8)
         paths = [a.file_path.encode("utf-8", "surrogateescape") for a in batch]
         poff = np.zeros(n + 1, dtype=np.uint64)
-        np.cumsum([len(x) for x in paths], out=poff[1:])
+        np.cumsum(np.array([len(x) for x in paths], dtype=np.uint64), out=poff[1:])
         pbuf = np.frombuffer(b"".join(paths) + b"\0" * 16, dtype=np.uint8)
-        d_data = torch.from_numpy(host).to(dev)
-        d_off = torch.from_numpy(off.view(np.int64)).to(dev)
-        d_paths = torch.from_numpy(pbuf.copy()).to(dev)
-        d_poff = torch.from_numpy(poff.view(np.int64)).to(dev)
-        torch.cuda.synchronize(dev)
-        eng = get_engine(self.device)
-        res = ctypes.c_void_p()
-        N.check(N.lib.tsg_scan_device(eng, self._rs.handle, ctypes.c_void_p(d_data.data_ptr()),
-                                      ctypes.c_void_p(d_off.data_ptr()), ctypes.c_void_p(d_paths.data_ptr()),
-                                      ctypes.c_void_p(d_poff.data_ptr()), n, ctypes.byref(res)))
+        bufs = [N.DeviceBuffer(x) for x in (host, off, pbuf, poff)]
         try:
-            return self._convert(res, batch)
+            res = ctypes.c_void_p()
+            N.check(N.lib.tsg_scan_device(get_engine(self.device), self._rs.handle, *[b.ptr for b in bufs], n,
+                                          ctypes.byref(res)))
+            try:
+                return self._convert(res, batch)
+            finally:
+                N.lib.tsg_result_free(res)
         finally:
-            N.lib.tsg_result_free(res)
+            for b in bufs:
+                b.free()
 
     def analyze_batch(self, batch: Sequence[ScanArgs]) -> List[Optional[Secret]]:
         """SecretAnalyzer.Analyze's per-file work on the GPU (tsg_analyze):
