@@ -193,7 +193,8 @@ def result_findings(N, res, f, rules):
 def oracle_findings(want):
     enc = lambda t: t.encode("utf-8", "surrogateescape")
     return [(x.RuleID, x.StartLine, x.EndLine, enc(x.Match),
-             tuple((ln.Number, enc(ln.Content), ln.IsCause, ln.FirstCause, ln.LastCause) for ln in x.Code["Lines"]))
+             tuple((ln["Number"], enc(ln["Content"]), ln["IsCause"], ln["FirstCause"], ln["LastCause"])
+                   for ln in x.Code["Lines"]))
             for x in want["Findings"]]
 
 

@@ -244,7 +244,7 @@ constexpr uint32_t kMaxCap = 64;  // capture slots of a SecretGroupName rule's r
 
 // Device-built findings (engine.hip k_censor / k_find_spans / k_find_copy),
 // records shared by the device and the host copy of a result.
-constexpr uint32_t kCodeLines = 5;  // Code window: lines [StartLine - 2, EndLine + 2), EndLine == StartLine
+constexpr uint32_t kCodeLines = 4;  // Code window: lines [StartLine - 2, EndLine + 2), EndLine == StartLine
 
 struct FindRec {
   uint32_t file, rule, line, n_lines;  // line = StartLine = EndLine (1-based, censored buffer)
@@ -255,9 +255,9 @@ struct FindRec {
 };
 
 struct CodeRec {
-  uint64_t src, off;   // file-relative source start / arena offset
-  uint32_t len, number;
-  uint32_t flags, pad;  // 1 IsCause, 2 FirstCause, 4 LastCause
+  uint64_t off;          // file-relative source start (k_find_spans), then arena offset (k_find_copy)
+  uint32_t len;
+  uint32_t number_flags;  // Number | flags << 29: 1 IsCause, 2 FirstCause, 4 LastCause
 };
 
 // Page-locked host blocks for the findings' string arena, recycled across
@@ -279,8 +279,20 @@ struct ResultImpl {
   std::vector<tsg_loc> locs;
   std::vector<uint8_t> file_flags;
   // findings in Scan order per file (sorted by file, then RuleID, then Match)
-  std::vector<FindRec> frec;
-  std::vector<CodeRec> code;  // kCodeLines per location, indexed by FindRec::loc
+  // (records, code lines and strings share one page-locked block: the D2H
+  // copies run at full PCIe rate)
+  template <class T>
+  struct View {
+    T* p = nullptr;
+    size_t n = 0;
+    T* begin() const { return p; }
+    T* end() const { return p + n; }
+    size_t size() const { return n; }
+    T& operator[](size_t i) const { return p[i]; }
+  };
+  View<FindRec> frec;
+  View<CodeRec> code;  // kCodeLines per location, indexed by FindRec::loc
+  const char* strs = nullptr;
   std::shared_ptr<PinnedBlock> arena;
   mutable std::mutex fmu;     // tsg_result_findings materialises a file's views once
   mutable std::unordered_map<uint32_t, std::pair<std::vector<tsg_finding>, std::vector<tsg_line>>> fcache;

@@ -2437,6 +2437,7 @@ struct FindParams {
   uint64_t arena_cap;
   uint64_t* sort_key;
   uint32_t* sort_idx;
+  uint32_t rank_bits;  // bits of RuleDev::id_rank: sort key = file << rank_bits | rank
   Ctrl* ctrl;
 };
 
@@ -2640,10 +2641,10 @@ __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
       const bool cause = ln >= sl && ln <= el;
       if (lane == 0) {
         CodeRec c{};
-        c.src = p;
+        c.off = p;  // source start until k_find_copy places it
         c.len = (uint32_t)(q - p);
-        c.number = ln + 1;
-        c.flags = (cause ? 1u : 0u) | (cause && !found_first ? 2u : 0u) | (cause && ln == el ? 4u : 0u);
+        const uint32_t flags = (cause ? 1u : 0u) | (cause && !found_first ? 2u : 0u) | (cause && ln == el ? 4u : 0u);
+        c.number_flags = (ln + 1) | (flags << 29);
         F.code[w * kCodeLines + k] = c;
       }
       found_first = found_first || cause;
@@ -2698,7 +2699,7 @@ __global__ __launch_bounds__(256) void k_find_copy(FindParams F) {
   dst += r.m_len;
   for (uint32_t k = 0; k < r.n_lines; ++k) {
     CodeRec c = F.code[w * kCodeLines + k];
-    wave_copy_censored(F, fs, g.x, g.y, c.src, c.len, dst, lane);
+    wave_copy_censored(F, fs, g.x, g.y, c.off, c.len, dst, lane);
     if (lane == 0) F.code[w * kCodeLines + k].off = dst;
     dst += c.len;
   }
@@ -2708,7 +2709,7 @@ __global__ __launch_bounds__(256) void k_find_copy(FindParams F) {
     // order here and are ordered by Match on the host
     const uint32_t rank = F.rules[r.rule].id_rank;
     F.rec[w].rank = rank;
-    F.sort_key[w] = ((uint64_t)r.file << 32) | rank;
+    F.sort_key[w] = ((uint64_t)r.file << F.rank_bits) | rank;
     F.sort_idx[w] = (uint32_t)w;
     if (w + 1 == F.n_locs) F.ctrl->find_bytes = dst;
   }
@@ -3670,8 +3671,8 @@ int launch_fold_windows(tsg_engine* e, const ScanParams& P, bool with_hits) {
 // Findings of the sorted kept locations (e->locs2): k_censor, k_find_spans,
 // the arena prefix, k_find_copy, the (file, RuleID rank) order; the records
 // and the string arena come back with the caller's final synchronisation.
-int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_off, uint64_t nbytes, uint64_t n_locs,
-                       tsg_result* res) {
+int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_off, uint64_t nbytes, uint64_t n_files,
+                       uint64_t n_locs, tsg_result* res) {
   hipStream_t s = e->stream;
   HIP_TRY(e->f_iv.ensure(2 * n_locs));
   HIP_TRY(e->f_grp.ensure(n_locs));
@@ -3698,6 +3699,10 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   F.sort_key = e->keys.p;
   F.sort_idx = e->vals.p;
   F.ctrl = e->ctrl.p;
+  F.rank_bits = 1;
+  while ((1u << F.rank_bits) < e->img.view.n_rules + 1) ++F.rank_bits;
+  int key_bits = (int)F.rank_bits + 1;
+  while (key_bits < 64 && (1ull << (key_bits - F.rank_bits)) <= n_files) ++key_bits;
   const uint32_t lane_blocks = (uint32_t)((n_locs + 255) / 256), wave_blocks = (uint32_t)((n_locs * 64 + 255) / 256);
   hipLaunchKernelGGL(k_censor, dim3(lane_blocks), dim3(256), 0, s, F);
   hipLaunchKernelGGL(k_find_spans, dim3(wave_blocks), dim3(256), 0, s, F);
@@ -3714,10 +3719,10 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
     HIP_TRY(hipGetLastError());
     size_t tmp2 = 0;
     HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
-                                               (int)n_locs, 0, 64, s));
+                                               (int)n_locs, 0, key_bits, s));
     HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
     HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
-                                               (int)n_locs, 0, 64, s));
+                                               (int)n_locs, 0, key_bits, s));
     hipLaunchKernelGGL(k_find_gather, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->vals2.p, n_locs,
                        e->f_rec2.p);
     HIP_TRY(hipGetLastError());
@@ -3731,17 +3736,20 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
     HIP_TRY(e->f_arena.ensure(e->f_arena_need));
   }
   auto& R = res->impl;
-  R.frec.resize(n_locs);
-  R.code.resize((size_t)kCodeLines * n_locs);
-  R.arena = pinned_get(e->pinned, std::max<uint64_t>(1, c.find_bytes));
+  const size_t rec_bytes = n_locs * sizeof(FindRec), code_bytes = (size_t)kCodeLines * n_locs * sizeof(CodeRec);
+  R.arena = pinned_get(e->pinned, rec_bytes + code_bytes + c.find_bytes + 1);
   if (!R.arena) {
     set_last_error("hipHostMalloc failed for the findings arena");
     return TSG_ERR_DEVICE;
   }
-  HIP_TRY(hipMemcpyAsync(R.frec.data(), e->f_rec2.p, n_locs * sizeof(FindRec), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(R.code.data(), e->f_code.p, R.code.size() * sizeof(CodeRec), hipMemcpyDeviceToHost, s));
+  uint8_t* base = (uint8_t*)R.arena->p;
+  R.frec = {(FindRec*)base, n_locs};
+  R.code = {(CodeRec*)(base + rec_bytes), (size_t)kCodeLines * n_locs};
+  R.strs = (const char*)(base + rec_bytes + code_bytes);
+  HIP_TRY(hipMemcpyAsync(R.frec.p, e->f_rec2.p, rec_bytes, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(R.code.p, e->f_code.p, code_bytes, hipMemcpyDeviceToHost, s));
   if (c.find_bytes)
-    HIP_TRY(hipMemcpyAsync(R.arena->p, e->f_arena.p, c.find_bytes, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(base + rec_bytes + code_bytes, e->f_arena.p, c.find_bytes, hipMemcpyDeviceToHost, s));
   return TSG_OK;
 }
 
@@ -3750,7 +3758,7 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
 // only runs with an equal (file, RuleID) are ordered here, by Match and then
 // (rule, start, end) -- the order the reference's matches arrive in.
 void order_finding_ties(ResultImpl& R) {
-  const uint8_t* A = R.arena ? (const uint8_t*)R.arena->p : nullptr;
+  const uint8_t* A = (const uint8_t*)R.strs;
   size_t i = 0;
   while (i < R.frec.size()) {
     size_t j = i + 1;
@@ -4195,7 +4203,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
                        e->vals2.p, n_locs, e->locs2.p);
     HIP_TRY(hipGetLastError());
     // ---- 8. findings (censored lines, Match, Code, order) on the device
-    if ((rc = build_findings_dev(e, d_data, d_off, nbytes, n_locs, res))) return rc;
+    if ((rc = build_findings_dev(e, d_data, d_off, nbytes, nf, n_locs, res))) return rc;
     hl.resize(n_locs);
     HIP_TRY(hipMemcpyAsync(hl.data(), e->locs2.p, n_locs * sizeof(DevLoc), hipMemcpyDeviceToHost, s));
   }
@@ -4721,7 +4729,7 @@ size_t tsg_result_findings(const tsg_result* r, size_t file, const tsg_finding**
   auto it = R.fcache.find((uint32_t)file);
   if (it == R.fcache.end()) {  // views into the result's string arena, built once per file
     auto& slot = R.fcache[(uint32_t)file];
-    const char* A = (const char*)R.arena->p;
+    const char* A = R.strs;
     size_t nl = 0;
     for (auto q = lo; q != hi; ++q) nl += q->n_lines;
     slot.second.reserve(nl);
@@ -4739,12 +4747,12 @@ size_t tsg_result_findings(const tsg_result* r, size_t file, const tsg_finding**
       for (uint32_t k = 0; k < q->n_lines; ++k) {
         const CodeRec& c = R.code[(size_t)q->loc * kCodeLines + k];
         tsg_line tl{};
-        tl.number = c.number;
+        tl.number = c.number_flags & 0x1FFFFFFFu;
         tl.content = A + c.off;
         tl.content_len = c.len;
-        tl.is_cause = (c.flags & 1) != 0;
-        tl.first_cause = (c.flags & 2) != 0;
-        tl.last_cause = (c.flags & 4) != 0;
+        tl.is_cause = (c.number_flags >> 29) & 1;
+        tl.first_cause = (c.number_flags >> 30) & 1;
+        tl.last_cause = (c.number_flags >> 31) & 1;
         slot.second.push_back(tl);
       }
       slot.first.push_back(fd);
