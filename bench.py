@@ -302,12 +302,12 @@ def gate_checks(N, c, rules, gates, words, seed, density, n_sample=200):
                 files_with_any_keyword_rule=int(sum(bool(x.any()) for x in g)))
 
 
-def traffic_bytes(content_bytes):
+def traffic_bytes(content_bytes, kernel="k_scan_fast"):
     """HBM bytes per k_scan_fast launch from the committed rocprofv3 FETCH_SIZE
     pass (profiles/traffic_k_scan_fast.json, written by tools/prof_summary.py:
     FETCH_SIZE KiB x 1024 x 2, the gfx950 correction), scaled to this launch's
     content bytes when the profiled corpus differs.  None without a profile."""
-    p = os.path.join(ROOT, "profiles", "traffic_k_scan_fast.json")
+    p = os.path.join(ROOT, "profiles", f"traffic_{kernel}.json")
     if not os.path.exists(p):
         return None
     t = json.load(open(p))
@@ -437,7 +437,10 @@ def main():
     st = [ctypes.c_uint32() for _ in range(4)]
     fast = ctypes.c_int()
     N.check(N.lib.tsg_ruleset_stats(rs, *[ctypes.byref(x) for x in st], ctypes.byref(fast)))
-    scan_kernel = "k_scan_fast" if fast.value else "k_scan_generic"
+    # k_scan_fast when the automaton fits its LDS image, else k_scan_big (the
+    # configs[4] automaton: dense + sparse rows in LDS); both are bracketed by
+    # the engine's HIP events (timings[17])
+    scan_kernel = "k_scan_fast" if fast.value else "k_scan_big"
     gate_words = (len(sc.rules) + 31) // 32
     gates = (ctypes.c_uint32 * (c["n_files"] * gate_words))() if args.config == 1 else None
 
@@ -621,7 +624,8 @@ def main():
             "pct_hbm_peak": round(100.0 * value / (HBM_PEAK_GBPS * world), 2),
             "roofline": {"bound": "hbm", "kernel": scan_kernel, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic_bytes(c["total"]) if args.config == 2 else None, "algorithmic_bytes_per_launch": c["total"],
+                         "traffic": traffic_bytes(c["total"], scan_kernel) if args.config in (2, 4) else None,
+                         "algorithmic_bytes_per_launch": c["total"],
                          "avg_launch_ms": round(scan_kernel_ms, 3)},
             "stages_ms": ({"prefilter_total": round(stage[0], 3), "scan_kernel": round(scan_kernel_ms, 3)}
                           if args.config == 1 else {k: round(v, 3) for k, v in zip(

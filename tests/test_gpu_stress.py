@@ -116,19 +116,20 @@ def test_stress_1000_rules_vs_oracle(stress_cfg):
     assert custom > 200  # the generated rules really fire
 
 
-def test_stress_big_record_overflow_matches(stress_cfg, monkeypatch):
-    """k_scan_big's deferred-output slots full (TSG_BIG_REC_CAP=1): the
-    outputs past a lane's slots are resolved inline, and the findings equal
-    the deferred-only run (which test_stress_1000_rules_vs_oracle pins)."""
+def test_stress_entry_points_agree(stress_cfg):
+    """The big-automaton path (k_scan_big + k_big_report) through the three
+    entry points -- host batch (tsg_scan), batch already in HBM
+    (tsg_scan_device) and the analyzer front end on CR-free files
+    (tsg_analyze) -- gives identical findings, Match and Code included, in
+    Scan order."""
     path, rules = stress_cfg
     files = stress_rules.make_corpus(13, rules, 40)
+    files = [(p, d.replace(b"\r", b"")) for p, d in files]
     sc_g = S.new_scanner(S.parse_config(path), device=0)
     batch = [S.ScanArgs(p, d) for p, d in files]
     want = sc_g.scan_batch(batch)
-    monkeypatch.setenv("TSG_BIG_REC_CAP", "1")
-    got = sc_g.scan_batch(batch)
-    monkeypatch.setenv("TSG_BIG_REC_CAP", "0")
-    got0 = sc_g.scan_batch(batch)
-    assert [_canon(_plain(g)) for g in got] == [_canon(_plain(w)) for w in want]
-    assert [_canon(_plain(g)) for g in got0] == [_canon(_plain(w)) for w in want]
+    dev = sc_g.scan_batch_device(batch)
+    ana = sc_g.analyze_batch(batch)
+    assert [_plain(g) for g in dev] == [_plain(w) for w in want]
+    assert [_plain(g) for g in ana if g is not None] == [_plain(w) for w, g in zip(want, ana) if g is not None]
     assert sum(len(w.Findings) for w in want) > 50

@@ -255,7 +255,7 @@ struct FindRec {
 };
 
 struct CodeRec {
-  uint64_t off;          // file-relative source start (k_find_spans), then arena offset (k_find_copy)
+  uint64_t off;          // arena offset of the line's text
   uint32_t len;
   uint32_t number_flags;  // Number | flags << 29: 1 IsCause, 2 FirstCause, 4 LastCause
 };

@@ -136,9 +136,6 @@ struct ScanParams {
   uint8_t* span_hi;               // per kNlBlock span: a byte >= 0x80 occurs (k_fold_special)
   uint64_t* fold_pos;             // fold-special runes: position << 2 | kind (FoldKind), ctrl->n_fold of them
   uint64_t fold_cap;
-  uint64_t* big_rec;              // k_scan_big deferred outputs: (p << 16 | state), lane-strided
-  uint32_t* big_nrec;             // records per lane
-  uint32_t big_rec_cap;           // records per lane before k_scan_big reports inline
 };
 
 // Fold-special runes (the only non-ASCII runes that Go's case rules tie to
@@ -335,161 +332,6 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_generic(ScanParams P) {
     }
     atomicAdd(&P.nl_blocks[p0 / kNlBlock], nl);
   }
-}
-
-// Scan with an automaton too large for an LDS table (configs[4]: 1000+
-// custom rules): everything in LDS anyway -- dense rows for the shallow
-// states (breadth-first numbering: where text keeps the automaton), sparse
-// rows + failure links for the rest (BigDev) -- so no step waits on global
-// memory.  One 128-byte chunk per lane per step (7 bytes of warm-up), bytes
-// straight from HBM in 16-byte vectors, 1024 threads per CU.
-constexpr uint32_t kBigThreads = 1024;
-constexpr uint32_t kBigLdsMax = 152 * 1024;
-
-__global__ __launch_bounds__(kBigThreads) void k_scan_big(ScanParams P) {
-  extern __shared__ __align__(16) uint8_t smem[];
-  const BigDev& B = P.big;
-  for (uint32_t i = threadIdx.x; i < B.blob_bytes / 4; i += kBigThreads)
-    ((uint32_t*)smem)[i] = ((const uint32_t*)B.blob)[i];
-  __syncthreads();
-  const uint8_t* cls = smem;
-  const uint16_t* dense = (const uint16_t*)(smem + 256);
-  const uint32_t* eoff = (const uint32_t*)(smem + B.o_eoff);
-  const uint32_t* eval = (const uint32_t*)(smem + B.o_eval);
-  const uint16_t* fl = (const uint16_t*)(smem + B.o_fail);
-  const uint32_t K = P.rs.ac.nclasses, ND = B.n_dense;
-  // timing ablations only (TSG_REPORT_MODE, wave-uniform): 8 = no inline
-  // reports, 16 = cold states answered by the root row (wrong results)
-  const bool no_report = P.report_mode & 8, dense_only = P.report_mode & 16;
-  auto next = [&](uint32_t st, uint32_t c) -> uint32_t {
-    if (dense_only && st >= ND) st = 0;
-    while (st >= ND) {
-      const uint32_t j = st - ND;
-      for (uint32_t k = eoff[j]; k < eoff[j + 1]; ++k) {
-        const uint32_t v = eval[k];
-        if ((v >> 16) == c) return v & 0xFFFFu;
-      }
-      st = fl[j];
-    }
-    return dense[st * K + c];
-  };
-  const uint64_t nchunks = (P.nbytes + kChunk - 1) / kChunk;
-  const uint64_t nfull = P.nbytes / kChunk;  // chunks with all 128 bytes in the batch
-  const uint64_t stride = (uint64_t)gridDim.x * kBigThreads;
-  uint64_t last_kw = ~0ull;
-  // Full chunks: the chunk's 128 bytes and the 16 before it (warm-up) are
-  // loaded as nine independent 16-byte vectors, and the lane's NEXT chunk is
-  // loaded while this one walks, so HBM latency is paid once per lane rather
-  // than once per 16 bytes (the walk itself is LDS-bound).
-  constexpr int kVecs = kChunk / 16;
-  uint4 cur[kVecs + 1], nxt[kVecs + 1];
-  auto load_chunk = [&](uint64_t c, uint4 (&v)[kVecs + 1]) {
-    const uint64_t p0 = c * kChunk;
-    v[0] = p0 >= 16 ? *(const uint4*)(P.data + p0 - 16) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (int k = 0; k < kVecs; ++k) v[k + 1] = *(const uint4*)(P.data + p0 + 16 * k);
-  };
-  uint64_t ch = (uint64_t)blockIdx.x * kBigThreads + threadIdx.x;
-  // outputs are deferred to k_big_report as lane-strided 8-byte records
-  // (resolving them inline cost 2/3 of the kernel: a call with spills, a file
-  // search and divergent output loops inside the LDS walk); a lane whose
-  // record space is full reports inline, so nothing is ever dropped
-  const uint64_t gl = (uint64_t)blockIdx.x * kBigThreads + threadIdx.x;
-  uint32_t nrec = 0;
-  auto output = [&](uint32_t st, uint64_t p) {
-    if (no_report) return;
-    if (nrec < P.big_rec_cap) P.big_rec[(uint64_t)nrec++ * stride + gl] = (p << 16) | st;
-    else report(P, st, p, &last_kw);
-  };
-  if (ch < nfull) load_chunk(ch, nxt);
-  for (; ch < nfull; ch += stride) {
-#pragma unroll
-    for (int k = 0; k <= kVecs; ++k) cur[k] = nxt[k];
-    if (ch + stride < nfull) load_chunk(ch + stride, nxt);
-    const uint64_t p0 = ch * kChunk;
-    uint32_t st = 0;
-    if (p0 >= (uint64_t)(kAcMaxLit - 1)) {  // warm-up: bytes p0-7 .. p0-1 (kAcMaxLit = 8)
-      const uint32_t w[4] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w};
-#pragma unroll
-      for (int i = 16 - (kAcMaxLit - 1); i < 16; ++i) st = next(st, cls[(w[i >> 2] >> (8 * (i & 3))) & 0xFFu]) & 0x7FFFu;
-    }
-    uint32_t nl = 0;
-#pragma unroll
-    for (int k = 0; k < kVecs; ++k) {
-      const uint32_t w[4] = {cur[k + 1].x, cur[k + 1].y, cur[k + 1].z, cur[k + 1].w};
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const uint32_t b = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-        nl += b == '\n';
-        const uint32_t nx = next(st, cls[b]);
-        st = nx & 0x7FFFu;
-        if (nx & 0x8000u) output(st, p0 + 16 * k + i);
-      }
-    }
-    atomicAdd(&P.nl_blocks[p0 / kNlBlock], nl);
-  }
-  // the partial last chunk (at most one in the batch), byte by byte
-  for (uint64_t c = nfull + (uint64_t)blockIdx.x * kBigThreads + threadIdx.x; c < nchunks; c += stride) {
-    const uint64_t p0 = c * kChunk;
-    uint32_t st = 0;
-    for (uint64_t p = p0 >= (uint64_t)(kAcMaxLit - 1) ? p0 - (kAcMaxLit - 1) : 0; p < p0; ++p)
-      st = next(st, cls[P.data[p]]) & 0x7FFFu;
-    uint32_t nl = 0;
-    for (uint64_t p = p0; p < P.nbytes; ++p) {
-      const uint32_t b = P.data[p];
-      nl += b == '\n';
-      const uint32_t nx = next(st, cls[b]);
-      st = nx & 0x7FFFu;
-      if (nx & 0x8000u) output(st, p);
-    }
-    atomicAdd(&P.nl_blocks[p0 / kNlBlock], nl);
-  }
-  P.big_nrec[gl] = nrec;
-}
-
-// k_scan_big's deferred outputs: one thread per scan lane resolves its
-// records (report_t: file lookup, confirm, keyword gates, anchor hits).
-// Anchor hits of k_big_report staged in LDS and appended to P.hits with one
-// global atomic per block (a global atomic per hit on the one counter
-// serialised at L2: 2.3 M hits cost 27 ms on configs[4]); overflow past the
-// stage goes straight to global.
-constexpr uint32_t kBigHitStage = 4096;
-struct LdsHitSink {
-  uint64_t* buf;
-  uint32_t* cnt;
-  __device__ void push(const ScanParams& P, uint64_t rec) {
-    const uint32_t i = atomicAdd(cnt, 1u);
-    if (i < kBigHitStage) {
-      buf[i] = rec;
-    } else {
-      GlobalHitSink g;
-      g.push(P, rec);
-    }
-  }
-};
-
-__global__ __launch_bounds__(256) void k_big_report(ScanParams P, uint64_t nlanes) {
-  __shared__ uint64_t stage[kBigHitStage];
-  __shared__ uint32_t n_stage;
-  __shared__ unsigned long long base;
-  if (threadIdx.x == 0) n_stage = 0;
-  __syncthreads();
-  const uint64_t gl = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  LdsHitSink sink{stage, &n_stage};
-  if (gl < nlanes) {
-    const uint32_t n = P.big_nrec[gl];
-    uint64_t last_kw = ~0ull;
-    for (uint32_t k = 0; k < n; ++k) {
-      const uint64_t r = P.big_rec[(uint64_t)k * nlanes + gl];
-      report_t<false>(P, (uint32_t)(r & 0xFFFFu), r >> 16, &last_kw, sink);
-    }
-  }
-  __syncthreads();
-  const uint32_t m = n_stage < kBigHitStage ? n_stage : kBigHitStage;
-  if (threadIdx.x == 0) base = m ? atomicAdd(&P.ctrl->hits, (unsigned long long)m) : 0ull;
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < m; i += 256)
-    if (base + i < P.hit_cap) P.hits[base + i] = stage[i];
 }
 
 // Fast scan: the HBM-bound hot loop — one pass of the keyword/anchor
@@ -815,6 +657,218 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
     u = un;
   }
   if (lane == 0) P.ev_counts[wave] = ev_count < P.ev_cap_per_wave ? ev_count : P.ev_cap_per_wave;
+}
+
+// Scan with an automaton too large for k_scan_fast's image (configs[4]: 1000+
+// custom rules), in k_scan_fast's shape: one 4 KiB span per lane (7 bytes of
+// warm-up), the span streamed through a 128-byte register ring, 1024 threads
+// and ONE LDS copy of the automaton per CU (BigDev: byte classes, dense rows of
+// the shallowest states, sparse rows + failure links for the rest).  The byte
+// class lookups do not depend on the state, so only the row lookup sits on the
+// dependent chain.  Outputs: entries carry bit 15; the OR over an 8-byte group
+// flags it, and a flagged group becomes a FastEvent (ballot/popcount into the
+// wave's segment) that k_big_report replays -- no per-byte output branch, no
+// global atomics, newlines counted SWAR and stored once per span.
+constexpr uint32_t kBigThreads = 1024;
+constexpr uint32_t kBigLdsMax = 152 * 1024;
+
+struct BigLds {
+  const uint8_t* cls;
+  const uint16_t* dense;
+  const uint32_t* eoff;
+  const uint32_t* eval;
+  const uint16_t* fl;
+  uint32_t K, ND;
+};
+
+__device__ inline BigLds big_lds(const BigDev& B, const uint8_t* smem, uint32_t K) {
+  return BigLds{smem, (const uint16_t*)(smem + 256), (const uint32_t*)(smem + B.o_eoff),
+                (const uint32_t*)(smem + B.o_eval), (const uint16_t*)(smem + B.o_fail), K, B.n_dense};
+}
+
+// delta(st, c): own entry of a cold state, else its failure state's (the
+// chain ends in a dense row).  Entry bit 15 = output state.
+__device__ inline uint32_t big_next(const BigLds& L, uint32_t st, uint32_t c) {
+  while (st >= L.ND) {
+    const uint32_t j = st - L.ND;
+    for (uint32_t k = L.eoff[j]; k < L.eoff[j + 1]; ++k) {
+      const uint32_t v = L.eval[k];
+      if ((v >> 16) == c) return v & 0xFFFFu;
+    }
+    st = L.fl[j];
+  }
+  return L.dense[st * L.K + c];
+}
+
+// 8 bytes (two dwords) through the automaton from entry e; returns the OR of
+// the entries (bit 15 = some output state was reached).
+__device__ inline uint32_t big_group(const BigLds& L, uint32_t& e, uint32_t d0, uint32_t d1) {
+  uint32_t c[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c[j] = L.cls[((j < 4 ? d0 : d1) >> (8 * (j & 3))) & 0xFFu];
+  uint32_t acc = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t nx = big_next(L, e, c[j]);
+    acc |= nx;
+    e = nx & 0x7FFFu;
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(kBigThreads) void k_scan_big(ScanParams P) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  const BigDev& B = P.big;
+  for (uint32_t i = threadIdx.x; i < B.blob_bytes / 4; i += kBigThreads)
+    ((uint32_t*)smem)[i] = ((const uint32_t*)B.blob)[i];
+  __syncthreads();
+  const BigLds L = big_lds(B, smem, P.rs.ac.nclasses);
+  constexpr int V = 8;
+  constexpr int kStep = V * 16;
+  constexpr int kSteps = kNlBlock / kStep;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t lanes_lt = (1ull << lane) - 1;
+  const uint32_t wave = blockIdx.x * (kBigThreads / 64) + (threadIdx.x >> 6);
+  const uint64_t nlanes = (uint64_t)gridDim.x * kBigThreads;
+  const uint64_t units = (P.nbytes + kNlBlock - 1) / kNlBlock;
+  FastEvent* ev_seg = P.events + (uint64_t)wave * P.ev_cap_per_wave;
+  uint32_t ev_count = 0;  // wave-uniform
+  uint64_t u = (uint64_t)blockIdx.x * kBigThreads + threadIdx.x;
+  uint4 cur[V], nxt[V];
+  uint64_t pos = u * kNlBlock;
+  if (u < units) {
+    const uint8_t* src = fast_src(P, pos);
+#pragma unroll
+    for (int k = 0; k < V; ++k) nxt[k] = *(const uint4*)(src + pos + 16 * k);
+  }
+  while (__ballot(u < units)) {
+    const bool live = u < units;
+    const uint64_t un = u + nlanes;
+    const uint64_t s0 = pos;
+    const uint2 h = live && s0 >= 8 ? *(const uint2*)(fast_src(P, s0 - 8) + s0 - 8) : make_uint2(0, 0);
+    uint32_t e = 0;
+    {  // warm-up: the 7 bytes before the span (automaton depth <= kAcMaxLit)
+#pragma unroll
+      for (int j = 1; j < 8; ++j) e = big_next(L, e, L.cls[((j < 4 ? h.x : h.y) >> (8 * (j & 3))) & 0xFFu]) & 0x7FFFu;
+    }
+    uint2 prev = h;
+    uint32_t nl = 0, hi = 0;
+    for (int step = 0; step < kSteps; ++step) {
+#pragma unroll
+      for (int k = 0; k < V; ++k) cur[k] = nxt[k];
+      const uint64_t np = step + 1 < kSteps ? pos + kStep : un * kNlBlock;
+      if (live && (step + 1 < kSteps || un < units)) {
+        const uint8_t* src = fast_src(P, np);
+#pragma unroll
+        for (int k = 0; k < V; ++k) nxt[k] = *(const uint4*)(src + np + 16 * k);
+      }
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const uint32_t d[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          const uint32_t d0 = d[2 * g], d1 = d[2 * g + 1];
+          nl += nl_count_dword(d0) + nl_count_dword(d1);
+          hi |= d0 | d1;
+          const uint32_t gs = e;
+          const uint32_t acc = big_group(L, e, d0, d1);
+          const uint64_t b = __ballot(live && (acc & 0x8000u));
+          if (b) {
+            if ((b >> lane) & 1) {
+              FastEvent r;
+              r.pos = pos + 16 * k + 8 * g;
+              r.entry = gs;
+              r.pad = 0;
+              r.prev = prev;
+              r.cur = make_uint2(d0, d1);
+              const uint32_t slot = ev_count + (uint32_t)__popcll(b & lanes_lt);
+              if (slot < P.ev_cap_per_wave) {
+                ev_seg[slot] = r;
+              } else {
+                unsigned long long ov = atomicAdd(&P.ctrl->ev_overflow, 1ull);
+                if (ov < P.ev_overflow_cap) P.ev_overflow[ov] = r;
+              }
+            }
+            ev_count += (uint32_t)__popcll(b);
+          }
+          prev = make_uint2(d0, d1);
+        }
+      }
+      pos = np;
+    }
+    if (live) {
+      P.nl_blocks[s0 / kNlBlock] = nl;
+      P.span_hi[s0 / kNlBlock] = (hi & 0x80808080u) ? 1 : 0;
+    }
+    u = un;
+  }
+  if (lane == 0) P.ev_counts[wave] = ev_count < P.ev_cap_per_wave ? ev_count : P.ev_cap_per_wave;
+}
+
+// k_scan_big's events: each flagged 8-byte group is replayed from its entry
+// state with the big automaton (blob in LDS) and every output state reached
+// is resolved by report_t (file lookup, confirm on the real bytes, keyword
+// gate bits, anchor hits).  Anchor hits are staged in LDS and appended to
+// P.hits with one global atomic per block (a global atomic per hit on the one
+// counter serialised at L2: 2.3 M hits cost 27 ms on configs[4]); overflow
+// past the stage goes straight to global.
+constexpr uint32_t kBigHitStage = 512;  // (blob <= kBigLdsMax + this stage fits the 160 KiB LDS)
+struct LdsHitSink {
+  uint64_t* buf;
+  uint32_t* cnt;
+  __device__ void push(const ScanParams& P, uint64_t rec) {
+    const uint32_t i = atomicAdd(cnt, 1u);
+    if (i < kBigHitStage) {
+      buf[i] = rec;
+    } else {
+      GlobalHitSink g;
+      g.push(P, rec);
+    }
+  }
+};
+
+__global__ __launch_bounds__(1024) void k_big_report(ScanParams P, uint32_t n_waves) {
+  extern __shared__ __align__(16) uint8_t smem[];  // blob, then the hit stage
+  const BigDev& B = P.big;
+  for (uint32_t i = threadIdx.x; i < B.blob_bytes / 4; i += blockDim.x)
+    ((uint32_t*)smem)[i] = ((const uint32_t*)B.blob)[i];
+  uint64_t* stage = (uint64_t*)(smem + ((B.blob_bytes + 15) & ~15u));
+  __shared__ uint32_t n_stage;
+  __shared__ unsigned long long base;
+  const BigLds L = big_lds(B, smem, P.rs.ac.nclasses);
+  uint64_t last_kw = ~0ull;
+  for (uint32_t w = blockIdx.x; w < n_waves + 1; w += gridDim.x) {
+    if (threadIdx.x == 0) n_stage = 0;
+    __syncthreads();
+    const FastEvent* seg;
+    uint64_t n;
+    if (w < n_waves) {
+      seg = P.events + (uint64_t)w * P.ev_cap_per_wave;
+      n = P.ev_counts[w];
+      if (threadIdx.x == 0 && n) atomicAdd(&P.ctrl->events, (unsigned long long)n);
+    } else {  // overflow bucket
+      seg = P.ev_overflow;
+      n = P.ctrl->ev_overflow < P.ev_overflow_cap ? P.ctrl->ev_overflow : P.ev_overflow_cap;
+    }
+    LdsHitSink sink{stage, &n_stage};
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const FastEvent ev = seg[i];
+      uint32_t e = ev.entry;
+#pragma unroll 1
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t nx = big_next(L, e, L.cls[((j < 4 ? ev.cur.x : ev.cur.y) >> (8 * (j & 3))) & 0xFFu]);
+        e = nx & 0x7FFFu;
+        if (nx & 0x8000u) report_t<false>(P, e, ev.pos + j, &last_kw, sink);
+      }
+    }
+    __syncthreads();
+    const uint32_t m = n_stage < kBigHitStage ? n_stage : kBigHitStage;
+    if (threadIdx.x == 0) base = m ? atomicAdd(&P.ctrl->hits, (unsigned long long)m) : 0ull;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
+      if (base + i < P.hit_cap) P.hits[base + i] = stage[i];
+    __syncthreads();
+  }
 }
 
 #ifdef TSG_EXPERIMENTS  // A/B shapes measured slower; not in the product library
@@ -2431,6 +2485,7 @@ struct FindParams {
   uint2* grp;          // per location: (first slot of its file group, intervals in it)
   FindRec* rec;
   CodeRec* code;       // kCodeLines per location
+  uint64_t* code_src;  // their file-relative source starts (k_find_copy may run twice: kept apart from off)
   uint64_t* len;       // per location: arena bytes
   uint64_t* arena_off; // exclusive prefix of len
   uint8_t* arena;
@@ -2641,7 +2696,7 @@ __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
       const bool cause = ln >= sl && ln <= el;
       if (lane == 0) {
         CodeRec c{};
-        c.off = p;  // source start until k_find_copy places it
+        F.code_src[w * kCodeLines + k] = p;
         c.len = (uint32_t)(q - p);
         const uint32_t flags = (cause ? 1u : 0u) | (cause && !found_first ? 2u : 0u) | (cause && ln == el ? 4u : 0u);
         c.number_flags = (ln + 1) | (flags << 29);
@@ -2698,8 +2753,8 @@ __global__ __launch_bounds__(256) void k_find_copy(FindParams F) {
   wave_copy_censored(F, fs, g.x, g.y, r.m_src, r.m_len, dst, lane);
   dst += r.m_len;
   for (uint32_t k = 0; k < r.n_lines; ++k) {
-    CodeRec c = F.code[w * kCodeLines + k];
-    wave_copy_censored(F, fs, g.x, g.y, c.off, c.len, dst, lane);
+    const CodeRec c = F.code[w * kCodeLines + k];
+    wave_copy_censored(F, fs, g.x, g.y, F.code_src[w * kCodeLines + k], c.len, dst, lane);
     if (lane == 0) F.code[w * kCodeLines + k].off = dst;
     dst += c.len;
   }
@@ -2911,8 +2966,6 @@ struct tsg_engine {
   hipStream_t stream = nullptr;
   std::mutex mu;
   DevImage img;
-  DBuf<uint64_t> big_rec;  // k_scan_big deferred output records
-  DBuf<uint32_t> big_nrec;
   DBuf<uint8_t> data;
   DBuf<uint64_t> off;
   DBuf<uint8_t> paths;
@@ -2960,7 +3013,7 @@ struct tsg_engine {
   double stage_ms[2] = {0, 0};  // last stage_host_batch: pack (+ overlapped H2D), H2D tail (host clock)
   std::vector<double> gate_tm;          // timings of the last tsg_gate_device call
   // device findings (build_findings_dev)
-  DBuf<uint64_t> f_iv, f_len, f_off;
+  DBuf<uint64_t> f_iv, f_len, f_off, f_csrc;
   DBuf<uint2> f_grp;
   DBuf<FindRec> f_rec, f_rec2;
   DBuf<CodeRec> f_code;
@@ -3614,22 +3667,42 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     hipLaunchKernelGGL(k_fold_special, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_spans + 255) / 256, 2048))),
                        dim3(256), 0, s, P, n_spans);
   } else if (P.big.blob && !experiment_env("TSG_NO_BIG")) {
-    const uint64_t nchunks = (P.nbytes + kChunk - 1) / kChunk;
-    const uint32_t blocks = (uint32_t)std::max<uint64_t>(
-        1, std::min<uint64_t>((nchunks + kBigThreads - 1) / kBigThreads, (uint64_t)e->num_cus));
+    // k_scan_fast's span / tail / event layout (one 4 KiB span per lane)
+    const uint32_t nt = kBigThreads;
+    P.tail_base = (P.nbytes / kNlBlock) * kNlBlock;
+    const uint64_t lead = P.tail_base >= 8 ? 8 : P.tail_base;
+    HIP_TRY(e->tail.ensure(8 + kFastUnitMax + 64));
+    HIP_TRY(hipMemsetAsync(e->tail.p, 0, 8 + kFastUnitMax + 64, s));
+    if (P.nbytes - P.tail_base + lead)
+      HIP_TRY(hipMemcpyAsync(e->tail.p + 8 - lead, P.data + P.tail_base - lead, P.nbytes - P.tail_base + lead,
+                             hipMemcpyDeviceToDevice, s));
+    P.tail = e->tail.p + 8 - P.tail_base;
+    const uint64_t units = (P.nbytes + kNlBlock - 1) / kNlBlock;
+    HIP_TRY(e->span_hi.ensure(units + 1));
+    P.span_hi = e->span_hi.p;
+    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((units + nt - 1) / nt, e->num_cus));
+    const uint64_t n_waves = (uint64_t)blocks * (nt / 64);
+    P.ev_cap_per_wave = std::max<uint64_t>(1024, (P.nbytes / 256) / n_waves + 256);
+    HIP_TRY(e->ev_buf.ensure(n_waves * P.ev_cap_per_wave));
+    HIP_TRY(e->ev_counts.ensure(n_waves));
+    HIP_TRY(e->ev_overflow.ensure(std::max<uint64_t>(1 << 20, e->ev_ovf_need)));
+    P.events = e->ev_buf.p;
+    P.ev_counts = e->ev_counts.p;
+    P.ev_overflow = e->ev_overflow.p;
+    P.ev_overflow_cap = e->ev_overflow.n;
+    HIP_TRY(hipMemsetAsync(&P.ctrl->ev_overflow, 0, 8, s));
     HIP_TRY(hipFuncSetAttribute((const void*)k_scan_big, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)P.big.blob_bytes));
-    const uint64_t nlanes = (uint64_t)blocks * kBigThreads;
-    P.big_rec_cap = 64;  // 8-byte records per lane (~9 per lane per 10 GB on configs[4])
-    // test hook (same results, exercises the inline fallback): tests/test_gpu_stress.py
-    if (const char* c = getenv("TSG_BIG_REC_CAP")) P.big_rec_cap = (uint32_t)std::max(0, atoi(c));
-    HIP_TRY(e->big_rec.ensure(nlanes * P.big_rec_cap));
-    HIP_TRY(e->big_nrec.ensure(nlanes));
-    P.big_rec = e->big_rec.p;
-    P.big_nrec = e->big_nrec.p;
-    hipLaunchKernelGGL(k_scan_big, dim3(blocks), dim3(kBigThreads), P.big.blob_bytes, s, P);
+    if (e->events) HIP_TRY(hipEventRecord(e->ev[10], s));
+    hipLaunchKernelGGL(k_scan_big, dim3(blocks), dim3(nt), P.big.blob_bytes, s, P);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_big_report, dim3((uint32_t)((nlanes + 255) / 256)), dim3(256), 0, s, P, nlanes);
+    if (e->events) HIP_TRY(hipEventRecord(e->ev[11], s));
+    e->fast_timed = e->events;
+    const uint32_t rep_lds = ((P.big.blob_bytes + 15) & ~15u) + kBigHitStage * 8;
+    HIP_TRY(hipFuncSetAttribute((const void*)k_big_report, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rep_lds));
+    hipLaunchKernelGGL(k_big_report, dim3((uint32_t)std::min<uint64_t>(n_waves + 1, e->num_cus)), dim3(1024), rep_lds, s,
+                       P, (uint32_t)n_waves);
+    HIP_TRY(hipGetLastError());
   } else {
     const size_t table_bytes = (size_t)ac.nstates * ac.nclasses * 2;
     const bool lds_table = table_bytes <= (size_t)kLdsTableMax;
@@ -3679,6 +3752,7 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   HIP_TRY(e->f_rec.ensure(n_locs));
   HIP_TRY(e->f_rec2.ensure(n_locs));
   HIP_TRY(e->f_code.ensure(kCodeLines * n_locs));
+  HIP_TRY(e->f_csrc.ensure(kCodeLines * n_locs));
   HIP_TRY(e->f_len.ensure(n_locs));
   HIP_TRY(e->f_off.ensure(n_locs));
   HIP_TRY(e->f_arena.ensure(std::max<uint64_t>(1 << 20, e->f_arena_need)));
@@ -3694,6 +3768,7 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   F.grp = e->f_grp.p;
   F.rec = e->f_rec.p;
   F.code = e->f_code.p;
+  F.code_src = e->f_csrc.p;
   F.len = e->f_len.p;
   F.arena_off = e->f_off.p;
   F.sort_key = e->keys.p;
@@ -3886,7 +3961,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     if ((rc = launch_fold_windows(e, P, true))) return rc;
     Ctrl c;
     if ((rc = read_ctrl(e, &c))) return rc;
-    const bool ev_lost = rs->ac.fast.size() && c.ev_overflow > e->ev_overflow.n;
+    const bool ev_lost = (rs->ac.fast.size() || P.big.blob) && c.ev_overflow > e->ev_overflow.n;
     const bool fold_lost = c.n_fold > P.fold_cap;
     if (c.hits <= hit_cap && !ev_lost && !fold_lost) {
       scanned = true;
@@ -4017,7 +4092,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     V.cap_cap = e->caps.n;
     V.caps_big = e->caps_big.p;
     V.cap_big_cap = e->caps_big.n;
-    V.span_hi = rs->ac.fast.size() && nbytes ? e->span_hi.p : nullptr;
+    V.span_hi = (rs->ac.fast.size() || P.big.blob) && nbytes ? e->span_hi.p : nullptr;
     const bool prof = experiment_env("TSG_PROFILE_VERIFY") != nullptr;
     if (prof) {  // diagnostics only: the job count on the host
       HIP_TRY(hipMemcpyAsync(&n_jobs, e->nsel.p, 4, hipMemcpyDeviceToHost, s));
@@ -4342,6 +4417,8 @@ void tsg_engine_free(tsg_engine* e) {
   if (e->h_stage) (void)hipHostFree(e->h_stage);
   e->gate_out.release(); e->gate_rules.release(); e->bin8.release(); e->strip_out.release();
   e->strip_off.release(); e->blk_kept.release(); e->blk_base.release(); e->chunk_pos.release(); e->n_drop.release();
+  e->f_iv.release(); e->f_len.release(); e->f_off.release(); e->f_csrc.release(); e->f_grp.release();
+  e->f_rec.release(); e->f_rec2.release(); e->f_code.release(); e->f_arena.release();
   if (e->events)
     for (auto& ev : e->ev) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream);
@@ -4644,7 +4721,7 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
     if ((rc = launch_scan(e, P))) return rc;
     Ctrl c;
     if ((rc = read_ctrl(e, &c))) return rc;
-    const bool ev_lost = rs->ac.fast.size() && c.ev_overflow > e->ev_overflow.n;
+    const bool ev_lost = (rs->ac.fast.size() || P.big.blob) && c.ev_overflow > e->ev_overflow.n;
     if (!ev_lost && c.n_fold <= P.fold_cap) {
       if ((rc = launch_fold_windows(e, P, false))) return rc;
       scanned = true;
