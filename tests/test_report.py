@@ -1,0 +1,72 @@
+"""Trivy's JSON report of secret findings (trivy_amd/report.py) against the
+reference's own golden report (integration/testdata/secrets.json.golden,
+copied to tests/golden/integration): the same findings render to the same
+bytes (pkg/report/json.go MarshalIndent, omitempty, Go string escaping).
+The GPU variant renders what the engine itself found in the golden repo."""
+import json
+import os
+
+import pytest
+
+from .conftest import GOLDEN
+
+R = pytest.importorskip("trivy_amd.report")
+T = pytest.importorskip("trivy_amd.types")
+
+GOLDEN_JSON = os.path.join(GOLDEN, "integration", "secrets.json.golden")
+
+
+def _secrets_from_golden(g):
+    out = []
+    for res in g["Results"]:
+        fs = []
+        for f in res["Secrets"]:
+            lines = [T.Line(**{k: v for k, v in ln.items()}) for ln in (f["Code"]["Lines"] or [])]
+            fs.append(T.SecretFinding(RuleID=f["RuleID"], Category=f["Category"], Severity=f["Severity"],
+                                      Title=f["Title"], StartLine=f["StartLine"], EndLine=f["EndLine"],
+                                      Code=T.Code(Lines=lines), Match=f["Match"]))
+        out.append(T.Secret(FilePath=res["Target"], Findings=fs))
+    return out
+
+
+def _render(g, secrets):
+    return R.report_json(secrets, artifact_name=g["ArtifactName"], artifact_type=g["ArtifactType"],
+                         created_at=g["CreatedAt"], metadata=g["Metadata"], schema_version=g["SchemaVersion"])
+
+
+def test_golden_report_round_trip():
+    text = open(GOLDEN_JSON, encoding="utf-8").read()
+    g = json.loads(text)
+    assert _render(g, _secrets_from_golden(g)) == text
+
+
+def test_go_escaping_and_omitempty():
+    f = T.SecretFinding(RuleID="r", Title="<a & b>", Match="x y", Code=T.Code(Lines=[]))
+    out = R.dumps(R.secret_results([T.Secret(FilePath="p", Findings=[f]), T.Secret(FilePath="q")]))
+    assert "\\u003ca \\u0026 b\\u003e" in out and "x\\u2028y" in out
+    assert '"Lines": null' in out and '"Target": "q"' not in out
+    ln = R.line_json(T.Line(Number=1, Content="", Highlighted=""))
+    assert "Highlighted" not in ln and list(ln) == ["Number", "Content", "IsCause", "Annotation", "Truncated",
+                                                    "FirstCause", "LastCause"]
+
+
+@pytest.mark.gpu
+def test_gpu_findings_render_the_golden_report():
+    from trivy_amd.analyzer import SecretAnalyzer
+
+    text = open(GOLDEN_JSON, encoding="utf-8").read()
+    g = json.loads(text)
+    repo = os.path.join(GOLDEN, "integration", "repo")
+    a = SecretAnalyzer()
+    a.init(os.path.join(repo, "trivy-secret.yaml"))
+    got = []
+    for name in sorted(os.listdir(repo)):
+        data = open(os.path.join(repo, name), "rb").read()
+        if not a.required(name, len(data)):
+            continue
+        res = a.analyze(name, data, ".")
+        for s in res or []:
+            # AnalysisResult.Sort (analyzer.go:218-229): findings by (RuleID, StartLine)
+            s.Findings.sort(key=lambda f: (f.RuleID, f.StartLine))
+            got.append(s)
+    assert _render(g, got) == text
