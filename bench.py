@@ -48,7 +48,8 @@ WORKLOADS = {
        "batched analyze (IsBinary, CR strip, scan, findings) per layer; PCIe-inclusive (pinned staging + H2D in "
        "the step); file shards = layers per rank",
     4: "configs[4]: stress, builtin + generated gitleaks-style custom rules (explosion rules, keyword-less rules), "
-       "mixed text corpus resident in HBM",
+       "mixed text corpus resident in HBM + 10 % C5 material (stress-rule instances, 16 MiB minified line, "
+       "binary-ish files)",
 }
 HBM_PEAK_GBPS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 
@@ -101,6 +102,77 @@ def build_corpus(N, torch, seed, gb, density, device):
     del d_chunks
     return dict(n_files=n_files, total=content, packed=total, off=off, d_data=d_data, d_off=d_off, d_paths=d_paths,
                 d_poff=d_poff, plants=plants, sizes=sizes)
+
+
+def stress_material(stress_rules, srules, seed, target_bytes):
+    """configs[4] C5 material: stress-rule corpus files (planted custom-rule
+    instances), one 16 MiB minified single-line file, binary-ish files; the
+    unique set is replicated under new paths up to target_bytes.  Returns
+    (unique files, all files) as (path bytes, content bytes)."""
+    files = stress_rules.make_corpus(seed + 44, srules, 3000, long_line_bytes=1 << 20)
+    big = stress_rules.make_corpus(seed + 45, srules, 0, long_line_bytes=16 << 20)[0]
+    uniq = [(p.encode(), d) for p, d in files] + [(b"stress/min/vendor.bundle.min.js", big[1])]
+    out, total, k = [], 0, 0
+    while total < target_bytes:
+        for p, d in uniq:
+            out.append((p if k == 0 else b"r%d/" % k + p, d))
+            total += len(d)
+        k += 1
+    return uniq, out
+
+
+def append_files(torch, c, files, device):
+    """The corpus dict with `files` appended (same layout: NUL after each
+    file, path offsets continuing), new device tensors."""
+    dev = torch.device("cuda", device)
+    n0 = c["n_files"]
+    sizes = np.array([len(d) for _, d in files], dtype=np.int64)
+    off_new = np.zeros(len(files) + 1, dtype=np.uint64)
+    off_new[1:] = np.cumsum(sizes + 1).astype(np.uint64)
+    blob = np.zeros(int(off_new[-1]), dtype=np.uint8)
+    for (_, d), o in zip(files, off_new[:-1]):
+        blob[int(o):int(o) + len(d)] = np.frombuffer(d, dtype=np.uint8)
+    packed = c["packed"]
+    d_data = torch.zeros(packed + len(blob) + 4096, dtype=torch.uint8, device=dev)
+    d_data[:packed] = c["d_data"][:packed]
+    d_data[packed:packed + len(blob)] = torch.from_numpy(blob).to(dev)
+    off = np.concatenate([c["off"], c["off"][-1] + off_new[1:]])
+    poff_old = c["d_poff"].cpu().numpy()
+    pb = b"".join(p for p, _ in files)
+    plen = np.array([len(p) for p, _ in files], dtype=np.int64)
+    poff_new = poff_old[-1] + np.concatenate([[0], np.cumsum(plen)])
+    d_paths = torch.zeros(int(poff_new[-1]) + 64, dtype=torch.uint8, device=dev)
+    d_paths[: int(poff_old[-1])] = c["d_paths"][: int(poff_old[-1])]
+    d_paths[int(poff_old[-1]): int(poff_new[-1])] = torch.from_numpy(np.frombuffer(pb, dtype=np.uint8).copy()).to(dev)
+    poff = np.concatenate([poff_old, poff_new[1:]]).astype(np.int64)
+    c2 = dict(c)
+    c2.update(n_files=n0 + len(files), total=c["total"] + int(sizes.sum()), packed=packed + len(blob), off=off,
+              d_data=d_data, d_off=torch.from_numpy(off.view(np.int64)).to(dev), d_paths=d_paths,
+              d_poff=torch.from_numpy(poff).to(dev), sizes=np.concatenate([c["sizes"], sizes]),
+              first_stress=n0)
+    return c2
+
+
+def stress_checks(N, res, rules, c, uniq, oracle_cfg, n_check=80):
+    """Oracle spot checks of the appended stress files (full findings, Match
+    and Code included), the minified 16 MiB line excluded (oracle time)."""
+    from oracle import secret_oracle as O
+
+    oracle = O.Scanner(O.parse_config(oracle_cfg))
+    f0 = c["first_stress"]
+    bad, found, custom = [], 0, 0
+    picks = list(range(0, len(uniq) - 1, max(1, (len(uniq) - 1) // n_check)))[:n_check]
+    picks += [i for i, (p, _) in enumerate(uniq) if b"/bin/" in p or b"/min/app" in p]
+    for i in sorted(set(picks)):
+        p, d = uniq[i]
+        want = oracle.scan(p.decode(), d)
+        found += len(want["Findings"])
+        custom += sum(x.RuleID.startswith("stress-") for x in want["Findings"])
+        if sorted(result_findings(N, res, f0 + i, rules)) != sorted(oracle_findings(want)):
+            bad.append(p.decode())
+    return dict(stress_files=len(set(picks)), stress_findings=found, stress_custom_findings=custom,
+                stress_mismatched=bad[:10], stress_mismatched_files=len(bad),
+                stress_bytes=int(sum(c["sizes"][c["first_stress"]:])))
 
 
 def build_layer_tar(host, off, sizes, pbytes, poff):
@@ -225,15 +297,16 @@ def parity_checks(N, S, c, locs, rules, seed, density, n_sample=300, oracle_cfg=
     # oracle spot checks
     rng = np.random.default_rng(seed + 7)
     sizes = c["sizes"]
+    n_gen = c.get("first_stress", c["n_files"])  # generated files (configs[4] appends stress files after them)
     fold = plants[plants["decoy"] == PLANT_FOLD]
     fold_files = [int(f) for f in np.unique(fold["file"]) if sizes[f] <= (8 << 20)]
-    nonascii = [f for f in range(c["n_files"]) if sizes[f] >= 600 and N.lib.tsg_gen_file_nonascii(seed, f)]
+    nonascii = [f for f in range(n_gen) if sizes[f] >= 600 and N.lib.tsg_gen_file_nonascii(seed, f)]
     extra_na = [f for f in nonascii if f not in set(fold_files) and sizes[f] <= (8 << 20)]
     na_pick = (fold_files + [int(x) for x in rng.permutation(extra_na)])[:nonascii_files]
-    big = np.nonzero((sizes >= (4 << 20)) & (sizes <= (16 << 20)))[0]
+    big = np.nonzero((sizes[:n_gen] >= (4 << 20)) & (sizes[:n_gen] <= (16 << 20)))[0]
     big_pick = [int(x) for x in rng.permutation(big)[:big_files]]
     cand = np.unique(np.concatenate([real["file"][: n_sample // 2].astype(np.int64),
-                                     rng.integers(0, c["n_files"], n_sample // 2)]))
+                                     rng.integers(0, n_gen, n_sample // 2)]))
     cand = sorted(set(int(f) for f in cand if sizes[f] <= (4 << 20)) | set(na_pick) | set(big_pick))
     by_file = {}
     for L in locs:
@@ -423,14 +496,20 @@ def main():
     c = build_corpus(N, torch, seed, args.gb, args.density, local_rank)
     torch.cuda.synchronize()
     cfg = None
+    stress_unique = []
     if args.config == 4:
         import tempfile
 
         from tests import stress_rules
 
+        srules = stress_rules.make_rules(20261019, args.stress_rules)
         cfg_path = os.path.join(tempfile.mkdtemp(), "trivy-secret.yaml")
-        stress_rules.write_config(cfg_path, stress_rules.make_rules(20261019, args.stress_rules))
+        stress_rules.write_config(cfg_path, srules)
         cfg = S.parse_config(cfg_path)
+        # custom-rule instances, a minified multi-MiB line and
+        # binary-ish files, appended to the HBM corpus as ~10 % of its bytes
+        stress_unique, stress_all = stress_material(stress_rules, srules, seed, int(c["total"] * 0.1))
+        c = append_files(torch, c, stress_all, local_rank)
     sc = S.new_scanner(cfg, device=local_rank)
     eng = S.get_engine(local_rank)
     rs = sc._rs.handle
@@ -594,6 +673,8 @@ def main():
             parity = parity_checks(N, S, c, locs, sc.rules, seed, args.density,
                                    n_sample=300 if args.config == 2 else 24, oracle_cfg=cfg_path if cfg else None,
                                    res=last if args.config in (0, 2, 4) else None)
+            if args.config == 4:
+                parity.update(stress_checks(N, last, sc.rules, c, stress_unique, cfg_path))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.config in (0, 2):
         cores = args.cpu_cores or min(16, len(os.sched_getaffinity(0)))
