@@ -2478,18 +2478,28 @@ struct FindParams {
   uint64_t data_end;  // bytes of the batch buffer (reads stay below it)
   const uint64_t* off;
   const uint32_t* nl_blocks;
+  const uint32_t* nl_pre;  // exclusive prefix of nl_blocks (n_nlb entries): newlines before each 4 KiB block
+  uint64_t n_nlb;
   const RuleDev* rules;
   DevLoc* locs;        // sorted by (file, start); lines rewritten by k_censor
   uint64_t n_locs;
   uint64_t* iv;        // merged censor intervals, 2 u64 per slot, at the group's slots
   uint2* grp;          // per location: (first slot of its file group, intervals in it)
   FindRec* rec;
-  CodeRec* code;       // kCodeLines per location
-  uint64_t* code_src;  // their file-relative source starts (k_find_copy may run twice: kept apart from off)
-  uint64_t* len;       // per location: arena bytes
-  uint64_t* arena_off; // exclusive prefix of len
+  CodeRec* code;       // kCodeLines per location (slot = location * kCodeLines + k)
+  uint64_t* line_key;  // per code slot: file << 32 | line start (~0: unused slot); sorted in place with slot ids
+  uint32_t* line_slot;
+  uint32_t* line_head; // per sorted slot: 1 at the first slot of each distinct line, then its inclusive prefix
+  uint32_t* line_uid;  // per code slot: index of its distinct line
+  // segments of the string arena: [0, n_locs) the Match windows, then one per
+  // distinct Code line (a line shared by several findings is stored once)
+  uint32_t* seg_file;
+  uint2* seg_grp;
+  uint64_t* seg_src;
+  uint64_t* seg_len;   // then, after the exclusive scan, seg_off
+  uint64_t* seg_off;
+  uint64_t n_seg_cap;  // n_locs + kCodeLines * n_locs
   uint8_t* arena;
-  uint64_t arena_cap;
   uint64_t* sort_key;
   uint32_t* sort_idx;
   uint32_t rank_bits;  // bits of RuleDev::id_rank: sort key = file << rank_bits | rank
@@ -2576,15 +2586,21 @@ __device__ inline uint32_t nl_mask16(uint4 v) {
   return m;
 }
 
-// First raw '\n' in [A, E) (absolute), or E: one 1 KiB chunk per wave step,
-// 4 KiB blocks without a newline skipped.  Wave-uniform arguments.
-__device__ uint64_t wave_nl_fwd(const FindParams& F, uint64_t A, uint64_t E, uint32_t lane) {
+// Block holding newline number k (0-based, whole batch): the largest b with
+// nl_pre[b] <= k (binary search over the prefix; wave-uniform).
+__device__ inline uint64_t nl_block_of(const FindParams& F, uint64_t k) {
+  uint64_t lo = 0, hi = F.n_nlb;  // nl_pre[lo] <= k < nl_pre[hi] (hi may be past the end)
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (F.nl_pre[mid] <= k) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// First raw '\n' in [A, B) within one 4 KiB block, or B: 1 KiB per wave step.
+__device__ uint64_t wave_nl_fwd_blk(const FindParams& F, uint64_t A, uint64_t E, uint32_t lane) {
   while (A < E) {
-    const uint64_t blk = A / kNlBlock;
-    if (F.nl_blocks[blk] == 0) {
-      A = (blk + 1) * kNlBlock;
-      continue;
-    }
     const uint64_t base = A & ~(uint64_t)15;
     const uint64_t p = base + 16ull * lane;
     uint32_t m = p < E ? nl_mask16(ld16_guard(F.data, p, F.data_end)) : 0u;
@@ -2601,15 +2617,9 @@ __device__ uint64_t wave_nl_fwd(const FindParams& F, uint64_t A, uint64_t E, uin
   return E;
 }
 
-// Last raw '\n' in [S, B) (absolute), or -1.
-__device__ int64_t wave_nl_bwd(const FindParams& F, uint64_t S, uint64_t B, uint32_t lane) {
+// Last raw '\n' in [S, B), or -1: 1 KiB per wave step, backwards.
+__device__ int64_t wave_nl_bwd_blk(const FindParams& F, uint64_t S, uint64_t B, uint32_t lane) {
   while (B > S) {
-    const uint64_t blk = (B - 1) / kNlBlock;
-    if (F.nl_blocks[blk] == 0) {
-      const uint64_t b0 = blk * kNlBlock;
-      B = b0 > S ? b0 : S;
-      continue;
-    }
     const uint64_t top = ((B - 1) & ~(uint64_t)15) + 16;  // chunk [top - 1024, top)
     const int64_t base = (int64_t)top - 1024;
     const int64_t p = base + 16ll * lane;
@@ -2628,6 +2638,39 @@ __device__ int64_t wave_nl_bwd(const FindParams& F, uint64_t S, uint64_t B, uint
     B = base > (int64_t)S ? (uint64_t)base : S;
   }
   return -1;
+}
+
+// First raw '\n' in [A, E) (absolute), or E: the rest of A's 4 KiB block,
+// then the block of the next newline by its number (O(log n) however long
+// the line: minified files hold multi-MiB lines).
+__device__ uint64_t wave_nl_fwd(const FindParams& F, uint64_t A, uint64_t E, uint32_t lane) {
+  if (A >= E) return E;
+  const uint64_t blk = A / kNlBlock;
+  const uint64_t bend = (blk + 1) * kNlBlock;
+  if (F.nl_blocks[blk]) {
+    const uint64_t i = wave_nl_fwd_blk(F, A, bend < E ? bend : E, lane);
+    if (i < (bend < E ? bend : E)) return i;
+  }
+  if (bend >= E || blk + 1 >= F.n_nlb) return E;
+  const uint64_t b = nl_block_of(F, F.nl_pre[blk + 1]);  // block of the next newline after blk
+  if (b * kNlBlock >= E || b >= F.n_nlb - 1 || F.nl_pre[b + 1] == F.nl_pre[b]) return E;
+  return wave_nl_fwd_blk(F, b * kNlBlock, (b + 1) * kNlBlock < E ? (b + 1) * kNlBlock : E, lane);
+}
+
+// Last raw '\n' in [S, B) (absolute), or -1 (same two steps backwards).
+__device__ int64_t wave_nl_bwd(const FindParams& F, uint64_t S, uint64_t B, uint32_t lane) {
+  if (B <= S) return -1;
+  const uint64_t blk = (B - 1) / kNlBlock;
+  const uint64_t b0 = blk * kNlBlock;
+  if (F.nl_blocks[blk]) {
+    const int64_t i = wave_nl_bwd_blk(F, b0 > S ? b0 : S, B, lane);
+    if (i >= 0) return i;
+  }
+  if (b0 <= S || F.nl_pre[blk] == 0) return -1;
+  const uint64_t b = nl_block_of(F, F.nl_pre[blk] - 1);  // block of the last newline before blk
+  const uint64_t e = (b + 1) * kNlBlock;
+  if (e <= S) return -1;
+  return wave_nl_bwd_blk(F, b * kNlBlock > S ? b * kNlBlock : S, e, lane);
 }
 
 // Censored-buffer line breaks of file [fs, fs + n) with intervals (g0, m):
@@ -2669,7 +2712,6 @@ __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
   r.start = L.start;
   r.end = L.end;
   r.loc = (uint32_t)w;
-  uint64_t total = 0;
   const uint64_t fs = F.off[L.file];
   const uint64_t n = F.off[L.file + 1] - 1 - fs;
   if (!L.flags && L.start <= L.end && L.end <= n) {
@@ -2683,7 +2725,6 @@ __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
     }
     r.m_src = ls;
     r.m_len = (uint32_t)(le - ls);
-    total = le - ls;
     // code lines (scanner.go:505-534), 0-based numbers [sl - 2, el + 2)
     const uint32_t sl = L.start_line - 1, el = L.end_line - 1;
     const uint32_t cs = sl >= 2 ? sl - 2 : 0, ce = el + 2;
@@ -2696,14 +2737,13 @@ __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
       const bool cause = ln >= sl && ln <= el;
       if (lane == 0) {
         CodeRec c{};
-        F.code_src[w * kCodeLines + k] = p;
         c.len = (uint32_t)(q - p);
         const uint32_t flags = (cause ? 1u : 0u) | (cause && !found_first ? 2u : 0u) | (cause && ln == el ? 4u : 0u);
         c.number_flags = (ln + 1) | (flags << 29);
         F.code[w * kCodeLines + k] = c;
+        F.line_key[w * kCodeLines + k] = ((uint64_t)L.file << 32) | p;  // (files < 4 GiB)
       }
       found_first = found_first || cause;
-      total += q - p;
       p = q + 1;
     }
     r.n_lines = k;
@@ -2711,63 +2751,100 @@ __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
   }
   if (lane == 0) {
     F.rec[w] = r;
-    F.len[w] = total;
+    for (uint32_t k = r.n_lines; k < kCodeLines; ++k) F.line_key[w * kCodeLines + k] = ~0ull;
+    for (uint32_t k = 0; k < kCodeLines; ++k) F.line_slot[w * kCodeLines + k] = (uint32_t)(w * kCodeLines + k);
+    F.seg_file[w] = r.file;
+    F.seg_grp[w] = F.grp[w];
+    F.seg_src[w] = r.m_src;
+    F.seg_len[w] = r.m_len;
   }
 }
 
-// One wave per location: copy the spans into the arena ('*' over censored bytes).
-__device__ inline void wave_copy_censored(const FindParams& F, uint64_t fs, uint32_t g0, uint32_t m, uint64_t src,
-                                          uint64_t len, uint64_t dst, uint32_t lane) {
-  if (dst + len > F.arena_cap) return;  // the host re-runs with a larger arena
-  uint32_t lo = 0, hi = m;  // first interval ending after src (intervals are disjoint and sorted)
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (F.iv[2 * (g0 + mid) + 1] <= src) lo = mid + 1;
-    else hi = mid;
+// Distinct Code lines: the code slots sorted by (file, line start); the first
+// slot of each run is a head (line_head), its inclusive prefix numbers them.
+__global__ void k_line_heads(const uint64_t* keys, uint64_t n, uint32_t* head) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) head[i] = keys[i] != ~0ull && (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+}
+
+__global__ void k_line_map(FindParams F, const uint64_t* keys, const uint32_t* slots, const uint32_t* scan,
+                           const uint32_t* head, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || keys[i] == ~0ull) return;
+  const uint32_t slot = slots[i], uid = scan[i] - 1;
+  F.line_uid[slot] = uid;
+  if (head[i]) {
+    const uint64_t sg = F.n_locs + uid;
+    F.seg_file[sg] = (uint32_t)(keys[i] >> 32);
+    F.seg_src[sg] = keys[i] & 0xFFFFFFFFull;
+    F.seg_len[sg] = F.code[slot].len;
+    F.seg_grp[sg] = F.grp[slot / kCodeLines];
   }
-  uint32_t j = lo;
-  for (uint64_t o = 0; o < len; o += 64) {
-    const uint64_t x = src + o + lane;  // this lane's byte
-    while (j < m && F.iv[2 * (g0 + j) + 1] <= src + o) ++j;  // wave-uniform advance to the chunk
-    if (o + lane < len) {
-      bool cens = false;
-      for (uint32_t t = j; t < m && F.iv[2 * (g0 + t)] <= x; ++t)
-        if (x < F.iv[2 * (g0 + t) + 1]) {
-          cens = true;
-          break;
+}
+
+__global__ void k_seg_total(FindParams F) {
+  if (threadIdx.x == 0 && blockIdx.x == 0)
+    F.ctrl->find_bytes = F.seg_off[F.n_seg_cap - 1] + F.seg_len[F.n_seg_cap - 1];
+}
+
+// The string arena, 16 bytes per lane over all segments (a multi-MiB line is
+// spread over the whole grid): the segment by binary search over seg_off,
+// source bytes from the batch, bytes inside the file's censor intervals as '*'.
+__global__ __launch_bounds__(256) void k_arena_fill(FindParams F) {
+  const uint64_t total = F.ctrl->find_bytes;
+  for (uint64_t a = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; a < total;
+       a += (uint64_t)gridDim.x * blockDim.x * 16) {
+    uint64_t lo = 0, hi = F.n_seg_cap;  // last segment with seg_off <= a
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (F.seg_off[mid] <= a) lo = mid;
+      else hi = mid;
+    }
+    uint64_t k = lo;
+    uint32_t w[4] = {0, 0, 0, 0};
+    uint64_t kk = ~0ull, fbase = 0;
+    uint32_t g0 = 0, gm = 0, t = 0;  // the segment's file intervals, t = first one ending after x
+    for (uint32_t j = 0; j < 16 && a + j < total; ++j) {
+      while (a + j >= F.seg_off[k] + F.seg_len[k]) ++k;  // (never past the last non-empty segment)
+      const uint64_t x = F.seg_src[k] + (a + j - F.seg_off[k]);  // file-relative
+      if (k != kk) {  // a new segment: its intervals and the first one ending after x (binary search)
+        kk = k;
+        fbase = F.off[F.seg_file[k]];
+        g0 = F.seg_grp[k].x;
+        gm = F.seg_grp[k].y;
+        uint32_t l2 = 0, h2 = gm;
+        while (l2 < h2) {
+          const uint32_t mid = (l2 + h2) >> 1;
+          if (F.iv[2 * (g0 + mid) + 1] <= x) l2 = mid + 1;
+          else h2 = mid;
         }
-      F.arena[dst + o + lane] = cens ? (uint8_t)'*' : F.data[fs + x];
+        t = l2;
+      }
+      while (t < gm && F.iv[2 * (g0 + t) + 1] <= x) ++t;
+      const bool cens = t < gm && F.iv[2 * (g0 + t)] <= x;
+      const uint32_t byte = cens ? (uint32_t)'*' : F.data[fbase + x];
+      w[j >> 2] |= byte << (8 * (j & 3));
+    }
+    if (a + 16 <= total) {
+      *(uint4*)(F.arena + a) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+      for (uint32_t j = 0; a + j < total; ++j) F.arena[a + j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
     }
   }
 }
 
-__global__ __launch_bounds__(256) void k_find_copy(FindParams F) {
-  const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t lane = threadIdx.x & 63;
+// Arena offsets into the records, and the (file, RuleID rank) sort keys.
+__global__ void k_find_finalize(FindParams F) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= F.n_locs) return;
-  FindRec r = F.rec[w];
-  const uint64_t fs = F.off[r.file];
-  const uint2 g = F.grp[w];
-  uint64_t dst = F.arena_off[w];
-  r.m_off = dst;
-  wave_copy_censored(F, fs, g.x, g.y, r.m_src, r.m_len, dst, lane);
-  dst += r.m_len;
-  for (uint32_t k = 0; k < r.n_lines; ++k) {
-    const CodeRec c = F.code[w * kCodeLines + k];
-    wave_copy_censored(F, fs, g.x, g.y, F.code_src[w * kCodeLines + k], c.len, dst, lane);
-    if (lane == 0) F.code[w * kCodeLines + k].off = dst;
-    dst += c.len;
-  }
-  if (lane == 0) {
-    F.rec[w].m_off = r.m_off;
-    // final order: (file, RuleID rank) -- ties (file, RuleID) keep (file, start)
-    // order here and are ordered by Match on the host
-    const uint32_t rank = F.rules[r.rule].id_rank;
-    F.rec[w].rank = rank;
-    F.sort_key[w] = ((uint64_t)r.file << F.rank_bits) | rank;
-    F.sort_idx[w] = (uint32_t)w;
-    if (w + 1 == F.n_locs) F.ctrl->find_bytes = dst;
-  }
+  FindRec& r = F.rec[w];
+  r.m_off = F.seg_off[w];
+  for (uint32_t k = 0; k < r.n_lines; ++k)
+    F.code[w * kCodeLines + k].off = F.seg_off[F.n_locs + F.line_uid[w * kCodeLines + k]];
+  const uint32_t rank = F.rules[r.rule].id_rank;
+  r.rank = rank;
+  F.sort_key[w] = ((uint64_t)r.file << F.rank_bits) | rank;
+  F.sort_idx[w] = (uint32_t)w;
 }
 
 __global__ void k_find_gather(const FindRec* in, const uint32_t* idx, uint64_t n, FindRec* out) {
@@ -3013,12 +3090,13 @@ struct tsg_engine {
   double stage_ms[2] = {0, 0};  // last stage_host_batch: pack (+ overlapped H2D), H2D tail (host clock)
   std::vector<double> gate_tm;          // timings of the last tsg_gate_device call
   // device findings (build_findings_dev)
-  DBuf<uint64_t> f_iv, f_len, f_off, f_csrc;
+  DBuf<uint64_t> f_iv, f_lkey, f_lkey2, f_ssrc, f_slen, f_soff;
+  DBuf<uint32_t> f_lslot, f_lslot2, f_lhead, f_lscan, f_luid, f_sfile;
+  DBuf<uint2> f_sgrp;
   DBuf<uint2> f_grp;
   DBuf<FindRec> f_rec, f_rec2;
   DBuf<CodeRec> f_code;
   DBuf<uint8_t> f_arena;
-  uint64_t f_arena_need = 0;  // arena size learnt from an overflowing call
   std::shared_ptr<PinnedPool> pinned = std::make_shared<PinnedPool>();
 };
 
@@ -3747,20 +3825,31 @@ int launch_fold_windows(tsg_engine* e, const ScanParams& P, bool with_hits) {
 int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_off, uint64_t nbytes, uint64_t n_files,
                        uint64_t n_locs, tsg_result* res) {
   hipStream_t s = e->stream;
+  const uint64_t n_slots = (uint64_t)kCodeLines * n_locs, n_seg = n_locs + n_slots;
   HIP_TRY(e->f_iv.ensure(2 * n_locs));
   HIP_TRY(e->f_grp.ensure(n_locs));
   HIP_TRY(e->f_rec.ensure(n_locs));
   HIP_TRY(e->f_rec2.ensure(n_locs));
-  HIP_TRY(e->f_code.ensure(kCodeLines * n_locs));
-  HIP_TRY(e->f_csrc.ensure(kCodeLines * n_locs));
-  HIP_TRY(e->f_len.ensure(n_locs));
-  HIP_TRY(e->f_off.ensure(n_locs));
-  HIP_TRY(e->f_arena.ensure(std::max<uint64_t>(1 << 20, e->f_arena_need)));
+  HIP_TRY(e->f_code.ensure(n_slots));
+  HIP_TRY(e->f_lkey.ensure(n_slots));
+  HIP_TRY(e->f_lkey2.ensure(n_slots));
+  HIP_TRY(e->f_lslot.ensure(n_slots));
+  HIP_TRY(e->f_lslot2.ensure(n_slots));
+  HIP_TRY(e->f_lhead.ensure(n_slots));
+  HIP_TRY(e->f_lscan.ensure(n_slots));
+  HIP_TRY(e->f_luid.ensure(n_slots));
+  HIP_TRY(e->f_sfile.ensure(n_seg));
+  HIP_TRY(e->f_sgrp.ensure(n_seg));
+  HIP_TRY(e->f_ssrc.ensure(n_seg));
+  HIP_TRY(e->f_slen.ensure(n_seg));
+  HIP_TRY(e->f_soff.ensure(n_seg));
   FindParams F{};
   F.data = d_data;
   F.data_end = nbytes;
   F.off = d_off;
   F.nl_blocks = e->nl_blocks.p;
+  F.nl_pre = e->nl_pre.p;
+  F.n_nlb = nbytes / kNlBlock + 2;
   F.rules = e->img.view.rules;
   F.locs = e->locs2.p;
   F.n_locs = n_locs;
@@ -3768,9 +3857,16 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   F.grp = e->f_grp.p;
   F.rec = e->f_rec.p;
   F.code = e->f_code.p;
-  F.code_src = e->f_csrc.p;
-  F.len = e->f_len.p;
-  F.arena_off = e->f_off.p;
+  F.line_key = e->f_lkey.p;
+  F.line_slot = e->f_lslot.p;
+  F.line_head = e->f_lhead.p;
+  F.line_uid = e->f_luid.p;
+  F.seg_file = e->f_sfile.p;
+  F.seg_grp = e->f_sgrp.p;
+  F.seg_src = e->f_ssrc.p;
+  F.seg_len = e->f_slen.p;
+  F.seg_off = e->f_soff.p;
+  F.n_seg_cap = n_seg;
   F.sort_key = e->keys.p;
   F.sort_idx = e->vals.p;
   F.ctrl = e->ctrl.p;
@@ -3779,39 +3875,51 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   int key_bits = (int)F.rank_bits + 1;
   while (key_bits < 64 && (1ull << (key_bits - F.rank_bits)) <= n_files) ++key_bits;
   const uint32_t lane_blocks = (uint32_t)((n_locs + 255) / 256), wave_blocks = (uint32_t)((n_locs * 64 + 255) / 256);
+  const uint32_t slot_blocks = (uint32_t)((n_slots + 255) / 256);
+  HIP_TRY(hipMemsetAsync(e->f_slen.p, 0, n_seg * 8, s));  // unused line segments stay empty
   hipLaunchKernelGGL(k_censor, dim3(lane_blocks), dim3(256), 0, s, F);
   hipLaunchKernelGGL(k_find_spans, dim3(wave_blocks), dim3(256), 0, s, F);
   HIP_TRY(hipGetLastError());
+  // distinct Code lines: sort the slots by (file, line start), number the runs
   size_t tmp = 0;
-  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->f_len.p, e->f_off.p, (int)n_locs, s));
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p, e->f_lslot2.p,
+                                             (int)n_slots, 0, 64, s));
   HIP_TRY(e->cub_tmp.ensure(tmp + 1));
-  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(e->cub_tmp.p, tmp, e->f_len.p, e->f_off.p, (int)n_locs, s));
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p,
+                                             e->f_lslot2.p, (int)n_slots, 0, 64, s));
+  hipLaunchKernelGGL(k_line_heads, dim3(slot_blocks), dim3(256), 0, s, e->f_lkey2.p, n_slots, e->f_lhead.p);
+  tmp = 0;
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, e->f_lhead.p, e->f_lscan.p, (int)n_slots, s));
+  HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(e->cub_tmp.p, tmp, e->f_lhead.p, e->f_lscan.p, (int)n_slots, s));
+  hipLaunchKernelGGL(k_line_map, dim3(slot_blocks), dim3(256), 0, s, F, e->f_lkey2.p, e->f_lslot2.p, e->f_lscan.p,
+                     e->f_lhead.p, n_slots);
+  // arena offsets of the segments (Match windows, then distinct lines)
+  tmp = 0;
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->f_slen.p, e->f_soff.p, (int)n_seg, s));
+  HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(e->cub_tmp.p, tmp, e->f_slen.p, e->f_soff.p, (int)n_seg, s));
+  hipLaunchKernelGGL(k_seg_total, dim3(1), dim3(64), 0, s, F);
+  hipLaunchKernelGGL(k_find_finalize, dim3(lane_blocks), dim3(256), 0, s, F);
+  HIP_TRY(hipGetLastError());
+  size_t tmp2 = 0;
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
+                                             (int)n_locs, 0, key_bits, s));
+  HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
+                                             (int)n_locs, 0, key_bits, s));
+  hipLaunchKernelGGL(k_find_gather, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->vals2.p, n_locs, e->f_rec2.p);
+  HIP_TRY(hipGetLastError());
   Ctrl c;
-  for (int attempt = 0;; ++attempt) {
-    F.arena = e->f_arena.p;
-    F.arena_cap = e->f_arena.n;
-    hipLaunchKernelGGL(k_find_copy, dim3(wave_blocks), dim3(256), 0, s, F);
-    HIP_TRY(hipGetLastError());
-    size_t tmp2 = 0;
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
-                                               (int)n_locs, 0, key_bits, s));
-    HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
-                                               (int)n_locs, 0, key_bits, s));
-    hipLaunchKernelGGL(k_find_gather, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->vals2.p, n_locs,
-                       e->f_rec2.p);
-    HIP_TRY(hipGetLastError());
-    if (int rc = read_ctrl(e, &c)) return rc;
-    if (c.find_bytes <= e->f_arena.n) break;
-    if (attempt == 1) {
-      set_last_error("internal: findings arena still overflowed after regrowing it");
-      return TSG_ERR_INTERNAL;
-    }
-    e->f_arena_need = c.find_bytes + (c.find_bytes >> 3);
-    HIP_TRY(e->f_arena.ensure(e->f_arena_need));
-  }
+  if (int rc = read_ctrl(e, &c)) return rc;  // the arena size
+  HIP_TRY(e->f_arena.ensure(c.find_bytes + 16));
+  F.arena = e->f_arena.p;
+  if (c.find_bytes)
+    hipLaunchKernelGGL(k_arena_fill, dim3((uint32_t)std::min<uint64_t>((c.find_bytes / 16 + 255) / 256 + 1, 8192)),
+                       dim3(256), 0, s, F);
+  HIP_TRY(hipGetLastError());
   auto& R = res->impl;
-  const size_t rec_bytes = n_locs * sizeof(FindRec), code_bytes = (size_t)kCodeLines * n_locs * sizeof(CodeRec);
+  const size_t rec_bytes = n_locs * sizeof(FindRec), code_bytes = n_slots * sizeof(CodeRec);
   R.arena = pinned_get(e->pinned, rec_bytes + code_bytes + c.find_bytes + 1);
   if (!R.arena) {
     set_last_error("hipHostMalloc failed for the findings arena");
@@ -3819,7 +3927,7 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   }
   uint8_t* base = (uint8_t*)R.arena->p;
   R.frec = {(FindRec*)base, n_locs};
-  R.code = {(CodeRec*)(base + rec_bytes), (size_t)kCodeLines * n_locs};
+  R.code = {(CodeRec*)(base + rec_bytes), n_slots};
   R.strs = (const char*)(base + rec_bytes + code_bytes);
   HIP_TRY(hipMemcpyAsync(R.frec.p, e->f_rec2.p, rec_bytes, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(R.code.p, e->f_code.p, code_bytes, hipMemcpyDeviceToHost, s));
@@ -4417,7 +4525,9 @@ void tsg_engine_free(tsg_engine* e) {
   if (e->h_stage) (void)hipHostFree(e->h_stage);
   e->gate_out.release(); e->gate_rules.release(); e->bin8.release(); e->strip_out.release();
   e->strip_off.release(); e->blk_kept.release(); e->blk_base.release(); e->chunk_pos.release(); e->n_drop.release();
-  e->f_iv.release(); e->f_len.release(); e->f_off.release(); e->f_csrc.release(); e->f_grp.release();
+  e->f_iv.release(); e->f_lkey.release(); e->f_lkey2.release(); e->f_ssrc.release(); e->f_slen.release();
+  e->f_soff.release(); e->f_lslot.release(); e->f_lslot2.release(); e->f_lhead.release(); e->f_lscan.release();
+  e->f_luid.release(); e->f_sfile.release(); e->f_sgrp.release(); e->f_grp.release();
   e->f_rec.release(); e->f_rec2.release(); e->f_code.release(); e->f_arena.release();
   if (e->events)
     for (auto& ev : e->ev) (void)hipEventDestroy(ev);
