@@ -2190,7 +2190,12 @@ __global__ __launch_bounds__(256) void k_warm(WarmRanges R, uint32_t* sink) {
 // reference, which would otherwise put the DFA path's IvIter (read on every
 // start) in scratch memory -- 35 K lanes of scratch thrash L2 and made each
 // dependent DFA step an HBM round trip (k_verify 1.96 ms at 50 GB).
-constexpr uint32_t kVerifyBlock = 64;  // one wave per block: jobs spread over every CU (UTCL1 reach per CU)
+// Block shapes: 64 lanes (one wave) spreads a short job list over every CU
+// (UTCL1 reach per CU); a long list (findings-heavy corpora: millions of
+// jobs) takes 256-lane blocks -- four waves share one staged DFA, so the
+// 64 KiB of LDS per block no longer caps a CU at two resident waves.
+constexpr uint32_t kVerifyBlock = 64;
+constexpr uint32_t kVerifyBlockWide = 256;
 
 // regexp.go allMatches over the whole file (rules without an anchor)
 __device__ __noinline__ void verify_full_job(const VerifyParams& V, uint32_t rule, uint32_t fi, const uint8_t* text,
@@ -2302,7 +2307,8 @@ __device__ __noinline__ void verify_vm_job(const VerifyParams& V, uint32_t rule,
 // lanes touch evict the table's translations from the small per-CU TLB).
 constexpr uint32_t kVerifyDfaLds = 64 * 1024;
 
-__global__ __launch_bounds__(kVerifyBlock) void k_verify(VerifyParams V) {
+template <uint32_t kBlock>
+__global__ __launch_bounds__(kBlock) void k_verify(VerifyParams V) {
   __shared__ __align__(16) uint16_t dfa_lds[kVerifyDfaLds / 2];
   __shared__ __align__(16) uint8_t cls_lds[128];
   const uint32_t nthreads = gridDim.x * blockDim.x;
@@ -4230,8 +4236,14 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
       hipLaunchKernelGGL(k_warm, dim3(8 * kWarmParts), dim3(256), 0, s, W, (uint32_t*)e->nsel.p);
       HIP_TRY(hipGetLastError());
     }
-    const uint32_t blocks = (uint32_t)std::min<uint64_t>((n_cands + kVerifyBlock - 1) / kVerifyBlock, e->vm_threads / kVerifyBlock);
-    hipLaunchKernelGGL(k_verify, dim3(std::max(1u, blocks)), dim3(kVerifyBlock), 0, s, V);
+    if (n_cands > (uint64_t)e->num_cus * kVerifyBlockWide * 4) {
+      const uint32_t blocks = (uint32_t)std::min<uint64_t>((n_cands + kVerifyBlockWide - 1) / kVerifyBlockWide,
+                                                           e->vm_threads / kVerifyBlockWide);  // (VM scratch per lane)
+      hipLaunchKernelGGL(k_verify<kVerifyBlockWide>, dim3(std::max(1u, blocks)), dim3(kVerifyBlockWide), 0, s, V);
+    } else {
+      const uint32_t blocks = (uint32_t)std::min<uint64_t>((n_cands + kVerifyBlock - 1) / kVerifyBlock, e->vm_threads / kVerifyBlock);
+      hipLaunchKernelGGL(k_verify<kVerifyBlock>, dim3(std::max(1u, blocks)), dim3(kVerifyBlock), 0, s, V);
+    }
     // capture stages over the device-side lists (one wave per CU with 140 KiB
     // of arenas, then kBigCapLanes lanes per CU with 36 KiB each)
     hipLaunchKernelGGL((k_captures<kVerifyThreads, kBsWords, false>), dim3(e->num_cus), dim3(kVerifyThreads), 0, s, V);
