@@ -1773,8 +1773,11 @@ struct IvIter {
       const uint32_t h = (uint32_t)((keys[ci++] & kPosMask) - fstart);
       if (h < a) continue;
       const uint32_t lo = (b == gre::kInf || h < b) ? 0u : h - b;
+      // window start: the alpha run before h, never walked below lo = h - b
+      // (a run reaching the previous hit joins that hit's window).  Walking to
+      // the previous hit when it lies below lo re-read whole minified lines.
       uint32_t p;
-      if (have_prev && h_prev <= h) {
+      if (have_prev && h_prev <= h && h_prev >= lo) {
         uint32_t q = h;
         while (q > h_prev && in_alpha(text[q - 1])) --q;
         p = (q == h_prev) ? (p_prev > lo ? p_prev : lo) : q;
@@ -4273,6 +4276,33 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
                 jq, dur(jq) / 1e5, (end(jq) - tmin) / 1e5, rs->rules[hp[2 * jq + 1] >> 32].id.c_str(),
                 (unsigned long long)(hp[2 * jq + 1] & 1), (unsigned long long)((hp[2 * jq + 1] & 0xFFFFFFFFull) >> 1),
                 (unsigned long long)(c1 - c0), tk[0] / 1e5, tk[1] / 1e5, tk[2] / 1e5);
+      }
+      {  // the jobs with the most DFA steps and the most candidates (the work, not the wave's wait)
+        std::vector<uint32_t> by(n_jobs);
+        for (uint32_t q = 0; q < n_jobs; ++q) by[q] = q;
+        auto steps = [&](uint32_t q) { return (hp[2 * q + 1] & 0xFFFFFFFFull) >> 1; };
+        auto cands = [&](uint32_t q) { return (uint64_t)((q + 1 < n_jobs ? hjs[q + 1] : n_cands) - hjs[q]); };
+        std::partial_sort(by.begin(), by.begin() + std::min<uint32_t>(8, n_jobs), by.end(),
+                          [&](uint32_t a, uint32_t b) { return steps(a) > steps(b); });
+        for (uint32_t q = 0; q < std::min<uint32_t>(8, n_jobs); ++q)
+          fprintf(stderr, "[verify] top-steps job %u rule %s file %u steps %llu cands %llu dur %.3f ms\n", by[q],
+                  rs->rules[hp[2 * by[q] + 1] >> 32].id.c_str(), 0u, (unsigned long long)steps(by[q]),
+                  (unsigned long long)cands(by[q]), dur(by[q]) / 1e5);
+        std::partial_sort(by.begin(), by.begin() + std::min<uint32_t>(8, n_jobs), by.end(),
+                          [&](uint32_t a, uint32_t b) { return dur(a) > dur(b); });
+        for (uint32_t q = 0; q < std::min<uint32_t>(8, n_jobs); ++q) {
+          const uint32_t* tk = (const uint32_t*)(hp.data() + 2ull * n_jobs) + 4 * by[q];
+          fprintf(stderr, "[verify] top-dur job %u rule %s steps %llu cands %llu dur %.3f ms dfa %.3f emit %.3f allow %.3f full %llu\n",
+                  by[q], rs->rules[hp[2 * by[q] + 1] >> 32].id.c_str(), (unsigned long long)steps(by[q]),
+                  (unsigned long long)cands(by[q]), dur(by[q]) / 1e5, tk[0] / 1e5, tk[1] / 1e5, tk[2] / 1e5,
+                  (unsigned long long)(hp[2 * by[q] + 1] & 1));
+        }
+        std::partial_sort(by.begin(), by.begin() + std::min<uint32_t>(8, n_jobs), by.end(),
+                          [&](uint32_t a, uint32_t b) { return cands(a) > cands(b); });
+        for (uint32_t q = 0; q < std::min<uint32_t>(8, n_jobs); ++q)
+          fprintf(stderr, "[verify] top-cands job %u rule %s steps %llu cands %llu dur %.3f ms full %llu\n", by[q],
+                  rs->rules[hp[2 * by[q] + 1] >> 32].id.c_str(), (unsigned long long)steps(by[q]),
+                  (unsigned long long)cands(by[q]), dur(by[q]) / 1e5, (unsigned long long)(hp[2 * by[q] + 1] & 1));
       }
       std::map<uint32_t, std::pair<uint64_t, uint64_t>> per_rule;
       for (uint32_t q = 0; q < n_jobs; ++q) {
