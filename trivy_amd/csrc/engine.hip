@@ -4475,6 +4475,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   auto& R = res->impl;
   R.file_flags.assign(e->h_flags, e->h_flags + nf);
   R.locs.clear();
+  R.locs.reserve(hl.size());
   for (auto& L : hl) {
     if (L.flags & 1) {
       set_last_error("secret group did not participate in the match (the Go reference panics here)");
