@@ -56,8 +56,8 @@ def _layer(seed, n):
     return buf.getvalue()
 
 
-def _oracle_layer(data, skip_files=(), skip_dirs=()):
-    oa = o.SecretAnalyzer("")
+def _oracle_layer(data, skip_files=(), skip_dirs=(), config=""):
+    oa = o.SecretAnalyzer(config)
     out = []
 
     def fn(path, size, is_dir, content):
@@ -128,3 +128,29 @@ def test_analyze_layer_finding_order():
     assert [(f.RuleID, f.StartLine) for f in got[0].Findings] == [("github-pat", 2), ("github-pat", 4)]
     want, _, _ = _oracle_layer(data)
     assert _plain(got) == _oracle_plain(want)
+
+
+def test_analyze_layer_custom_rules_vs_oracle(tmp_path):
+    """configs[3]'s workload names builtin + custom trivy-secret.yaml rules: a
+    layer of stress-rule files (custom-rule instances, a minified line,
+    binary-ish files) analysed with a 60-rule custom config, against the
+    oracle's walk + Analyze with the same config."""
+    from . import stress_rules
+
+    rules = stress_rules.make_rules(777, 60)
+    cfg = str(tmp_path / "trivy-secret.yaml")
+    stress_rules.write_config(cfg, rules)
+    files = stress_rules.make_corpus(778, rules, 120, long_line_bytes=40_000)
+    buf = io.BytesIO()
+    with tarfile.open(fileobj=buf, mode="w", format=tarfile.PAX_FORMAT) as tf:
+        for p, d in files:
+            ti = tarfile.TarInfo("app/" + p)
+            ti.size = len(d)
+            tf.addfile(ti, io.BytesIO(d))
+    data = buf.getvalue()
+    a = SecretAnalyzer()
+    a.init(cfg)
+    got, _, _ = W.analyze_layer(a, data)
+    want, _, _ = _oracle_layer(data, config=cfg)
+    assert _plain(got) == _oracle_plain(want)
+    assert sum(f.RuleID.startswith("stress-") for s in got for f in s.Findings) > 50

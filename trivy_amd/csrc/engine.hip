@@ -1963,9 +1963,8 @@ __device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, uint
 // Returns false when the match does not fit the arena (`words` LDS words; the
 // caller then defers it to a larger arena, or runs the Pike capture VM) —
 // never a different answer.
-constexpr uint32_t kVerifyThreads = 64;
 constexpr uint32_t kBsWords = 560;        // k_verify: LDS words per lane (140 KiB per block)
-constexpr uint32_t kBigCapLanes = 4;      // k_captures_big: lanes per block
+constexpr uint32_t kCapActive = 8;        // k_captures: searching lanes per 64-lane block (8 blocks per CU)
 constexpr uint32_t kBigBsWords = 9216;    // and their arenas (36 KiB: P x W <= 294 K (pc, pos) bits)
 
 __device__ bool bitstate_captures(const gre::ProgView& p, const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me,
@@ -2140,11 +2139,16 @@ __device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, ui
 
 // Capture stages: a fixed grid walks the list the previous stage filled,
 // its length read on the device (no host round trip between the stages).
-template <uint32_t kLanes, uint32_t kWords, bool kLast>
+// Only kActive lanes of each 64-lane block search (each with its own arena):
+// the backtracker's control flow differs per job, so jobs sharing a wave run
+// one after another; few active lanes per wave and many waves per CU keep
+// each wave to about one job and let the CU overlap their load latencies.
+template <uint32_t kLanes, uint32_t kActive, uint32_t kWords, bool kLast>
 __global__ __launch_bounds__(kLanes) void k_captures(VerifyParams V) {
-  __shared__ uint32_t bs_lds[kLanes * kWords];
+  __shared__ uint32_t bs_lds[kActive * kWords];
+  if (threadIdx.x >= kActive) return;
   uint32_t* bs_area = bs_lds + threadIdx.x * kWords;
-  const uint32_t nthreads = gridDim.x * blockDim.x;
+  const uint32_t nthreads = gridDim.x * kActive;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   gre::VmScratch sc = make_scratch(V.scratch + (uint64_t)t * V.scratch_stride, V.rs);
   const uint4* list = kLast ? V.caps_big : V.caps;
@@ -4247,10 +4251,13 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
       const uint32_t blocks = (uint32_t)std::min<uint64_t>((n_cands + kVerifyBlock - 1) / kVerifyBlock, e->vm_threads / kVerifyBlock);
       hipLaunchKernelGGL(k_verify<kVerifyBlock>, dim3(std::max(1u, blocks)), dim3(kVerifyBlock), 0, s, V);
     }
-    // capture stages over the device-side lists (one wave per CU with 140 KiB
-    // of arenas, then kBigCapLanes lanes per CU with 36 KiB each)
-    hipLaunchKernelGGL((k_captures<kVerifyThreads, kBsWords, false>), dim3(e->num_cus), dim3(kVerifyThreads), 0, s, V);
-    hipLaunchKernelGGL((k_captures<kBigCapLanes, kBigBsWords, true>), dim3(e->num_cus), dim3(kBigCapLanes), 0, s, V);
+    // capture stages over the device-side lists: 8 searching lanes per wave with
+    // 560-word arenas, then one lane per wave with 36 KiB for what does not fit
+
+
+    // (grids keep every lane's VM scratch slot below vm_threads: 512 / 256 per CU)
+    hipLaunchKernelGGL((k_captures<64, kCapActive, kBsWords, false>), dim3(e->num_cus * 8), dim3(64), 0, s, V);
+    hipLaunchKernelGGL((k_captures<64, 1, kBigBsWords, true>), dim3(e->num_cus * 4), dim3(64), 0, s, V);
     HIP_TRY(hipGetLastError());
     if (prof) {  // the jobs that end last (their waves set k_verify's length), per-rule totals
       std::vector<uint64_t> hp(4ull * n_jobs);
