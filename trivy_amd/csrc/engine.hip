@@ -4253,8 +4253,6 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     }
     // capture stages over the device-side lists: 8 searching lanes per wave with
     // 560-word arenas, then one lane per wave with 36 KiB for what does not fit
-
-
     // (grids keep every lane's VM scratch slot below vm_threads: 512 / 256 per CU)
     hipLaunchKernelGGL((k_captures<64, kCapActive, kBsWords, false>), dim3(e->num_cus * 8), dim3(64), 0, s, V);
     hipLaunchKernelGGL((k_captures<64, 1, kBigBsWords, true>), dim3(e->num_cus * 4), dim3(64), 0, s, V);
