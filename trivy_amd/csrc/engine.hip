@@ -2519,48 +2519,101 @@ struct FindParams {
   Ctrl* ctrl;
 };
 
-// One lane per location; the head of each file group does the group.
-__global__ __launch_bounds__(256) void k_censor(FindParams F) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= F.n_locs || (i > 0 && F.locs[i - 1].file == F.locs[i].file)) return;
-  const uint32_t file = F.locs[i].file;
-  uint64_t j = i;
-  while (j < F.n_locs && F.locs[j].file == file) ++j;
-  // merged intervals [a, b) with the raw newline prefix counts P(a), P(b)
-  uint32_t m = 0;
-  uint64_t a = 0, b = 0;
-  uint32_t pa = 0, pb = 0;
-  for (uint64_t k = i; k < j; ++k) {
-    const DevLoc L = F.locs[k];
-    if (L.flags) continue;
-    if (m && L.start <= b) {
-      if (L.end > b) {
-        b = L.end;
-        pb = L.end_line;
-      }
-      F.iv[2 * (i + m - 1) + 1] = b;
-      F.sort_idx[i + m - 1] = pb;  // (scratch: P(b) of the interval)
-    } else {
-      a = L.start, b = L.end, pa = L.start_line, pb = L.end_line;
-      F.iv[2 * (i + m)] = a;
-      F.iv[2 * (i + m) + 1] = b;
-      F.sort_key[i + m] = pa;      // (scratch: P(a))
-      F.sort_idx[i + m] = pb;
-      ++m;
-    }
+// Wave-wide scans (inclusive) over the 64 lanes.
+__device__ inline uint64_t wave_incl_max64(uint64_t v, uint32_t lane) {
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t o = __shfl_up(v, d);
+    if (lane >= d) v = v > o ? v : o;
   }
-  uint32_t q = 0, before = 0;  // newlines censored in intervals wholly before the current location
-  for (uint64_t k = i; k < j; ++k) {
-    F.grp[k] = make_uint2((uint32_t)i, m);
+  return v;
+}
+__device__ inline uint32_t wave_incl_sum32(uint32_t v, uint32_t lane) {
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(v, d);
+    if (lane >= d) v += o;
+  }
+  return v;
+}
+
+// One wave per file group (the wave of the group's first location; the rest
+// exit), 64 locations per step with carries: (1) merged censor intervals --
+// a location opens one when it starts past the running maximum end, the
+// interval's end is that running maximum (packed end << 32 | P(end), so the
+// raw newline count travels with it); (2) the exclusive prefix of censored
+// newlines per interval, P(b) - P(a); (3) each location's censored line:
+// P(a) of its interval minus the newlines censored before it, + 1 (every
+// location of one interval shares it; EndLine == StartLine).  Scratch:
+// sort_key / sort_idx hold P(a) / P(b) per interval slot, line_uid the
+// location's interval, line_head the prefix (all reused later).
+__global__ __launch_bounds__(256) void k_censor(FindParams F) {
+  const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  if (i >= F.n_locs || (i > 0 && F.locs[i - 1].file == F.locs[i].file)) return;  // wave-uniform
+  const uint32_t file = F.locs[i].file;
+  uint64_t j = i + 1;  // group end: wave-wide probe 64 at a time
+  for (;;) {
+    const uint64_t k = j + lane;
+    const bool same = k < F.n_locs && F.locs[k].file == file;
+    const uint64_t m = __ballot(!same);
+    if (m) {
+      j += __builtin_ctzll(m);
+      break;
+    }
+    j += 64;
+  }
+  const uint64_t lanes_lt = (1ull << lane) - 1;
+  uint64_t carry = 0;  // running max (end << 32 | P(end)) over the file's valid locations so far
+  uint32_t m_cnt = 0;  // intervals opened so far
+  bool have = false;
+  for (uint64_t k0 = i; k0 < j; k0 += 64) {
+    const uint64_t k = k0 + lane;
+    DevLoc L{};
+    if (k < j) L = F.locs[k];
+    const bool valid = k < j && !L.flags;
+    const uint64_t packed = valid ? ((L.end << 32) | L.end_line) : 0;
+    uint64_t incl = wave_incl_max64(packed, lane);
+    uint64_t excl = __shfl_up(incl, 1);
+    if (lane == 0) excl = 0;
+    excl = excl > carry ? excl : carry;
+    incl = incl > carry ? incl : carry;
+    const uint64_t vmask = __ballot(valid);
+    const bool before = have || (vmask & lanes_lt) != 0;
+    const bool opens = valid && (!before || L.start > (excl >> 32));
+    const uint64_t omask = __ballot(opens);
+    const uint32_t id = m_cnt + (uint32_t)__popcll(omask & (lanes_lt | (1ull << lane))) - 1;
+    if (valid) {
+      F.line_uid[k] = id;
+      if (opens) {
+        F.iv[2 * (i + id)] = L.start;
+        F.sort_key[i + id] = L.start_line;  // P(a)
+      }
+      // last valid location of its interval in this step: write the interval's end
+      const uint64_t later = vmask & ~(lanes_lt | (1ull << lane));
+      const bool last = !later || ((omask >> __builtin_ctzll(later)) & 1);
+      if (last) {
+        F.iv[2 * (i + id) + 1] = incl >> 32;
+        F.sort_idx[i + id] = (uint32_t)incl;  // P(b)
+      }
+    }
+    carry = __shfl(incl, 63);
+    m_cnt += (uint32_t)__popcll(omask);
+    have = have || vmask != 0;
+  }
+  // exclusive prefix of censored newlines over the intervals
+  uint32_t run = 0;
+  for (uint32_t q0 = 0; q0 < m_cnt; q0 += 64) {
+    const uint32_t q = q0 + lane;
+    const uint32_t d = q < m_cnt ? F.sort_idx[i + q] - (uint32_t)F.sort_key[i + q] : 0u;
+    const uint32_t inc = wave_incl_sum32(d, lane);
+    if (q < m_cnt) F.line_head[i + q] = run + inc - d;
+    run += __shfl(inc, 63);
+  }
+  for (uint64_t k = i + lane; k < j; k += 64) {
+    F.grp[k] = make_uint2((uint32_t)i, m_cnt);
     DevLoc& L = F.locs[k];
     if (L.flags) continue;
-    while (q < m && F.iv[2 * (i + q) + 1] <= L.start) {
-      before += F.sort_idx[i + q] - (uint32_t)F.sort_key[i + q];
-      ++q;
-    }
-    uint32_t hidden = before;
-    if (q < m && F.iv[2 * (i + q)] < L.start) hidden += L.start_line - (uint32_t)F.sort_key[i + q];
-    const uint32_t line = L.start_line - hidden + 1;
+    const uint32_t id = F.line_uid[k];
+    const uint32_t line = (uint32_t)F.sort_key[i + id] - F.line_head[i + id] + 1;
     L.start_line = line;
     L.end_line = line;
   }
@@ -3890,7 +3943,7 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   const uint32_t lane_blocks = (uint32_t)((n_locs + 255) / 256), wave_blocks = (uint32_t)((n_locs * 64 + 255) / 256);
   const uint32_t slot_blocks = (uint32_t)((n_slots + 255) / 256);
   HIP_TRY(hipMemsetAsync(e->f_slen.p, 0, n_seg * 8, s));  // unused line segments stay empty
-  hipLaunchKernelGGL(k_censor, dim3(lane_blocks), dim3(256), 0, s, F);
+  hipLaunchKernelGGL(k_censor, dim3(wave_blocks), dim3(256), 0, s, F);
   hipLaunchKernelGGL(k_find_spans, dim3(wave_blocks), dim3(256), 0, s, F);
   HIP_TRY(hipGetLastError());
   // distinct Code lines: sort the slots by (file, line start), number the runs
