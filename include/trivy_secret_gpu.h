@@ -201,6 +201,38 @@ void tsg_result_free(tsg_result* r);
  * Analyze hands it to Scan; findings are built from it. */
 int tsg_analyze(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, size_t n_files, tsg_result** out);
 
+/* Byte-range split of ONE large file across GPUs (the reference
+ * scans a file of any size whole, scanner.go:371-452, and the walker spools
+ * tar entries >= 100 MiB to disk and still scans them, walker/cached_file.go:36-52).
+ * Every rank runs the scan pass over its byte range [own_lo, own_hi) and
+ * exports that range's scan state (keyword bits, the anchor hits whose
+ * literal starts inside it, per-4 KiB newline counts); the file's owner
+ * merges the parts and runs candidates / FindAll / exclude / lines / findings
+ * over the whole file, so the result equals tsg_scan_device on the whole file.
+ *
+ * tsg_part_halo: the view a part must see, *left bytes before own_lo (clipped
+ * at 0) and *right bytes after own_hi (clipped at the file end). */
+int tsg_part_halo(const tsg_ruleset* rs, uint64_t* left, uint64_t* right);
+
+/* d_text = file bytes [text_base, text_base + text_len) in HBM, plus one more
+ * readable byte (any value: only literals starting past own_hi touch it, and
+ * the next part owns those).  text_base and
+ * own_lo are multiples of 4096; own_hi is too unless it is file_len.  *blob
+ * (free with tsg_part_free) is opaque and position-independent: ship it to the
+ * owner with any transport. */
+int tsg_scan_part_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_text, uint64_t text_base,
+                         uint64_t text_len, uint64_t own_lo, uint64_t own_hi, uint64_t file_len,
+                         const char* path, uint8_t** blob, size_t* blob_len);
+void tsg_part_free(uint8_t* blob);
+
+/* The owner: d_file = the whole file in HBM followed by its NUL separator
+ * (d_file[file_len] == 0); the parts must tile [0, file_len) (any order).
+ * The result is a one-file result (file index 0), as tsg_scan_device's.
+ * Files (here and in every entry point) may be up to 1 TiB. */
+int tsg_scan_merge_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_file, uint64_t file_len,
+                          const char* path, const uint8_t* const* blobs, const size_t* blob_lens, size_t n_parts,
+                          tsg_result** out);
+
 /* Prefilter-only pass (BASELINE config 2): per-file rule gate bitmasks
  * (rule i passes iff bit i set), exactly MatchKeywords (scanner.go:169-181). */
 int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,

@@ -112,22 +112,27 @@ def test_random_patterns_as_custom_rules_on_gpu():
     from .test_gpu_parity import _canon, _oracle_plain, _plain
 
     # rules that cannot match empty text and do not fire on every other byte
-    cases = [c for c in _cases(777, 400)
+    # (the first 250 seeded cases: case 354 sends the oracle's backtracker
+    # exponential).  Each rule is path-scoped to its own file (Rule.Path,
+    # scanner.go:165-167), so the oracle runs each pattern only on the texts
+    # it was generated with; the GPU evaluates the path gates itself.
+    cases = [c for c in _cases(777, 250)
              if not c[1].match_string(b"") and all(len(c[1].find_all_index(t)) <= 12 for t in c[2])][:120]
-    rules = [S.Rule(id=f"fz-{i:03d}", category="Fuzz", title="fuzz", severity="HIGH", regex=pat,
+    path = [f"src/f{i:04d}.txt" for i in range(len(cases))]
+    scope = [r"^src/f%04d\.txt$" % i for i in range(len(cases))]
+    rules = [S.Rule(id=f"fz-{i:03d}", category="Fuzz", title="fuzz", severity="HIGH", regex=pat, path=scope[i],
                     keywords=[] if i % 3 else [next((c for c in pat if c.isalpha()), "a")])
              for i, (pat, _, _) in enumerate(cases)]
     cfg = S.Config(enable_builtin_rule_ids=["__none__"], custom_rules=rules)
     sc = S.new_scanner(cfg, device=0)
     oracle = o.Scanner(None)
     oracle.rules = [o.Rule(id=r.id, category=r.category, title=r.title, severity=r.severity,
-                           regex=o.GoRegexp(r.regex), keywords=r.keywords) for r in rules]
-    files = [(f"src/f{i:04d}.txt", b"\n".join(t for _, _, ts in cases[i % len(cases):i % len(cases) + 3] for t in ts))
-             for i in range(200)]
+                           regex=o.GoRegexp(r.regex), keywords=r.keywords, path=o.GoRegexp(r.path)) for r in rules]
+    files = [(path[i], b"\n".join(cases[i][2])) for i in range(len(cases))]
     got = sc.scan_batch([S.ScanArgs(p, d) for p, d in files])
     n = 0
     for (p, d), g in zip(files, got):
         want = _oracle_plain(oracle.scan(p, d))
         n += len(want["Findings"])
         assert _canon(_plain(g)) == _canon(want), p
-    assert n > 200
+    assert n > 100

@@ -123,6 +123,16 @@ _SIGS = {
     "tsg_scan_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                        ctypes.POINTER(ctypes.c_void_p)]),
+    "tsg_part_halo": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "tsg_scan_part_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                            ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                            ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p),
+                                            ctypes.POINTER(ctypes.c_size_t)]),
+    "tsg_part_free": (None, [ctypes.c_void_p]),
+    "tsg_scan_merge_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                             ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p),
+                                             ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t,
+                                             ctypes.POINTER(ctypes.c_void_p)]),
     "tsg_result_loc_count": (ctypes.c_size_t, [ctypes.c_void_p]),
     "tsg_result_locs": (ctypes.POINTER(LocC), [ctypes.c_void_p]),
     "tsg_result_file_count": (ctypes.c_size_t, [ctypes.c_void_p]),

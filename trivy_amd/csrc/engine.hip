@@ -62,6 +62,11 @@ constexpr uint32_t kFileSpecial = 2u;
 constexpr uint32_t kFullFlag = 0x80000000u;
 constexpr int kPosBits = 44;
 constexpr uint64_t kPosMask = (1ull << kPosBits) - 1;
+// (file, file-relative position) sort keys: files below 1 TiB, batches below 2^24 files
+constexpr int kKeyPosBits = 40;
+constexpr uint64_t kKeyPosMask = (1ull << kKeyPosBits) - 1;
+constexpr uint64_t kMaxFileBytes = 1ull << kKeyPosBits;
+constexpr uint64_t kMaxBatchFiles = 1ull << (64 - kKeyPosBits);
 
 // k_scan geometry: 256 threads = 4 waves; each lane owns a 128-byte chunk,
 // stored in LDS as a 144-byte row (16-byte halo of the previous chunk first).
@@ -1170,7 +1175,11 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
               const uint64_t key = ((uint64_t)fi << 32) | pd.kw;  // per-lane dedupe of repeated keywords
               if (last_kw != key) {
                 last_kw = key;
-                atomicOr(&P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)], 1u << (pd.kw & 31));
+                // most outputs repeat a keyword the file already has: an L2 read
+                // instead of a memory-side atomic for those
+                uint32_t* wp = &P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)];
+                const uint32_t bit = 1u << (pd.kw & 31);
+                if (!(__hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(wp, bit);
               }
             }
             if (want_hit) {
@@ -2406,11 +2415,11 @@ __global__ __launch_bounds__(256) void k_exclude(const uint8_t* data, const uint
   }
 }
 
-// (file, start) sort keys of the kept locations (files < 4 GiB: start fits 32 bits)
+// (file, start) sort keys of the kept locations
 __global__ void k_loc_keys(const DevLoc* locs, uint64_t n, uint64_t* keys, uint32_t* idx) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  keys[i] = ((uint64_t)locs[i].file << 32) | (uint32_t)locs[i].start;
+  keys[i] = ((uint64_t)locs[i].file << kKeyPosBits) | locs[i].start;
   idx[i] = (uint32_t)i;
 }
 
@@ -2500,7 +2509,7 @@ struct FindParams {
   uint2* grp;          // per location: (first slot of its file group, intervals in it)
   FindRec* rec;
   CodeRec* code;       // kCodeLines per location (slot = location * kCodeLines + k)
-  uint64_t* line_key;  // per code slot: file << 32 | line start (~0: unused slot); sorted in place with slot ids
+  uint64_t* line_key;  // per code slot: file << kKeyPosBits | line start (~0: unused slot); sorted with slot ids
   uint32_t* line_slot;
   uint32_t* line_head; // per sorted slot: 1 at the first slot of each distinct line, then its inclusive prefix
   uint32_t* line_uid;  // per code slot: index of its distinct line
@@ -2562,7 +2571,9 @@ __global__ __launch_bounds__(256) void k_censor(FindParams F) {
     j += 64;
   }
   const uint64_t lanes_lt = (1ull << lane) - 1;
-  uint64_t carry = 0;  // running max (end << 32 | P(end)) over the file's valid locations so far
+  // running max of end and of P(end) over the file's valid locations so far
+  // (P is monotone in the position, so the two maxima belong together)
+  uint64_t carry = 0, carry_p = 0;
   uint32_t m_cnt = 0;  // intervals opened so far
   bool have = false;
   for (uint64_t k0 = i; k0 < j; k0 += 64) {
@@ -2570,15 +2581,16 @@ __global__ __launch_bounds__(256) void k_censor(FindParams F) {
     DevLoc L{};
     if (k < j) L = F.locs[k];
     const bool valid = k < j && !L.flags;
-    const uint64_t packed = valid ? ((L.end << 32) | L.end_line) : 0;
-    uint64_t incl = wave_incl_max64(packed, lane);
+    uint64_t incl = wave_incl_max64(valid ? L.end : 0, lane);
+    uint64_t incl_p = wave_incl_max64(valid ? (uint64_t)L.end_line : 0, lane);
+    incl_p = incl_p > carry_p ? incl_p : carry_p;
     uint64_t excl = __shfl_up(incl, 1);
     if (lane == 0) excl = 0;
     excl = excl > carry ? excl : carry;
     incl = incl > carry ? incl : carry;
     const uint64_t vmask = __ballot(valid);
     const bool before = have || (vmask & lanes_lt) != 0;
-    const bool opens = valid && (!before || L.start > (excl >> 32));
+    const bool opens = valid && (!before || L.start > excl);
     const uint64_t omask = __ballot(opens);
     const uint32_t id = m_cnt + (uint32_t)__popcll(omask & (lanes_lt | (1ull << lane))) - 1;
     if (valid) {
@@ -2591,11 +2603,12 @@ __global__ __launch_bounds__(256) void k_censor(FindParams F) {
       const uint64_t later = vmask & ~(lanes_lt | (1ull << lane));
       const bool last = !later || ((omask >> __builtin_ctzll(later)) & 1);
       if (last) {
-        F.iv[2 * (i + id) + 1] = incl >> 32;
-        F.sort_idx[i + id] = (uint32_t)incl;  // P(b)
+        F.iv[2 * (i + id) + 1] = incl;
+        F.sort_idx[i + id] = (uint32_t)incl_p;  // P(b)
       }
     }
     carry = __shfl(incl, 63);
+    carry_p = __shfl(incl_p, 63);
     m_cnt += (uint32_t)__popcll(omask);
     have = have || vmask != 0;
   }
@@ -2807,7 +2820,7 @@ __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
         const uint32_t flags = (cause ? 1u : 0u) | (cause && !found_first ? 2u : 0u) | (cause && ln == el ? 4u : 0u);
         c.number_flags = (ln + 1) | (flags << 29);
         F.code[w * kCodeLines + k] = c;
-        F.line_key[w * kCodeLines + k] = ((uint64_t)L.file << 32) | p;  // (files < 4 GiB)
+        F.line_key[w * kCodeLines + k] = ((uint64_t)L.file << kKeyPosBits) | p;
       }
       found_first = found_first || cause;
       p = q + 1;
@@ -2841,8 +2854,8 @@ __global__ void k_line_map(FindParams F, const uint64_t* keys, const uint32_t* s
   F.line_uid[slot] = uid;
   if (head[i]) {
     const uint64_t sg = F.n_locs + uid;
-    F.seg_file[sg] = (uint32_t)(keys[i] >> 32);
-    F.seg_src[sg] = keys[i] & 0xFFFFFFFFull;
+    F.seg_file[sg] = (uint32_t)(keys[i] >> kKeyPosBits);
+    F.seg_src[sg] = keys[i] & kKeyPosMask;
     F.seg_len[sg] = F.code[slot].len;
     F.seg_grp[sg] = F.grp[slot / kCodeLines];
   }
@@ -4025,10 +4038,153 @@ void order_finding_ties(ResultImpl& R) {
   }
 }
 
+// ------------------------------------------------- byte-range split (§8(e)) --
+// One large file scanned by several GPUs: every rank runs the scan pass (the
+// HBM-bound part) over its byte range [own_lo, own_hi) and exports the scan
+// state that range owns; the file's owner imports the union and runs the rest
+// of the pipeline (candidates, FindAll, exclude, lines, findings) over the
+// whole file, so the result is the single-GPU result by construction.  The
+// scan state is position-local: keyword bits (OR), anchor hits owned by their
+// literal start, and per-4 KiB-span newline counts and >= 0x80 flags.
+constexpr uint64_t kPartMagic = 0x3174726170677374ull;  // "tsgpart1"
+struct PartHeader {
+  uint64_t magic, ruleset_id, file_len, own_lo, own_hi, n_hits;
+  uint32_t kw_words, flags, n_spans, has_span_hi;
+};
+struct SplitIo {
+  int mode = 0;  // 1: export the part [own_lo, own_hi) of a view; 2: merge parts
+  uint64_t text_base = 0, own_lo = 0, own_hi = 0, file_len = 0;
+  std::vector<uint8_t>* blob = nullptr;                        // mode 1 output
+  const std::vector<std::pair<const uint8_t*, size_t>>* parts = nullptr;  // mode 2 input
+};
+
+uint64_t part_right_halo(const tsg_ruleset* rs) {
+  // a literal (with its class extension) starting before own_hi lies wholly
+  // inside the view; k_fold_windows reads a pattern length around a rune
+  size_t m = 0;
+  for (auto& p : rs->patterns) m = std::max(m, p.lower.size() + p.ext_cols.size());
+  return ((m + 64 + kNlBlock - 1) / kNlBlock) * kNlBlock;
+}
+
+int export_part(tsg_engine* e, const tsg_ruleset* rs, const ScanParams& P, uint64_t n_hits, const SplitIo& sp) {
+  hipStream_t s = e->stream;
+  const uint64_t base = sp.text_base;
+  const uint64_t sp0 = (sp.own_lo - base) / kNlBlock, sp1 = (sp.own_hi - base + kNlBlock - 1) / kNlBlock;
+  const uint32_t n_spans = (uint32_t)(sp1 - sp0);
+  const bool has_hi = P.span_hi != nullptr;
+  std::vector<uint64_t> h(n_hits);
+  std::vector<uint32_t> kw(P.rs.kw_words + 1), nl(n_spans + 1);
+  std::vector<uint8_t> hi(n_spans + 1, 0);
+  uint32_t flags = 0;
+  if (n_hits) HIP_TRY(hipMemcpyAsync(h.data(), e->hits.p, n_hits * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(kw.data(), e->file_kw.p, P.rs.kw_words * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&flags, e->file_flags.p, 4, hipMemcpyDeviceToHost, s));
+  if (n_spans) HIP_TRY(hipMemcpyAsync(nl.data(), e->nl_blocks.p + sp0, n_spans * 4, hipMemcpyDeviceToHost, s));
+  if (n_spans && has_hi) HIP_TRY(hipMemcpyAsync(hi.data(), P.span_hi + sp0, n_spans, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  uint64_t kept = 0;
+  for (uint64_t i = 0; i < n_hits; ++i) {
+    const uint64_t start = ((h[i] & ~kFoldHit) >> 16) + base;
+    if (start < sp.own_lo || start >= sp.own_hi) continue;
+    h[kept++] = (start << 16) | (h[i] & (kFoldHit | 0xFFFFull));
+  }
+  PartHeader H{kPartMagic, rs->id, sp.file_len, sp.own_lo, sp.own_hi, kept, P.rs.kw_words, flags, n_spans,
+               has_hi ? 1u : 0u};
+  auto& b = *sp.blob;
+  b.resize(sizeof(H) + kept * 8 + P.rs.kw_words * 4 + n_spans * 4 + n_spans);
+  uint8_t* w = b.data();
+  memcpy(w, &H, sizeof(H));
+  w += sizeof(H);
+  memcpy(w, h.data(), kept * 8);
+  w += kept * 8;
+  memcpy(w, kw.data(), P.rs.kw_words * 4);
+  w += P.rs.kw_words * 4;
+  memcpy(w, nl.data(), n_spans * 4);
+  w += n_spans * 4;
+  memcpy(w, hi.data(), n_spans);
+  return TSG_OK;
+}
+
+// The owner's side: parts must tile [0, file_len) of this ruleset's scans.
+int import_parts(tsg_engine* e, const tsg_ruleset* rs, ScanParams& P, const SplitIo& sp, uint64_t* n_hits_out) {
+  hipStream_t s = e->stream;
+  const auto& parts = *sp.parts;
+  std::vector<const PartHeader*> hs;
+  for (auto& pr : parts) {
+    if (pr.second < sizeof(PartHeader)) {
+      set_last_error("split: a part blob is truncated");
+      return TSG_ERR_INVALID_ARG;
+    }
+    const PartHeader* H = (const PartHeader*)pr.first;
+    const size_t need = sizeof(PartHeader) + H->n_hits * 8 + (size_t)H->kw_words * 4 + (size_t)H->n_spans * 5;
+    if (H->magic != kPartMagic || H->ruleset_id != rs->id || H->kw_words != P.rs.kw_words ||
+        H->file_len != sp.file_len || pr.second != need) {
+      set_last_error("split: a part blob belongs to another file or ruleset, or is corrupt");
+      return TSG_ERR_INVALID_ARG;
+    }
+    hs.push_back(H);
+  }
+  std::vector<size_t> order(hs.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return hs[a]->own_lo < hs[b]->own_lo; });
+  uint64_t at = 0, total = 0;
+  for (size_t i : order) {
+    if (hs[i]->own_lo != at || hs[i]->own_hi <= hs[i]->own_lo) {
+      set_last_error("split: the parts do not tile the file");
+      return TSG_ERR_INVALID_ARG;
+    }
+    at = hs[i]->own_hi;
+    total += hs[i]->n_hits;
+  }
+  if (at != sp.file_len && !(sp.file_len == 0 && hs.empty())) {
+    set_last_error("split: the parts do not tile the file");
+    return TSG_ERR_INVALID_ARG;
+  }
+  const uint64_t n_nlb = P.nbytes / kNlBlock + 2, n_spans = (P.nbytes + kNlBlock - 1) / kNlBlock;
+  std::vector<uint64_t> hits;
+  hits.reserve(total);
+  std::vector<uint32_t> kw(P.rs.kw_words + 1, 0), nl(n_nlb, 0);
+  std::vector<uint8_t> hi(n_spans + 1, 0);
+  uint32_t flags = 0;
+  for (size_t i : order) {
+    const PartHeader* H = hs[i];
+    const uint8_t* r = (const uint8_t*)(H + 1);
+    const uint64_t* hp = (const uint64_t*)r;
+    hits.insert(hits.end(), hp, hp + H->n_hits);
+    r += H->n_hits * 8;
+    const uint32_t* kp = (const uint32_t*)r;
+    for (uint32_t k = 0; k < H->kw_words; ++k) kw[k] |= kp[k];
+    r += (size_t)H->kw_words * 4;
+    const uint64_t s0 = H->own_lo / kNlBlock;
+    memcpy(nl.data() + s0, r, (size_t)H->n_spans * 4);
+    r += (size_t)H->n_spans * 4;
+    memcpy(hi.data() + s0, r, H->n_spans);
+    flags |= H->flags & ~kFileAllowed;  // the owner's path gate decides AllowPath
+  }
+  HIP_TRY(e->hits.ensure(std::max<uint64_t>(total, 1)));
+  if (total) HIP_TRY(hipMemcpyAsync(e->hits.p, hits.data(), total * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(e->file_kw.p, kw.data(), P.rs.kw_words * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(e->nl_blocks.ensure(n_nlb));
+  HIP_TRY(hipMemcpyAsync(e->nl_blocks.p, nl.data(), n_nlb * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(e->span_hi.ensure(n_spans + 1));
+  HIP_TRY(hipMemcpyAsync(e->span_hi.p, hi.data(), n_spans + 1, hipMemcpyHostToDevice, s));
+  P.span_hi = e->span_hi.p;
+  const uint64_t n_regions = P.nbytes / kNlBlock + 1;
+  HIP_TRY(e->region_file.ensure(n_regions + 1));
+  HIP_TRY(hipMemsetAsync(e->region_file.p, 0, (n_regions + 1) * 4, s));  // one file
+  uint32_t f0 = 0;
+  HIP_TRY(hipMemcpyAsync(&f0, e->file_flags.p, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  f0 |= flags;
+  HIP_TRY(hipMemcpy(e->file_flags.p, &f0, 4, hipMemcpyHostToDevice));
+  *n_hits_out = total;
+  return TSG_OK;
+}
+
 // Run the device pipeline on a batch already in HBM.  Fills r->impl.locs and flags.
 int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, const uint64_t* d_off,
                  const uint8_t* d_paths, const uint64_t* d_path_off, size_t n_files, uint64_t nbytes,
-                 tsg_result* res) {
+                 tsg_result* res, const SplitIo* sp = nullptr) {
   const auto wall0 = std::chrono::steady_clock::now();
   e->fast_timed = false;
   int rc = upload_ruleset(e, rs);
@@ -4036,6 +4192,10 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   const DevImage& im = e->img;
   const RuleSetDev& RS = im.view;
   hipStream_t s = e->stream;
+  if (n_files >= kMaxBatchFiles) {
+    set_last_error("a batch holds fewer than 2^24 files (40-bit positions in the sort keys)");
+    return TSG_ERR_UNSUPPORTED;
+  }
   const uint32_t nf = (uint32_t)n_files;
   const uint32_t rule_words = std::max<uint32_t>(1, (RS.n_rules + 31) / 32);
   HIP_TRY(e->ctrl.ensure(1));
@@ -4124,7 +4284,17 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   HIP_TRY(e->nl_blocks.ensure(n_nlb));
   HIP_TRY(e->nl_pre.ensure(n_nlb));
   P.nl_blocks = e->nl_blocks.p;
-  bool scanned = nbytes == 0;
+  const bool merge = sp && sp->mode == 2;
+  bool scanned = nbytes == 0 || merge;
+  if (merge) {  // the scan state comes from the parts (ev[8..9] bracket the import)
+    HIP_TRY(hipEventRecord(e->ev[8], s));
+    uint64_t nh = 0;
+    if ((rc = import_parts(e, rs, P, *sp, &nh))) return rc;
+    P.nl_blocks = e->nl_blocks.p;
+    P.hits = e->hits.p;
+    HIP_TRY(hipMemcpyAsync(&e->ctrl.p->hits, &nh, 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipEventRecord(e->ev[9], s));
+  }
   for (int attempt = 0; attempt < 3 && !scanned; ++attempt) {
     HIP_TRY(hipMemsetAsync(e->nl_blocks.p, 0, n_nlb * 4, s));
     HIP_TRY(hipEventRecord(e->ev[8], s));
@@ -4167,6 +4337,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   const uint64_t scan_overflow = c.ev_overflow;
   const uint64_t n_outputs = c.outputs;
   const uint64_t n_events = scan_overflow + c.events;
+  if (sp && sp->mode == 1) return export_part(e, rs, P, n_hits, *sp);
   // ---- 3. candidates
   uint64_t cand_cap = std::max<uint64_t>(1 << 16, n_hits * 2 + nf / 4);
   ExpandParams E{};
@@ -4662,6 +4833,126 @@ int tsg_scan_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
   }
 }
 
+// One-file batch layout for the split entry points: offsets {0, len + 1} and
+// the path, in the engine's own staging buffers.
+static int stage_one_file(tsg_engine* e, uint64_t len, const char* path) {
+  const uint64_t off[2] = {0, len + 1};
+  const size_t plen = path ? strlen(path) : 0;
+  const uint64_t poff[2] = {0, plen};
+  if (e->off.ensure(2) != hipSuccess || e->paths.ensure(plen + 16) != hipSuccess || e->path_off.ensure(2) != hipSuccess) {
+    set_last_error("hipMalloc failed");
+    return TSG_ERR_DEVICE;
+  }
+  HIP_TRY(hipMemcpy(e->off.p, off, 16, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->path_off.p, poff, 16, hipMemcpyHostToDevice));
+  if (plen) HIP_TRY(hipMemcpy(e->paths.p, path, plen, hipMemcpyHostToDevice));
+  return TSG_OK;
+}
+
+int tsg_part_halo(const tsg_ruleset* rs, uint64_t* left, uint64_t* right) {
+  if (!rs || !left || !right) return TSG_ERR_INVALID_ARG;
+  *left = kNlBlock;
+  *right = part_right_halo(rs);
+  return TSG_OK;
+}
+
+static int scan_part_impl(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_text, uint64_t text_base,
+                          uint64_t text_len, uint64_t own_lo, uint64_t own_hi, uint64_t file_len, const char* path,
+                          uint8_t** blob, size_t* blob_len) {
+  if (!e || !rs || !blob || !blob_len || (text_len && !d_text)) return TSG_ERR_INVALID_ARG;
+  *blob = nullptr;
+  *blob_len = 0;
+  const uint64_t left = kNlBlock, right = part_right_halo(rs);
+  const bool aligned = text_base % kNlBlock == 0 && own_lo % kNlBlock == 0 && (own_hi % kNlBlock == 0 || own_hi == file_len);
+  const bool covers = own_lo < own_hi && own_hi <= file_len && text_base + std::min(own_lo, left) <= own_lo &&
+                      text_base + text_len >= std::min(file_len, own_hi + right) && text_base + text_len <= file_len;
+  if (!aligned || !covers || text_len >= (1ull << 40)) {
+    set_last_error("split: the part's view does not satisfy tsg_part_halo / 4 KiB alignment");
+    return TSG_ERR_INVALID_ARG;
+  }
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->device));
+  int rc = stage_one_file(e, text_len, path);
+  if (rc) return rc;
+  std::vector<uint8_t> out;
+  SplitIo sp;
+  sp.mode = 1;
+  sp.text_base = text_base;
+  sp.own_lo = own_lo;
+  sp.own_hi = own_hi;
+  sp.file_len = file_len;
+  sp.blob = &out;
+  tsg_result tmp;
+  if ((rc = run_pipeline(e, rs, d_text, e->off.p, e->paths.p, e->path_off.p, 1, text_len + 1, &tmp, &sp))) return rc;
+  *blob = (uint8_t*)malloc(out.size());
+  if (!*blob) return TSG_ERR_INTERNAL;
+  memcpy(*blob, out.data(), out.size());
+  *blob_len = out.size();
+  return TSG_OK;
+}
+
+int tsg_scan_part_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_text, uint64_t text_base,
+                         uint64_t text_len, uint64_t own_lo, uint64_t own_hi, uint64_t file_len, const char* path,
+                         uint8_t** blob, size_t* blob_len) {
+  try {
+    return scan_part_impl(e, rs, d_text, text_base, text_len, own_lo, own_hi, file_len, path, blob, blob_len);
+  } catch (const std::exception& ex) {
+    set_last_error(std::string("internal error: ") + ex.what());
+    return TSG_ERR_INTERNAL;
+  }
+}
+
+void tsg_part_free(uint8_t* blob) { free(blob); }
+
+static int scan_merge_impl(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_file, uint64_t file_len,
+                           const char* path, const uint8_t* const* blobs, const size_t* blob_lens, size_t n_parts,
+                           tsg_result** out) {
+  if (!e || !rs || !out || !d_file || (n_parts && (!blobs || !blob_lens))) return TSG_ERR_INVALID_ARG;
+  *out = nullptr;
+  if (file_len >= kMaxFileBytes) {
+    set_last_error("split: the merged file must be below 1 TiB (40-bit file-relative sort keys)");
+    return TSG_ERR_UNSUPPORTED;
+  }
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->device));
+  uint8_t sep = 1;
+  HIP_TRY(hipMemcpy(&sep, d_file + file_len, 1, hipMemcpyDeviceToHost));
+  if (sep != 0) {
+    set_last_error("split: d_file[file_len] must be the NUL separator");
+    return TSG_ERR_INVALID_ARG;
+  }
+  int rc = stage_one_file(e, file_len, path);
+  if (rc) return rc;
+  std::vector<std::pair<const uint8_t*, size_t>> parts;
+  for (size_t i = 0; i < n_parts; ++i) {
+    if (!blobs[i]) return TSG_ERR_INVALID_ARG;
+    parts.push_back({blobs[i], blob_lens[i]});
+  }
+  SplitIo sp;
+  sp.mode = 2;
+  sp.file_len = file_len;
+  sp.parts = &parts;
+  auto* res = new tsg_result();
+  rc = run_pipeline(e, rs, d_file, e->off.p, e->paths.p, e->path_off.p, 1, file_len + 1, res, &sp);
+  if (rc) {
+    delete res;
+    return rc;
+  }
+  *out = res;
+  return TSG_OK;
+}
+
+int tsg_scan_merge_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_file, uint64_t file_len,
+                          const char* path, const uint8_t* const* blobs, const size_t* blob_lens, size_t n_parts,
+                          tsg_result** out) {
+  try {
+    return scan_merge_impl(e, rs, d_file, file_len, path, blobs, blob_lens, n_parts, out);
+  } catch (const std::exception& ex) {
+    set_last_error(std::string("internal error: ") + ex.what());
+    return TSG_ERR_INTERNAL;
+  }
+}
+
 // Host files -> device batch layout (contents each followed by one NUL, then
 // paths) in e->data / e->off / e->paths / e->path_off: packed into the
 // engine's pinned staging buffer by up to 16 threads (the copy, not PCIe,
@@ -4669,8 +4960,8 @@ int tsg_scan_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
 static int stage_host_batch(tsg_engine* e, const tsg_file* files, size_t n_files, uint64_t* nbytes_out) {
   std::vector<uint64_t> off(n_files + 1, 0), poff(n_files + 1, 0);
   for (size_t i = 0; i < n_files; ++i) {
-    if (files[i].len >= (1ull << 32)) {
-      set_last_error("files of 4 GiB or more are outside this engine's coverage");
+    if (files[i].len >= kMaxFileBytes) {
+      set_last_error("files of 1 TiB or more are outside this engine's coverage");
       return TSG_ERR_UNSUPPORTED;
     }
     off[i + 1] = off[i] + files[i].len + 1;

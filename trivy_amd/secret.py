@@ -278,6 +278,62 @@ class Scanner:
             for b in bufs:
                 b.free()
 
+    # ---- byte-range split of one large file (tsg_scan_part_device /
+    # tsg_scan_merge_device); trivy_amd.shard.scan_split drives it across ranks
+    def part_halo(self):
+        """(left, right): the bytes a part's view must hold around its range."""
+        lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+        N.check(N.lib.tsg_part_halo(self._rs.handle, ctypes.byref(lo), ctypes.byref(hi)))
+        return lo.value, hi.value
+
+    def scan_part(self, view, text_base: int, own_lo: int, own_hi: int, file_len: int, file_path: str) -> bytes:
+        """Scan pass over file bytes [own_lo, own_hi): `view` holds file bytes
+        [text_base, text_base + len(view)) covering part_halo() around the
+        range.  Returns the part's scan state (opaque bytes) for the owner."""
+        import numpy as np
+
+        get_engine(self.device)
+        # + one readable byte after the view: a NUL, which only literals starting
+        # past own_hi could touch (the next part owns those)
+        host = np.zeros(len(view) + 1, dtype=np.uint8)
+        host[:len(view)] = np.frombuffer(bytes(view), dtype=np.uint8)
+        buf = N.DeviceBuffer(host)
+        try:
+            blob, n = ctypes.c_void_p(), ctypes.c_size_t()
+            N.check(N.lib.tsg_scan_part_device(get_engine(self.device), self._rs.handle, buf.ptr, text_base, len(view),
+                                               own_lo, own_hi, file_len, file_path.encode("utf-8", "surrogateescape"),
+                                               ctypes.byref(blob), ctypes.byref(n)))
+            try:
+                return ctypes.string_at(blob, n.value)
+            finally:
+                N.lib.tsg_part_free(blob)
+        finally:
+            buf.free()
+
+    def scan_merge(self, args: ScanArgs, parts: Sequence[bytes]) -> Secret:
+        """The owner's side: the whole file in HBM + the parts' scan states ->
+        the same Secret tsg_scan_device gives for the file."""
+        import numpy as np
+
+        get_engine(self.device)
+        host = np.zeros(len(args.content) + 16, dtype=np.uint8)
+        host[:len(args.content)] = np.frombuffer(bytes(args.content), dtype=np.uint8)
+        buf = N.DeviceBuffer(host)
+        keep = [ctypes.create_string_buffer(bytes(p), len(p)) for p in parts]
+        ptrs = (ctypes.c_void_p * max(1, len(parts)))(*[ctypes.cast(k, ctypes.c_void_p) for k in keep])
+        lens = (ctypes.c_size_t * max(1, len(parts)))(*[len(p) for p in parts])
+        try:
+            res = ctypes.c_void_p()
+            N.check(N.lib.tsg_scan_merge_device(get_engine(self.device), self._rs.handle, buf.ptr, len(args.content),
+                                                args.file_path.encode("utf-8", "surrogateescape"), ptrs, lens,
+                                                len(parts), ctypes.byref(res)))
+            try:
+                return self._convert(res, [args])[0]
+            finally:
+                N.lib.tsg_result_free(res)
+        finally:
+            buf.free()
+
     def analyze_batch(self, batch: Sequence[ScanArgs]) -> List[Optional[Secret]]:
         """SecretAnalyzer.Analyze's per-file work on the GPU (tsg_analyze):
         IsBinary gate, '\r' deletion, Scan.  `content` is the raw file; None

@@ -20,6 +20,16 @@ the layer tars, sizes = their byte lengths, scan_fn = a closure over
 
 The merge is the only communication; with world size 1 (or no process group)
 it is a plain call.
+
+One file larger than a rank's share is split by byte range instead
+(`scan_split`): rank r runs the scan pass over
+[cut_r, cut_{r+1}) with the halo `Scanner.part_halo()` asks for
+(tsg_scan_part_device), the per-part scan states (keyword bits, owned anchor
+hits, per-4 KiB newline counts: KiB, not the file) are gathered on the owner,
+which runs the rest of the pipeline over the whole file
+(tsg_scan_merge_device).  The result equals the single-GPU scan of the file by
+construction, whatever straddles a cut: a private key or a JWT across two
+parts is verified by the owner over the whole file.
 """
 from __future__ import annotations
 
@@ -85,3 +95,52 @@ def scan_sharded(scan_fn: Callable[[List[Any]], List[Any]], batch: Sequence[Any]
     if seen != len(batch):
         raise RuntimeError(f"merge saw {seen} results for {len(batch)} files")
     return out
+
+
+SPAN = 4096  # cuts and views fall on the engine's 4 KiB line-count spans
+
+
+def split_ranges(file_len: int, n_parts: int, halo) -> List[tuple]:
+    """Byte ranges of a split file: (own_lo, own_hi, view_lo, view_hi) per
+    part, own ranges tiling [0, file_len) at 4 KiB-aligned cuts (fewer parts
+    when the file is too small for n), views widened by halo = (left, right)."""
+    if n_parts < 1:
+        raise ValueError("n_parts must be >= 1")
+    left, right = halo
+    cuts = sorted({0, file_len} | {(file_len * r // n_parts) // SPAN * SPAN for r in range(1, n_parts)})
+    out = []
+    for lo, hi in zip(cuts, cuts[1:]):
+        if hi <= lo:
+            continue
+        v_lo = max(0, lo - left) // SPAN * SPAN
+        v_hi = min(file_len, hi + right)
+        out.append((lo, hi, v_lo, v_hi))
+    return out
+
+
+def scan_split(scanner, args, group=None, owner: int = 0, n_parts: Optional[int] = None):
+    """Byte-range split of ONE file over the ranks of `group` (every rank
+    calls it with the same args).  Part p is scanned by rank p % world; the
+    parts go to `owner` (gather_object: host bytes), whose engine merges
+    them; every rank returns the file's Secret.  With no process group the
+    parts run one after another on this rank's engine."""
+    dist = _dist()
+    world = dist.get_world_size(group) if dist else 1
+    rank = dist.get_rank(group) if dist else 0
+    data = args.content
+    n = len(data)
+    ranges = split_ranges(n, n_parts or world, scanner.part_halo())
+    mine = []
+    for p, (lo, hi, v_lo, v_hi) in enumerate(ranges):
+        if p % world == rank:
+            mine.append((p, scanner.scan_part(memoryview(data)[v_lo:v_hi], v_lo, lo, hi, n, args.file_path)))
+    if world == 1:
+        parts = [b for _, b in sorted(mine)]
+    else:
+        gathered = [None] * world if rank == owner else None
+        dist.gather_object(mine, gathered, dst=owner, group=group)
+        parts = [b for _, b in sorted(x for g in gathered for x in g)] if rank == owner else None
+    result = [scanner.scan_merge(args, parts) if rank == owner else None]
+    if world > 1:
+        dist.broadcast_object_list(result, src=owner, group=group)
+    return result[0]
