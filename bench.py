@@ -615,10 +615,16 @@ def main():
             N.lib.tsg_result_free(r)
             nk = c["n_kept"][k].value
             assert nk == int(cuts[k + 1] - cuts[k]) and all(c["kept"][k][i] == i for i in range(0, nk, 997))
+    # warm-up steps keep the previous result alive as the timed loop does, so
+    # the engine's pinned pool already holds the two result blocks it cycles
+    prev = None
     for _ in range(args.warmup):
         r = one_step()
-        if r is not None:
-            N.lib.tsg_result_free(r)
+        if prev is not None:
+            N.lib.tsg_result_free(prev)
+        prev = r
+    if prev is not None:
+        N.lib.tsg_result_free(prev)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()

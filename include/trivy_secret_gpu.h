@@ -228,7 +228,8 @@ void tsg_part_free(uint8_t* blob);
 /* The owner: d_file = the whole file in HBM followed by its NUL separator
  * (d_file[file_len] == 0); the parts must tile [0, file_len) (any order).
  * The result is a one-file result (file index 0), as tsg_scan_device's.
- * Files (here and in every entry point) may be up to 1 TiB. */
+ * file_len must be below 2 GiB, as for every entry point that verifies (the
+ * match search runs on 31-bit file positions): TSG_ERR_UNSUPPORTED otherwise. */
 int tsg_scan_merge_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_file, uint64_t file_len,
                           const char* path, const uint8_t* const* blobs, const size_t* blob_lens, size_t n_parts,
                           tsg_result** out);

@@ -1,12 +1,16 @@
-"""One file of more than 4 GiB (the reference scans any size, scanner.go:371-452;
-the walker spools entries >= 100 MiB and still scans them, cached_file.go:36-52).
+"""The largest file the engine verifies: 2 GiB - 1 bytes (the reference scans
+any size, scanner.go:371-452; the walker spools entries >= 100 MiB and still
+scans them, cached_file.go:36-52).  The match search runs on 32-bit
+file-relative positions with signed capture slots, so a file of 2 GiB or more
+is rejected with TSG_ERR_UNSUPPORTED (never mis-scanned); that is checked too.
 
-The file is N identical filler lines followed by a tail of secrets that starts
-just below byte 2^32, so a private key straddles the 4 GiB offset.  Its
-findings are the oracle's findings for (10 filler lines + the same tail) with
-every line number moved by N - 10: the filler holds no keyword and no match,
-and the two Code lines before the first finding are filler either way.
-Checked through the whole-file device scan and the two-part byte-range split."""
+The file is N identical filler lines, a pad, and a tail of secrets ending at
+byte 2^31 - 1, so every match sits just below 2^31 (no signed-position slip)
+and the last one ends on the last byte.  Its findings are the oracle's findings
+for (10 filler lines + pad + the same tail) with every line number moved by
+N - 10: the filler holds no keyword and no match, and the Code lines before
+the first finding are filler either way.  Checked through the whole-file
+device scan and the two-part byte-range split."""
 import dataclasses
 import json
 
@@ -37,16 +41,17 @@ def _shift(findings, d):
 
 
 @pytest.mark.gpu
-def test_gpu_file_over_4gib_whole_and_split():
+def test_gpu_largest_file_whole_and_split_and_one_more_byte_rejected():
     import trivy_amd.secret as S
     from oracle import secret_oracle as o
     from trivy_amd.shard import scan_split
 
     from .test_gpu_parity import _canon, _plain
-    tail = _tail()
-    n = (2 ** 32 - 200) // len(FILLER)
-    size = n * len(FILLER) + len(tail)
-    assert n * len(FILLER) < 2 ** 32 < n * len(FILLER) + 400
+    size = 2 ** 31 - 1
+    t0 = _tail()
+    n = (size - len(t0) - 1) // len(FILLER)
+    tail = b"x" * (size - n * len(FILLER) - len(t0) - 1) + b"\n" + t0
+    assert n * len(FILLER) + len(tail) == size
     arr = np.empty(size, dtype=np.uint8)
     arr[:n * len(FILLER)].reshape(n, len(FILLER))[:] = np.frombuffer(FILLER, dtype=np.uint8)
     arr[n * len(FILLER):] = np.frombuffer(tail, dtype=np.uint8)
@@ -63,3 +68,10 @@ def test_gpu_file_over_4gib_whole_and_split():
     print("[large] whole-file scan done", flush=True)
     assert _canon(_plain(got)) == want
     assert _canon(_plain(scan_split(sc, args, n_parts=2))) == want
+    # one byte more: rejected, not mis-scanned
+    import trivy_amd._native as N
+    big = S.ScanArgs("big.log", data + b"\n")
+    del data
+    with pytest.raises(N.EngineError) as ei:
+        sc.scan_batch_device([big])
+    assert ei.value.code == N.TSG_ERR_UNSUPPORTED

@@ -67,6 +67,10 @@ constexpr int kKeyPosBits = 40;
 constexpr uint64_t kKeyPosMask = (1ull << kKeyPosBits) - 1;
 constexpr uint64_t kMaxFileBytes = 1ull << kKeyPosBits;
 constexpr uint64_t kMaxBatchFiles = 1ull << (64 - kKeyPosBits);
+// The match search runs on 32-bit file-relative positions (verify DFA, Pike
+// VM) and signed 32-bit capture slots (backtracker): a file longer than this
+// is rejected with TSG_ERR_UNSUPPORTED by every entry point that verifies.
+constexpr uint64_t kMaxVerifyFile = 0x7FFFFFFFull;
 
 // k_scan geometry: 256 threads = 4 waves; each lane owns a 128-byte chunk,
 // stored in LDS as a 144-byte row (16-byte halo of the previous chunk first).
@@ -92,6 +96,7 @@ struct Ctrl {
   unsigned long long find_bytes; // string arena bytes of the findings (k_find_copy)
   unsigned long long n_caps;     // matches whose secret-group spans k_captures resolves
   unsigned long long n_caps_big; // ... and those too long for its arenas (k_captures_big)
+  unsigned long long long_files; // files longer than kMaxVerifyFile (k_region_mark)
 };
 
 struct DevLoc {
@@ -165,9 +170,10 @@ __device__ inline void note_fold(const ScanParams& P, uint64_t pos, uint32_t kin
 // with off[f] <= r * kNlBlock: each file marks the first region boundary at or
 // after its start (atomicMax), an inclusive max-scan fills the rest.
 __global__ __launch_bounds__(256) void k_region_mark(const uint64_t* off, uint32_t n_files, uint64_t n_regions,
-                                                     uint32_t* region_file) {
+                                                     uint32_t* region_file, Ctrl* ctrl) {
   const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= n_files) return;
+  if (off[f + 1] - off[f] - 1 > kMaxVerifyFile) atomicAdd(&ctrl->long_files, 1ull);
   const uint64_t r = (off[f] + kNlBlock - 1) / kNlBlock;
   if (r < n_regions) atomicMax(&region_file[r], (uint32_t)f);
 }
@@ -3722,7 +3728,7 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     HIP_TRY(e->region_tmp.ensure(P.n_regions + 1));
     HIP_TRY(hipMemsetAsync(e->region_tmp.p, 0, (P.n_regions + 1) * 4, s));
     hipLaunchKernelGGL(k_region_mark, dim3((P.n_files + 255) / 256), dim3(256), 0, s, P.off, P.n_files,
-                       P.n_regions, e->region_tmp.p);
+                       P.n_regions, e->region_tmp.p, P.ctrl);
     HIP_TRY(hipGetLastError());
     size_t tmp = 0;
     HIP_TRY(hipcub::DeviceScan::InclusiveScan(nullptr, tmp, e->region_tmp.p, e->region_file.p, hipcub::Max(),
@@ -4338,6 +4344,10 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   const uint64_t n_outputs = c.outputs;
   const uint64_t n_events = scan_overflow + c.events;
   if (sp && sp->mode == 1) return export_part(e, rs, P, n_hits, *sp);
+  if (c.long_files) {
+    set_last_error("a file of 2 GiB or more: the match search runs on 31-bit file positions");
+    return TSG_ERR_UNSUPPORTED;
+  }
   // ---- 3. candidates
   uint64_t cand_cap = std::max<uint64_t>(1 << 16, n_hits * 2 + nf / 4);
   ExpandParams E{};
@@ -4866,7 +4876,7 @@ static int scan_part_impl(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d
   const bool aligned = text_base % kNlBlock == 0 && own_lo % kNlBlock == 0 && (own_hi % kNlBlock == 0 || own_hi == file_len);
   const bool covers = own_lo < own_hi && own_hi <= file_len && text_base + std::min(own_lo, left) <= own_lo &&
                       text_base + text_len >= std::min(file_len, own_hi + right) && text_base + text_len <= file_len;
-  if (!aligned || !covers || text_len >= (1ull << 40)) {
+  if (!aligned || !covers || text_len >= kMaxFileBytes) {
     set_last_error("split: the part's view does not satisfy tsg_part_halo / 4 KiB alignment");
     return TSG_ERR_INVALID_ARG;
   }
@@ -4909,8 +4919,8 @@ static int scan_merge_impl(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* 
                            tsg_result** out) {
   if (!e || !rs || !out || !d_file || (n_parts && (!blobs || !blob_lens))) return TSG_ERR_INVALID_ARG;
   *out = nullptr;
-  if (file_len >= kMaxFileBytes) {
-    set_last_error("split: the merged file must be below 1 TiB (40-bit file-relative sort keys)");
+  if (file_len > kMaxVerifyFile) {
+    set_last_error("split: the merged file must be below 2 GiB (31-bit positions in the match search)");
     return TSG_ERR_UNSUPPORTED;
   }
   std::lock_guard<std::mutex> lk(e->mu);
@@ -4960,8 +4970,8 @@ int tsg_scan_merge_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d
 static int stage_host_batch(tsg_engine* e, const tsg_file* files, size_t n_files, uint64_t* nbytes_out) {
   std::vector<uint64_t> off(n_files + 1, 0), poff(n_files + 1, 0);
   for (size_t i = 0; i < n_files; ++i) {
-    if (files[i].len >= kMaxFileBytes) {
-      set_last_error("files of 1 TiB or more are outside this engine's coverage");
+    if (files[i].len > kMaxVerifyFile) {
+      set_last_error("files of 2 GiB or more are outside this engine's coverage (31-bit match-search positions)");
       return TSG_ERR_UNSUPPORTED;
     }
     off[i + 1] = off[i] + files[i].len + 1;
