@@ -7,7 +7,7 @@
   mixing classes, negation, (?i) fold closure and bracket classes.
 * Compile errors: an unknown name is Go's "invalid character class range"
   (TSG_ERR_REGEX, "regexp compile error" at config decode); a feature outside
-  this engine's coverage (a non-ASCII keyword) is TSG_ERR_UNSUPPORTED (5).
+  this engine's coverage (a keyword with invalid UTF-8) is TSG_ERR_UNSUPPORTED (5).
 * GPU: custom rules with \\p{L} and \\p{Greek} through the C-ABI scan, findings
   compared field by field with the oracle Scanner.
 """
@@ -94,11 +94,11 @@ def test_unknown_class_is_go_compile_error(bad, expr):
         o.GoRegexp(bad)
 
 
-def test_outside_coverage_is_unsupported(tmp_path):
-    cfg = tmp_path / "trivy-secret.yaml"
-    cfg.write_text("rules:\n  - id: nonascii-kw\n    regex: 'clé=\\w+'\n    keywords: ['clé']\n")
+def test_outside_coverage_is_unsupported():
+    # a keyword with invalid UTF-8 (Go would lower it through RuneError)
+    bad = S.Rule(id="bad-kw", category="c", title="t", severity="HIGH", regex="x", keywords=["cl\udce9"])
     with pytest.raises(N.EngineError) as ei:
-        S.new_scanner(S.parse_config(str(cfg)))
+        S.new_scanner(S.Config(custom_rules=[bad]))
     assert ei.value.code == N.TSG_ERR_UNSUPPORTED
 
 

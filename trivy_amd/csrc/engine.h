@@ -220,6 +220,7 @@ struct tsg_ruleset {
   std::vector<int> global_allow_path;   // AllowRules with Path
   std::vector<int> global_exclude;
   std::vector<std::string> keywords;     // unique lowercased keywords
+  std::vector<uint8_t> kw_uni;           // per keyword: 1 = holds a non-ASCII rune (k_uni_keywords, not the automaton)
   std::vector<tsg::PatternHost> patterns;
   tsg::AcHost ac;
   bool any_path_rules = false;  // some rule has Path or per-rule allow paths

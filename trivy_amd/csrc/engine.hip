@@ -38,6 +38,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "gre_lower_table.h"
 #include "pikevm.h"
 
 namespace tsg {
@@ -1245,6 +1246,99 @@ __global__ __launch_bounds__(256) void k_fold_special(ScanParams P, uint64_t n_s
         }
         b2 = b1;
         b1 = c;
+      }
+    }
+  }
+}
+
+// Keywords whose lowercase holds a non-ASCII rune (MatchKeywords over
+// bytes.ToLower(content), scanner.go:169-181): such an occurrence holds a
+// content byte >= 0x80 (ToLower keeps ASCII ASCII; invalid bytes become
+// U+FFFD), so only the spans k_scan_fast / k_scan_big flagged (span_hi), or
+// every span when no flag exists, are searched, from uni_back bytes before
+// the span on.  One wave per span, a 64th of the starts per lane: at each
+// rune start the content is lowered rune by rune (unicode.ToLower,
+// kLowerMap) and compared with the keyword's bytes.
+struct UniKw {
+  const uint8_t* bytes;
+  const uint32_t* meta;  // 3 per keyword: offset, length, keyword id
+  uint32_t n;
+  uint32_t back;
+  const uint32_t* lower;  // {rune, lowercase} pairs, sorted
+  uint32_t n_lower;
+};
+
+__device__ inline uint32_t go_lower_rune(const UniKw& U, uint32_t r) {
+  if (r < 0x80) return (r >= 'A' && r <= 'Z') ? r + 32 : r;
+  uint32_t lo = 0, hi = U.n_lower;
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (U.lower[2 * m] < r) lo = m + 1;
+    else hi = m;
+  }
+  return lo < U.n_lower && U.lower[2 * lo] == r ? U.lower[2 * lo + 1] : r;
+}
+
+__device__ inline uint32_t utf8_encode(uint32_t r, uint8_t* e) {
+  if (r < 0x80) { e[0] = (uint8_t)r; return 1; }
+  if (r < 0x800) { e[0] = (uint8_t)(0xC0 | (r >> 6)); e[1] = (uint8_t)(0x80 | (r & 0x3F)); return 2; }
+  if (r < 0x10000) {
+    e[0] = (uint8_t)(0xE0 | (r >> 12)); e[1] = (uint8_t)(0x80 | ((r >> 6) & 0x3F)); e[2] = (uint8_t)(0x80 | (r & 0x3F));
+    return 3;
+  }
+  e[0] = (uint8_t)(0xF0 | (r >> 18)); e[1] = (uint8_t)(0x80 | ((r >> 12) & 0x3F));
+  e[2] = (uint8_t)(0x80 | ((r >> 6) & 0x3F)); e[3] = (uint8_t)(0x80 | (r & 0x3F));
+  return 4;
+}
+
+__global__ __launch_bounds__(256) void k_uni_keywords(ScanParams P, UniKw U, uint64_t n_spans) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  for (uint64_t g = w0 * 64; g < n_spans; g += nw * 64) {
+    uint64_t m = __ballot(g + lane < n_spans && (!P.span_hi || P.span_hi[g + lane]));
+    while (m) {
+      const uint64_t sp = g + (uint64_t)__ffsll((long long)m) - 1;
+      m &= m - 1;
+      const uint64_t a0 = sp * kNlBlock >= U.back ? sp * kNlBlock - U.back : 0;
+      const uint64_t a1 = (sp + 1) * kNlBlock < P.nbytes ? (sp + 1) * kNlBlock : P.nbytes;
+      const uint64_t per = (a1 - a0 + 63) / 64;
+      const uint64_t qa = a0 + lane * per, qb = qa + per < a1 ? qa + per : a1;
+      for (uint64_t q = qa; q < qb; ++q) {
+        const uint64_t b0 = q >= 3 ? q - 3 : 0;
+        const uint64_t avail = P.nbytes - b0;
+        const uint32_t nb = (uint32_t)(avail < (1u << 30) ? avail : (1u << 30));
+        if (!gre::is_rune_start(P.data + b0, nb, (uint32_t)(q - b0))) continue;
+        for (uint32_t u = 0; u < U.n; ++u) {
+          const uint8_t* kw = U.bytes + U.meta[3 * u];
+          const uint32_t len = U.meta[3 * u + 1];
+          uint64_t j = q;
+          uint32_t k = 0;
+          bool ok = true;
+          while (ok && k < len) {
+            const uint64_t rem = P.nbytes - j;
+            uint32_t w = 0;
+            const int r = gre::decode_rune(P.data + j, (uint32_t)(rem < 4 ? rem : 4), 0, &w);
+            if (r < 0) {
+              ok = false;
+              break;
+            }
+            uint8_t e[4];
+            const uint32_t el = utf8_encode(go_lower_rune(U, (uint32_t)r), e);
+            if (k + el > len) {
+              ok = false;
+              break;
+            }
+            for (uint32_t t = 0; t < el; ++t) ok = ok && e[t] == kw[k + t];
+            k += el;
+            j += w;
+          }
+          if (ok) {
+            const uint32_t fi = file_of_pos(P, q);
+            const uint32_t id = U.meta[3 * u + 2];
+            atomicOr(&P.file_kw[(size_t)fi * P.rs.kw_words + (id >> 5)], 1u << (id & 31));
+          }
+        }
       }
     }
   }
@@ -3105,6 +3199,10 @@ struct DevImage {
   DBuf<uint8_t> pac;  // path literal automaton blob (k_path_gate)
   DBuf<uint16_t> dfa_delta;
   DBuf<uint8_t> dfa_bytes;
+  DBuf<uint8_t> uni_bytes;   // lowercased non-ASCII keywords (k_uni_keywords)
+  DBuf<uint32_t> uni_meta;   // per such keyword: byte offset, byte length, keyword id
+  DBuf<uint32_t> lower_map;  // kLowerMap: {rune, lowercase} pairs
+  uint32_t n_uni = 0, uni_back = 0;
   uint32_t pac_states = 0, pac_classes = 0, pac_bytes = 0;
   uint32_t o_pac_cls = 0, o_pac_out_off = 0, o_pac_out = 0, o_pac_lits = 0, o_pac_req = 0, o_pac_bit = 0;
   uint64_t pac_always = 0;
@@ -3118,6 +3216,7 @@ struct DevImage {
     u32.release(); rule_path.release(); delta.release(); cls.release(); out_off.release();
     out_pat.release(); pats.release(); pat_bytes.release(); pat_rules.release(); fast.release();
     prog_lit_off.release(); prog_lits.release(); follow_delta.release(); follow_cls.release(); pac.release(); dfa_delta.release(); dfa_bytes.release();
+    uni_bytes.release(); uni_meta.release(); lower_map.release();
   }
 };
 
@@ -3693,6 +3792,32 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   v.ac = AcDev{im.delta.p, im.cls.p, im.out_off.p, im.out_pat.p, im.pats.p, im.pat_bytes.p, im.pat_rules.p,
                ac.nstates, ac.nclasses, fast, (uint32_t)ac.fast.size(), ac.fast_out_entry, ac.depth,
                rep_bytes, o_out_off, o_out_pat, o_pats, o_pbytes};
+  // keywords whose lowercase holds a non-ASCII rune (k_uni_keywords)
+  {
+    std::vector<uint8_t> ub;
+    std::vector<uint32_t> um;
+    uint32_t max_len = 0;
+    for (size_t k = 0; k < rs->keywords.size(); ++k) {
+      if (!rs->kw_uni[k]) continue;
+      um.push_back((uint32_t)ub.size());
+      um.push_back((uint32_t)rs->keywords[k].size());
+      um.push_back((uint32_t)k);
+      ub.insert(ub.end(), rs->keywords[k].begin(), rs->keywords[k].end());
+      max_len = std::max<uint32_t>(max_len, (uint32_t)rs->keywords[k].size());
+    }
+    im.n_uni = (uint32_t)(um.size() / 3);
+    // an occurrence in the content is at most 4 bytes per keyword rune (a lone
+    // invalid byte lowers to the 3-byte U+FFFD): <= 4 * its byte length
+    im.uni_back = 4 * max_len;
+    if (im.n_uni) {
+      HIP_TRY(im.uni_bytes.ensure(ub.size() + 1));
+      HIP_TRY(im.uni_meta.ensure(um.size() + 1));
+      HIP_TRY(im.lower_map.ensure(2 * kLowerMapLen + 2));
+      HIP_TRY(hipMemcpy(im.uni_bytes.p, ub.data(), ub.size(), hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(im.uni_meta.p, um.data(), um.size() * 4, hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(im.lower_map.p, kLowerMap, sizeof(kLowerMap), hipMemcpyHostToDevice));
+    }
+  }
   im.rs_id = rs->id;
   // VM scratch
   e->scratch_stride = (scratch_bytes(max_ninst, max_ncap, max_ninst_cap) + 255) & ~255ull;
@@ -3900,6 +4025,17 @@ int launch_fold_windows(tsg_engine* e, const ScanParams& P, bool with_hits) {
   if (!im.n_fold_items) return TSG_OK;
   const FoldItems F{im.u32.p + im.o_fold, im.n_fold_items, with_hits ? 1u : 0u};
   hipLaunchKernelGGL(k_fold_windows, dim3(std::max(1u, e->num_cus) * 2), dim3(256), 0, e->stream, P, F);
+  HIP_TRY(hipGetLastError());
+  return TSG_OK;
+}
+
+// Non-ASCII keyword bits (k_uni_keywords), after the scan flagged its spans.
+int launch_uni_keywords(tsg_engine* e, const ScanParams& P) {
+  const DevImage& im = e->img;
+  if (!im.n_uni || !P.nbytes) return TSG_OK;
+  const UniKw U{im.uni_bytes.p, im.uni_meta.p, im.n_uni, im.uni_back, im.lower_map.p, (uint32_t)kLowerMapLen};
+  const uint64_t n_spans = (P.nbytes + kNlBlock - 1) / kNlBlock;
+  hipLaunchKernelGGL(k_uni_keywords, dim3(std::max(1u, e->num_cus) * 4), dim3(256), 0, e->stream, P, U, n_spans);
   HIP_TRY(hipGetLastError());
   return TSG_OK;
 }
@@ -4152,6 +4288,7 @@ int import_parts(tsg_engine* e, const tsg_ruleset* rs, ScanParams& P, const Spli
   std::vector<uint32_t> kw(P.rs.kw_words + 1, 0), nl(n_nlb, 0);
   std::vector<uint8_t> hi(n_spans + 1, 0);
   uint32_t flags = 0;
+  bool all_hi = true;
   for (size_t i : order) {
     const PartHeader* H = hs[i];
     const uint8_t* r = (const uint8_t*)(H + 1);
@@ -4166,6 +4303,7 @@ int import_parts(tsg_engine* e, const tsg_ruleset* rs, ScanParams& P, const Spli
     r += (size_t)H->n_spans * 4;
     memcpy(hi.data() + s0, r, H->n_spans);
     flags |= H->flags & ~kFileAllowed;  // the owner's path gate decides AllowPath
+    all_hi = all_hi && H->has_span_hi;
   }
   HIP_TRY(e->hits.ensure(std::max<uint64_t>(total, 1)));
   if (total) HIP_TRY(hipMemcpyAsync(e->hits.p, hits.data(), total * 8, hipMemcpyHostToDevice, s));
@@ -4174,10 +4312,12 @@ int import_parts(tsg_engine* e, const tsg_ruleset* rs, ScanParams& P, const Spli
   HIP_TRY(hipMemcpyAsync(e->nl_blocks.p, nl.data(), n_nlb * 4, hipMemcpyHostToDevice, s));
   HIP_TRY(e->span_hi.ensure(n_spans + 1));
   HIP_TRY(hipMemcpyAsync(e->span_hi.p, hi.data(), n_spans + 1, hipMemcpyHostToDevice, s));
-  P.span_hi = e->span_hi.p;
+  P.span_hi = all_hi ? e->span_hi.p : nullptr;  // (no flags: k_uni_keywords searches every span)
   const uint64_t n_regions = P.nbytes / kNlBlock + 1;
   HIP_TRY(e->region_file.ensure(n_regions + 1));
   HIP_TRY(hipMemsetAsync(e->region_file.p, 0, (n_regions + 1) * 4, s));  // one file
+  P.n_regions = n_regions;  // (k_uni_keywords' file lookup reads them through P)
+  P.region_file = e->region_file.p;
   uint32_t f0 = 0;
   HIP_TRY(hipMemcpyAsync(&f0, e->file_flags.p, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
@@ -4336,6 +4476,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     set_last_error("internal: scan buffers still overflowed after regrowing them twice");
     return TSG_ERR_INTERNAL;
   }
+  if ((rc = launch_uni_keywords(e, P))) return rc;
   HIP_TRY(hipEventRecord(e->ev[2], s));
   Ctrl c;
   if ((rc = read_ctrl(e, &c))) return rc;
@@ -5236,6 +5377,7 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
     const bool ev_lost = (rs->ac.fast.size() || P.big.blob) && c.ev_overflow > e->ev_overflow.n;
     if (!ev_lost && c.n_fold <= P.fold_cap) {
       if ((rc = launch_fold_windows(e, P, false))) return rc;
+      if ((rc = launch_uni_keywords(e, P))) return rc;
       scanned = true;
       break;
     }

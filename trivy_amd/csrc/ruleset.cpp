@@ -11,6 +11,7 @@
 #include <mutex>
 
 #include "engine.h"
+#include "gre_lower_table.h"
 #include "pikevm.h"
 
 namespace {
@@ -31,6 +32,41 @@ std::string ascii_lower(const std::string& s) {
   for (auto& c : o)
     if (c >= 'A' && c <= 'Z') c = (char)(c + 32);
   return o;
+}
+
+// strings.ToLower (scanner.go:174-176, keywords): Go's unicode.ToLower per
+// rune (gre_lower_table.h); false for invalid UTF-8 (RuneError substitution
+// in a keyword is outside this engine's coverage).
+bool go_lower_utf8(const std::string& in, std::string* out) {
+  out->clear();
+  const uint8_t* b = (const uint8_t*)in.data();
+  const uint32_t n = (uint32_t)in.size();
+  for (uint32_t i = 0; i < n;) {
+    uint32_t w = 0;
+    int r = gre::decode_rune(b, n, i, &w);
+    if (r == 0xFFFD && !(w == 3 && b[i] == 0xEF && b[i + 1] == 0xBF && b[i + 2] == 0xBD)) return false;
+    uint32_t lr = (uint32_t)r;
+    if (lr < 0x80) {
+      if (lr >= 'A' && lr <= 'Z') lr += 32;
+    } else {
+      int lo = 0, hi = kLowerMapLen;
+      while (lo < hi) {
+        const int m = (lo + hi) / 2;
+        if (kLowerMap[m][0] < lr) lo = m + 1;
+        else hi = m;
+      }
+      if (lo < kLowerMapLen && kLowerMap[lo][0] == lr) lr = kLowerMap[lo][1];
+    }
+    char e[4];
+    int k = 0;
+    if (lr < 0x80) e[k++] = (char)lr;
+    else if (lr < 0x800) { e[k++] = (char)(0xC0 | (lr >> 6)); e[k++] = (char)(0x80 | (lr & 0x3F)); }
+    else if (lr < 0x10000) { e[k++] = (char)(0xE0 | (lr >> 12)); e[k++] = (char)(0x80 | ((lr >> 6) & 0x3F)); e[k++] = (char)(0x80 | (lr & 0x3F)); }
+    else { e[k++] = (char)(0xF0 | (lr >> 18)); e[k++] = (char)(0x80 | ((lr >> 12) & 0x3F)); e[k++] = (char)(0x80 | ((lr >> 6) & 0x3F)); e[k++] = (char)(0x80 | (lr & 0x3F)); }
+    out->append(e, k);
+    i += w;
+  }
+  return true;
 }
 
 bool is_ascii(const std::string& s) {
@@ -400,12 +436,14 @@ int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_r
       if (r.regex < 0) return fail(TSG_ERR_REGEX);
     }
     for (size_t k = 0; k < in.n_keywords; ++k) {
-      std::string kw = in.keywords[k] ? in.keywords[k] : "";
-      if (!is_ascii(kw)) {
-        e = "rule " + r.id + ": non-ASCII keyword is outside this engine's coverage";
+      std::string kw = in.keywords[k] ? in.keywords[k] : "", lw;
+      // a keyword whose lowercase holds a non-ASCII rune is found by
+      // k_uni_keywords around the batch's non-ASCII bytes, not by the automaton
+      if (!go_lower_utf8(kw, &lw) || lw.find('\0') != std::string::npos) {
+        e = "rule " + r.id + ": a keyword with invalid UTF-8 or NUL is outside this engine's coverage";
         return fail(TSG_ERR_UNSUPPORTED);
       }
-      r.keywords.push_back(ascii_lower(kw));
+      r.keywords.push_back(lw);
     }
     if (in.path) {
       r.path = add_regex(rs, in.path, &e);
@@ -482,12 +520,14 @@ int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_r
         int id = (int)rs->keywords.size();
         kwid[kw] = id;
         rs->keywords.push_back(kw);
+        rs->kw_uni.push_back(is_ascii(kw) ? 0 : 1);
       }
     }
     rs->rules.push_back(std::move(r));
   }
   // patterns: keywords, anchor literals, fold-special sequences
   for (size_t k = 0; k < rs->keywords.size(); ++k) {
+    if (rs->kw_uni[k]) continue;
     int p = add_pattern(rs, rs->keywords[k]);
     rs->patterns[p].kw = (int)k;
   }
