@@ -64,6 +64,7 @@ struct RuleDev {
   uint32_t grp_fast;
   int32_t grp_pre, grp_len, grp_suf;
   uint32_t id_rank;  // position of the rule ID in sorted (ID, index) order: findings sort (scanner.go:441-446)
+  uint32_t no_nl;    // no instruction of the program consumes '\n': every match lies inside one line
 };
 
 struct PatDev {

@@ -1815,9 +1815,13 @@ __global__ __launch_bounds__(256) void k_full_jobs(ExpandParams E) {
 // the previous candidate exceeds max_len + (off_max - off_min) and a 4 KiB
 // line is crossed — no match found before the split can reach a start
 // window after it, so the pieces replay Go's sequential FindAll exactly and
-// long files no longer serialise on one lane.
+// long files no longer serialise on one lane.  A rule whose program consumes
+// no '\n' (unbounded ones too: JWTs, `{17,}` tokens) keeps every match inside
+// one line, so a run is also split where a newline lies between the previous
+// hit and the next hit's start window (found within kNlSplitScan bytes).
+constexpr uint32_t kNlSplitScan = 512;
 __global__ void k_mark_jobs(const uint64_t* keys, const uint32_t* vals, uint64_t n, const RuleDev* rules,
-                            uint8_t* flags) {
+                            const uint8_t* data, uint8_t* flags) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint8_t f = 1;
@@ -1830,6 +1834,11 @@ __global__ void k_mark_jobs(const uint64_t* keys, const uint32_t* vals, uint64_t
       if (rd.max_len != gre::kInf && rd.off_max != gre::kInf && (h0 >> 12) != (h1 >> 12)) {
         const uint64_t need = (uint64_t)rd.max_len + (rd.off_max - rd.off_min) + 8;
         f = h1 - h0 > need;
+      }
+      if (!f && rd.no_nl && rd.off_max != gre::kInf && (h0 >> 12) != (h1 >> 12) && h1 > h0 + rd.off_max) {
+        const uint64_t lim = h1 - rd.off_max;  // the next hit's earliest match start
+        const uint64_t end = lim < h0 + kNlSplitScan ? lim : h0 + kNlSplitScan;
+        for (uint64_t q = h0; q < end && !f; ++q) f = data[q] == '\n';
       }
     }
   }
@@ -3446,6 +3455,12 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
       }
       d.use_groups = !r.group_name.empty();
       d.max_len = c.max_len;
+      d.no_nl = 1;
+      for (auto& in : c.prog.inst) {
+        const bool nl = in.op == gre::I_ANY || (in.op == gre::I_RUNE1 && in.arg == '\n') ||
+                        (in.op == gre::I_RUNE && ((c.prog.classes[in.arg].ascii['\n' >> 5] >> ('\n' & 31)) & 1));
+        if (nl) d.no_nl = 0;
+      }
       d.group_off = (uint32_t)group_slots.size();
       if (d.use_groups)
         for (size_t g = 0; g < c.prog.cap_names.size(); ++g)
@@ -4568,7 +4583,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(e->job_start.ensure(n_cands));
     HIP_TRY(e->nsel.ensure(1));
     hipLaunchKernelGGL(k_mark_jobs, dim3((uint32_t)((n_cands + 255) / 256)), dim3(256), 0, s, e->keys2.p,
-                       e->vals2.p, n_cands, RS.rules, e->flags8.p);
+                       e->vals2.p, n_cands, RS.rules, d_data, e->flags8.p);
     hipcub::CountingInputIterator<uint32_t> cnt(0);
     size_t tmp2 = 0;
     HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tmp2, cnt, e->flags8.p, e->job_start.p, e->nsel.p,
