@@ -9,15 +9,20 @@ BUILD    = build
 LIB      = trivy_amd/libtrivy_secret_gpu.so
 
 HOST_SRCS = $(SRC_DIR)/gre.cpp $(SRC_DIR)/ruleset.cpp $(SRC_DIR)/follow.cpp $(SRC_DIR)/dfa.cpp $(SRC_DIR)/layertar.cpp
-HIP_SRCS  = $(SRC_DIR)/engine.hip $(SRC_DIR)/corpus.hip
+HIP_SRCS  = $(SRC_DIR)/engine.hip
 HDRS      = $(wildcard $(SRC_DIR)/*.h) include/trivy_secret_gpu.h
 
 OBJS = $(patsubst $(SRC_DIR)/%.cpp,$(BUILD)/%.o,$(HOST_SRCS)) $(patsubst $(SRC_DIR)/%.hip,$(BUILD)/%.o,$(HIP_SRCS))
 
 # bench-only CPU baseline (bench.py cpu_baseline): not part of the product library
 BENCH_LIB = bench_cpu/libtsg_cpu_scan.so
+# bench / test corpus generator (bench.py, tests): not part of the product library
+GEN_LIB   = bench_gen/libtsg_corpus.so
 
-all: $(LIB) $(BENCH_LIB)
+all: $(LIB) $(BENCH_LIB) $(GEN_LIB)
+
+$(GEN_LIB): bench_gen/corpus.hip bench_gen/tsg_corpus.h include/trivy_secret_gpu.h
+	$(HIPCC) $(HIPFLAGS) -Ibench_gen -shared -o $@ $<
 
 $(BENCH_LIB): bench_cpu/cpu_scan.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $< -lpthread
@@ -53,6 +58,6 @@ $(EXP_LIB): $(EXP_OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(EXP_OBJS) -lamdhip64
 
 clean:
-	rm -rf $(BUILD) build_exp $(LIB) $(BENCH_LIB) $(EXP_LIB)
+	rm -rf $(BUILD) build_exp $(LIB) $(BENCH_LIB) $(GEN_LIB) $(EXP_LIB)
 
 .PHONY: all clean exp

@@ -76,7 +76,7 @@ def build_corpus(N, torch, seed, gb, density, device):
     off[1:] = np.cumsum(sizes + 1).astype(np.uint64)
     total = int(off[-1])
     content = int(sizes.sum())
-    chunk = N.lib.tsg_gen_chunk_bytes()
+    chunk = N.gen.tsg_gen_chunk_bytes()
     nchunks = (sizes + chunk - 1) // chunk
     file_of = np.repeat(np.arange(n_files, dtype=np.uint64), nchunks)
     first = np.repeat(np.cumsum(nchunks) - nchunks, nchunks)
@@ -89,11 +89,11 @@ def build_corpus(N, torch, seed, gb, density, device):
     d_paths = torch.empty(n_files * 31 + 64, dtype=torch.uint8, device=dev)
     d_poff = torch.empty(n_files + 1, dtype=torch.int64, device=dev)
     plant_cap = max(1 << 16, int(total * density * 4) + 1024)
-    rec = N.lib.tsg_gen_plant_record_size()
+    rec = N.gen.tsg_gen_plant_record_size()
     assert rec == PLANT_DTYPE.itemsize
     d_plants = torch.empty(plant_cap * rec, dtype=torch.uint8, device=dev)
     d_np = torch.zeros(1, dtype=torch.int64, device=dev)
-    N.check(N.lib.tsg_gen_corpus_device(
+    N.check(N.gen.tsg_gen_corpus_device(
         ctypes.c_void_p(d_data.data_ptr()), ctypes.c_void_p(d_off.data_ptr()), ctypes.c_void_p(d_chunks.data_ptr()),
         len(chunk_ids), ctypes.c_void_p(d_paths.data_ptr()), ctypes.c_void_p(d_poff.data_ptr()), n_files,
         seed, density, ctypes.c_void_p(d_plants.data_ptr()), plant_cap, ctypes.c_void_p(d_np.data_ptr())))
@@ -248,7 +248,7 @@ def read_result(N, res):
 
 def template_rules(N):
     """Rule ID of each corpus.hip template (one per builtin rule)."""
-    return [N.lib.tsg_gen_template_rule(i).decode() for i in range(N.lib.tsg_gen_template_count())]
+    return [N.gen.tsg_gen_template_rule(i).decode() for i in range(N.gen.tsg_gen_template_count())]
 
 
 def result_findings(N, res, f, rules):
@@ -303,7 +303,7 @@ def parity_checks(N, S, c, locs, rules, seed, density, n_sample=300, oracle_cfg=
     n_gen = c.get("first_stress", c["n_files"])  # generated files (configs[4] appends stress files after them)
     fold = plants[plants["decoy"] == PLANT_FOLD]
     fold_files = [int(f) for f in np.unique(fold["file"]) if sizes[f] <= (8 << 20)]
-    nonascii = [f for f in range(n_gen) if sizes[f] >= 600 and N.lib.tsg_gen_file_nonascii(seed, f)]
+    nonascii = [f for f in range(n_gen) if sizes[f] >= 600 and N.gen.tsg_gen_file_nonascii(seed, f)]
     extra_na = [f for f in nonascii if f not in set(fold_files) and sizes[f] <= (8 << 20)]
     na_pick = (fold_files + [int(x) for x in rng.permutation(extra_na)])[:nonascii_files]
     big = np.nonzero((sizes[:n_gen] >= (4 << 20)) & (sizes[:n_gen] <= (16 << 20)))[0]
@@ -321,7 +321,7 @@ def parity_checks(N, S, c, locs, rules, seed, density, n_sample=300, oracle_cfg=
     for f in cand:
         n = int(sizes[f])
         buf = (ctypes.c_uint8 * max(1, n))()
-        N.check(N.lib.tsg_gen_file(seed, f, n, density, buf))
+        N.check(N.gen.tsg_gen_file(seed, f, n, density, buf))
         data = bytes(buf)[:n]
         path = bytes(c["d_paths"][f * 31:(f + 1) * 31].cpu().numpy()).decode()
         want = oracle.scan(path, data, with_offsets=True)
@@ -367,7 +367,7 @@ def gate_checks(N, c, rules, gates, words, seed, density, n_sample=200):
     for f in cand:
         n = int(c["sizes"][f])
         buf = (ctypes.c_uint8 * max(1, n))()
-        N.check(N.lib.tsg_gen_file(seed, f, n, density, buf))
+        N.check(N.gen.tsg_gen_file(seed, f, n, density, buf))
         data = bytes(buf)[:n]
         low = O.go_bytes_to_lower(data)
         want = [O.Scanner.match_keywords(r, data, low) for r in orules]
@@ -446,8 +446,8 @@ def cpu_baseline(N, c, locs, rs, seconds, threads):
     return dict(value=nbytes / dt / 1e9, unit="GB/s", cores=threads, kind="cpp-restatement",
                 physical_cores=phys,
                 sample=f"{k} files / {nbytes / 1e6:.1f} MB of the same corpus (first files in index order, copied "
-                       f"from HBM), {dt:.1f}s wall on {threads} threads (this box's CPU share"
-                       + (f" of {phys} physical cores" if phys else "") + "); "
+                       f"from HBM), {dt:.1f}s wall on {threads} threads (every CPU in this process's affinity "
+                       "set" + (f"; the host has {phys} physical cores" if phys else "") + "); "
                        "bench_cpu/cpu_scan.cpp: Scanner.Scan restated in C++ on the repo's host Go-regexp VM "
                        "(not Go: no Go toolchain in the image); per-file finding counts equal the GPU's on "
                        f"{agree}/{k} files",
@@ -687,7 +687,8 @@ def main():
                 parity.update(stress_checks(N, last, sc.rules, c, stress_unique, cfg_path))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.config in (0, 2):
-        cores = args.cpu_cores or min(16, len(os.sched_getaffinity(0)))
+        # every CPU this process may run on (N = the cores used, stated)
+        cores = args.cpu_cores or len(os.sched_getaffinity(0))
         cpu = cpu_baseline(N, c, locs, rs, args.cpu_seconds, cores)
     if last is not None and args.config != 3:
         N.lib.tsg_result_free(last)

@@ -20,7 +20,8 @@
 #include <cstdint>
 #include <cstring>
 
-#include "trivy_secret_gpu.h"
+#include "tsg_corpus.h"
+#include "trivy_secret_gpu.h"  // TSG_OK / TSG_ERR_DEVICE
 
 namespace {
 

@@ -215,8 +215,9 @@ int tsg_analyze(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, siz
 int tsg_part_halo(const tsg_ruleset* rs, uint64_t* left, uint64_t* right);
 
 /* d_text = file bytes [text_base, text_base + text_len) in HBM, plus one more
- * readable byte (any value: only literals starting past own_hi touch it, and
- * the next part owns those).  text_base and
+ * readable byte: the file's next byte, or the NUL separator when the view
+ * reaches the file end (checked: TSG_ERR_INVALID_ARG otherwise; only literals
+ * starting past own_hi touch it, and the next part owns those).  text_base and
  * own_lo are multiples of 4096; own_hi is too unless it is file_len.  *blob
  * (free with tsg_part_free) is opaque and position-independent: ship it to the
  * owner with any transport. */
@@ -234,7 +235,7 @@ int tsg_scan_merge_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d
                           const char* path, const uint8_t* const* blobs, const size_t* blob_lens, size_t n_parts,
                           tsg_result** out);
 
-/* Prefilter-only pass (BASELINE config 2): per-file rule gate bitmasks
+/* Prefilter-only pass (BASELINE.json configs[1]): per-file rule gate bitmasks
  * (rule i passes iff bit i set), exactly MatchKeywords (scanner.go:169-181). */
 int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
                     const uint64_t* d_offsets, size_t n_files, uint32_t* h_gates_out,
@@ -294,27 +295,6 @@ int tsg_analyze_layer(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* tar, 
 int tsg_ruleset_allow_path(const tsg_ruleset* rs, const char* path, size_t len, int* allowed);
 /* doublestar.Match (bmatcuk/doublestar v4, walk.go:43): 1/0 in *matched; -1 on a bad pattern. */
 int tsg_glob_match(const char* pattern, const char* path, int* matched);
-
-/* ---- synthetic corpus (bench / test utility, not the scan path) ----------
- * SURVEY.md §8(d) text model with planted builtin-rule secrets.  The device
- * generator and the host twin produce identical bytes for a (seed, file). */
-int tsg_gen_corpus_device(uint8_t* d_data, const uint64_t* d_offsets, const uint64_t* d_chunk_ids,
-                          uint64_t n_chunks, uint8_t* d_paths, uint64_t* d_path_offsets, uint64_t n_files,
-                          uint64_t seed, double density, void* d_plants, uint64_t plant_cap,
-                          unsigned long long* d_nplants);
-int tsg_gen_file(uint64_t seed, uint32_t file, uint64_t len, double density, uint8_t* out);
-/* As tsg_gen_file, plus the file's plant records (tsg_gen_plant_record_size
- * bytes each: file, template, start, end, kind 0 real / 1 one-char-short
- * decoy / 2 EXAMPLE decoy / 3 K-or-ſ-spelled instance) into plants[0..cap). */
-int tsg_gen_file_plants(uint64_t seed, uint32_t file, uint64_t len, double density, uint8_t* out, void* plants,
-                        size_t plant_cap, size_t* n_plants);
-/* 1 if file `file` of corpus `seed` is one of the 0.1 % carrying non-ASCII runes. */
-int tsg_gen_file_nonascii(uint64_t seed, uint32_t file);
-/* The planted-secret templates: one per builtin rule; the rule ID of template i. */
-size_t tsg_gen_template_count(void);
-const char* tsg_gen_template_rule(size_t i);
-size_t tsg_gen_plant_record_size(void);
-uint32_t tsg_gen_chunk_bytes(void);
 
 #ifdef __cplusplus
 }

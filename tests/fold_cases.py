@@ -21,7 +21,7 @@ def build(N, case):
     own line after the first newline at or past fraction x of the file."""
     n = case["size"]
     buf = (ctypes.c_uint8 * n)()
-    N.check(N.lib.tsg_gen_file(case["seed"], case["file"], n, case["density"], buf))
+    N.check(N.gen.tsg_gen_file(case["seed"], case["file"], n, case["density"], buf))
     data = bytes(buf)
     for frac, text in sorted(case["inserts"], key=lambda t: -t[0]):
         p = data.index(b"\n", int(len(data) * frac))

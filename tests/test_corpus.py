@@ -1,4 +1,4 @@
-"""The synthetic corpus generator (trivy_amd/csrc/corpus.hip, host twin) against
+"""The synthetic corpus generator (bench_gen/corpus.hip, host twin) against
 the oracle: every builtin rule has a template, every real plant is found by
 Scanner.Scan at its recorded location, no decoy (one char short, EXAMPLE
 allow-listed) is, and the 0.1 % non-ASCII files carry K/ſ/İ/é runes.  This is
@@ -21,16 +21,16 @@ def _gen(seed, f, n, dens):
     buf = (ctypes.c_uint8 * max(1, n))()
     pl = np.zeros(4096, dtype=PLANT)
     npl = ctypes.c_size_t()
-    N.check(N.lib.tsg_gen_file_plants(seed, f, n, dens, buf, pl.ctypes.data, len(pl), ctypes.byref(npl)))
+    N.check(N.gen.tsg_gen_file_plants(seed, f, n, dens, buf, pl.ctypes.data, len(pl), ctypes.byref(npl)))
     return bytes(buf)[:n], pl[:min(npl.value, len(pl))]
 
 
 def _rules():
-    return [N.lib.tsg_gen_template_rule(i).decode() for i in range(N.lib.tsg_gen_template_count())]
+    return [N.gen.tsg_gen_template_rule(i).decode() for i in range(N.gen.tsg_gen_template_count())]
 
 
 def test_one_template_per_builtin_rule():
-    assert N.lib.tsg_gen_plant_record_size() == PLANT.itemsize
+    assert N.gen.tsg_gen_plant_record_size() == PLANT.itemsize
     assert sorted(_rules()) == sorted(r.id for r in O.Scanner(None).rules)
 
 
@@ -57,7 +57,7 @@ def test_plants_match_oracle():
 
 def test_nonascii_files():
     seed = 20261017
-    files = [f for f in range(20000) if N.lib.tsg_gen_file_nonascii(seed, f)]
+    files = [f for f in range(20000) if N.gen.tsg_gen_file_nonascii(seed, f)]
     assert 5 <= len(files) <= 45  # 0.1 %
     hi = special = 0
     for f in files:

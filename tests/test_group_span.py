@@ -35,7 +35,7 @@ def _gen_files(seed, n_files, size=1 << 16, density=2e-3):
     out = []
     for f in range(n_files):
         buf = ctypes.create_string_buffer(size)
-        N.check(N.lib.tsg_gen_file(seed, f, size, density, buf))
+        N.check(N.gen.tsg_gen_file(seed, f, size, density, buf))
         out.append(buf.raw)
     return out
 

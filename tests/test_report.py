@@ -50,6 +50,24 @@ def test_go_escaping_and_omitempty():
                                                     "FirstCause", "LastCause"]
 
 
+def test_invalid_utf8_renders_as_go_does():
+    """encoding/json (go1.22 encode.go appendString): utf8.DecodeRuneInString
+    returns RuneError of width 1 for every byte that starts no valid sequence,
+    and each such byte is written as the escape text \\ufffd; a valid U+FFFD
+    (EF BF BD) is written raw.  Cases: a truncated 3-byte sequence, a lone
+    continuation byte, an encoded surrogate (ED A0 80: three invalid bytes),
+    an overlong NUL (C0 80), a byte that never starts a rune (FF).  Parity
+    unpinned (no reference fixture holds invalid UTF-8): the expected text is
+    Go's documented escaping rule restated here."""
+    raw = b"a\xe2\x82b \x80 \xed\xa0\x80 \xc0\x80 \xff \xef\xbf\xbd z"
+    s = raw.decode("utf-8", "surrogateescape")
+    f = T.SecretFinding(RuleID="r", Match=s, Code=T.Code(Lines=[T.Line(Number=1, Content=s, Highlighted=s)]))
+    out = R.dumps(R.secret_results([T.Secret(FilePath="p", Findings=[f])]))
+    want = 'a\\ufffd\\ufffdb \\ufffd \\ufffd\\ufffd\\ufffd \\ufffd\\ufffd \\ufffd � z'
+    assert out.count(want) == 3  # Match, Content, Highlighted
+    out.encode("utf-8")  # no lone surrogate left
+
+
 @pytest.mark.gpu
 def test_gpu_findings_render_the_golden_report():
     from trivy_amd.analyzer import SecretAnalyzer

@@ -94,6 +94,31 @@ def test_two_rank_gloo_split_exchange(tmp_path):
         assert json.load(open(f"{out}.{r}")) == {"path": "big.bin", "parts": 5}
 
 
+def _subgroup_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # a subgroup that does not start at global rank 0: owner 1 is group
+        # rank 1 = global rank 2 (collectives address it by its global rank)
+        grp = dist.new_group([1, 2])
+        if rank in (1, 2):
+            data = bytes(random.Random(2).getrandbits(8) for _ in range(200000))
+            res = scan_split(_FakeScanner(), _Args("sub.bin", data), group=grp, owner=1, n_parts=3)
+            with open(f"{out_path}.{rank}", "w") as f:
+                json.dump(res, f)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_split_over_a_subgroup_maps_the_owner_rank(tmp_path):
+    out = str(tmp_path / "sub")
+    mp.start_processes(_subgroup_worker, args=(3, _free_port(), out), nprocs=3, join=True, start_method="spawn")
+    for r in (1, 2):
+        assert json.load(open(f"{out}.{r}")) == {"path": "sub.bin", "parts": 3}
+    assert not os.path.exists(f"{out}.0")
+
+
 def test_world_one_split_runs_parts_in_turn():
     data = bytes(range(256)) * 1000
     assert scan_split(_FakeScanner(), _Args("f", data), n_parts=7) == {"path": "f", "parts": 7}

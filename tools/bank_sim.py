@@ -50,7 +50,7 @@ def corpus(regions, seed):
     while pos < size:
         n = min(1 << 16, size - pos)
         buf = ctypes.create_string_buffer(n)
-        N.check(N.lib.tsg_gen_file(seed, f, n, 1e-6, buf))
+        N.check(N.gen.tsg_gen_file(seed, f, n, 1e-6, buf))
         out[pos: pos + n] = np.frombuffer(buf.raw, dtype=np.uint8)
         pos += n
         f += 1

@@ -67,5 +67,5 @@ if __name__ == "__main__":
         sizes = bench.file_sizes(seed, int(50e9))
         n = int(sizes[f])
         buf = (ctypes.c_uint8 * n)()
-        N.lib.tsg_gen_file(seed, f, n, 1e-6, buf)
+        N.gen.tsg_gen_file(seed, f, n, 1e-6, buf)
         compare("src00/pkg000/file%010d.txt" % f, bytes(buf))

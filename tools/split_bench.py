@@ -36,7 +36,7 @@ def main():
     import trivy_amd.secret as S
     dev = torch.device("cuda", 0)
     size = min(int(a.gb * 1e9), 2 ** 31 - 1)
-    chunk = N.lib.tsg_gen_chunk_bytes()
+    chunk = N.gen.tsg_gen_chunk_bytes()
     nch = (size + chunk - 1) // chunk
     ids = np.arange(nch, dtype=np.uint64)  # file 0, chunk k
     d_data = torch.zeros(size + 4096, dtype=torch.uint8, device=dev)
@@ -45,10 +45,10 @@ def main():
     d_paths = torch.empty(64, dtype=torch.uint8, device=dev)
     d_poff = torch.empty(2, dtype=torch.int64, device=dev)
     cap = max(1 << 16, int(size * 1e-6 * 4) + 1024)
-    rec = N.lib.tsg_gen_plant_record_size()
+    rec = N.gen.tsg_gen_plant_record_size()
     d_pl = torch.empty(cap * rec, dtype=torch.uint8, device=dev)
     d_np = torch.zeros(1, dtype=torch.int64, device=dev)
-    N.check(N.lib.tsg_gen_corpus_device(
+    N.check(N.gen.tsg_gen_corpus_device(
         ctypes.c_void_p(d_data.data_ptr()), ctypes.c_void_p(d_off.data_ptr()), ctypes.c_void_p(d_ids.data_ptr()),
         nch, ctypes.c_void_p(d_paths.data_ptr()), ctypes.c_void_p(d_poff.data_ptr()), 1, 2024, 1e-6,
         ctypes.c_void_p(d_pl.data_ptr()), cap, ctypes.c_void_p(d_np.data_ptr())))

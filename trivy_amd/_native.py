@@ -148,19 +148,6 @@ _SIGS = {
                                                ctypes.POINTER(ctypes.c_size_t)]),
     "tsg_gate_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t]),
-    "tsg_gen_corpus_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
-                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
-                                             ctypes.c_double, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
-    "tsg_gen_file": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double,
-                                    ctypes.c_void_p]),
-    "tsg_gen_file_plants": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double,
-                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
-                                           ctypes.POINTER(ctypes.c_size_t)]),
-    "tsg_gen_file_nonascii": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32]),
-    "tsg_gen_template_count": (ctypes.c_size_t, []),
-    "tsg_gen_template_rule": (ctypes.c_char_p, [ctypes.c_size_t]),
-    "tsg_gen_plant_record_size": (ctypes.c_size_t, []),
-    "tsg_gen_chunk_bytes": (ctypes.c_uint32, []),
     "tsg_regex_match": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t,
                                        ctypes.POINTER(ctypes.c_int)]),
     "tsg_regex_find_all": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t,
@@ -189,6 +176,40 @@ for _name, (_res, _args) in _SIGS.items():
     _fn.argtypes = _args
 
 EXPORTED = sorted(_SIGS)
+
+# The synthetic-corpus generator (bench.py, tests) lives in its own library,
+# bench_gen/libtsg_corpus.so (header bench_gen/tsg_corpus.h), outside the
+# product ABI; `gen` loads it on first use.
+GEN_PATH = os.path.join(os.path.dirname(_HERE), "bench_gen", "libtsg_corpus.so")
+_GEN_SIGS = {
+    "tsg_gen_corpus_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                             ctypes.c_double, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+    "tsg_gen_file": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double,
+                                    ctypes.c_void_p]),
+    "tsg_gen_file_plants": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.POINTER(ctypes.c_size_t)]),
+    "tsg_gen_file_nonascii": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32]),
+    "tsg_gen_template_count": (ctypes.c_size_t, []),
+    "tsg_gen_template_rule": (ctypes.c_char_p, [ctypes.c_size_t]),
+    "tsg_gen_plant_record_size": (ctypes.c_size_t, []),
+    "tsg_gen_chunk_bytes": (ctypes.c_uint32, []),
+}
+
+
+def __getattr__(name):
+    if name != "gen":
+        raise AttributeError(name)
+    if not os.path.exists(GEN_PATH):
+        raise ImportError(f"{GEN_PATH} is missing: build it with `make`")
+    g = ctypes.CDLL(GEN_PATH)
+    for fn_name, (res, args) in _GEN_SIGS.items():
+        f = getattr(g, fn_name)
+        f.restype = res
+        f.argtypes = args
+    globals()["gen"] = g
+    return g
 
 
 class EngineError(RuntimeError):

@@ -2233,11 +2233,11 @@ __device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, ui
   if (rd.grp_fast) {  // the group's span follows from [ms, me) on ASCII text (gre::group_span)
     // ASCII: the scan's per-4 KiB-span flags, byte by byte only in a flagged span
     bool ascii = true;
-    if (V.span_hi) {
+    if (V.span_hi && me > ms) {  // (an empty match holds no byte: nothing to check)
       const uint64_t a = (uint64_t)(text - V.data) + ms, b = (uint64_t)(text - V.data) + me;
-      for (uint64_t sp = a / kNlBlock; sp <= (b - 1) / kNlBlock && ascii; ++sp) ascii = V.span_hi[sp] == 0;
+      for (uint64_t sp = a / kNlBlock; sp < (b + kNlBlock - 1) / kNlBlock && ascii; ++sp) ascii = V.span_hi[sp] == 0;
     }
-    if (!ascii || !V.span_hi) {
+    if (!ascii || (!V.span_hi && me > ms)) {
       ascii = true;
       for (uint32_t q = ms; q < me && ascii; ++q) ascii = as_global<gu8>(text)[q] < 0x80;
     }
@@ -4295,9 +4295,25 @@ int import_parts(tsg_engine* e, const tsg_ruleset* rs, ScanParams& P, const Spli
       return TSG_ERR_INVALID_ARG;
     }
     const PartHeader* H = (const PartHeader*)pr.first;
-    const size_t need = sizeof(PartHeader) + H->n_hits * 8 + (size_t)H->kw_words * 4 + (size_t)H->n_spans * 5;
-    if (H->magic != kPartMagic || H->ruleset_id != rs->id || H->kw_words != P.rs.kw_words ||
-        H->file_len != sp.file_len || pr.second != need) {
+    // every size field checked against the file and the blob before any
+    // arithmetic with it (blobs travel over arbitrary transports)
+    const size_t body = pr.second - sizeof(PartHeader);
+    bool ok = H->magic == kPartMagic && H->ruleset_id == rs->id && H->kw_words == P.rs.kw_words &&
+              H->file_len == sp.file_len && H->own_lo < H->own_hi && H->own_hi <= sp.file_len &&
+              H->own_lo % kNlBlock == 0 && (H->own_hi % kNlBlock == 0 || H->own_hi == sp.file_len) &&
+              H->n_spans == (H->own_hi - H->own_lo + kNlBlock - 1) / kNlBlock && H->n_hits <= body / 8;
+    if (ok) {
+      const size_t need = (size_t)H->n_hits * 8 + (size_t)H->kw_words * 4 + (size_t)H->n_spans * 5;
+      ok = body == need;
+    }
+    if (ok) {  // every hit's literal starts inside the part's own range
+      const uint64_t* hp = (const uint64_t*)(H + 1);
+      for (uint64_t i = 0; i < H->n_hits && ok; ++i) {
+        const uint64_t start = (hp[i] & ~kFoldHit) >> 16;
+        ok = start >= H->own_lo && start < H->own_hi;
+      }
+    }
+    if (!ok) {
       set_last_error("split: a part blob belongs to another file or ruleset, or is corrupt");
       return TSG_ERR_INVALID_ARG;
     }
@@ -5068,6 +5084,14 @@ static int scan_part_impl(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d
   }
   std::lock_guard<std::mutex> lk(e->mu);
   HIP_TRY(hipSetDevice(e->device));
+  if (text_base + text_len == file_len) {  // the view reaches the file end: its extra byte is the NUL separator
+    uint8_t sep = 1;
+    HIP_TRY(hipMemcpy(&sep, d_text + text_len, 1, hipMemcpyDeviceToHost));
+    if (sep != 0) {
+      set_last_error("split: a view that ends at the file end must be followed by the NUL separator");
+      return TSG_ERR_INVALID_ARG;
+    }
+  }
   int rc = stage_one_file(e, text_len, path);
   if (rc) return rc;
   std::vector<uint8_t> out;

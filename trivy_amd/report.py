@@ -8,7 +8,9 @@ Restates what a Trivy user reads after a secret scan:
     empty; `Layer` rendered as `{}` -- a struct is never empty for omitempty);
   * pkg/report/json.go:20-30: json.MarshalIndent(report, "", "  ") plus a
     newline, with encoding/json's string escaping (HTML characters and
-    U+2028/U+2029 as \\u escapes, invalid UTF-8 as U+FFFD).
+    U+2028/U+2029 as \\u escapes; each byte of invalid UTF-8 -- a rune
+    utf8.DecodeRuneInString returns as RuneError of width 1 -- as the
+    six-character escape \\ufffd, while a valid U+FFFD stays raw).
 
 The findings come from the engine (device-built Match / Code), so this module
 only formats; it never scans.
@@ -16,6 +18,7 @@ only formats; it never scans.
 from __future__ import annotations
 
 import json
+import re
 from typing import Iterable, List, Optional
 
 from .types import Secret
@@ -23,9 +26,13 @@ from .types import Secret
 _GO_ESCAPES = {"<": "\\u003c", ">": "\\u003e", "&": "\\u0026", " ": "\\u2028", " ": "\\u2029"}
 
 
+# surrogateescape'd bytes (U+DC80-U+DCFF) are exactly the bytes Go's decoder
+# rejects one at a time; dumps() writes each as the escape text \ufffd
+_INVALID = re.compile("[\udc80-\udcff]")
+
+
 def _go_str(s: str) -> str:
-    # Go renders invalid UTF-8 (our surrogateescape'd bytes) as U+FFFD
-    return s.encode("utf-8", "surrogateescape").decode("utf-8", "replace")
+    return s
 
 
 def line_json(ln) -> dict:
@@ -60,7 +67,7 @@ def dumps(obj) -> str:
     text = json.dumps(obj, indent=2, ensure_ascii=False, separators=(",", ": "))
     for k, v in _GO_ESCAPES.items():
         text = text.replace(k, v)
-    return text + "\n"
+    return _INVALID.sub(lambda m: "\\ufffd", text) + "\n"
 
 
 def report_json(secrets: Iterable[Optional[Secret]], artifact_name: str = "", artifact_type: str = "",

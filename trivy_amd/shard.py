@@ -120,13 +120,18 @@ def split_ranges(file_len: int, n_parts: int, halo) -> List[tuple]:
 
 def scan_split(scanner, args, group=None, owner: int = 0, n_parts: Optional[int] = None):
     """Byte-range split of ONE file over the ranks of `group` (every rank
-    calls it with the same args).  Part p is scanned by rank p % world; the
-    parts go to `owner` (gather_object: host bytes), whose engine merges
-    them; every rank returns the file's Secret.  With no process group the
-    parts run one after another on this rank's engine."""
+    calls it with the same args).  Part p is scanned by group rank p % world;
+    the parts go to `owner` -- a rank WITHIN `group` (gather_object: host
+    bytes) -- whose engine merges them; every rank returns the file's Secret.
+    With no process group the parts run one after another on this rank's
+    engine."""
     dist = _dist()
     world = dist.get_world_size(group) if dist else 1
     rank = dist.get_rank(group) if dist else 0
+    if not 0 <= owner < world:
+        raise ValueError(f"owner {owner} is not a rank of the group (size {world})")
+    # collectives address processes by global rank
+    owner_global = dist.get_global_rank(group, owner) if dist and group is not None else owner
     data = args.content
     n = len(data)
     ranges = split_ranges(n, n_parts or world, scanner.part_halo())
@@ -138,9 +143,9 @@ def scan_split(scanner, args, group=None, owner: int = 0, n_parts: Optional[int]
         parts = [b for _, b in sorted(mine)]
     else:
         gathered = [None] * world if rank == owner else None
-        dist.gather_object(mine, gathered, dst=owner, group=group)
+        dist.gather_object(mine, gathered, dst=owner_global, group=group)
         parts = [b for _, b in sorted(x for g in gathered for x in g)] if rank == owner else None
     result = [scanner.scan_merge(args, parts) if rank == owner else None]
     if world > 1:
-        dist.broadcast_object_list(result, src=owner, group=group)
+        dist.broadcast_object_list(result, src=owner_global, group=group)
     return result[0]
