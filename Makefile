@@ -8,7 +8,7 @@ SRC_DIR  = trivy_amd/csrc
 BUILD    = build
 LIB      = trivy_amd/libtrivy_secret_gpu.so
 
-HOST_SRCS = $(SRC_DIR)/gre.cpp $(SRC_DIR)/ruleset.cpp $(SRC_DIR)/follow.cpp $(SRC_DIR)/dfa.cpp $(SRC_DIR)/layertar.cpp
+HOST_SRCS = $(SRC_DIR)/gre.cpp $(SRC_DIR)/ruleset.cpp $(SRC_DIR)/follow.cpp $(SRC_DIR)/dfa.cpp $(SRC_DIR)/nfa.cpp $(SRC_DIR)/layertar.cpp
 HIP_SRCS  = $(SRC_DIR)/engine.hip
 HDRS      = $(wildcard $(SRC_DIR)/*.h) include/trivy_secret_gpu.h
 

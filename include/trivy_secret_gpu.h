@@ -154,6 +154,15 @@ int tsg_ruleset_follow_check(const tsg_ruleset* rs, size_t i, const uint8_t* tex
 int tsg_ruleset_dfa_check(const tsg_ruleset* rs, size_t i, const uint8_t* text, size_t len, size_t s,
                           int* result, size_t* me, uint32_t* n_states);
 
+/* Bit-parallel Glushkov NFA of rule i (the verify fallback for rules whose
+ * DFA state count explodes, or with \b / (?m) assertions), on host text with
+ * threads started at every boundary in [s, inj_hi]: *result = 1 (anchored,
+ * inj_hi == s: the match from s ends at *me and nowhere else; unanchored: a
+ * match ends at *me first), 0 (none) or 2 (undecidable: the Pike VM decides);
+ * *n_pos = its positions (0 = the rule has no NFA). */
+int tsg_ruleset_nfa_check(const tsg_ruleset* rs, size_t i, const uint8_t* text, size_t len, size_t s, size_t inj_hi,
+                          int* result, size_t* me, uint32_t* n_pos);
+
 /* Automaton diagnostics: states/classes of the keyword+anchor automaton and
  * whether it fits k_scan_fast's LDS image (fast_path = 1). */
 int tsg_ruleset_stats(const tsg_ruleset* rs, uint32_t* n_states, uint32_t* n_classes, uint32_t* n_patterns,

@@ -1,0 +1,200 @@
+"""Bit-parallel Glushkov NFA exactness (nfa.cpp, the host build of the tables
+k_verify walks for rules without a verify DFA; BASELINE.json north_star (1)
+"bit-parallel Glushkov/shift-and NFA fallback when a rule's DFA state count
+explodes").  Go's FindAllIndex (regexp.go allMatches, scanner.go:107) is
+rebuilt the way k_verify does it -- the first start (in order) whose anchored
+walk finds a match wins, and the walk's end is taken only when it is the only
+end a match from that start can have (else the Pike VM decides that start;
+here the oracle's restatement stands in for it) -- and must equal the oracle's
+FindAllIndex (oracle/secret_oracle.py, independent of gre.cpp).  CPU only."""
+import ctypes
+import random
+
+import pytest
+
+from oracle import secret_oracle as O
+from trivy_amd import _native as N
+import trivy_amd.secret as S
+
+from . import stress_rules
+
+
+def _scanner(pats):
+    rules = [S.Rule(id=f"r{i}", category="c", title="t", severity="HIGH", regex=p, keywords=[])
+             for i, p in enumerate(pats)]
+    return S.Scanner(rules, [], S.ExcludeBlock())
+
+
+def _npos(rs, i):
+    res, me, npos = ctypes.c_int(), ctypes.c_size_t(), ctypes.c_uint32()
+    N.check(N.lib.tsg_ruleset_nfa_check(rs, i, b"x", 1, 0, 0, ctypes.byref(res), ctypes.byref(me), ctypes.byref(npos)))
+    return npos.value
+
+
+def _nfa_find_all(rs, i, t, oracle_rx, stats):
+    res, me, npos = ctypes.c_int(), ctypes.c_size_t(), ctypes.c_uint32()
+    n = len(t)
+    txt = t.decode("ascii")
+    out, pos = [], 0
+    while pos < n:
+        # the window pass (every start in [pos, n)) first: no match -> done
+        N.check(N.lib.tsg_ruleset_nfa_check(rs, i, t, n, pos, n, ctypes.byref(res), ctypes.byref(me),
+                                            ctypes.byref(npos)))
+        if res.value == 0:
+            break
+        hit = None
+        for s in range(pos, n):
+            N.check(N.lib.tsg_ruleset_nfa_check(rs, i, t, n, s, s, ctypes.byref(res), ctypes.byref(me),
+                                                ctypes.byref(npos)))
+            if res.value == 2:  # the VM's start (two possible ends): Go's priorities decide
+                stats["vm"] += 1
+                m = oracle_rx.match(txt, s)
+                if m:
+                    hit = (s, m.end())
+                    break
+                continue
+            stats["nfa"] += 1
+            if res.value == 1:
+                hit = (s, me.value)
+                break
+        if hit is None:
+            break
+        assert hit[1] > hit[0]
+        out.append(list(hit))
+        pos = hit[1]
+    return out
+
+
+PATTERNS = [
+    r"(?:x|y)*x(?:x|y){12}dape",            # configs[4] explosion family: 2^12 DFA states
+    r"(?:a|b)*a(?:a|b){13}zz",
+    r"\bJULE[0-9]{12}\b",                   # \b: no verify DFA
+    r"\Bqq[a-z]{3}\b",
+    r"(?m)^key=[a-z0-9]{4,8}$",
+    r"(?m)^\s*token[:=]\s*[A-Za-z0-9]{8}",
+    r"(?i)\b(?:ghp|gho)_[0-9a-z]{6}\b",
+    r"\b(?:foo|foobar)[0-9]+\b",
+    r"(?:ab|a)(?:bc|c)d",
+    r"[a-c]{2,5}x[0-9]{1,3}\b",
+    r"(?:x|y)*xy{3}(?:q|r)+\b",
+    r"\bkey=[a-z0-9]{4,8}",                 # several ends from one start: the VM decides those
+    r"\b(?:foo|foobar)[0-9]*",
+    r"\bfoo(?:bar)??",
+    r"\b[0-9]+?[0-9]",
+]
+
+
+def _texts(rng):
+    alpha = "xyabcdqrzJULE0123456789ghpo_ =:\n\tkeytoknKEYfoobarABC-"
+    texts = []
+    for _ in range(40):
+        texts.append("".join(rng.choice(alpha) for _ in range(rng.randint(0, 300))).encode())
+    # planted instances of the patterns above
+    for _ in range(40):
+        parts = [
+            "".join(rng.choice("xy") for _ in range(rng.randint(0, 6))) + "x" +
+            "".join(rng.choice("xy") for _ in range(12)) + "dape",
+            "JULE" + "".join(rng.choice("0123456789") for _ in range(rng.choice([11, 12, 13]))),
+            "key=" + "".join(rng.choice("abc019") for _ in range(rng.randint(3, 9))),
+            rng.choice(["ghp_", "GHO_", "gho_"]) + "".join(rng.choice("ab09") for _ in range(6)),
+            rng.choice(["foo", "foobar"]) + "".join(rng.choice("0123") for _ in range(rng.randint(0, 3))),
+            "abcd acd abd", "aaab" * rng.randint(1, 4) + "zz",
+        ]
+        rng.shuffle(parts)
+        texts.append(rng.choice([" ", "\n", "_", "x", "-"]).join(parts).encode())
+    return texts
+
+
+def test_nfa_findall_equals_oracle():
+    sc = _scanner(PATTERNS)
+    rs = sc._rs.handle
+    rng = random.Random(11)
+    texts = _texts(rng)
+    stats = {"nfa": 0, "vm": 0}
+    with_nfa = 0
+    total = 0
+    for i, pat in enumerate(PATTERNS):
+        if not _npos(rs, i):
+            continue
+        with_nfa += 1
+        orx = O.GoRegexp(pat)
+        for t in texts:
+            want = orx.find_all_index(t)
+            assert _nfa_find_all(rs, i, t, orx.rx, stats) == want, (pat, t[:200])
+            total += len(want)
+    assert with_nfa >= 13, with_nfa
+    assert total > 150 and stats["vm"] > 0 and stats["nfa"] > 20 * stats["vm"], (total, stats)
+
+
+def test_configs4_rules_without_a_dfa_get_an_nfa():
+    rules = stress_rules.make_rules(20261019, 1000)
+    pats = [r["regex"] for r, _ in rules]
+    sc = _scanner(pats)
+    rs = sc._rs.handle
+    res, me, ns = ctypes.c_int(), ctypes.c_size_t(), ctypes.c_uint32()
+    no_dfa = with_nfa = 0
+    for i in range(len(pats)):
+        N.check(N.lib.tsg_ruleset_dfa_check(rs, i, b"x", 1, 0, ctypes.byref(res), ctypes.byref(me), ctypes.byref(ns)))
+        if ns.value:
+            assert _npos(rs, i) == 0  # the DFA stays the first choice
+            continue
+        no_dfa += 1
+        with_nfa += _npos(rs, i) > 0
+    assert no_dfa >= 150 and with_nfa == no_dfa, (no_dfa, with_nfa)
+
+
+def test_stress_rule_instances_through_the_nfa():
+    """The configs[4] rules that lost their DFA (explosion family, \\b
+    family), on the stress corpus text: NFA FindAll == the oracle's."""
+    rules = stress_rules.make_rules(20261019, 200)
+    pats = [r["regex"] for r, _ in rules]
+    sc = _scanner(pats)
+    rs = sc._rs.handle
+    files = stress_rules.make_corpus(5, rules, 30, long_line_bytes=4000)
+    texts = [d for _, d in files if max(d, default=0) < 0x80]
+    stats = {"nfa": 0, "vm": 0}
+    total = 0
+    for i, pat in enumerate(pats):
+        if not _npos(rs, i):
+            continue
+        orx = O.GoRegexp(pat)
+        for t in texts:
+            want = orx.find_all_index(t)
+            if not want and len(t) > 2000:
+                continue
+            assert _nfa_find_all(rs, i, t, orx.rx, stats) == want, (pat, t[:200])
+            total += len(want)
+    assert total > 20 and stats["nfa"] > 0, (total, stats)
+
+
+def _yaml(pats):
+    lines = ["rules:"]
+    for i, p in enumerate(pats):
+        lines += [f"  - id: nfa-{i:02d}", "    category: c", "    title: t", "    severity: HIGH",
+                  "    regex: '" + p.replace("'", "''") + "'"]
+    return "\n".join(lines) + "\n"
+
+
+@pytest.mark.gpu
+def test_gpu_nfa_rules_vs_oracle(tmp_path):
+    """The NFA patterns as custom rules through the device scan (k_verify's
+    NFA path, the Pike VM only for two-end starts and non-ASCII), findings
+    field by field against the oracle Scanner, plus non-ASCII and
+    binary-ish files (the walk's undecidable case)."""
+    from .test_gpu_parity import _canon, _oracle_plain, _plain
+    cfg = tmp_path / "trivy-secret.yaml"
+    cfg.write_text(_yaml(PATTERNS))
+    sc_o = O.Scanner(O.parse_config(str(cfg)))
+    sc_g = S.new_scanner(S.parse_config(str(cfg)), device=0)
+    rng = random.Random(23)
+    texts = _texts(rng)
+    texts += [t.replace(b"_", "é".encode()) for t in texts[40:60]]
+    texts += [bytes(rng.randrange(256) for _ in range(300)) + b" JULE123456789012 " + t for t in texts[60:70]]
+    files = [(f"src/f{i:03d}.txt", t) for i, t in enumerate(texts)]
+    got = sc_g.scan_batch([S.ScanArgs(p, d) for p, d in files])
+    seen = set()
+    for (p, d), g in zip(files, got):
+        want = _oracle_plain(sc_o.scan(p, d))
+        seen |= {f["RuleID"] for f in want["Findings"]}
+        assert _canon(_plain(g)) == _canon(want), p
+    assert len(seen) >= 10, seen

@@ -11,7 +11,7 @@ SAN      = -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarc
 FLAGS    = -O1 -g -fno-omit-frame-pointer -std=c++17 -fPIC -Wall -Wno-unused-function -Iinclude -Itrivy_amd/csrc \
            -x hip --offload-arch=$(ARCH) -munsafe-fp-atomics $(SAN)
 SRC_DIR  = trivy_amd/csrc
-SRCS     = gre.cpp ruleset.cpp follow.cpp dfa.cpp layertar.cpp engine.hip
+SRCS     = gre.cpp ruleset.cpp follow.cpp dfa.cpp nfa.cpp layertar.cpp engine.hip
 OBJS     = $(patsubst %,build_asan/%.o,$(SRCS))
 LIB      = trivy_amd/libtrivy_secret_gpu_asan.so
 HDRS     = $(wildcard $(SRC_DIR)/*.h) include/trivy_secret_gpu.h

@@ -110,6 +110,9 @@ _SIGS = {
     "tsg_ruleset_dfa_check": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
                                              ctypes.c_size_t, ctypes.POINTER(ctypes.c_int),
                                              ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_uint32)]),
+    "tsg_ruleset_nfa_check": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                                             ctypes.c_size_t, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int),
+                                             ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_uint32)]),
     "tsg_ruleset_follow_check": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
                                                 ctypes.c_size_t, ctypes.POINTER(ctypes.c_int),
                                                 ctypes.POINTER(ctypes.c_uint32)]),

@@ -65,6 +65,8 @@ struct RuleDev {
   int32_t grp_pre, grp_len, grp_suf;
   uint32_t id_rank;  // position of the rule ID in sorted (ID, index) order: findings sort (scanner.go:441-446)
   uint32_t no_nl;    // no instruction of the program consumes '\n': every match lies inside one line
+  uint32_t nfa_off;  // bit-parallel NFA (nfa.cpp): byte offset of its NfaDev record (kNoFollow = none)
+  uint32_t nfa_bytes;
 };
 
 struct PatDev {
@@ -112,6 +114,7 @@ struct RuleSetDev {
   const uint8_t* follow_cls;
   const uint16_t* dfa_delta;     // all rules' verify DFAs (dfa.cpp)
   const uint8_t* dfa_bytes;      // their class maps and match flags
+  const uint8_t* nfa_bytes;      // all rules' bit-parallel NFAs (nfa.cpp), 16-byte aligned records
   const gre::ProgView* progs;
   const uint32_t* prog_lit_off;  // per program: range of prefilter literals (n_progs + 1)
   const uint8_t* prog_lits;      // kLitRec-byte records
@@ -164,6 +167,58 @@ bool build_dfa(const gre::Compiled& c, DfaHost* out);
 int dfa_anchored(const DfaHost& d, const uint8_t* text, size_t n, size_t s, size_t* me);
 bool follow_accepts(const FollowDfa& f, const uint8_t* text, size_t n, size_t h);
 
+// Bit-parallel Glushkov NFA (nfa.cpp), the fallback for rules whose verify
+// DFA explodes past kDfaMaxStates or that use assertions the DFA does not
+// model (\b, \B, (?m)^ / $).  Positions = the program's consuming
+// instructions (<= kNfaMaxPos, two 64-bit words); the Glushkov follow relation
+// is stored LimEx-style: up to kNfaShifts (delta, mask) pairs cover the edges
+// p -> p + delta, and the few positions with other edges (or edges through an
+// assertion) are exceptions with explicit follow masks.
+constexpr uint32_t kNfaMaxPos = 128;
+constexpr uint32_t kNfaShifts = 6;
+constexpr uint32_t kNfaMaxCond = 4;    // conditional start / accept masks (edges through assertions)
+constexpr uint32_t kNfaMaxExc = 48;    // exception positions
+constexpr uint32_t kNfaExcCond = 2;    // conditional follows per exception
+constexpr uint32_t kNfaNoExc = 0xFF;
+constexpr uint32_t kNfaWalkMax = 8192; // bytes an NFA walk may take before the Pike VM decides
+
+struct U128 {
+  uint64_t lo, hi;
+};
+
+// The device record of one rule's NFA: this header, then reach[ncls], then
+// exc[n_exc] (nfa_blob lays them out 16-byte aligned).
+struct NfaDev {
+  uint32_t npos, nshift, ncls, n_exc;
+  int32_t shift[kNfaShifts];
+  uint32_t n_first_c, n_last_c;
+  U128 smask[kNfaShifts];
+  U128 first_u, last_u, exc_mask;
+  U128 first_c[kNfaMaxCond], last_c[kNfaMaxCond];
+  uint32_t first_r[kNfaMaxCond], last_r[kNfaMaxCond];  // required EmptyOp flags of each conditional mask
+  uint32_t has_cond, bytes, o_reach, o_exc;             // bytes: the whole record
+  uint8_t cls[128];                                      // ASCII byte -> reach class
+  uint8_t exc_of[kNfaMaxPos];                            // position -> exception record (kNfaNoExc: none)
+};
+struct NfaExc {
+  U128 follow_u;                // unconditional follow
+  U128 follow_c[kNfaExcCond];   // follow through assertions
+  uint32_t r[kNfaExcCond];      // their required flags
+  uint32_t n_c, pad;
+};
+
+struct NfaHost {
+  bool valid = false;
+  uint32_t npos = 0, n_exc = 0;
+  std::vector<uint8_t> blob;  // NfaDev | reach | exc
+};
+bool build_nfa(const gre::Compiled& c, NfaHost* out);
+// Host mirror of the device walk (tests / diagnostics).  From s, threads
+// injected at every position in [s, inj_hi]; anchored (inj_hi == s): 1 = the
+// only match end *me, 0 = no match, 2 = undecidable (the Pike VM decides: a
+// byte >= 0x80, two match ends, or kNfaWalkMax); unanchored: 1 = some match.
+int nfa_walk_host(const NfaHost& d, const uint8_t* text, size_t n, size_t s, size_t inj_hi, size_t* me);
+
 struct RuleHost {
   std::string id;
   int regex = -1;  // index into regexes, -1 => never matches
@@ -176,6 +231,7 @@ struct RuleHost {
   RuleMode mode = MODE_NEVER;
   FollowDfa follow;  // MODE_ANCHORED only
   DfaHost dfa;       // MODE_ANCHORED only
+  NfaHost nfa;       // MODE_ANCHORED without a verify DFA
   bool gate_implied = false;  // every anchor literal contains one of the keywords
   gre::GroupSpan grp;         // secret-group span rule (valid: k_verify skips the capture search)
   bool fold_gate = false;     // an anchor literal has a case-free k / s: K/ſ spellings of it
@@ -278,8 +334,6 @@ struct PinnedBlock {
 std::shared_ptr<PinnedBlock> pinned_get(const std::shared_ptr<PinnedPool>& pool, size_t bytes);
 
 struct ResultImpl {
-  std::vector<tsg_loc> locs;
-  std::vector<uint8_t> file_flags;
   // findings in Scan order per file (sorted by file, then RuleID, then Match)
   // (records, code lines and strings share one page-locked block: the D2H
   // copies run at full PCIe rate)
@@ -290,8 +344,16 @@ struct ResultImpl {
     T* begin() const { return p; }
     T* end() const { return p + n; }
     size_t size() const { return n; }
+    T* data() const { return p; }
     T& operator[](size_t i) const { return p[i]; }
   };
+  // everything lives in ONE page-locked block (arena): the kept locations as
+  // tsg_loc records and the per-file flags next to the findings, all written
+  // by the device and copied back with the call's final synchronisation
+  View<tsg_loc> locs;
+  View<uint8_t> file_flags;
+  View<uint32_t> ties;        // findings equal to their predecessor in (file, RuleID, Match prefix)
+  size_t ties_cap = 0, ctrl_off = 0;  // (the block also holds a copy of the device counters)
   View<FindRec> frec;
   View<CodeRec> code;  // kCodeLines per location, indexed by FindRec::loc
   const char* strs = nullptr;

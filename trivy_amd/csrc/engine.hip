@@ -40,6 +40,7 @@
 
 #include "engine.h"
 #include "gre_lower_table.h"
+#include "nfa_walk.h"
 #include "pikevm.h"
 
 namespace tsg {
@@ -99,6 +100,8 @@ struct Ctrl {
   unsigned long long n_caps;     // matches whose secret-group spans k_captures resolves
   unsigned long long n_caps_big; // ... and those too long for its arenas (k_captures_big)
   unsigned long long long_files; // files longer than kMaxVerifyFile (k_region_mark)
+  unsigned long long n_panic;    // kept locations whose secret group did not participate (k_out_locs)
+  unsigned long long n_ties;     // findings whose (file, RuleID, Match prefix) equals the previous one's
 };
 
 struct DevLoc {
@@ -2292,8 +2295,8 @@ __global__ __launch_bounds__(kLanes) void k_captures(VerifyParams V) {
 // costs an HBM round trip per step.  Block b serves XCD b % 8 (round-robin
 // dispatch), part b / 8 of each range; nothing is written.
 struct WarmRanges {
-  const uint8_t* p[8];
-  uint64_t n[8];
+  const uint8_t* p[10];
+  uint64_t n[10];
   uint32_t k;
 };
 constexpr uint32_t kWarmParts = 8;
@@ -2427,6 +2430,79 @@ __device__ __noinline__ void verify_vm_job(const VerifyParams& V, uint32_t rule,
   }
 }
 
+// The text of a job read in aligned 16-byte blocks (one dwordx4 load per
+// block; the batch is padded past its end), for the NFA walk's byte stream.
+struct VecText {
+  const uint8_t* base;
+  uintptr_t blk;
+  u32x4 v;
+  __device__ explicit VecText(const uint8_t* b) : base(b), blk(~(uintptr_t)0), v{0, 0, 0, 0} {}
+  __device__ uint32_t operator[](uint32_t i) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(base) + i;
+    const uintptr_t b = a & ~(uintptr_t)15;
+    if (b != blk) {
+      blk = b;
+      v = *as_global<__attribute__((address_space(1))) const u32x4>(reinterpret_cast<const void*>(b));
+    }
+    const uint32_t o = (uint32_t)(a & 15);
+    const uint32_t wd = o < 8 ? (o < 4 ? v.x : v.y) : (o < 12 ? v.z : v.w);  // no dynamically indexed array
+    return (wd >> (8 * (o & 3))) & 0xFFu;
+  }
+};
+
+// FindAll over the anchor windows with the bit-parallel NFA (nfa.cpp; rules
+// whose verify DFA exploded or that use \b / (?m) assertions): one walk
+// with a thread started at every permitted start of the window tells whether
+// any of them matches (most windows: no -- done); then the starts in order,
+// each with an anchored walk, the first that matches is Go's leftmost match,
+// and its end is the walk's when that is the only end a match from that start
+// can have.  A start the walk cannot decide (a byte >= 0x80, two possible
+// ends -- Go's priorities choose -- or a walk past kNfaWalkMax) is decided by
+// the Pike VM anchored there.
+template <bool kWide>
+__device__ __noinline__ uint32_t verify_nfa_job(const VerifyParams& V, uint32_t rule, uint32_t fi, uint64_t c0,
+                                                uint64_t c1, uint64_t fstart, const uint8_t* text, uint32_t n,
+                                                gre::VmScratch& sc, const uint8_t* nfa) {
+  const NfaDev& N = *(const NfaDev*)nfa;
+  const U128* reach = (const U128*)(nfa + N.o_reach);
+  const NfaExc* exc = (const NfaExc*)(nfa + N.o_exc);
+  const uint32_t prog = V.rs.rules[rule].prog;
+  uint32_t steps = 0;
+  IvIter it;
+  iv_init(it, V, rule, c0, c1, fstart, text, n);
+  uint32_t pos = 0, ms, me;
+  while (it.have) {
+    bool found = false;
+    const uint32_t s0 = it.cs > pos ? it.cs : pos;
+    const uint32_t s1 = it.ce < n ? it.ce : n;
+    int any = 0;
+    if (s0 <= s1) {
+      VecText T(text);
+      any = nfa_walk<kWide>(N, reach, exc, T, n, s0, s1, &me, &steps);
+    }
+    for (uint32_t sp = s0; any && sp <= s1 && sp < n; ++sp) {
+      if (!gre::is_rune_start(text, n, sp)) continue;
+      const uint32_t b0 = as_global<gu8>(text)[sp];
+      if (b0 < 0x80 && !nfa_first_ok(N, reach, b0)) continue;  // first-byte skip
+      VecText T(text);
+      int r = nfa_walk<kWide>(N, reach, exc, T, n, sp, sp, &me, &steps);
+      if (r == 2) {
+        OneStart one{sp};
+        r = vm_search_starts(V.rs.progs[prog], text, n, sp, one, sc, &ms, &me) ? 1 : 0;
+      }
+      if (r == 1) {
+        emit_match(V, rule, fi, text, n, sp, me, sc);
+        pos = me;
+        found = true;
+        break;
+      }
+    }
+    if (!found) it.advance();
+    else while (it.have && it.ce < pos) it.advance();
+  }
+  return steps;
+}
+
 // The block (one wave) stages the verify DFA of its first job's rule in LDS:
 // jobs are sorted by rule, so nearly every lane walks that table, and an LDS
 // step costs no L2 round trip and no TLB lookup (the random text pages the
@@ -2444,11 +2520,17 @@ __global__ __launch_bounds__(kBlock) void k_verify(VerifyParams V) {
     const uint32_t r0 = (uint32_t)(V.keys[V.job_start[jb]] >> kPosBits);
     const RuleDev& rd0 = V.rs.rules[r0];
     const bool staged = rd0.dfa_off != kNoFollow && rd0.dfa_size * 2 <= kVerifyDfaLds;
+    // (or its bit-parallel NFA record, rules without a DFA)
+    const bool staged_nfa = !staged && rd0.dfa_off == kNoFollow && rd0.nfa_off != kNoFollow &&
+                            rd0.nfa_bytes <= kVerifyDfaLds;
     __syncthreads();  // the previous group's walks are done with the table
     if (staged) {
       const uint32_t* src = (const uint32_t*)(V.rs.dfa_delta + rd0.dfa_off);  // dfa_off is even (build pads)
       for (uint32_t i = threadIdx.x; i < (rd0.dfa_size + 1) / 2; i += blockDim.x) ((uint32_t*)dfa_lds)[i] = src[i];
       for (uint32_t i = threadIdx.x; i < 128; i += blockDim.x) cls_lds[i] = V.rs.dfa_bytes[rd0.dfa_cls_off + i];
+    } else if (staged_nfa) {
+      const uint32_t* src = (const uint32_t*)(V.rs.nfa_bytes + rd0.nfa_off);  // 16-byte aligned records
+      for (uint32_t i = threadIdx.x; i < rd0.nfa_bytes / 4; i += blockDim.x) ((uint32_t*)dfa_lds)[i] = src[i];
     }
     __syncthreads();
     const uint32_t j = jb + threadIdx.x;
@@ -2468,7 +2550,11 @@ __global__ __launch_bounds__(kBlock) void k_verify(VerifyParams V) {
     else if (staged && rule == r0) steps = verify_dfa_job<true>(V, rule, fi, c0, c1, fstart, text, n, sc, dfa_lds, cls_lds, V.tck ? V.tck + 4 * j : nullptr);
     else if (V.rs.rules[rule].dfa_off != kNoFollow)
       steps = verify_dfa_job<false>(V, rule, fi, c0, c1, fstart, text, n, sc, nullptr, nullptr, V.tck ? V.tck + 4 * j : nullptr);
-    else verify_vm_job(V, rule, fi, c0, c1, fstart, text, n, sc);
+    else if (V.rs.rules[rule].nfa_off != kNoFollow) {
+      const uint8_t* nfa = staged_nfa && rule == r0 ? (const uint8_t*)dfa_lds : V.rs.nfa_bytes + V.rs.rules[rule].nfa_off;
+      steps = ((const NfaDev*)nfa)->npos > 64 ? verify_nfa_job<true>(V, rule, fi, c0, c1, fstart, text, n, sc, nfa)
+                                              : verify_nfa_job<false>(V, rule, fi, c0, c1, fstart, text, n, sc, nfa);
+    } else verify_vm_job(V, rule, fi, c0, c1, fstart, text, n, sc);
     if (V.prof) {  // diagnostics (TSG_PROFILE_VERIFY): duration | end, rule | full
       const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
       V.prof[2 * j] = (t1 - t0) | ((t1 & 0xFFFFFFFFull) << 32);
@@ -3041,6 +3127,47 @@ __global__ void k_find_gather(const FindRec* in, const uint32_t* idx, uint64_t n
   if (i < n) out[i] = in[idx[i]];
 }
 
+// Scan's sort (scanner.go:441-446) is by (RuleID, Match): the first 8 bytes
+// of each Match window (from the filled arena, zero-padded, big-endian) are
+// a sort key, so the device orders (file, RuleID rank, Match prefix) and the
+// host only breaks ties of equal prefixes.
+__global__ void k_match_prefix(const FindRec* rec, const uint8_t* arena, uint64_t n, uint64_t* key, uint32_t* idx) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const FindRec& r = rec[i];
+  uint64_t k = 0;
+  for (uint32_t j = 0; j < 8; ++j) k = (k << 8) | (j < r.m_len ? arena[r.m_off + j] : 0u);
+  key[i] = k;
+  idx[i] = (uint32_t)i;
+}
+
+__global__ void k_gather_u64(const uint64_t* in, const uint32_t* idx, uint64_t n, uint64_t* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = in[idx[i]];
+}
+
+// Positions i (> 0) of the ordered findings whose (file, rank) key AND Match
+// prefix equal those of i - 1: the only places the host has to compare whole
+// Match strings (appended unordered; the host sorts the short list).
+__global__ void k_tie_list(const uint64_t* fr_key, const uint64_t* prefix, const uint32_t* order, uint64_t n,
+                           uint32_t* ties, uint64_t cap, Ctrl* ctrl) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0 || i >= n) return;
+  if (fr_key[i] != fr_key[i - 1] || prefix[order[i]] != prefix[order[i - 1]]) return;
+  const unsigned long long k = atomicAdd(&ctrl->n_ties, 1ull);
+  if (k < cap) ties[k] = (uint32_t)i;
+}
+
+// The kept locations as the ABI's tsg_loc records, in (file, start) order;
+// a secret group that did not participate (the reference panics) is counted.
+__global__ void k_out_locs(const DevLoc* locs, uint64_t n, tsg_loc* out, Ctrl* ctrl) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const DevLoc L = locs[i];
+  out[i] = tsg_loc{L.file, L.rule, L.start, L.end, L.start_line, L.end_line};
+  if (L.flags & 1) atomicAdd(&ctrl->n_panic, 1ull);
+}
+
 // ---- SecretAnalyzer front end (tsg_analyze) --------------------------------
 // utils.IsBinary (utils.go:77-95) per byte of the head.
 __device__ inline bool is_binary_byte(uint32_t b) {
@@ -3209,6 +3336,7 @@ struct DevImage {
   DBuf<uint8_t> pac;  // path literal automaton blob (k_path_gate)
   DBuf<uint16_t> dfa_delta;
   DBuf<uint8_t> dfa_bytes;
+  DBuf<uint8_t> nfa;         // bit-parallel NFA records (nfa.cpp)
   DBuf<uint8_t> uni_bytes;   // lowercased non-ASCII keywords (k_uni_keywords)
   DBuf<uint32_t> uni_meta;   // per such keyword: byte offset, byte length, keyword id
   DBuf<uint32_t> lower_map;  // kLowerMap: {rune, lowercase} pairs
@@ -3225,7 +3353,7 @@ struct DevImage {
     inst.release(); classes.release(); ranges.release(); progs.release(); rules.release();
     u32.release(); rule_path.release(); delta.release(); cls.release(); out_off.release();
     out_pat.release(); pats.release(); pat_bytes.release(); pat_rules.release(); fast.release();
-    prog_lit_off.release(); prog_lits.release(); follow_delta.release(); follow_cls.release(); pac.release(); dfa_delta.release(); dfa_bytes.release();
+    prog_lit_off.release(); prog_lits.release(); follow_delta.release(); follow_cls.release(); pac.release(); dfa_delta.release(); dfa_bytes.release(); nfa.release();
     uni_bytes.release(); uni_meta.release(); lower_map.release();
   }
 };
@@ -3265,8 +3393,6 @@ struct tsg_engine {
   uint64_t ev_ovf_need = 0;  // overflow-event capacity learnt from a lost scan
   bool fast_timed = false;   // ev[10..11] bracket the last k_scan_fast launch
   DBuf<uint8_t> fflags8;     // per-file result flags, u8
-  uint8_t* h_flags = nullptr;  // pinned staging for them
-  size_t h_flags_n = 0;
   uint32_t num_cus = 0;
   DBuf<ExclJob> excl_jobs;
   DBuf<ExclRange> excl_out;
@@ -3289,6 +3415,8 @@ struct tsg_engine {
   DBuf<uint2> f_sgrp;
   DBuf<uint2> f_grp;
   DBuf<FindRec> f_rec, f_rec2;
+  DBuf<uint32_t> f_ties;   // k_tie_list
+  DBuf<tsg_loc> out_locs;  // k_out_locs
   DBuf<CodeRec> f_code;
   DBuf<uint8_t> f_arena;
   std::shared_ptr<PinnedPool> pinned = std::make_shared<PinnedPool>();
@@ -3402,7 +3530,7 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   for (size_t k = 0; k < rs->keywords.size(); ++k) kwid[rs->keywords[k]] = (uint32_t)k;
   std::vector<uint32_t> kw_ids, group_slots, allow_progs, apath_off, apath, full_rules, path_rules;
   std::vector<uint16_t> fdelta, ddelta;
-  std::vector<uint8_t> fcls, dbytes;
+  std::vector<uint8_t> fcls, dbytes, nbytes;
   std::set<uint32_t> kw_needed_ids;
   std::vector<std::string> ids;  // sorted distinct rule IDs: the findings' RuleID order
   for (auto& r : rs->rules) ids.push_back(r.id);
@@ -3429,6 +3557,12 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
       d.dfa_smatch = (r.dfa.match[r.dfa.start[0]] ? 1u : 0u) | (r.dfa.match[r.dfa.start[1]] ? 2u : 0u);
       d.dfa_sym = r.dfa.sym_base | (r.dfa.na_ok ? 0x80000000u : 0u);
       ddelta.insert(ddelta.end(), r.dfa.delta.begin(), r.dfa.delta.end());
+    }
+    d.nfa_off = kNoFollow;
+    if (r.nfa.valid) {  // (records are multiples of 16 bytes: every one stays 16-byte aligned)
+      d.nfa_off = (uint32_t)nbytes.size();
+      d.nfa_bytes = (uint32_t)r.nfa.blob.size();
+      nbytes.insert(nbytes.end(), r.nfa.blob.begin(), r.nfa.blob.end());
     }
     if (r.follow.valid) {
       d.follow_off = (uint32_t)fdelta.size();
@@ -3535,6 +3669,8 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
     HIP_TRY(hipMemcpy(im.dfa_delta.p, ddelta.data(), ddelta.size() * 2, hipMemcpyHostToDevice));
   HIP_TRY(im.dfa_bytes.ensure(dbytes.size() + 1));
   if (!dbytes.empty()) HIP_TRY(hipMemcpy(im.dfa_bytes.p, dbytes.data(), dbytes.size(), hipMemcpyHostToDevice));
+  HIP_TRY(im.nfa.ensure(nbytes.size() + 16));
+  if (!nbytes.empty()) HIP_TRY(hipMemcpy(im.nfa.p, nbytes.data(), nbytes.size(), hipMemcpyHostToDevice));
   HIP_TRY(im.follow_cls.ensure(fcls.size() + 1));
   if (!fcls.empty()) HIP_TRY(hipMemcpy(im.follow_cls.p, fcls.data(), fcls.size(), hipMemcpyHostToDevice));
   HIP_TRY(im.rule_path.ensure(rule_path.size() + 1));
@@ -3770,6 +3906,7 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   v.follow_cls = im.follow_cls.p;
   v.dfa_delta = im.dfa_delta.p;
   v.dfa_bytes = im.dfa_bytes.p;
+  v.nfa_bytes = im.nfa.p;
   v.progs = im.progs.p;
   v.prog_lit_off = im.prog_lit_off.p;
   v.prog_lits = im.prog_lits.p;
@@ -4139,14 +4276,6 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   hipLaunchKernelGGL(k_seg_total, dim3(1), dim3(64), 0, s, F);
   hipLaunchKernelGGL(k_find_finalize, dim3(lane_blocks), dim3(256), 0, s, F);
   HIP_TRY(hipGetLastError());
-  size_t tmp2 = 0;
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
-                                             (int)n_locs, 0, key_bits, s));
-  HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
-                                             (int)n_locs, 0, key_bits, s));
-  hipLaunchKernelGGL(k_find_gather, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->vals2.p, n_locs, e->f_rec2.p);
-  HIP_TRY(hipGetLastError());
   Ctrl c;
   if (int rc = read_ctrl(e, &c)) return rc;  // the arena size
   HIP_TRY(e->f_arena.ensure(c.find_bytes + 16));
@@ -4155,9 +4284,40 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
     hipLaunchKernelGGL(k_arena_fill, dim3((uint32_t)std::min<uint64_t>((c.find_bytes / 16 + 255) / 256 + 1, 8192)),
                        dim3(256), 0, s, F);
   HIP_TRY(hipGetLastError());
+  // order: (file, RuleID rank) major, Match prefix minor -- two stable radix
+  // sorts, least significant key first (f_lkey / f_lkey2 / f_lslot* are free now)
+  hipLaunchKernelGGL(k_match_prefix, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->f_arena.p, n_locs, e->f_lkey.p,
+                     e->f_lslot.p);
+  size_t tmp2 = 0;
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p, e->f_lslot2.p,
+                                             (int)n_locs, 0, 64, s));
+  HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p,
+                                             e->f_lslot2.p, (int)n_locs, 0, 64, s));
+  hipLaunchKernelGGL(k_gather_u64, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lslot2.p, n_locs, e->keys2.p);
+  tmp2 = 0;
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->keys2.p, e->keys.p, e->f_lslot2.p, e->vals2.p,
+                                             (int)n_locs, 0, key_bits, s));
+  HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys2.p, e->keys.p, e->f_lslot2.p, e->vals2.p,
+                                             (int)n_locs, 0, key_bits, s));
+  hipLaunchKernelGGL(k_find_gather, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->vals2.p, n_locs, e->f_rec2.p);
+  const uint64_t tie_cap = std::max<uint64_t>(1024, n_locs / 8);
+  HIP_TRY(e->f_ties.ensure(tie_cap));
+  hipLaunchKernelGGL(k_tie_list, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lkey.p, e->vals2.p, n_locs,
+                     e->f_ties.p, tie_cap, e->ctrl.p);
+  HIP_TRY(hipGetLastError());
+  // the kept locations as tsg_loc records
+  HIP_TRY(e->out_locs.ensure(n_locs));
+  hipLaunchKernelGGL(k_out_locs, dim3(lane_blocks), dim3(256), 0, s, e->locs2.p, n_locs, e->out_locs.p, e->ctrl.p);
+  HIP_TRY(hipGetLastError());
   auto& R = res->impl;
   const size_t rec_bytes = n_locs * sizeof(FindRec), code_bytes = n_slots * sizeof(CodeRec);
-  R.arena = pinned_get(e->pinned, rec_bytes + code_bytes + c.find_bytes + 1);
+  const size_t o_locs = (rec_bytes + code_bytes + c.find_bytes + 15) & ~(size_t)15;
+  const size_t o_flags = o_locs + n_locs * sizeof(tsg_loc);
+  const size_t o_ties = (o_flags + n_files + 15) & ~(size_t)15;
+  const size_t o_ctrl = (o_ties + tie_cap * 4 + 15) & ~(size_t)15;
+  R.arena = pinned_get(e->pinned, o_ctrl + sizeof(Ctrl));
   if (!R.arena) {
     set_last_error("hipHostMalloc failed for the findings arena");
     return TSG_ERR_DEVICE;
@@ -4166,10 +4326,17 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   R.frec = {(FindRec*)base, n_locs};
   R.code = {(CodeRec*)(base + rec_bytes), n_slots};
   R.strs = (const char*)(base + rec_bytes + code_bytes);
+  R.locs = {(tsg_loc*)(base + o_locs), n_locs};
+  R.file_flags = {base + o_flags, n_files};
+  R.ties = {(uint32_t*)(base + o_ties), 0};
+  R.ctrl_off = o_ctrl;
   HIP_TRY(hipMemcpyAsync(R.frec.p, e->f_rec2.p, rec_bytes, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(R.code.p, e->f_code.p, code_bytes, hipMemcpyDeviceToHost, s));
   if (c.find_bytes)
     HIP_TRY(hipMemcpyAsync(base + rec_bytes + code_bytes, e->f_arena.p, c.find_bytes, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(R.locs.p, e->out_locs.p, n_locs * sizeof(tsg_loc), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(R.ties.p, e->f_ties.p, tie_cap * 4, hipMemcpyDeviceToHost, s));
+  R.ties_cap = tie_cap;
   return TSG_OK;
 }
 
@@ -4177,7 +4344,7 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
 // ordered the records by (file, RuleID rank) keeping (file, start) order, so
 // only runs with an equal (file, RuleID) are ordered here, by Match and then
 // (rule, start, end) -- the order the reference's matches arrive in.
-void order_finding_ties(ResultImpl& R) {
+void order_finding_ties(ResultImpl& R, bool all_runs) {
   const uint8_t* A = (const uint8_t*)R.strs;
   auto less = [&](const FindRec& x, const FindRec& y) {
     const int c = memcmp(A + x.m_off, A + y.m_off, std::min(x.m_len, y.m_len));
@@ -4187,18 +4354,31 @@ void order_finding_ties(ResultImpl& R) {
     if (x.start != y.start) return x.start < y.start;
     return x.end < y.end;
   };
-  // runs of equal (file, RuleID): each is ordered on its own, so large
-  // results spread the runs over up to 16 host threads
+  // the device ordered (file, RuleID, Match prefix); runs of equal
+  // (file, RuleID, prefix) -- the positions k_tie_list flagged, each equal to
+  // its predecessor -- are ordered here, on up to 16 host threads when large
   std::vector<std::pair<size_t, size_t>> runs;
-  size_t i = 0, work = 0;
-  while (i < R.frec.size()) {
-    size_t j = i + 1;
-    while (j < R.frec.size() && R.frec[j].file == R.frec[i].file && R.frec[j].rank == R.frec[i].rank) ++j;
-    if (j - i > 1) {
-      runs.push_back({i, j});
-      work += j - i;
+  size_t work = 0;
+  if (all_runs) {  // the tie list overflowed: every run of equal (file, RuleID)
+    for (size_t i = 0; i < R.frec.size();) {
+      size_t j = i + 1;
+      while (j < R.frec.size() && R.frec[j].file == R.frec[i].file && R.frec[j].rank == R.frec[i].rank) ++j;
+      if (j - i > 1) {
+        runs.push_back({i, j});
+        work += j - i;
+      }
+      i = j;
     }
-    i = j;
+  } else {
+    std::vector<uint32_t> t(R.ties.p, R.ties.p + R.ties.n);
+    std::sort(t.begin(), t.end());
+    for (size_t k = 0; k < t.size();) {
+      size_t q = k + 1;
+      while (q < t.size() && t[q] == t[q - 1] + 1) ++q;
+      runs.push_back({(size_t)t[k] - 1, (size_t)t[q - 1] + 1});  // a run starts at its first flag's predecessor
+      work += q - k + 1;
+      k = q;
+    }
   }
   auto sort_run = [&](const std::pair<size_t, size_t>& r) {
     std::stable_sort(R.frec.begin() + r.first, R.frec.begin() + r.second, less);
@@ -4655,7 +4835,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     if (attempt == 0) {
       WarmRanges W{};
       auto add = [&](const void* ptr, uint64_t bytes) {
-        if (ptr && bytes && W.k < 8) {
+        if (ptr && bytes && W.k < 10) {
           W.p[W.k] = (const uint8_t*)ptr;
           W.n[W.k++] = bytes;
         }
@@ -4668,6 +4848,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
       add(im.dfa_delta.p, im.dfa_delta.n * 2);
       add(im.dfa_bytes.p, im.dfa_bytes.n);
       add(im.u32.p, im.u32.n * 4);
+      add(im.nfa.p, im.nfa.n);
       hipLaunchKernelGGL(k_warm, dim3(8 * kWarmParts), dim3(256), 0, s, W, (uint32_t*)e->nsel.p);
       HIP_TRY(hipGetLastError());
     }
@@ -4770,8 +4951,8 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   }
   HIP_TRY(hipEventRecord(e->ev[5], s));
   // ---- 6. exclude blocks (only when the config has any)
-  std::vector<DevLoc> hl(n_locs);
   if (n_locs && rs->any_exclude) {
+    std::vector<DevLoc> hl(n_locs);
     HIP_TRY(hipMemcpyAsync(hl.data(), e->locs.p, n_locs * sizeof(DevLoc), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     // tags: (file, 0) = global block, (file, rule+1) = that rule's block
@@ -4862,24 +5043,27 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(hipGetLastError());
     // ---- 8. findings (censored lines, Match, Code, order) on the device
     if ((rc = build_findings_dev(e, d_data, d_off, nbytes, nf, n_locs, res))) return rc;
-    hl.resize(n_locs);
-    HIP_TRY(hipMemcpyAsync(hl.data(), e->locs2.p, n_locs * sizeof(DevLoc), hipMemcpyDeviceToHost, s));
   }
   HIP_TRY(hipEventRecord(e->ev[7], s));
-  // per-file flags as bytes through pinned staging
+  auto& R = res->impl;
+  if (!n_locs) {  // no findings: the block holds the flags and the counters
+    R.arena = pinned_get(e->pinned, ((size_t)nf + 15) / 16 * 16 + sizeof(Ctrl));
+    if (!R.arena) {
+      set_last_error("hipHostMalloc failed for the result block");
+      return TSG_ERR_DEVICE;
+    }
+    R.file_flags = {(uint8_t*)R.arena->p, nf};
+    R.ctrl_off = ((size_t)nf + 15) / 16 * 16;
+  }
+  // per-file flags as bytes, and the counters, into the result's block
   if (nf) {
     HIP_TRY(e->fflags8.ensure(nf));
     hipLaunchKernelGGL(k_flags8, dim3((nf + 255) / 256), dim3(256), 0, s, e->file_flags.p, e->fflags8.p, nf);
     HIP_TRY(hipGetLastError());
-    if (e->h_flags_n < nf) {
-      if (e->h_flags) HIP_TRY(hipHostFree(e->h_flags));
-      e->h_flags = nullptr;
-      e->h_flags_n = 0;
-      HIP_TRY(hipHostMalloc((void**)&e->h_flags, (size_t)nf + (nf >> 2) + 64, hipHostMallocDefault));
-      e->h_flags_n = (size_t)nf + (nf >> 2) + 64;
-    }
-    HIP_TRY(hipMemcpyAsync(e->h_flags, e->fflags8.p, nf, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(R.file_flags.p, e->fflags8.p, nf, hipMemcpyDeviceToHost, s));
   }
+  Ctrl* hc = (Ctrl*)((uint8_t*)R.arena->p + R.ctrl_off);
+  HIP_TRY(hipMemcpyAsync(hc, e->ctrl.p, sizeof(Ctrl), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   const auto wall1 = std::chrono::steady_clock::now();
   for (int k = 0; k < 7; ++k) {
@@ -4905,27 +5089,21 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(hipEventElapsedTime(&ms, e->ev[10], e->ev[11]));
     tm[17] = ms;
   }
-  auto& R = res->impl;
-  R.file_flags.assign(e->h_flags, e->h_flags + nf);
-  R.locs.clear();
-  R.locs.reserve(hl.size());
-  for (auto& L : hl) {
-    if (L.flags & 1) {
-      set_last_error("secret group did not participate in the match (the Go reference panics here)");
-      return TSG_ERR_PANIC;
-    }
-    R.locs.push_back(tsg_loc{L.file, L.rule, L.start, L.end, L.start_line, L.end_line});
+  if (hc->n_panic) {
+    set_last_error("secret group did not participate in the match (the Go reference panics here)");
+    return TSG_ERR_PANIC;
   }
+  R.ties.n = n_locs ? (size_t)std::min<unsigned long long>(hc->n_ties, R.ties_cap) : 0;
 #ifdef TSG_EXPERIMENTS
   const auto wall_t = std::chrono::steady_clock::now();
 #endif
-  order_finding_ties(R);
+  order_finding_ties(R, hc->n_ties > R.ties_cap);
   R.have_findings = true;
   const auto wall2 = std::chrono::steady_clock::now();
 #ifdef TSG_EXPERIMENTS
-  fprintf(stderr, "[post] locs %.3f ms, tie order %.3f ms (%zu records)\n",
+  fprintf(stderr, "[post] locs %.3f ms, tie order %.3f ms (%zu records, %zu ties)\n",
           std::chrono::duration<double, std::milli>(wall_t - wall1).count(),
-          std::chrono::duration<double, std::milli>(wall2 - wall_t).count(), R.frec.size());
+          std::chrono::duration<double, std::milli>(wall2 - wall_t).count(), R.frec.size(), R.ties.n);
 #endif
   tm[15] = std::chrono::duration<double, std::milli>(wall2 - wall0).count();  // whole call, host clock
   tm[16] = std::chrono::duration<double, std::milli>(wall2 - wall1).count();  // host post-processing
@@ -5005,7 +5183,6 @@ void tsg_engine_free(tsg_engine* e) {
   e->scratch.release(); e->ctrl.release(); e->excl_jobs.release(); e->excl_out.release();
   e->nl_blocks.release(); e->nl_pre.release(); e->tail.release(); e->region_file.release(); e->region_tmp.release();
   e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->fold_pos.release(); e->caps.release(); e->caps_big.release(); e->vprof.release(); e->fflags8.release();
-  if (e->h_flags) (void)hipHostFree(e->h_flags);
   if (e->h_stage) (void)hipHostFree(e->h_stage);
   e->gate_out.release(); e->gate_rules.release(); e->bin8.release(); e->strip_out.release();
   e->strip_off.release(); e->blk_kept.release(); e->blk_base.release(); e->chunk_pos.release(); e->n_drop.release();
@@ -5013,6 +5190,7 @@ void tsg_engine_free(tsg_engine* e) {
   e->f_soff.release(); e->f_lslot.release(); e->f_lslot2.release(); e->f_lhead.release(); e->f_lscan.release();
   e->f_luid.release(); e->f_sfile.release(); e->f_sgrp.release(); e->f_grp.release();
   e->f_rec.release(); e->f_rec2.release(); e->f_code.release(); e->f_arena.release();
+  e->f_ties.release(); e->out_locs.release();
   if (e->events)
     for (auto& ev : e->ev) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(e->stream);

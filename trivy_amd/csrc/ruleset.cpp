@@ -495,7 +495,10 @@ int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_r
       else r.mode = c.anchor.valid ? MODE_ANCHORED : MODE_FULL;
       if (r.mode == MODE_ANCHORED) {
         build_follow(c, &r.follow);
-        build_dfa(c, &r.dfa);
+        // the verify DFA; past its state budget (or with \b, (?m) ^ $) the
+        // bit-parallel Glushkov NFA (nfa.cpp), and the Pike VM only when
+        // neither exists
+        if (!build_dfa(c, &r.dfa)) build_nfa(c, &r.nfa);
       }
       // implied gate: every anchor literal contains one of the rule's keywords
       // (so a hit proves MatchKeywords, scanner.go:169-181)
@@ -690,6 +693,21 @@ int tsg_ruleset_dfa_check(const tsg_ruleset* rs, size_t i, const uint8_t* text, 
   if (n_states) *n_states = d.valid ? d.nstates : 0;
   size_t e = 0;
   *result = dfa_anchored(d, text, len, s, &e);
+  if (me) *me = e;
+  return TSG_OK;
+}
+
+// Bit-parallel NFA of rule i on host text (nfa_walk_host): threads started
+// at every boundary in [s, inj_hi]; *result 1 = match (anchored: the only end
+// *me; unanchored: the first end), 0 = none, 2 = the Pike VM decides;
+// *n_pos = its positions (0 = the rule has no NFA).
+int tsg_ruleset_nfa_check(const tsg_ruleset* rs, size_t i, const uint8_t* text, size_t len, size_t s, size_t inj_hi,
+                          int* result, size_t* me, uint32_t* n_pos) {
+  if (!rs || i >= rs->rules.size() || !result || inj_hi < s) return TSG_ERR_INVALID_ARG;
+  const NfaHost& d = rs->rules[i].nfa;
+  if (n_pos) *n_pos = d.valid ? d.npos : 0;
+  size_t e = 0;
+  *result = nfa_walk_host(d, text, len, s, inj_hi, &e);
   if (me) *me = e;
   return TSG_OK;
 }
