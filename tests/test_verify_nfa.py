@@ -198,3 +198,70 @@ def test_gpu_nfa_rules_vs_oracle(tmp_path):
         seen |= {f["RuleID"] for f in want["Findings"]}
         assert _canon(_plain(g)) == _canon(want), p
     assert len(seen) >= 10, seen
+
+
+def _rune_starts(t: bytes):
+    s = t.decode("utf-8", "surrogateescape")
+    out, b = [], 0
+    for ch in s:
+        out.append(b)
+        cp = ord(ch)
+        b += 1 if (0xDC80 <= cp <= 0xDCFF or cp < 0x80) else 2 if cp < 0x800 else 3 if cp < 0x10000 else 4
+    return out
+
+
+def test_nfa_rune_symbols_equal_oracle():
+    """Non-ASCII text (é, K U+212A, ſ U+017F, İ, U+FFFD, invalid bytes, 4-byte
+    runes): the walk decodes runes into the five symbols; FindAll over rune
+    starts equals the oracle's, the oracle deciding the starts the walk
+    leaves undecided."""
+    pats = PATTERNS + [r"(?i)\bsk[a-z]{2}\b", r"(?i)(?:k|x)*kk\w{2}\b", r"\b[^\x00-\x7f]{2}x\b", r"\bq.{2}q\b"]
+    sc = _scanner(pats)
+    rs = sc._rs.handle
+    rng = random.Random(29)
+    base = _texts(rng)
+    extra = [x.encode() for x in ["é", "K", "ſ", "İ", "\ufffd", "\U0001F600"]] + [b"\xff", b"\x80", b"\xe2\x82"]
+    texts = []
+    for t in base[:60]:
+        for _ in range(rng.randint(1, 4)):
+            p = rng.randrange(len(t) + 1)
+            t = t[:p] + rng.choice(extra) + t[p:]
+        texts.append(t)
+    texts += ["SKab skaß KKk9 ſKab qéxq qééq éé x ÿÿx".encode(), b"q\xff\xfeq \xc3\xa9\xc3\xa9x kk\xe2\x84\xaaab"]
+    res, me, npos = ctypes.c_int(), ctypes.c_size_t(), ctypes.c_uint32()
+    decided = vm = total = 0
+    for i, pat in enumerate(pats):
+        if not _npos(rs, i):
+            continue
+        orx = O.GoRegexp(pat)
+        for t in texts:
+            want = orx.find_all_index(t)
+            ds, off = O._decode(t)
+            idx = {int(b): k for k, b in enumerate(off)}
+            starts = _rune_starts(t)
+            got, pos, n = [], 0, len(t)
+            while True:
+                hit = None
+                for s in starts:
+                    if s < pos:
+                        continue
+                    N.check(N.lib.tsg_ruleset_nfa_check(rs, i, t, n, s, s, ctypes.byref(res), ctypes.byref(me),
+                                                        ctypes.byref(npos)))
+                    if res.value == 2:
+                        vm += 1
+                        m = orx.rx.match(ds, idx[s])
+                        if m:
+                            hit = (s, int(off[m.end()]))
+                            break
+                        continue
+                    decided += 1
+                    if res.value == 1:
+                        hit = (s, me.value)
+                        break
+                if hit is None:
+                    break
+                got.append(list(hit))
+                pos = hit[1]
+            assert got == want, (pat, t[:160])
+            total += len(want)
+    assert total > 50 and decided > 20 * max(1, vm), (total, decided, vm)

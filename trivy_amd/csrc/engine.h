@@ -197,6 +197,11 @@ struct NfaDev {
   U128 first_c[kNfaMaxCond], last_c[kNfaMaxCond];
   uint32_t first_r[kNfaMaxCond], last_r[kNfaMaxCond];  // required EmptyOp flags of each conditional mask
   uint32_t has_cond, bytes, o_reach, o_exc;             // bytes: the whole record
+  // decoded non-ASCII runes (utf8.DecodeRune; an invalid byte is U+FFFD of
+  // width 1) as dfa.cpp's five rune symbols: K, ſ, İ, U+FFFD, any other --
+  // the last only when every position treats all other runes alike (na_ok)
+  U128 reach_sym[kDfaRuneSyms];
+  uint32_t na_ok, pad_[3];
   uint8_t cls[128];                                      // ASCII byte -> reach class
   uint8_t exc_of[kNfaMaxPos];                            // position -> exception record (kNfaNoExc: none)
 };

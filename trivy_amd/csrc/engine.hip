@@ -4919,14 +4919,19 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
                   (unsigned long long)cands(by[q]), dur(by[q]) / 1e5, (unsigned long long)(hp[2 * by[q] + 1] & 1));
       }
       std::map<uint32_t, std::pair<uint64_t, uint64_t>> per_rule;
+      std::map<uint32_t, std::pair<uint64_t, uint64_t>> per_rule_n;  // jobs, DFA / NFA steps
       for (uint32_t q = 0; q < n_jobs; ++q) {
         auto& pr = per_rule[(uint32_t)(hp[2 * q + 1] >> 32)];
         pr.first += dur(q);
         pr.second = std::max<uint64_t>(pr.second, dur(q));
+        auto& pn = per_rule_n[(uint32_t)(hp[2 * q + 1] >> 32)];
+        pn.first += 1;
+        pn.second += (hp[2 * q + 1] & 0xFFFFFFFFull) >> 1;
       }
       for (auto& kv : per_rule)
-        fprintf(stderr, "[verify] rule %s total %.3f ms max %.3f ms\n", rs->rules[kv.first].id.c_str(),
-                kv.second.first / 1e5, kv.second.second / 1e5);
+        fprintf(stderr, "[verify] rule %s total %.3f ms max %.3f ms jobs %llu steps %llu\n",
+                rs->rules[kv.first].id.c_str(), kv.second.first / 1e5, kv.second.second / 1e5,
+                (unsigned long long)per_rule_n[kv.first].first, (unsigned long long)per_rule_n[kv.first].second);
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(&n_jobs, e->nsel.p, 4, hipMemcpyDeviceToHost, s));  // (read by read_ctrl's sync)

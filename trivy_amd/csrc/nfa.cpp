@@ -56,6 +56,58 @@ bool consumes_ascii(const gre::Prog& p, const Inst& in, int c) {
   return false;
 }
 
+// Non-ASCII rune symbols (dfa.cpp's): K, ſ, İ, U+FFFD, then "any other rune".
+constexpr uint32_t kSymRune[kDfaRuneSyms - 1] = {0x212A, 0x17F, 0x130, 0xFFFD};
+
+bool class_has(const gre::Prog& p, const gre::ClassDesc& cd, uint32_t r) {
+  for (uint32_t k = 0; k < cd.nranges; ++k)
+    if (p.ranges[cd.range_off + 2 * k] <= r && r <= p.ranges[cd.range_off + 2 * k + 1]) return true;
+  return false;
+}
+
+bool consumes_rune(const gre::Prog& p, const Inst& in, uint32_t r) {
+  switch (in.op) {
+    case gre::I_RUNE: return class_has(p, p.classes[in.arg], r);
+    case gre::I_RUNE1: return in.arg == r;
+    case gre::I_ANY:
+    case gre::I_ANYNL: return true;
+  }
+  return false;
+}
+
+// Non-ASCII runes other than kSymRune an instruction consumes: 0 none, -1 all,
+// 1 some (then "other" is not one symbol for this program).
+int other_runes(const gre::Prog& p, const Inst& in) {
+  auto in_dom = [](uint64_t r) { return r >= 0x80 && r <= 0x10FFFF && !(r >= 0xD800 && r <= 0xDFFF); };
+  const uint64_t dom = (0x10FFFF - 0x80 + 1) - 0x800 - (kDfaRuneSyms - 1);
+  switch (in.op) {
+    case gre::I_ANY:
+    case gre::I_ANYNL: return -1;
+    case gre::I_RUNE1: {
+      if (!in_dom(in.arg)) return 0;
+      for (uint32_t r : kSymRune)
+        if (r == in.arg) return 0;
+      return 1;
+    }
+    case gre::I_RUNE: {
+      const gre::ClassDesc& cd = p.classes[in.arg];
+      uint64_t cnt = 0;
+      for (uint32_t k = 0; k < cd.nranges; ++k) {
+        const uint64_t lo = std::max<uint64_t>(p.ranges[cd.range_off + 2 * k], 0x80);
+        const uint64_t hi = std::min<uint64_t>(p.ranges[cd.range_off + 2 * k + 1], 0x10FFFF);
+        if (lo > hi) continue;
+        cnt += hi - lo + 1;
+        const uint64_t slo = std::max<uint64_t>(lo, 0xD800), shi = std::min<uint64_t>(hi, 0xDFFF);
+        if (slo <= shi) cnt -= shi - slo + 1;
+        for (uint32_t r : kSymRune)
+          if (r >= lo && r <= hi && in_dom(r)) --cnt;
+      }
+      return cnt == 0 ? 0 : cnt == dom ? -1 : 1;
+    }
+  }
+  return 0;
+}
+
 constexpr int kMatchTarget = -2;
 
 // Epsilon closure from pc0: every (target, required EmptyOp flags) pair, the
@@ -261,6 +313,16 @@ bool build_nfa(const gre::Compiled& c, NfaHost* out) {
     N.cls[ch] = (uint8_t)it->second;
   }
   N.ncls = (uint32_t)reach.size();
+  // non-ASCII rune symbols
+  N.na_ok = 1;
+  for (uint32_t i = 0; i < m; ++i) {
+    const Inst& in = p.inst[pcs[i]];
+    for (uint32_t j = 0; j + 1 < kDfaRuneSyms; ++j)
+      if (consumes_rune(p, in, kSymRune[j])) set_bit(N.reach_sym[j], (int)i);
+    const int o = other_runes(p, in);
+    if (o == -1) set_bit(N.reach_sym[kDfaRuneSyms - 1], (int)i);
+    if (o == 1) N.na_ok = 0;
+  }
   N.o_reach = (uint32_t)sizeof(NfaDev);
   N.o_exc = N.o_reach + N.ncls * (uint32_t)sizeof(U128);
   N.bytes = N.o_exc + N.n_exc * (uint32_t)sizeof(NfaExc);

@@ -9,9 +9,10 @@
 //      | first                                        (a thread starts at q)
 //   D' = F & reach[cls[c]]
 // A match ends at boundary q when D meets `last` (edges to MATCH; the
-// conditional ones with the EmptyOp context at q).  The walk is over ASCII
-// only: a byte >= 0x80 ends it as undecidable, and the Pike VM decides (as for
-// the verify DFA, dfa.cpp).
+// conditional ones with the EmptyOp context at q).  Non-ASCII text is decoded
+// rune by rune (utf8.DecodeRune) into dfa.cpp's five rune symbols; a rune the
+// symbols cannot stand for (a program telling other runes apart) ends the walk
+// as undecidable, and the Pike VM decides.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -67,12 +68,53 @@ __host__ __device__ inline U128 nfa_follow(const NfaDev& N, const NfaExc* exc, U
 
 __host__ __device__ inline int nfa_ctx_rune(uint32_t b) { return b < 0x80 ? (int)b : 0xFFFD; }
 
-// From s, threads injected at every boundary in [s, inj_hi] (text[0..n)).
-// Anchored (inj_hi == s): 1 = the match from s ends at *me and nowhere else,
-// 0 = no match from s, 2 = undecidable here (a byte >= 0x80 to consume, a
-// second match end -- Go's priorities pick among them -- or kNfaWalkMax).
-// Unanchored: 1 = some thread reaches a match (*me = the first end), 0 = none,
-// 2 = undecidable.
+// utf8.DecodeRune at i (text[i] >= 0x80) through the walk's byte accessor:
+// the rune symbol (0 K, 1 ſ, 2 İ, 3 U+FFFD, 4 any other rune) and its width.
+template <class Text>
+__host__ __device__ inline uint32_t nfa_rune_sym(Text& t, uint32_t n, uint32_t i, uint32_t* w) {
+  const uint32_t c0 = t[i];
+  uint32_t need, lo = 0x80, hi = 0xBF;
+  *w = 1;
+  if (c0 >= 0xC2 && c0 <= 0xDF) {
+    need = 2;
+  } else if (c0 >= 0xE0 && c0 <= 0xEF) {
+    need = 3;
+    if (c0 == 0xE0) lo = 0xA0;
+    if (c0 == 0xED) hi = 0x9F;
+  } else if (c0 >= 0xF0 && c0 <= 0xF4) {
+    need = 4;
+    if (c0 == 0xF0) lo = 0x90;
+    if (c0 == 0xF4) hi = 0x8F;
+  } else {
+    return 3;
+  }
+  if (i + need > n) return 3;
+  const uint32_t c1 = t[i + 1];
+  if (c1 < lo || c1 > hi) return 3;
+  uint32_t r;
+  if (need == 2) {
+    r = ((c0 & 0x1F) << 6) | (c1 & 0x3F);
+  } else {
+    const uint32_t c2 = t[i + 2];
+    if (c2 < 0x80 || c2 > 0xBF) return 3;
+    if (need == 3) {
+      r = ((c0 & 0x0F) << 12) | ((c1 & 0x3F) << 6) | (c2 & 0x3F);
+    } else {
+      const uint32_t c3 = t[i + 3];
+      if (c3 < 0x80 || c3 > 0xBF) return 3;
+      r = 0x10000;  // (no rune symbol lies past the BMP)
+    }
+  }
+  *w = need;
+  return r == 0x212A ? 0u : r == 0x17F ? 1u : r == 0x130 ? 2u : r == 0xFFFD ? 3u : 4u;
+}
+
+// From s (a rune boundary), threads injected at every rune boundary in
+// [s, inj_hi] (text[0..n)).  Anchored (inj_hi == s): 1 = the match from s
+// ends at *me and nowhere else, 0 = no match from s, 2 = undecidable here (a
+// rune the symbols do not cover, a second match end -- Go's priorities pick
+// among them -- or kNfaWalkMax).  Unanchored: 1 = some thread reaches a match
+// (*me = the first end), 0 = none, 2 = undecidable.
 template <bool kWide, class Text>
 __host__ __device__ inline int nfa_walk(const NfaDev& N, const U128* reach, const NfaExc* exc, Text text, uint32_t n,
                                         uint32_t s, uint32_t inj_hi, uint32_t* me, uint32_t* steps) {
@@ -80,7 +122,7 @@ __host__ __device__ inline int nfa_walk(const NfaDev& N, const U128* reach, cons
   uint32_t nacc = 0, e = 0;
   const bool anchored = inj_hi == s;
   int prev = s ? nfa_ctx_rune(text[s - 1]) : -1;
-  for (uint32_t q = s;; ++q) {
+  for (uint32_t q = s;;) {
     const uint32_t c = q < n ? (uint32_t)text[q] : 0u;
     const int next = q < n ? nfa_ctx_rune(c) : -1;
     const uint32_t ctx = N.has_cond ? gre::empty_ctx(prev, next) : 0u;
@@ -100,15 +142,25 @@ __host__ __device__ inline int nfa_walk(const NfaDev& N, const U128* reach, cons
     const bool inj = q <= inj_hi;
     if (!inj && !u128_any(D)) break;
     if (q >= n) break;
-    if (c >= 0x80 || q - s >= kNfaWalkMax) return 2;
+    if (q - s >= kNfaWalkMax) return 2;
+    uint32_t w = 1;
+    U128 R;
+    if (c < 0x80) {
+      R = reach[N.cls[c]];
+    } else {  // a decoded rune: one of the symbols (the context sees a non-word, non-newline rune)
+      const uint32_t j = nfa_rune_sym(text, n, q, &w);
+      if (j == kDfaRuneSyms - 1 && !N.na_ok) return 2;
+      R = N.reach_sym[j];
+    }
     U128 F = nfa_follow<kWide>(N, exc, D, ctx);
     if (inj) {
       F = u128_or(F, N.first_u);
       for (uint32_t k = 0; k < N.n_first_c; ++k)
         if ((N.first_r[k] & ~ctx) == 0) F = u128_or(F, N.first_c[k]);
     }
-    D = u128_and(F, reach[N.cls[c]]);
-    prev = (int)c;
+    D = u128_and(F, R);
+    prev = nfa_ctx_rune(c);
+    q += w;
     ++*steps;
   }
   if (!nacc) return 0;
