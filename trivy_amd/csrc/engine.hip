@@ -102,6 +102,8 @@ struct Ctrl {
   unsigned long long long_files; // files longer than kMaxVerifyFile (k_region_mark)
   unsigned long long n_panic;    // kept locations whose secret group did not participate (k_out_locs)
   unsigned long long n_ties;     // findings whose (file, RuleID, Match prefix) equals the previous one's
+  unsigned long long n_redo;     // speculative job chains re-run from a conflict (k_chain_fix)
+  unsigned long long n_dropped;  // locations of the conflicting speculative jobs (k_drop_spec)
 };
 
 struct DevLoc {
@@ -110,7 +112,7 @@ struct DevLoc {
   uint64_t start, end;
   uint32_t start_line, end_line;
   uint32_t flags;  // 1 = secret group did not participate (reference panics)
-  uint32_t pad;
+  uint32_t job;    // the verify job that found it (kJobRedo | job: a re-run chain's)
 };
 
 // k_scan_big's LDS blob (automata too large for one LDS table): the byte
@@ -1763,6 +1765,26 @@ __device__ inline bool follow_accepts_dev(const RuleSetDev& rs, const RuleDev& r
   return true;
 }
 
+// The backward half of the candidate filter: every match [s, e) holding the
+// anchor literal at h has h - s >= off_min and [s, h) inside the anchor
+// alphabet (gre::Anchor), so the off_min bytes right before a hit must all be
+// alphabet bytes (and lie in the file) -- else no match can contain it.  (The
+// explosion-rule family `(?:x|y)*x(?:x|y){k}lit` anchors on lit with
+// off_min = k + 1: almost every occurrence of lit fails this.)  The first
+// kPrecedeMax bytes are checked.
+constexpr uint32_t kPrecedeMax = 64;
+__device__ inline bool precede_accepts_dev(const RuleDev& rd, const uint8_t* data, uint64_t h, uint64_t fstart) {
+  const uint32_t a = rd.off_min;
+  if (a == 0) return true;
+  if (h - fstart < a) return false;
+  const uint32_t k = a < kPrecedeMax ? a : kPrecedeMax;
+  for (uint32_t i = 1; i <= k; ++i) {
+    const uint8_t c = data[h - i];
+    if (!((rd.alpha[c >> 6] >> (c & 63)) & 1)) return false;
+  }
+  return true;
+}
+
 __device__ inline void emit_cand(const ExpandParams& E, uint32_t rule, uint64_t gpos, uint32_t val) {
   unsigned long long idx = atomicAdd(&E.ctrl->cands, 1ull);
   if (idx < E.cand_cap) {
@@ -1794,6 +1816,7 @@ __global__ __launch_bounds__(256) void k_expand(ExpandParams E) {
     // a K/ſ spelling does not (ToLower(ſ) == ſ)
     if ((fold || !rd.gate_implied) && !rule_gate(E.rs, rd, kw)) continue;
     if (!follow_accepts_dev(E.rs, rd, E.data, gpos, fend)) continue;
+    if (!precede_accepts_dev(rd, E.data, gpos, E.off[fi])) continue;
     emit_cand(E, r, gpos, fi);
   }
 }
@@ -1822,12 +1845,17 @@ __global__ __launch_bounds__(256) void k_full_jobs(ExpandParams E) {
 // no '\n' (unbounded ones too: JWTs, `{17,}` tokens) keeps every match inside
 // one line, so a run is also split where a newline lies between the previous
 // hit and the next hit's start window (found within kNlSplitScan bytes).
+constexpr uint8_t kSplitHard = 1, kSplitSoft = 2;
+// Every other gap between candidates whose start windows cannot overlap is a
+// soft split (kSplitSoft): the jobs on both sides run in parallel and
+// k_chain_fix checks that FindAll's sequence was not broken there.
 constexpr uint32_t kNlSplitScan = 512;
+constexpr uint32_t kSoftGapUnbounded = 64;  // soft-split gap for rules with an unbounded window
 __global__ void k_mark_jobs(const uint64_t* keys, const uint32_t* vals, uint64_t n, const RuleDev* rules,
                             const uint8_t* data, uint8_t* flags) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint8_t f = 1;
+  uint8_t f = kSplitHard;
   if (i > 0) {
     const uint32_t r = (uint32_t)(keys[i] >> kPosBits);
     f = (r != (uint32_t)(keys[i - 1] >> kPosBits)) || ((vals[i] & ~kFullFlag) != (vals[i - 1] & ~kFullFlag));
@@ -1843,12 +1871,35 @@ __global__ void k_mark_jobs(const uint64_t* keys, const uint32_t* vals, uint64_t
         const uint64_t end = lim < h0 + kNlSplitScan ? lim : h0 + kNlSplitScan;
         for (uint64_t q = h0; q < end && !f; ++q) f = data[q] == '\n';
       }
+      if (!f) {
+        const uint64_t gap = rd.off_max == gre::kInf ? kSoftGapUnbounded : (uint64_t)(rd.off_max - rd.off_min) + 8;
+        if (h1 - h0 > gap) f = kSplitSoft;
+      }
     }
   }
   flags[i] = f;
 }
 
 // ----------------------------------------------------------------- verify --
+// A secret-group capture job (k_captures): a kept match [ms, me) of a group
+// rule, with the verify job that found it (speculative-job bookkeeping).
+struct CapJob {
+  uint32_t file, rule, job, pad;
+  uint64_t ms, me;
+};
+
+// Speculative job chains: a run of candidates of one (file, rule) is cut into
+// jobs that are verified in parallel, each as if FindAll began at its first
+// window; k_chain_fix then checks, job by job in order, that a job's first
+// match starts at or after the previous match's end -- then the job's result
+// equals the sequential one (FindAll would have tested the same starts) --
+// and re-runs a chain sequentially from the first job where that fails.
+constexpr uint32_t kJobRedo = 0x80000000u;  // DevLoc::job / CapJob::job of a re-run chain's output
+struct RedoRec {
+  uint32_t job, last;  // jobs [job, last] of one chain, re-run in order
+  uint64_t pos;        // FindAll's search position at `job` (file-relative)
+};
+
 struct VerifyParams {
   const uint8_t* data;
   const uint64_t* off;
@@ -1865,11 +1916,20 @@ struct VerifyParams {
   uint64_t scratch_stride;
   uint64_t* prof;  // diagnostics (TSG_PROFILE_VERIFY): per job {duration | end (100 MHz), rule << 32 | full}
   uint32_t* tck;   // diagnostics: per job, 100 MHz ticks spent in DFA walks / in emit_match
-  uint4* caps;     // capture jobs {file, rule, ms, me} for k_captures
+  CapJob* caps;     // capture jobs for k_captures
   uint64_t cap_cap;
-  uint4* caps_big; // those too long for its arenas, for k_captures_big
+  CapJob* caps_big; // those too long for its arenas, for k_captures_big
   uint64_t cap_big_cap;
   const uint8_t* span_hi;  // k_scan_fast's per-span ">= 0x80 occurs" flags (nullptr: not computed)
+  // speculative jobs: per job the first match start / last match end
+  // (file-relative; ~0 / 0 = no match), the split kind at each job start
+  // (flags8 of its first candidate), the conflicting jobs, the re-runs
+  uint64_t* job_fms;
+  uint64_t* job_lme;
+  const uint8_t* split;
+  uint8_t* job_bad;
+  RedoRec* redo;
+  uint64_t redo_cap;
 };
 
 // Candidate start windows of one (file, rule) job, in increasing order
@@ -2173,9 +2233,9 @@ __device__ bool bitstate_captures(const gre::ProgView& p, const uint8_t* text, u
 // of `words` words; a match too long for it goes on to the next stage's list
 // (`next`, k_captures -> k_captures_big), and only past the last arena does
 // the capture VM run.
-__device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t rule, uint32_t fi,
+__device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t rule, uint32_t fi, uint32_t job,
                             const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me, gre::VmScratch& sc,
-                            uint32_t* bs_area, uint32_t words, uint4* next, uint64_t next_cap,
+                            uint32_t* bs_area, uint32_t words, CapJob* next, uint64_t next_cap,
                             unsigned long long* next_n) {
   const gre::ProgView& pv = V.rs.progs[rd.prog];
   const uint32_t* gnum = V.rs.group_slots + rd.group_off;
@@ -2183,7 +2243,7 @@ __device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t r
   const bool bs_ok = bitstate_captures(pv, text, n, ms, me, gnum, rd.group_n, bs_area, words, gcap);
   if (!bs_ok && next) {
     const unsigned long long idx = atomicAdd(next_n, 1ull);
-    if (idx < next_cap) next[idx] = make_uint4(fi, rule, ms, me);
+    if (idx < next_cap) next[idx] = CapJob{fi, rule, job, 0, ms, me};
     return;
   }
   if (bs_ok) {
@@ -2191,8 +2251,8 @@ __device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t r
       const int32_t s = gcap[2 * g], e = gcap[2 * g + 1];
       unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
       if (idx < V.loc_cap) {
-        if (s < 0 || e < 0) V.locs[idx] = DevLoc{fi, rule, 0, 0, 0, 0, 1, 0};
-        else V.locs[idx] = DevLoc{fi, rule, (uint64_t)s, (uint64_t)e, 0, 0, 0, 0};
+        if (s < 0 || e < 0) V.locs[idx] = DevLoc{fi, rule, 0, 0, 0, 0, 1, job};
+        else V.locs[idx] = DevLoc{fi, rule, (uint64_t)s, (uint64_t)e, 0, 0, 0, job};
       }
     }
     return;
@@ -2205,8 +2265,8 @@ __device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t r
     const int32_t s = out[2 * slot], e = out[2 * slot + 1];
     unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
     if (idx < V.loc_cap) {
-      if (s < 0 || e < 0) V.locs[idx] = DevLoc{fi, rule, 0, 0, 0, 0, 1, 0};
-      else V.locs[idx] = DevLoc{fi, rule, (uint64_t)s, (uint64_t)e, 0, 0, 0, 0};
+      if (s < 0 || e < 0) V.locs[idx] = DevLoc{fi, rule, 0, 0, 0, 0, 1, job};
+      else V.locs[idx] = DevLoc{fi, rule, (uint64_t)s, (uint64_t)e, 0, 0, 0, job};
     }
   }
 }
@@ -2214,8 +2274,8 @@ __device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t r
 // A match k_verify found: allow rules, then the whole-match location or, for
 // rules with a secret group, a capture job for k_captures (whose bit-state
 // arenas take LDS that would cap the search at one wave per CU).
-__device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, uint32_t fi, const uint8_t* text,
-                                        uint32_t n, uint32_t ms, uint32_t me, gre::VmScratch& sc,
+__device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, uint32_t fi, uint32_t job,
+                                        const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me, gre::VmScratch& sc,
                                         uint32_t* tck = nullptr) {
   const uint64_t t0 = tck ? __builtin_amdgcn_s_memrealtime() : 0;
   const RuleDev& rd = V.rs.rules[rule];
@@ -2230,7 +2290,7 @@ __device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, ui
     if (match_string_pf(V.rs, V.rs.allow_progs[allow_off + k], text + ms, me - ms, sc)) return;
   if (!rd.use_groups) {
     unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
-    if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, ms, me, 0, 0, 0, 0};
+    if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, ms, me, 0, 0, 0, job};
     return;
   }
   if (rd.grp_fast) {  // the group's span follows from [ms, me) on ASCII text (gre::group_span)
@@ -2249,14 +2309,14 @@ __device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, ui
       const int64_t ge = rd.grp_suf >= 0 ? (int64_t)me - rd.grp_suf : gs + rd.grp_len;
       if (gs >= (int64_t)ms && gs <= ge && ge <= (int64_t)me) {
         unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
-        if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, (uint64_t)gs, (uint64_t)ge, 0, 0, 0, 0};
+        if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, (uint64_t)gs, (uint64_t)ge, 0, 0, 0, job};
         return;
       }
       // (unreachable for a real match of the rule; the capture search decides)
     }
   }
   unsigned long long idx = atomicAdd(&V.ctrl->n_caps, 1ull);
-  if (idx < V.cap_cap) V.caps[idx] = make_uint4(fi, rule, ms, me);
+  if (idx < V.cap_cap) V.caps[idx] = CapJob{fi, rule, job, 0, ms, me};
 }
 
 // Capture stages: a fixed grid walks the list the previous stage filled,
@@ -2273,19 +2333,20 @@ __global__ __launch_bounds__(kLanes) void k_captures(VerifyParams V) {
   const uint32_t nthreads = gridDim.x * kActive;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   gre::VmScratch sc = make_scratch(V.scratch + (uint64_t)t * V.scratch_stride, V.rs);
-  const uint4* list = kLast ? V.caps_big : V.caps;
+  const CapJob* list = kLast ? V.caps_big : V.caps;
   const unsigned long long cnt = kLast ? V.ctrl->n_caps_big : V.ctrl->n_caps;
   const uint64_t cap = kLast ? V.cap_big_cap : V.cap_cap;
   const uint64_t n_caps = cnt < cap ? cnt : cap;
   // job i -> block i % grid, lane i / grid: a short list spreads over every CU
   // (few divergent lanes per wave) instead of filling the first waves
   for (uint64_t i = blockIdx.x + (uint64_t)threadIdx.x * gridDim.x; i < n_caps; i += nthreads) {
-    const uint4 c = list[i];
-    const RuleDev rd = V.rs.rules[c.y];
-    const uint64_t fstart = V.off[c.x];
-    const uint32_t n = (uint32_t)(V.off[c.x + 1] - 1 - fstart);
-    emit_groups(V, rd, c.y, c.x, V.data + fstart, n, c.z, c.w, sc, bs_area, kWords, kLast ? nullptr : V.caps_big,
-                V.cap_big_cap, &V.ctrl->n_caps_big);
+    const CapJob c = list[i];
+    if (!(c.job & kJobRedo) && V.job_bad[c.job]) continue;  // a conflicting speculative job's match
+    const RuleDev rd = V.rs.rules[c.rule];
+    const uint64_t fstart = V.off[c.file];
+    const uint32_t n = (uint32_t)(V.off[c.file + 1] - 1 - fstart);
+    emit_groups(V, rd, c.rule, c.file, c.job, V.data + fstart, n, (uint32_t)c.ms, (uint32_t)c.me, sc, bs_area, kWords,
+                kLast ? nullptr : V.caps_big, V.cap_big_cap, &V.ctrl->n_caps_big);
   }
 }
 
@@ -2327,8 +2388,8 @@ constexpr uint32_t kVerifyBlock = 64;
 constexpr uint32_t kVerifyBlockWide = 256;
 
 // regexp.go allMatches over the whole file (rules without an anchor)
-__device__ __noinline__ void verify_full_job(const VerifyParams& V, uint32_t rule, uint32_t fi, const uint8_t* text,
-                                             uint32_t n, gre::VmScratch& sc) {
+__device__ __noinline__ void verify_full_job(const VerifyParams& V, uint32_t rule, uint32_t fi, uint32_t job,
+                                             const uint8_t* text, uint32_t n, gre::VmScratch& sc) {
   const gre::ProgView& pv = V.rs.progs[V.rs.rules[rule].prog];
   uint32_t pos = 0, ms, me;
   int64_t prev_end = -1;
@@ -2345,8 +2406,17 @@ __device__ __noinline__ void verify_full_job(const VerifyParams& V, uint32_t rul
       pos = me;
     }
     prev_end = me;
-    if (accept) emit_match(V, rule, fi, text, n, ms, me, sc);
+    if (accept) emit_match(V, rule, fi, job, text, n, ms, me, sc);
   }
+}
+
+// A job's first match start and last match end (every match FindAll took,
+// allow-listed ones included: they move its position all the same), for
+// k_chain_fix; a re-run chain (kJobRedo) records nothing.
+__device__ inline void job_record(const VerifyParams& V, uint32_t job, uint32_t fms, uint32_t lme) {
+  if (job & kJobRedo) return;
+  V.job_fms[job] = fms == 0xFFFFFFFFu ? ~0ull : (uint64_t)fms;
+  V.job_lme[job] = lme;
 }
 
 __device__ inline void iv_init(IvIter& it, const VerifyParams& V, uint32_t rule, uint64_t c0, uint64_t c1,
@@ -2370,10 +2440,10 @@ __device__ inline void iv_init(IvIter& it, const VerifyParams& V, uint32_t rule,
 // start (>= pos) that matches is Go's leftmost match; a start the DFA cannot
 // decide (byte >= 0x80) is decided by the Pike VM alone, anchored there.
 template <bool kLds>
-__device__ __noinline__ uint32_t verify_dfa_job(const VerifyParams& V, uint32_t rule, uint32_t fi, uint64_t c0,
-                                                uint64_t c1, uint64_t fstart, const uint8_t* text, uint32_t n,
-                                                gre::VmScratch& sc, const uint16_t* lds_T, const uint8_t* lds_cls,
-                                                uint32_t* tck) {
+__device__ __noinline__ uint32_t verify_dfa_job(const VerifyParams& V, uint32_t rule, uint32_t fi, uint32_t job,
+                                                uint32_t pos0, uint64_t c0, uint64_t c1, uint64_t fstart,
+                                                const uint8_t* text, uint32_t n, gre::VmScratch& sc,
+                                                const uint16_t* lds_T, const uint8_t* lds_cls, uint32_t* tck) {
   uint32_t steps = 0;  // DFA transitions taken (diagnostics)
   uint32_t tck_dfa = 0, tck_emit = 0;
   const RuleDev& rd = V.rs.rules[rule];
@@ -2383,7 +2453,8 @@ __device__ __noinline__ uint32_t verify_dfa_job(const VerifyParams& V, uint32_t 
   const uint32_t prog = rd.prog;
   IvIter it;
   iv_init(it, V, rule, c0, c1, fstart, text, n);
-  uint32_t pos = 0, ms, me;
+  uint32_t pos = pos0, ms, me, fms = 0xFFFFFFFFu, lme = 0;
+  while (it.have && it.ce < pos) it.advance();
   while (it.have) {
     bool found = false;
     const uint32_t s0 = it.cs > pos ? it.cs : pos;
@@ -2401,8 +2472,10 @@ __device__ __noinline__ uint32_t verify_dfa_job(const VerifyParams& V, uint32_t 
       }
       if (r == 1) {
         const uint64_t tb = tck ? __builtin_amdgcn_s_memrealtime() : 0;
-        emit_match(V, rule, fi, text, n, sp, me, sc, tck);
+        emit_match(V, rule, fi, job, text, n, sp, me, sc, tck);
         if (tck) tck_emit += (uint32_t)(__builtin_amdgcn_s_memrealtime() - tb);
+        if (fms == 0xFFFFFFFFu) fms = sp;
+        lme = me;
         pos = me;
         found = true;
         break;
@@ -2412,22 +2485,27 @@ __device__ __noinline__ uint32_t verify_dfa_job(const VerifyParams& V, uint32_t 
     else while (it.have && it.ce < pos) it.advance();
   }
   if (tck) { tck[0] = tck_dfa; tck[1] = tck_emit; }
+  job_record(V, job, fms, lme);
   return steps;
 }
 
 // The same FindAll with the Pike VM (rules without a verify DFA)
-__device__ __noinline__ void verify_vm_job(const VerifyParams& V, uint32_t rule, uint32_t fi, uint64_t c0, uint64_t c1,
-                                           uint64_t fstart, const uint8_t* text, uint32_t n, gre::VmScratch& sc) {
+__device__ __noinline__ void verify_vm_job(const VerifyParams& V, uint32_t rule, uint32_t fi, uint32_t job,
+                                           uint32_t pos0, uint64_t c0, uint64_t c1, uint64_t fstart,
+                                           const uint8_t* text, uint32_t n, gre::VmScratch& sc) {
   const gre::ProgView& pv = V.rs.progs[V.rs.rules[rule].prog];
   IvIter it;
   iv_init(it, V, rule, c0, c1, fstart, text, n);
-  uint32_t pos = 0, ms, me;
+  uint32_t pos = pos0, ms, me, fms = 0xFFFFFFFFu, lme = 0;
   while (it.have) {
     if (!vm_search_starts(pv, text, n, pos, it, sc, &ms, &me)) break;
-    emit_match(V, rule, fi, text, n, ms, me, sc);
+    emit_match(V, rule, fi, job, text, n, ms, me, sc);
+    if (fms == 0xFFFFFFFFu) fms = ms;
+    lme = me;
     if (me == ms) break;  // cannot happen for anchored rules (non-empty literal)
     pos = me;
   }
+  job_record(V, job, fms, lme);
 }
 
 // The text of a job read in aligned 16-byte blocks (one dwordx4 load per
@@ -2460,9 +2538,10 @@ struct VecText {
 // ends -- Go's priorities choose -- or a walk past kNfaWalkMax) is decided by
 // the Pike VM anchored there.
 template <bool kWide>
-__device__ __noinline__ uint32_t verify_nfa_job(const VerifyParams& V, uint32_t rule, uint32_t fi, uint64_t c0,
-                                                uint64_t c1, uint64_t fstart, const uint8_t* text, uint32_t n,
-                                                gre::VmScratch& sc, const uint8_t* nfa) {
+__device__ __noinline__ uint32_t verify_nfa_job(const VerifyParams& V, uint32_t rule, uint32_t fi, uint32_t job,
+                                                uint32_t pos0, uint64_t c0, uint64_t c1, uint64_t fstart,
+                                                const uint8_t* text, uint32_t n, gre::VmScratch& sc,
+                                                const uint8_t* nfa) {
   const NfaDev& N = *(const NfaDev*)nfa;
   const U128* reach = (const U128*)(nfa + N.o_reach);
   const NfaExc* exc = (const NfaExc*)(nfa + N.o_exc);
@@ -2470,7 +2549,8 @@ __device__ __noinline__ uint32_t verify_nfa_job(const VerifyParams& V, uint32_t 
   uint32_t steps = 0;
   IvIter it;
   iv_init(it, V, rule, c0, c1, fstart, text, n);
-  uint32_t pos = 0, ms, me;
+  uint32_t pos = pos0, ms, me, fms = 0xFFFFFFFFu, lme = 0;
+  while (it.have && it.ce < pos) it.advance();
   while (it.have) {
     bool found = false;
     const uint32_t s0 = it.cs > pos ? it.cs : pos;
@@ -2491,7 +2571,9 @@ __device__ __noinline__ uint32_t verify_nfa_job(const VerifyParams& V, uint32_t 
         r = vm_search_starts(V.rs.progs[prog], text, n, sp, one, sc, &ms, &me) ? 1 : 0;
       }
       if (r == 1) {
-        emit_match(V, rule, fi, text, n, sp, me, sc);
+        emit_match(V, rule, fi, job, text, n, sp, me, sc);
+        if (fms == 0xFFFFFFFFu) fms = sp;
+        lme = me;
         pos = me;
         found = true;
         break;
@@ -2500,6 +2582,7 @@ __device__ __noinline__ uint32_t verify_nfa_job(const VerifyParams& V, uint32_t 
     if (!found) it.advance();
     else while (it.have && it.ce < pos) it.advance();
   }
+  job_record(V, job, fms, lme);
   return steps;
 }
 
@@ -2508,6 +2591,39 @@ __device__ __noinline__ uint32_t verify_nfa_job(const VerifyParams& V, uint32_t 
 // step costs no L2 round trip and no TLB lookup (the random text pages the
 // lanes touch evict the table's translations from the small per-CU TLB).
 constexpr uint32_t kVerifyDfaLds = 64 * 1024;
+
+// One job's FindAll over candidates [c0, c1) from search position pos0, with
+// the rule's verify DFA, else its NFA, else the Pike VM; full-scan jobs run
+// the VM over the whole file.  lds_dfa / lds_nfa: the block's staged table
+// when this job's rule is the one staged (else null: global tables).
+__device__ inline uint32_t run_job(const VerifyParams& V, uint32_t job, uint32_t pos0, uint64_t c0, uint64_t c1,
+                                   gre::VmScratch& sc, const uint16_t* lds_dfa, const uint8_t* lds_cls,
+                                   const uint8_t* lds_nfa, bool* full_out) {
+  const uint32_t rule = (uint32_t)(V.keys[c0] >> kPosBits);
+  const uint32_t fi = V.vals[c0] & ~kFullFlag;
+  bool full = false;
+  for (uint64_t c = c0; c < c1 && !full; ++c) full = (V.vals[c] & kFullFlag) != 0;
+  *full_out = full;
+  const uint64_t fstart = V.off[fi];
+  const uint8_t* text = V.data + fstart;
+  const uint32_t n = (uint32_t)(V.off[fi + 1] - 1 - fstart);  // NUL separator excluded
+  uint32_t* tck = V.tck && !(job & kJobRedo) ? V.tck + 4 * job : nullptr;
+  const RuleDev& rd = V.rs.rules[rule];
+  if (full) {
+    verify_full_job(V, rule, fi, job, text, n, sc);
+    return 0;
+  }
+  if (lds_dfa) return verify_dfa_job<true>(V, rule, fi, job, pos0, c0, c1, fstart, text, n, sc, lds_dfa, lds_cls, tck);
+  if (rd.dfa_off != kNoFollow)
+    return verify_dfa_job<false>(V, rule, fi, job, pos0, c0, c1, fstart, text, n, sc, nullptr, nullptr, tck);
+  if (rd.nfa_off != kNoFollow) {
+    const uint8_t* nfa = lds_nfa ? lds_nfa : V.rs.nfa_bytes + rd.nfa_off;
+    return ((const NfaDev*)nfa)->npos > 64 ? verify_nfa_job<true>(V, rule, fi, job, pos0, c0, c1, fstart, text, n, sc, nfa)
+                                           : verify_nfa_job<false>(V, rule, fi, job, pos0, c0, c1, fstart, text, n, sc, nfa);
+  }
+  verify_vm_job(V, rule, fi, job, pos0, c0, c1, fstart, text, n, sc);
+  return 0;
+}
 
 template <uint32_t kBlock>
 __global__ __launch_bounds__(kBlock) void k_verify(VerifyParams V) {
@@ -2539,28 +2655,75 @@ __global__ __launch_bounds__(kBlock) void k_verify(VerifyParams V) {
     const uint64_t c0 = V.job_start[j];
     const uint64_t c1 = (j + 1 < n_jobs) ? V.job_start[j + 1] : V.n_cands;
     const uint32_t rule = (uint32_t)(V.keys[c0] >> kPosBits);
-    const uint32_t fi = V.vals[c0] & ~kFullFlag;
     bool full = false;
-    for (uint64_t c = c0; c < c1 && !full; ++c) full = (V.vals[c] & kFullFlag) != 0;
-    const uint64_t fstart = V.off[fi];
-    const uint8_t* text = V.data + fstart;
-    const uint32_t n = (uint32_t)(V.off[fi + 1] - 1 - fstart);  // NUL separator excluded
-    uint32_t steps = 0;
-    if (full) verify_full_job(V, rule, fi, text, n, sc);
-    else if (staged && rule == r0) steps = verify_dfa_job<true>(V, rule, fi, c0, c1, fstart, text, n, sc, dfa_lds, cls_lds, V.tck ? V.tck + 4 * j : nullptr);
-    else if (V.rs.rules[rule].dfa_off != kNoFollow)
-      steps = verify_dfa_job<false>(V, rule, fi, c0, c1, fstart, text, n, sc, nullptr, nullptr, V.tck ? V.tck + 4 * j : nullptr);
-    else if (V.rs.rules[rule].nfa_off != kNoFollow) {
-      const uint8_t* nfa = staged_nfa && rule == r0 ? (const uint8_t*)dfa_lds : V.rs.nfa_bytes + V.rs.rules[rule].nfa_off;
-      steps = ((const NfaDev*)nfa)->npos > 64 ? verify_nfa_job<true>(V, rule, fi, c0, c1, fstart, text, n, sc, nfa)
-                                              : verify_nfa_job<false>(V, rule, fi, c0, c1, fstart, text, n, sc, nfa);
-    } else verify_vm_job(V, rule, fi, c0, c1, fstart, text, n, sc);
+    const uint32_t steps = run_job(V, j, 0, c0, c1, sc, staged && rule == r0 ? dfa_lds : nullptr, cls_lds,
+                                   staged_nfa && rule == r0 ? (const uint8_t*)dfa_lds : nullptr, &full);
     if (V.prof) {  // diagnostics (TSG_PROFILE_VERIFY): duration | end, rule | full
       const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
       V.prof[2 * j] = (t1 - t0) | ((t1 & 0xFFFFFFFFull) << 32);
       V.prof[2 * j + 1] = ((uint64_t)rule << 32) | (steps << 1) | (full ? 1u : 0u);
     }
   }
+}
+
+// The speculative chains (one lane per chain head -- a job whose first
+// candidate starts a hard split -- over the soft-split jobs after it): the
+// first job whose first match starts before the previous match's end is a
+// conflict; that job and the rest of its chain are re-run in order from that
+// end (k_verify_redo), and their speculative output is dropped.
+__global__ void k_chain_fix(VerifyParams V) {
+  const uint32_t n_jobs = *V.n_jobs_dev;
+  const uint32_t j0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j0 >= n_jobs || V.split[V.job_start[j0]] != kSplitHard) return;
+  if (j0 + 1 >= n_jobs || V.split[V.job_start[j0 + 1]] != kSplitSoft) return;  // a chain of one
+  uint32_t last = j0 + 1;
+  while (last + 1 < n_jobs && V.split[V.job_start[last + 1]] == kSplitSoft) ++last;
+  uint64_t end = V.job_fms[j0] != ~0ull ? V.job_lme[j0] : 0;
+  for (uint32_t j = j0 + 1; j <= last; ++j) {
+    const uint64_t f = V.job_fms[j];
+    if (f == ~0ull) continue;
+    if (f < end) {
+      for (uint32_t q = j; q <= last; ++q) V.job_bad[q] = 1;
+      const unsigned long long k = atomicAdd(&V.ctrl->n_redo, 1ull);
+      if (k < V.redo_cap) V.redo[k] = RedoRec{j, last, end};
+      return;
+    }
+    end = V.job_lme[j];
+  }
+}
+
+// One lane per conflict: the chain's remaining jobs in order, as ONE job
+// (their candidates are consecutive), from the conflict's search position.
+__global__ __launch_bounds__(64) void k_verify_redo(VerifyParams V) {
+  const uint64_t n = V.ctrl->n_redo < V.redo_cap ? V.ctrl->n_redo : V.redo_cap;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  gre::VmScratch sc = make_scratch(V.scratch + (uint64_t)t * V.scratch_stride, V.rs);
+  const uint32_t n_jobs = *V.n_jobs_dev;
+  for (uint64_t i = t; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const RedoRec R = V.redo[i];
+    const uint64_t c0 = V.job_start[R.job];
+    const uint64_t c1 = R.last + 1 < n_jobs ? V.job_start[R.last + 1] : V.n_cands;
+    bool full;
+    run_job(V, kJobRedo | R.job, (uint32_t)R.pos, c0, c1, sc, nullptr, nullptr, nullptr, &full);
+  }
+}
+
+// Locations of conflicting speculative jobs are flagged dropped (flags bit
+// 2) and counted; the host compacts them away.
+__global__ void k_drop_spec(VerifyParams V) {
+  const uint64_t n_locs = V.ctrl->locs < V.loc_cap ? V.ctrl->locs : V.loc_cap;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_locs; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t job = V.locs[i].job;
+    if (!(job & kJobRedo) && V.job_bad[job]) {
+      V.locs[i].flags |= 2;
+      atomicAdd(&V.ctrl->n_dropped, 1ull);
+    }
+  }
+}
+
+__global__ void k_keep_flags(const DevLoc* locs, uint64_t n, uint8_t* keep) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) keep[i] = (locs[i].flags & 2) ? 0 : 1;
 }
 
 // --------------------------------------------------------------- exclude --
@@ -3388,7 +3551,10 @@ struct tsg_engine {
   DBuf<uint8_t> span_hi;
   DBuf<uint64_t> fold_pos;    // fold-special rune occurrences (k_fold_windows)
   uint64_t fold_need = 0;     // fold-position capacity learnt from a lost scan
-  DBuf<uint4> caps, caps_big;
+  DBuf<CapJob> caps, caps_big;
+  DBuf<uint64_t> job_fms, job_lme;  // speculative jobs (k_chain_fix)
+  DBuf<uint8_t> job_bad;
+  DBuf<RedoRec> redo;
   DBuf<uint32_t> ev_counts;
   uint64_t ev_ovf_need = 0;  // overflow-event capacity learnt from a lost scan
   bool fast_timed = false;   // ev[10..11] bracket the last k_scan_fast launch
@@ -4795,14 +4961,21 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   // ---- 5. verify
   uint64_t loc_cap = std::max<uint64_t>(1 << 16, n_cands);
   uint64_t caps_cap = std::max<uint64_t>(1 << 14, n_cands / 2), caps_big_cap = std::max<uint64_t>(1 << 12, n_cands / 16);
-  uint64_t n_locs = 0;
+  uint64_t redo_cap = std::max<uint64_t>(1 << 12, n_cands / 64);
+  uint64_t n_locs = 0, n_dropped = 0;
   bool verified = n_cands == 0;
   for (int attempt = 0; attempt < 4 && !verified; ++attempt) {
     HIP_TRY(e->locs.ensure(loc_cap));
     HIP_TRY(e->caps.ensure(caps_cap));
     HIP_TRY(e->caps_big.ensure(caps_big_cap));
+    HIP_TRY(e->job_fms.ensure(n_cands));
+    HIP_TRY(e->job_lme.ensure(n_cands));
+    HIP_TRY(e->job_bad.ensure(n_cands));
+    HIP_TRY(e->redo.ensure(redo_cap));
+    HIP_TRY(hipMemsetAsync(e->job_bad.p, 0, n_cands, s));
     HIP_TRY(hipMemsetAsync(&e->ctrl.p->locs, 0, 8, s));
     HIP_TRY(hipMemsetAsync(&e->ctrl.p->n_caps, 0, 16, s));  // n_caps, n_caps_big
+    HIP_TRY(hipMemsetAsync(&e->ctrl.p->n_redo, 0, 16, s));  // n_redo, n_dropped
     VerifyParams V{};
     V.data = d_data;
     V.off = d_off;
@@ -4821,6 +4994,12 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     V.cap_cap = e->caps.n;
     V.caps_big = e->caps_big.p;
     V.cap_big_cap = e->caps_big.n;
+    V.job_fms = e->job_fms.p;
+    V.job_lme = e->job_lme.p;
+    V.split = e->flags8.p;
+    V.job_bad = e->job_bad.p;
+    V.redo = e->redo.p;
+    V.redo_cap = e->redo.n;
     V.span_hi = (rs->ac.fast.size() || P.big.blob) && nbytes ? e->span_hi.p : nullptr;
     const bool prof = experiment_env("TSG_PROFILE_VERIFY") != nullptr;
     if (prof) {  // diagnostics only: the job count on the host
@@ -4860,11 +5039,18 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
       const uint32_t blocks = (uint32_t)std::min<uint64_t>((n_cands + kVerifyBlock - 1) / kVerifyBlock, e->vm_threads / kVerifyBlock);
       hipLaunchKernelGGL(k_verify<kVerifyBlock>, dim3(std::max(1u, blocks)), dim3(kVerifyBlock), 0, s, V);
     }
+    // speculative chains: conflicts re-run in order (grid: one lane per job
+    // start at most; the re-run grid keeps every lane's VM scratch slot below
+    // vm_threads)
+    hipLaunchKernelGGL(k_chain_fix, dim3((uint32_t)((n_cands + 255) / 256)), dim3(256), 0, s, V);
+    hipLaunchKernelGGL(k_verify_redo, dim3(e->num_cus * 2), dim3(64), 0, s, V);
+    HIP_TRY(hipGetLastError());
     // capture stages over the device-side lists: 8 searching lanes per wave with
     // 560-word arenas, then one lane per wave with 36 KiB for what does not fit
     // (grids keep every lane's VM scratch slot below vm_threads: 512 / 256 per CU)
     hipLaunchKernelGGL((k_captures<64, kCapActive, kBsWords, false>), dim3(e->num_cus * 8), dim3(64), 0, s, V);
     hipLaunchKernelGGL((k_captures<64, 1, kBigBsWords, true>), dim3(e->num_cus * 4), dim3(64), 0, s, V);
+    hipLaunchKernelGGL(k_drop_spec, dim3(e->num_cus * 4), dim3(256), 0, s, V);
     HIP_TRY(hipGetLastError());
     if (prof) {  // the jobs that end last (their waves set k_verify's length), per-rule totals
       std::vector<uint64_t> hp(4ull * n_jobs);
@@ -4937,7 +5123,8 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(hipMemcpyAsync(&n_jobs, e->nsel.p, 4, hipMemcpyDeviceToHost, s));  // (read by read_ctrl's sync)
     if ((rc = read_ctrl(e, &c))) return rc;
     n_locs = c.locs;
-    if (n_locs <= e->locs.n && c.n_caps <= e->caps.n && c.n_caps_big <= e->caps_big.n) {
+    n_dropped = c.n_dropped;
+    if (n_locs <= e->locs.n && c.n_caps <= e->caps.n && c.n_caps_big <= e->caps_big.n && c.n_redo <= e->redo.n) {
       verified = true;
       break;
     }
@@ -4945,6 +5132,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     loc_cap = std::max<uint64_t>(loc_cap, n_locs);
     caps_cap = std::max<uint64_t>(caps_cap, c.n_caps);
     caps_big_cap = std::max<uint64_t>(caps_big_cap, c.n_caps_big);
+    redo_cap = std::max<uint64_t>(redo_cap, c.n_redo);
   }
   if (!verified) {
     set_last_error("internal: location buffers still overflowed after regrowing them");
@@ -4953,6 +5141,21 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   if (c.err) {
     set_last_error("internal: capture re-run disagreed with the whole-match run");
     return TSG_ERR_INTERNAL;
+  }
+  if (n_dropped) {  // the conflicting speculative jobs' locations out (rare): compact in order
+    HIP_TRY(e->locs2.ensure(n_locs));
+    HIP_TRY(e->flags8.ensure(n_locs));
+    HIP_TRY(e->nsel.ensure(2));
+    hipLaunchKernelGGL(k_keep_flags, dim3((uint32_t)((n_locs + 255) / 256)), dim3(256), 0, s, e->locs.p, n_locs,
+                       e->flags8.p);
+    size_t tmp = 0;
+    HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tmp, e->locs.p, e->flags8.p, e->locs2.p, e->nsel.p + 1,
+                                          (int)n_locs, s));
+    HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+    HIP_TRY(hipcub::DeviceSelect::Flagged(e->cub_tmp.p, tmp, e->locs.p, e->flags8.p, e->locs2.p, e->nsel.p + 1,
+                                          (int)n_locs, s));
+    n_locs -= n_dropped;
+    HIP_TRY(hipMemcpyAsync(e->locs.p, e->locs2.p, n_locs * sizeof(DevLoc), hipMemcpyDeviceToDevice, s));
   }
   HIP_TRY(hipEventRecord(e->ev[5], s));
   // ---- 6. exclude blocks (only when the config has any)
@@ -5187,7 +5390,8 @@ void tsg_engine_free(tsg_engine* e) {
   e->job_start.release(); e->nsel.release(); e->cub_tmp.release(); e->locs.release(); e->locs2.release();
   e->scratch.release(); e->ctrl.release(); e->excl_jobs.release(); e->excl_out.release();
   e->nl_blocks.release(); e->nl_pre.release(); e->tail.release(); e->region_file.release(); e->region_tmp.release();
-  e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->fold_pos.release(); e->caps.release(); e->caps_big.release(); e->vprof.release(); e->fflags8.release();
+  e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->fold_pos.release(); e->caps.release(); e->caps_big.release();
+  e->job_fms.release(); e->job_lme.release(); e->job_bad.release(); e->redo.release(); e->vprof.release(); e->fflags8.release();
   if (e->h_stage) (void)hipHostFree(e->h_stage);
   e->gate_out.release(); e->gate_rules.release(); e->bin8.release(); e->strip_out.release();
   e->strip_off.release(); e->blk_kept.release(); e->blk_base.release(); e->chunk_pos.release(); e->n_drop.release();
