@@ -13,7 +13,7 @@ from oracle import secret_oracle as O
 import trivy_amd.secret as S
 
 RULES = [
-    ("span-begin", r"BEGIN[\s\S]*?END", ["begin"]),                       # later BEGINs inside a match
+    ("span-begin", r"BEGIN[^#]*?END", ["begin"]),                          # later BEGINs inside a match
     ("greedy-eq", r"(?i)key[a-z ]{0,300}=[0-9]{3}", ["key"]),            # a match reaches over later "key"s
     ("tok", r"tk_[a-z0-9]{8}", ["tk_"]),                                  # dense, independent hits
     ("unb", r"(?:x|y)*xq[0-9]{2}", ["xq"]),                               # unbounded window (alphabet run)
