@@ -217,6 +217,16 @@ def build_layer_tar(host, off, sizes, pbytes, poff):
     return out
 
 
+def shared_layer_set(seed, gb_total, n_layers):
+    """configs[3] shared list: the byte sizes of an image's `n_layers` layers
+    (lognormal around the mean, sigma 0.6, scaled to gb_total), the same on
+    every rank; layer k's files come from seed + 7919 k, so a layer's content
+    does not depend on which rank builds it."""
+    rng = np.random.default_rng(seed + 77)
+    w = rng.lognormal(0.0, 0.6, n_layers)
+    return [max(0.002, gb_total * x / w.sum()) for x in w]
+
+
 def scan_device(N, eng, rs, c):
     res = ctypes.c_void_p()
     N.check(N.lib.tsg_scan_device(eng, rs, ctypes.c_void_p(c["d_data"].data_ptr()),
@@ -454,6 +464,141 @@ def cpu_baseline(N, c, locs, rs, seconds, threads):
                 files_agree=agree, files=k)
 
 
+def shared_layers_main(args, N, S, torch, dist, barrier, rank, world, device, red_dev):
+    """configs[3] as one shared image: every rank derives the same layer list
+    (shared_layer_set), trivy_amd.shard.partition assigns layers to ranks by
+    bytes (LPT), each rank builds ITS layers as ustar tars in host memory, and
+    a timed step is one trivy_amd.shard.scan_sharded call: the rank's layers
+    walked on host threads ahead of one tsg_analyze_layer per layer, then the
+    per-layer results (kept member indices + locations) gathered to every rank
+    over the process group (all_gather_object) and returned in layer order --
+    the reference's per-layer fan-out (pkg/fanal/artifact/image/image.go:201-240)
+    with its merge.  Parity: --dump writes the merged result, which must not
+    depend on the number of ranks (tests/test_bench_shared.py)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from trivy_amd import shard
+
+    n_layers = args.total_layers or args.layers * world
+    layer_gb = shared_layer_set(args.seed, args.image_gb or args.gb * world, n_layers)
+    plan = shard.partition([int(g * 1e9) for g in layer_gb], world)
+    mine = plan[rank]
+    sc = S.new_scanner(None, device=device)
+    eng = S.get_engine(device)
+    rs = sc._rs.handle
+    t_tar = time.perf_counter()
+    tars = {}
+    content = {}
+    for k in mine:
+        ck = build_corpus(N, torch, args.seed + 7919 * k, layer_gb[k], args.density, device)
+        host = ck["d_data"][: ck["packed"]].cpu().numpy()
+        poff = ck["d_poff"].cpu().numpy().astype(np.int64)
+        pbytes = ck["d_paths"][: int(poff[-1])].cpu().numpy()
+        tars[k] = (ck["n_files"], build_layer_tar(host, ck["off"], ck["sizes"], pbytes, poff))
+        content[k] = ck["total"]
+        del ck, host
+    torch.cuda.empty_cache()
+    build_s = time.perf_counter() - t_tar
+    pool = ThreadPoolExecutor(max_workers=4)
+
+    def walk_one(layer):
+        w = ctypes.c_void_p()
+        N.check(N.lib.tsg_layer_tar_walk(ctypes.c_void_p(layer.ctypes.data), len(layer), None, 0, None, 0,
+                                         ctypes.byref(w)))
+        return w
+
+    scan_ms = []
+
+    def scan_fn(idxs):
+        """This rank's layers, pipelined: walks run ahead on host threads, one
+        analyze per layer; returns (kept member indices, locations) per layer."""
+        futs = [pool.submit(walk_one, tars[k][1]) for k in idxs]
+        out, ms = [], 0.0
+        for k, f in zip(idxs, futs):
+            nf, x = tars[k]
+            w = f.result()
+            kept = (ctypes.c_uint32 * (nf + 1))()
+            nk = ctypes.c_size_t()
+            r = ctypes.c_void_p()
+            try:
+                N.check(N.lib.tsg_analyze_layer(eng, rs, ctypes.c_void_p(x.ctypes.data), len(x), w, b"", kept,
+                                                ctypes.byref(nk), ctypes.byref(r)))
+            finally:
+                N.lib.tsg_tar_walk_free(w)
+            try:
+                locs, tm = read_result(N, r)
+            finally:
+                N.lib.tsg_result_free(r)
+            ms += tm[17] if len(tm) > 17 and tm[17] > 0 else tm[7]
+            out.append((np.ctypeslib.as_array(kept)[: nk.value].copy(), locs))
+        scan_ms.append(ms)
+        return out
+
+    sizes = [int(g * 1e9) for g in layer_gb]
+    step = lambda: shard.scan_sharded(scan_fn, list(range(n_layers)), sizes=sizes)  # noqa: E731
+    merged = None
+    for _ in range(args.warmup):
+        merged = step()
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        merged = step()
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    mine_bytes = float(sum(content[k] for k in mine))
+    if dist is not None:
+        t = torch.tensor([dt], device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        tb = torch.tensor([mine_bytes], device=red_dev, dtype=torch.float64)
+        dist.all_reduce(tb, op=dist.ReduceOp.SUM)
+        total_all = float(tb.item())
+    else:
+        total_all = mine_bytes
+    if rank == 0 and args.dump and merged is not None:
+        arrs = {}
+        for k, (kept, locs) in enumerate(merged):
+            arrs[f"kept{k}"] = kept
+            arrs[f"locs{k}"] = locs
+        np.savez(args.dump, **arrs)
+    if rank == 0:
+        n_found = sum(len(locs) for _, locs in merged) if merged else 0
+        out = {
+            "metric": "secret-scan GB/s (whole node), builtin rules, 1/2/4/8 MI355X; % HBM peak",
+            "value": round(total_all * args.steps / dt / 1e9, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak" if not args.image_gb else "strong",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded SURVEY.md §8(d) text model, builtin-rule secrets planted at "
+                    f"{args.density:g}/byte, one corpus seed per layer)",
+            "config": {"workload": "configs[3]: ONE shared image of %d layers (%.3f GB) LPT-partitioned over the "
+                                   "ranks by bytes (trivy_amd.shard.scan_sharded); per rank: native layer walks "
+                                   "on host threads + one tsg_analyze_layer per layer; per-layer results gathered "
+                                   "to every rank in the step; PCIe-inclusive" % (n_layers, total_all / 1e9),
+                       "layers": n_layers, "layers_per_rank": [len(p) for p in plan],
+                       "bytes_per_rank": [int(sum(sizes[k] for k in p)) for p in plan],
+                       "dist_backend": args.dist_backend if world > 1 else None,
+                       "layer_build_s": round(build_s, 1),
+                       "parallelism": f"layer shards x{world} (LPT), all_gather of per-layer results"},
+            "stages_ms": {"scan_kernels_rank0": round(float(np.mean(scan_ms[-args.steps:])), 3)},
+            "counts": {"locs": int(n_found)},
+            "roofline": None,
+            "cpu_baseline": None,
+            "parity": None,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -471,32 +616,54 @@ def main():
     ap.add_argument("--cpu-cores", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group for N > 1 (nccl = RCCL; gloo for several ranks on one GPU in tests)")
+    ap.add_argument("--shared", action="store_true",
+                    help="configs[3] as ONE shared layer list: every rank sees the same image, layers are "
+                         "LPT-partitioned by bytes (trivy_amd.shard), each rank builds and analyzes its layers, "
+                         "and the per-layer results are gathered to every rank inside the timed step")
+    ap.add_argument("--total-layers", type=int, default=0, help="--shared: layers in the image (default layers x N)")
+    ap.add_argument("--image-gb", type=float, default=0.0,
+                    help="--shared: bytes of the whole image (default --gb x N: fixed work per GPU)")
+    ap.add_argument("--dump", default="", help="--shared: rank 0 writes the merged per-layer results (.npz)")
     args = ap.parse_args()
     if args.gb is None:
         args.gb = {0: 1.0, 1: 20.0, 3: 4.0}.get(args.config, 50.0)
+    if args.shared and args.config != 3:
+        ap.error("--shared is the configs[3] layer-set mode")
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
 
-    torch.cuda.set_device(local_rank)
+    # ranks beyond the visible GPUs share them (gloo tests: two ranks on one GPU);
+    # device_count() does not initialise the GPU
+    device = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
+    # reductions of the timing live on the GPU for RCCL, on the host for gloo
+    red_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    os.environ["TSG_DEVICE"] = str(local_rank)
+    os.environ["TSG_DEVICE"] = str(device)
     from trivy_amd import _native as N
     import trivy_amd.secret as S
 
+    if args.shared:
+        return shared_layers_main(args, N, S, torch, dist, barrier, rank, world, device, red_dev)
     seed = args.seed + 1000 * rank
-    c = build_corpus(N, torch, seed, args.gb, args.density, local_rank)
+    c = build_corpus(N, torch, seed, args.gb, args.density, device)
     torch.cuda.synchronize()
     cfg = None
     stress_unique = []
@@ -513,9 +680,9 @@ def main():
         # minified line and binary-ish files, appended to the HBM corpus as 2 %
         # of its bytes (~0.6 M findings: 20x the builtin plants' findings)
         stress_unique, stress_all = stress_material(stress_rules, srules, seed, int(c["total"] * 0.02))
-        c = append_files(torch, c, stress_all, local_rank)
-    sc = S.new_scanner(cfg, device=local_rank)
-    eng = S.get_engine(local_rank)
+        c = append_files(torch, c, stress_all, device)
+    sc = S.new_scanner(cfg, device=device)
+    eng = S.get_engine(device)
     rs = sc._rs.handle
     st = [ctypes.c_uint32() for _ in range(4)]
     fast = ctypes.c_int()
@@ -651,10 +818,10 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([dt], device="cuda")
+        t = torch.tensor([dt], device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        tb = torch.tensor([float(c["total"])], device="cuda", dtype=torch.float64)
+        tb = torch.tensor([float(c["total"])], device=red_dev, dtype=torch.float64)
         dist.all_reduce(tb, op=dist.ReduceOp.SUM)
         total_all = float(tb.item())
     else:
