@@ -417,6 +417,29 @@ def physical_cores():
     return len(pairs) or None
 
 
+def cpu_quota():
+    """CPUs this process may actually use: the affinity set, capped by the
+    cgroup CPU quota (cpu.max / cfs_quota_us) -- on the GPU box the affinity set
+    lists the whole machine while the quota is the box's share, and threads
+    beyond the quota only time-slice."""
+    n = len(os.sched_getaffinity(0))
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            parts = open(path).read().split()
+        except OSError:
+            continue
+        if path.endswith("cpu.max"):
+            if parts and parts[0] != "max":
+                n = min(n, max(1, -(-int(parts[0]) // int(parts[1]))))
+        else:
+            q = int(parts[0])
+            period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                n = min(n, max(1, -(-q // period)))
+        break
+    return n
+
+
 def cpu_baseline(N, c, locs, rs, seconds, threads):
     """Time bench_cpu/libtsg_cpu_scan.so — Scanner.Scan restated in C++ on
     the repo's host Go-regexp VM, `threads` threads — on a bounded sample of the
@@ -456,8 +479,9 @@ def cpu_baseline(N, c, locs, rs, seconds, threads):
     return dict(value=nbytes / dt / 1e9, unit="GB/s", cores=threads, kind="cpp-restatement",
                 physical_cores=phys,
                 sample=f"{k} files / {nbytes / 1e6:.1f} MB of the same corpus (first files in index order, copied "
-                       f"from HBM), {dt:.1f}s wall on {threads} threads (every CPU in this process's affinity "
-                       "set" + (f"; the host has {phys} physical cores" if phys else "") + "); "
+                       f"from HBM), {dt:.1f}s wall on {threads} threads (every CPU this process may use: its affinity "
+                       f"set of {len(os.sched_getaffinity(0))} capped by the cgroup CPU quota"
+                       + (f"; the host has {phys} physical cores" if phys else "") + "); "
                        "bench_cpu/cpu_scan.cpp: Scanner.Scan restated in C++ on the repo's host Go-regexp VM "
                        "(not Go: no Go toolchain in the image); per-file finding counts equal the GPU's on "
                        f"{agree}/{k} files",
@@ -628,7 +652,7 @@ def main():
     ap.add_argument("--dump", default="", help="--shared: rank 0 writes the merged per-layer results (.npz)")
     args = ap.parse_args()
     if args.gb is None:
-        args.gb = {0: 1.0, 1: 20.0, 3: 4.0}.get(args.config, 50.0)
+        args.gb = {0: 1.0, 1: 20.0, 3: 4.0, 4: 10.0}.get(args.config, 50.0)
     if args.shared and args.config != 3:
         ap.error("--shared is the configs[3] layer-set mode")
 
@@ -854,8 +878,9 @@ def main():
                 parity.update(stress_checks(N, last, sc.rules, c, stress_unique, cfg_path))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.config in (0, 2):
-        # every CPU this process may run on (N = the cores used, stated)
-        cores = args.cpu_cores or len(os.sched_getaffinity(0))
+        # every CPU this process may run on: the affinity set capped by the
+        # cgroup quota (N = the cores used, stated)
+        cores = args.cpu_cores or cpu_quota()
         cpu = cpu_baseline(N, c, locs, rs, args.cpu_seconds, cores)
     if last is not None and args.config != 3:
         N.lib.tsg_result_free(last)

@@ -14,7 +14,8 @@
 //   k_verify      one lane per (file, rule) job: Go leftmost-first Pike VM restricted to
 //                 the anchor windows, FindAll iteration, allow rules, secret groups
 //                 (FindLocations / FindSubmatchLocations / AllowLocation, scanner.go:97-163)
-//   k_exclude     exclude-block FindAll for files with kept locations (scanner.go:232-270)
+//   k_exclude_tags exclude-block FindAll per (file, scope) group of the kept locations, then
+//                 the containment filter on the device (scanner.go:232-270)
 //   k_lines       StartLine / EndLine of every kept location (findLocation, scanner.go:481-503)
 //
 // Host code (findings.cpp) then censors and cuts Match/Code from the caller's
@@ -869,23 +870,32 @@ __global__ __launch_bounds__(1024) void k_big_report(ScanParams P, uint32_t n_wa
       n = P.ctrl->ev_overflow < P.ev_overflow_cap ? P.ctrl->ev_overflow : P.ev_overflow_cap;
     }
     LdsHitSink sink{stage, &n_stage};
-    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
-      const FastEvent ev = seg[i];
-      uint32_t e = ev.entry;
+    // one event per thread per round, the stage flushed after every round (a
+    // segment of a hit-dense stretch -- a minified line full of rule
+    // instances -- holds thousands of hits: beyond the stage they would go
+    // through the one global counter, which serialises at L2)
+    for (uint64_t r0 = 0; r0 < n; r0 += blockDim.x) {
+      const uint64_t i = r0 + threadIdx.x;
+      if (i < n) {
+        const FastEvent ev = seg[i];
+        uint32_t e = ev.entry;
 #pragma unroll 1
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t nx = big_next(L, e, L.cls[((j < 4 ? ev.cur.x : ev.cur.y) >> (8 * (j & 3))) & 0xFFu]);
-        e = nx & 0x7FFFu;
-        if (nx & 0x8000u) report_t<false>(P, e, ev.pos + j, &last_kw, sink);
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t nx = big_next(L, e, L.cls[((j < 4 ? ev.cur.x : ev.cur.y) >> (8 * (j & 3))) & 0xFFu]);
+          e = nx & 0x7FFFu;
+          if (nx & 0x8000u) report_t<false>(P, e, ev.pos + j, &last_kw, sink);
+        }
       }
+      __syncthreads();
+      const uint32_t m = n_stage < kBigHitStage ? n_stage : kBigHitStage;
+      if (threadIdx.x == 0) base = m ? atomicAdd(&P.ctrl->hits, (unsigned long long)m) : 0ull;
+      __syncthreads();
+      for (uint32_t k = threadIdx.x; k < m; k += blockDim.x)
+        if (base + k < P.hit_cap) P.hits[base + k] = stage[k];
+      __syncthreads();
+      if (threadIdx.x == 0) n_stage = 0;
+      __syncthreads();
     }
-    __syncthreads();
-    const uint32_t m = n_stage < kBigHitStage ? n_stage : kBigHitStage;
-    if (threadIdx.x == 0) base = m ? atomicAdd(&P.ctrl->hits, (unsigned long long)m) : 0ull;
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
-      if (base + i < P.hit_cap) P.hits[base + i] = stage[i];
-    __syncthreads();
   }
 }
 
@@ -2727,33 +2737,64 @@ __global__ void k_keep_flags(const DevLoc* locs, uint64_t n, uint8_t* keep) {
 }
 
 // --------------------------------------------------------------- exclude --
-struct ExclJob {
-  uint32_t file;
-  uint32_t prog;
-  uint32_t tag;  // index of the (file, scope) group the ranges belong to
-  uint32_t pad;
-};
 struct ExclRange {
   uint32_t tag;
   uint32_t pad;
   uint64_t s, e;
 };
 
-__global__ __launch_bounds__(256) void k_exclude(const uint8_t* data, const uint64_t* off, RuleSetDev rs,
-                                                 const ExclJob* jobs, uint32_t n_jobs, ExclRange* out,
-                                                 uint64_t cap, Ctrl* ctrl, uint8_t* scratch,
-                                                 uint64_t stride) {
+// Exclude blocks on the device (Blocks.Match / find, scanner.go:232-270,413-419):
+// a kept location needs the FindAll ranges of its file's global blocks (scope
+// 0) and of its rule's blocks (scope rule + 1).  The (file, scope) groups are
+// the unique keys of k_excl_keys (sorted, ~0 = none); k_exclude_tags runs the
+// FindAll of every (group, exclude regex) pair; the ranges sorted by (group,
+// start) with a running maximum of their ends per group (k_excl_pmax) answer
+// "some range of the group contains [start, end)" with one binary search
+// (k_excl_filter) -- no location leaves the device.
+struct ExclDev {
+  const uint32_t* xoff;   // per rule: its exclude regexes xprog[xoff[r], xoff[r + 1])
+  const uint32_t* xprog;
+  const uint32_t* gx;     // global exclude regexes
+  uint32_t n_gx, max_x;   // max_x: most regexes of one scope
+};
+
+__global__ void k_excl_keys(const DevLoc* locs, uint64_t n, ExclDev X, uint64_t* keys, uint32_t* idx) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const DevLoc L = locs[i];
+  keys[2 * i] = X.n_gx ? ((uint64_t)L.file << 32) : ~0ull;
+  keys[2 * i + 1] = X.xoff[L.rule + 1] > X.xoff[L.rule] ? (((uint64_t)L.file << 32) | (L.rule + 1)) : ~0ull;
+  idx[2 * i] = (uint32_t)(2 * i);
+  idx[2 * i + 1] = (uint32_t)(2 * i + 1);
+}
+
+__global__ void k_excl_uniq(const uint64_t* keys, uint64_t n, uint8_t* flags) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) flags[i] = keys[i] != ~0ull && (i == 0 || keys[i] != keys[i - 1]);
+}
+
+__global__ __launch_bounds__(256) void k_exclude_tags(const uint8_t* data, const uint64_t* off, RuleSetDev rs,
+                                                      ExclDev X, const uint64_t* skeys, const uint32_t* tidx,
+                                                      const uint32_t* n_tags_dev,
+                                                      ExclRange* out, uint64_t cap, Ctrl* ctrl, uint8_t* scratch,
+                                                      uint64_t stride) {
   const uint32_t nthreads = gridDim.x * blockDim.x;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   gre::VmScratch sc = make_scratch(scratch + (uint64_t)t * stride, rs);
-  for (uint32_t j = t; j < n_jobs; j += nthreads) {
-    const ExclJob jb = jobs[j];
-    const uint8_t* text = data + off[jb.file];
-    const uint32_t n = (uint32_t)(off[jb.file + 1] - 1 - off[jb.file]);
-    const gre::ProgView& pv = rs.progs[jb.prog];
+  const uint64_t n_jobs = (uint64_t)*n_tags_dev * X.max_x;
+  for (uint64_t j = t; j < n_jobs; j += nthreads) {
+    const uint32_t tag = (uint32_t)(j / X.max_x), k = (uint32_t)(j % X.max_x);
+    const uint64_t key = skeys[tidx[tag]];
+    const uint32_t file = (uint32_t)(key >> 32), scope = (uint32_t)key;
+    const uint32_t nx = scope == 0 ? X.n_gx : X.xoff[scope] - X.xoff[scope - 1];
+    if (k >= nx) continue;
+    const uint32_t prog = scope == 0 ? X.gx[k] : X.xprog[X.xoff[scope - 1] + k];
+    const uint8_t* text = data + off[file];
+    const uint32_t n = (uint32_t)(off[file + 1] - 1 - off[file]);
+    const gre::ProgView& pv = rs.progs[prog];
     uint32_t pos = 0, ms, me;
     int64_t prev_end = -1;
-    while (pos <= n) {
+    while (pos <= n) {  // FindAllIndex iteration (regexp.go allMatches)
       LimitStarts ls{n};
       if (!vm_search_starts(pv, text, n, pos, ls, sc, &ms, &me)) break;
       bool accept = true;
@@ -2768,10 +2809,65 @@ __global__ __launch_bounds__(256) void k_exclude(const uint8_t* data, const uint
       prev_end = me;
       if (accept) {
         unsigned long long idx = atomicAdd(&ctrl->excl, 1ull);
-        if (idx < cap) out[idx] = ExclRange{jb.tag, 0, ms, me};
+        if (idx < cap) out[idx] = ExclRange{tag, 0, ms, me};
       }
     }
   }
+}
+
+// (group, start) keys of the ranges (start < 2^40: kMaxFileBytes)
+__global__ void k_excl_rkeys(const ExclRange* r, uint64_t n, uint64_t* keys, uint32_t* idx) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  keys[i] = ((uint64_t)r[i].tag << kKeyPosBits) | r[i].s;
+  idx[i] = (uint32_t)i;
+}
+
+// running maximum of the ends inside each group's run, in (group, start)
+// order (one lane per run)
+__global__ void k_excl_pmax(const uint64_t* keys, const uint32_t* idx, const ExclRange* r, uint64_t* pmax,
+                            uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || (i > 0 && (keys[i] >> kKeyPosBits) == (keys[i - 1] >> kKeyPosBits))) return;
+  const uint64_t g = keys[i] >> kKeyPosBits;
+  uint64_t m = 0;
+  for (uint64_t j = i; j < n && (keys[j] >> kKeyPosBits) == g; ++j) {
+    const uint64_t e = r[idx[j]].e;
+    m = e > m ? e : m;
+    pmax[j] = m;
+  }
+}
+
+__device__ inline bool excl_contains(const uint64_t* skeys, const uint32_t* tidx, uint32_t n_tags,
+                                     const uint64_t* rkeys, const uint64_t* pmax, uint64_t n_r, uint64_t key,
+                                     uint64_t s, uint64_t e) {
+  uint32_t lo = 0, hi = n_tags;  // the group's index
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (skeys[tidx[m]] < key) lo = m + 1; else hi = m;
+  }
+  if (lo >= n_tags || skeys[tidx[lo]] != key) return false;
+  // last range of the group starting at or before s
+  const uint64_t want = ((uint64_t)lo << kKeyPosBits) | s;
+  uint64_t a = 0, b = n_r;
+  while (a < b) {
+    const uint64_t m = (a + b) >> 1;
+    if (rkeys[m] <= want) a = m + 1; else b = m;
+  }
+  return a > 0 && (rkeys[a - 1] >> kKeyPosBits) == lo && pmax[a - 1] >= e;
+}
+
+__global__ void k_excl_filter(const DevLoc* locs, uint64_t n, ExclDev X, const uint64_t* skeys, const uint32_t* tidx,
+                              const uint32_t* n_tags_dev, const uint64_t* rkeys, const uint64_t* pmax, uint64_t n_r,
+                              uint8_t* keep) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const DevLoc L = locs[i];
+  const uint32_t nt = *n_tags_dev;
+  bool ex = X.n_gx && excl_contains(skeys, tidx, nt, rkeys, pmax, n_r, (uint64_t)L.file << 32, L.start, L.end);
+  if (!ex && X.xoff[L.rule + 1] > X.xoff[L.rule])
+    ex = excl_contains(skeys, tidx, nt, rkeys, pmax, n_r, ((uint64_t)L.file << 32) | (L.rule + 1), L.start, L.end);
+  keep[i] = !ex;
 }
 
 // (file, start) sort keys of the kept locations
@@ -3511,6 +3607,7 @@ struct DevImage {
   // offsets into u32
   uint32_t o_gpath = 0, n_gpath = 0, o_apoff = 0, o_ap = 0, o_full = 0, n_full = 0, o_prules = 0, n_prules = 0;
   uint32_t o_fold = 0, n_fold_items = 0;  // k_fold_windows work items
+  uint32_t o_xoff = 0, o_xprog = 0, o_gx = 0, n_gx = 0, max_x = 0;  // exclude blocks (ExclDev)
   void release() {
     big.release();
     inst.release(); classes.release(); ranges.release(); progs.release(); rules.release();
@@ -3560,7 +3657,6 @@ struct tsg_engine {
   bool fast_timed = false;   // ev[10..11] bracket the last k_scan_fast launch
   DBuf<uint8_t> fflags8;     // per-file result flags, u8
   uint32_t num_cus = 0;
-  DBuf<ExclJob> excl_jobs;
   DBuf<ExclRange> excl_out;
   uint32_t vm_threads = 0;
   uint64_t scratch_stride = 0;
@@ -3805,6 +3901,21 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   im.n_prules = (uint32_t)path_rules.size();
   im.o_full = append(full_rules);
   im.n_full = (uint32_t)full_rules.size();
+  {  // exclude blocks: per rule offsets into its regex list, the global list
+    std::vector<uint32_t> xoff, xprog;
+    im.max_x = (uint32_t)rs->global_exclude.size();
+    for (const auto& r : rs->rules) {
+      xoff.push_back((uint32_t)xprog.size());
+      for (int x : r.exclude) xprog.push_back((uint32_t)x);
+      im.max_x = std::max<uint32_t>(im.max_x, (uint32_t)r.exclude.size());
+    }
+    xoff.push_back((uint32_t)xprog.size());
+    std::vector<uint32_t> gx(rs->global_exclude.begin(), rs->global_exclude.end());
+    im.o_xoff = append(xoff);
+    im.o_xprog = append(xprog);
+    im.o_gx = append(gx);
+    im.n_gx = (uint32_t)gx.size();
+  }
   {
     // k_fold_windows items: keywords a fold rune can spell (İ -> i, K -> k in
     // bytes.ToLower) and anchor literals with a case-free k / s ((?i) K, ſ)
@@ -5160,66 +5271,90 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   HIP_TRY(hipEventRecord(e->ev[5], s));
   // ---- 6. exclude blocks (only when the config has any)
   if (n_locs && rs->any_exclude) {
-    std::vector<DevLoc> hl(n_locs);
-    HIP_TRY(hipMemcpyAsync(hl.data(), e->locs.p, n_locs * sizeof(DevLoc), hipMemcpyDeviceToHost, s));
+    // (device-only: the (file, scope) groups, their FindAll ranges and the
+    // containment filter; the host reads two counts)
+    ExclDev X{im.u32.p + im.o_xoff, im.u32.p + im.o_xprog, im.u32.p + im.o_gx, im.n_gx, std::max(1u, im.max_x)};
+    const uint64_t nk = 2 * n_locs;
+    HIP_TRY(e->keys.ensure(nk));
+    HIP_TRY(e->keys2.ensure(nk));
+    HIP_TRY(e->vals.ensure(nk));
+    HIP_TRY(e->vals2.ensure(nk));
+    HIP_TRY(e->job_start.ensure(nk));
+    HIP_TRY(e->flags8.ensure(std::max<uint64_t>(nk, n_locs)));
+    HIP_TRY(e->nsel.ensure(2));
+    hipLaunchKernelGGL(k_excl_keys, dim3((uint32_t)((n_locs + 255) / 256)), dim3(256), 0, s, e->locs.p, n_locs, X,
+                       e->keys.p, e->vals.p);
+    size_t tmp = 0;
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p, (int)nk,
+                                               0, 64, s));
+    HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
+                                               (int)nk, 0, 64, s));
+    hipLaunchKernelGGL(k_excl_uniq, dim3((uint32_t)((nk + 255) / 256)), dim3(256), 0, s, e->keys2.p, nk,
+                       e->flags8.p);
+    HIP_TRY(hipGetLastError());
+    // the groups: indices of the unique sorted keys (tidx = job_start[0, n_tags));
+    // n_tags stays on the device
+    {
+      hipcub::CountingInputIterator<uint32_t> cnt(0);
+      HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tmp, cnt, e->flags8.p, e->job_start.p, e->nsel.p, (int)nk, s));
+      HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+      HIP_TRY(hipcub::DeviceSelect::Flagged(e->cub_tmp.p, tmp, cnt, e->flags8.p, e->job_start.p, e->nsel.p, (int)nk,
+                                            s));
+    }
+    uint64_t cap = std::max<uint64_t>(1 << 16, n_locs);
+    for (int attempt = 0; attempt < 3; ++attempt) {
+      HIP_TRY(e->excl_out.ensure(cap));
+      HIP_TRY(hipMemsetAsync(&e->ctrl.p->excl, 0, 8, s));
+      const uint32_t blocks = std::min<uint32_t>((uint32_t)((nk * X.max_x + 255) / 256), e->vm_threads / 256);
+      hipLaunchKernelGGL(k_exclude_tags, dim3(std::max(1u, blocks)), dim3(256), 0, s, d_data, d_off, RS, X,
+                         (const uint64_t*)e->keys2.p, (const uint32_t*)e->job_start.p, (const uint32_t*)e->nsel.p,
+                         e->excl_out.p, (uint64_t)e->excl_out.n, e->ctrl.p, e->scratch.p, e->scratch_stride);
+      HIP_TRY(hipGetLastError());
+      if ((rc = read_ctrl(e, &c))) return rc;
+      if (c.excl <= e->excl_out.n) break;
+      if (attempt == 2) {
+        set_last_error("internal: exclude-block buffers still overflowed after regrowing them");
+        return TSG_ERR_INTERNAL;
+      }
+      cap = c.excl;
+    }
+    const uint64_t n_r = c.excl;
+    // ranges sorted by (group, start), running max of the ends per group
+    HIP_TRY(e->f_iv.ensure(n_r + 1));     // keys
+    HIP_TRY(e->f_lkey2.ensure(n_r + 1));  // sorted keys
+    HIP_TRY(e->f_ssrc.ensure(n_r + 1));   // running max of the ends
+    HIP_TRY(e->f_lslot.ensure(n_r + 1));  // range index
+    HIP_TRY(e->f_lslot2.ensure(n_r + 1)); // ... in sorted order
+    if (n_r) {
+      hipLaunchKernelGGL(k_excl_rkeys, dim3((uint32_t)((n_r + 255) / 256)), dim3(256), 0, s, e->excl_out.p, n_r,
+                         e->f_iv.p, e->f_lslot.p);
+      HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, e->f_iv.p, e->f_lkey2.p, e->f_lslot.p, e->f_lslot2.p,
+                                                 (int)n_r, 0, 64, s));
+      HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+      HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp, e->f_iv.p, e->f_lkey2.p, e->f_lslot.p,
+                                                 e->f_lslot2.p, (int)n_r, 0, 64, s));
+      hipLaunchKernelGGL(k_excl_pmax, dim3((uint32_t)((n_r + 255) / 256)), dim3(256), 0, s, e->f_lkey2.p,
+                         e->f_lslot2.p, e->excl_out.p, e->f_ssrc.p, n_r);
+    }
+    hipLaunchKernelGGL(k_excl_filter, dim3((uint32_t)((n_locs + 255) / 256)), dim3(256), 0, s, e->locs.p, n_locs,
+                       X, (const uint64_t*)e->keys2.p, (const uint32_t*)e->job_start.p, (const uint32_t*)e->nsel.p,
+                       e->f_lkey2.p, e->f_ssrc.p, n_r, e->flags8.p);
+    HIP_TRY(hipGetLastError());
+    // the kept locations, compacted in order (a non-participating group never
+    // reaches censoring in Go if excluded)
+    HIP_TRY(e->locs2.ensure(n_locs));
+    HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tmp, e->locs.p, e->flags8.p, e->locs2.p, e->nsel.p + 1,
+                                          (int)n_locs, s));
+    HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+    HIP_TRY(hipcub::DeviceSelect::Flagged(e->cub_tmp.p, tmp, e->locs.p, e->flags8.p, e->locs2.p, e->nsel.p + 1,
+                                          (int)n_locs, s));
+    uint32_t kept = 0;
+    HIP_TRY(hipMemcpyAsync(&kept, e->nsel.p + 1, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    // tags: (file, 0) = global block, (file, rule+1) = that rule's block
-    std::map<std::pair<uint32_t, uint32_t>, uint32_t> tag_of;
-    std::vector<ExclJob> jobs;
-    for (auto& L : hl) {
-      auto add_scope = [&](uint32_t scope, const std::vector<int>& progs) {
-        auto key = std::make_pair(L.file, scope);
-        if (progs.empty() || tag_of.count(key)) return;
-        uint32_t tag = (uint32_t)tag_of.size();
-        tag_of[key] = tag;
-        for (int p : progs) jobs.push_back(ExclJob{L.file, (uint32_t)p, tag, 0});
-      };
-      add_scope(0, rs->global_exclude);
-      add_scope(L.rule + 1, rs->rules[L.rule].exclude);
-    }
-    std::vector<ExclRange> ranges;
-    if (!jobs.empty()) {
-      HIP_TRY(e->excl_jobs.ensure(jobs.size()));
-      HIP_TRY(hipMemcpyAsync(e->excl_jobs.p, jobs.data(), jobs.size() * sizeof(ExclJob), hipMemcpyHostToDevice, s));
-      uint64_t cap = 1 << 16;
-      for (int attempt = 0; attempt < 3; ++attempt) {
-        HIP_TRY(e->excl_out.ensure(cap));
-        HIP_TRY(hipMemsetAsync(&e->ctrl.p->excl, 0, 8, s));
-        uint32_t blocks = std::min<uint32_t>(((uint32_t)jobs.size() + 255) / 256, e->vm_threads / 256);
-        hipLaunchKernelGGL(k_exclude, dim3(std::max(1u, blocks)), dim3(256), 0, s, d_data, d_off, RS,
-                           e->excl_jobs.p, (uint32_t)jobs.size(), e->excl_out.p, (uint64_t)e->excl_out.n,
-                           e->ctrl.p, e->scratch.p, e->scratch_stride);
-        HIP_TRY(hipGetLastError());
-        if ((rc = read_ctrl(e, &c))) return rc;
-        if (c.excl <= e->excl_out.n) break;
-        if (attempt == 2) {
-          set_last_error("internal: exclude-block buffers still overflowed after regrowing them");
-          return TSG_ERR_INTERNAL;
-        }
-        cap = c.excl;
-      }
-      ranges.resize(c.excl);
-      if (c.excl)
-        HIP_TRY(hipMemcpy(ranges.data(), e->excl_out.p, c.excl * sizeof(ExclRange), hipMemcpyDeviceToHost));
-    }
-    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> by_tag(tag_of.size());
-    for (auto& rg : ranges) by_tag[rg.tag].push_back({rg.s, rg.e});
-    std::vector<DevLoc> kept;
-    for (auto& L : hl) {
-      bool excluded = false;
-      for (uint32_t scope : {0u, L.rule + 1}) {
-        auto it = tag_of.find({L.file, scope});
-        if (it == tag_of.end()) continue;
-        for (auto& pr : by_tag[it->second])
-          if (pr.first <= L.start && L.end <= pr.second) excluded = true;
-      }
-      // a non-participating group never reaches censoring in Go if excluded
-      if (!excluded) kept.push_back(L);
-    }
-    hl.swap(kept);
-    n_locs = hl.size();
+    n_locs = kept;
     if (n_locs)
-      HIP_TRY(hipMemcpyAsync(e->locs.p, hl.data(), n_locs * sizeof(DevLoc), hipMemcpyHostToDevice, s));
+      HIP_TRY(hipMemcpyAsync(e->locs.p, e->locs2.p, n_locs * sizeof(DevLoc), hipMemcpyDeviceToDevice, s));
   }
   HIP_TRY(hipEventRecord(e->ev[6], s));
   // ---- 7. line numbers
@@ -5388,7 +5523,7 @@ void tsg_engine_free(tsg_engine* e) {
   e->file_kw.release(); e->file_flags.release(); e->path_mask.release(); e->hits.release();
   e->keys.release(); e->keys2.release(); e->vals.release(); e->vals2.release(); e->flags8.release();
   e->job_start.release(); e->nsel.release(); e->cub_tmp.release(); e->locs.release(); e->locs2.release();
-  e->scratch.release(); e->ctrl.release(); e->excl_jobs.release(); e->excl_out.release();
+  e->scratch.release(); e->ctrl.release(); e->excl_out.release();
   e->nl_blocks.release(); e->nl_pre.release(); e->tail.release(); e->region_file.release(); e->region_tmp.release();
   e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->fold_pos.release(); e->caps.release(); e->caps_big.release();
   e->job_fms.release(); e->job_lme.release(); e->job_bad.release(); e->redo.release(); e->vprof.release(); e->fflags8.release();
