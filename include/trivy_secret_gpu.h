@@ -141,6 +141,16 @@ int tsg_ruleset_rule_prog(const tsg_ruleset* rs, size_t i, uint32_t* n_inst, uin
  * match [ms, me) is [ms + *pre, me - *suf), *len filling a side that is -1
  * (k_verify then skips the capture search); *valid = 0: the search decides. */
 int tsg_ruleset_group_span(const tsg_ruleset* rs, size_t i, int* valid, int* pre, int* len, int* suf);
+/* Byte-run secret-group rule of rule i, used when tsg_ruleset_group_span is
+ * not valid (diagnostics / tests): on an ASCII match [ms, me) the group ends
+ * where the trailing run of s_alpha bytes begins and starts *len bytes before
+ * that (a group of fixed length) or, with *len == -1, where the run of b_alpha
+ * bytes before its end begins (never below ms).  s_alpha / b_alpha: 4 u32
+ * words each (bit b = ASCII byte b).  Replaces the capture search of
+ * getMatchSubgroupsLocations (pkg/fanal/secret/scanner.go:150-163) for such
+ * rules. */
+int tsg_ruleset_group_run(const tsg_ruleset* rs, size_t i, int* valid, int* len, uint32_t* s_alpha,
+                          uint32_t* b_alpha);
 
 /* Candidate filter of rule i, run on host text from anchor position h:
  * *accept = 0 only when no match of the rule can contain an anchor hit at h

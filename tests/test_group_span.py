@@ -101,3 +101,103 @@ def test_group_span_analysis(regex, want):
             t = "".join(rng.choice("abcxy0123 ks") for _ in range(rng.randint(0, 40))).encode()
             for m in rx.find_all_submatch_index(t):
                 assert (m[2], m[3]) == _derive(want, m[0], m[1])
+
+
+# --- byte runs (gre::group_run): groups between variable-length parts --------
+
+def _run_rule(sc, i):
+    v, ln = ctypes.c_int(), ctypes.c_int()
+    sa = (ctypes.c_uint32 * 4)()
+    ba = (ctypes.c_uint32 * 4)()
+    N.check(N.lib.tsg_ruleset_group_run(sc._rs.handle, i, ctypes.byref(v), ctypes.byref(ln), sa, ba))
+    return v.value, list(sa), list(ba), ln.value
+
+
+def _derive_run(rr, t, ms, me):
+    _, sa, ba, ln = rr
+    inn = lambda m, c: (m[c >> 5] >> (c & 31)) & 1  # noqa: E731
+    ge = me
+    while ge > ms and inn(sa, t[ge - 1]):
+        ge -= 1
+    if ln >= 0:
+        return ge - ln, ge
+    gs = ge
+    while gs > ms and inn(ba, t[gs - 1]):
+        gs -= 1
+    return gs, ge
+
+
+def _check_run_rules(sc, texts, min_checked):
+    accepted, checked, seen = 0, 0, set()
+    for i, r in enumerate(sc.rules):
+        if not r.secret_group_name or _span(sc, i)[0]:
+            continue
+        rr = _run_rule(sc, i)
+        if not rr[0]:
+            continue
+        accepted += 1
+        rx = O.GoRegexp(r.regex)
+        g = rx.subexp_names().index(r.secret_group_name)
+        for t in texts:
+            for m in rx.find_all_submatch_index(t):
+                ms, me = m[0], m[1]
+                if any(b >= 0x80 for b in t[ms:me]):
+                    continue
+                assert (m[2 * g], m[2 * g + 1]) == _derive_run(rr, t, ms, me), (r.id, t[ms:me])
+                checked += 1
+                seen.add(r.id)
+    assert checked >= min_checked, (accepted, checked)
+    return accepted, seen
+
+
+def test_builtin_group_runs_equal_oracle_captures():
+    """aws-secret-access-key (an optional quote, [.,] and a whitespace run
+    after the secret) and every other builtin group rule the span shortcut
+    refuses but the run analysis accepts."""
+    sc = S.new_scanner(None)
+    accepted, seen = _check_run_rules(sc, _texts(777), 50)
+    assert "aws-secret-access-key" in seen
+    assert len(seen) == accepted
+
+
+def test_stress_group_runs_equal_oracle_captures():
+    """The configs[4] gitleaks-shaped rules: keyword, separator class {0,20},
+    quote runs, operator, quote-or-space {0,5}, the secret, a terminator or $."""
+    from tests import stress_rules
+    rules = stress_rules.make_rules(20261019, 120)
+    custom = [S.Rule(id=r["id"], regex=r["regex"], keywords=r.get("keywords", []),
+                     secret_group_name=r.get("secret-group-name", "")) for r, _ in rules]
+    sc = S.new_scanner(S.Config(enable_builtin_rule_ids=["__none__"], custom_rules=custom))
+    rng = random.Random(5)
+    texts = []
+    gens = [g for _, g in rules if g is not None]
+    for _ in range(300):
+        parts = [rng.choice(gens)(rng) for _ in range(rng.randint(1, 6))]
+        texts.append((rng.choice(["", " ", "\n", "x=", "'"]).join(parts) + rng.choice(["", "\n", " ", ";"])).encode())
+    accepted, seen = _check_run_rules(sc, texts, 300)
+    fam = [r["id"] for i, (r, _) in enumerate(rules) if i % 10 in (0, 1, 2, 3)]
+    assert accepted >= len(fam) * 0.9, (accepted, len(fam))
+
+
+@pytest.mark.parametrize("regex,valid", [
+    (r"k[a-z ]{0,5}=\s*['\"]?(?P<secret>[0-9a-f]{8,40})['\"]?(\s|$)", 1),
+    (r"k *=(?P<secret>[0-9a-z]+)[a-z]*", 0),        # the tail can eat the secret's bytes
+    (r"k[0-9]*(?P<secret>[0-9]+)x+", 0),            # the head can end in the secret's bytes
+    (r"k *=(?P<secret>[0-9]*)x+", 0),               # the group may be empty
+    (r"k *=(?P<secret>[0-9a-f]{12})['\"]?;*", 1),   # fixed length: only the end needs the runs
+    (r"(?:k=(?P<secret>[0-9]+);)+", 0),             # the group repeats
+])
+def test_group_run_analysis(regex, valid):
+    cfg = S.Config(enable_builtin_rule_ids=["__none__"],
+                   custom_rules=[S.Rule(id="r", regex=regex, keywords=[], secret_group_name="secret")])
+    sc = S.new_scanner(cfg)
+    assert _span(sc, 0)[0] == 0
+    rr = _run_rule(sc, 0)
+    assert rr[0] == valid
+    if valid:
+        rx = O.GoRegexp(regex)
+        rng = random.Random(2)
+        for _ in range(400):
+            t = "".join(rng.choice("k= '\"0123abcf9x") for _ in range(rng.randint(0, 60))).encode()
+            for m in rx.find_all_submatch_index(t):
+                assert (m[2], m[3]) == _derive_run(rr, t, m[0], m[1])

@@ -10,7 +10,7 @@ With W GPUs the parts run concurrently, so the split step is projected as
 max(part) + merge (+ the part blobs' transfer: KiB); the merge's findings are
 checked equal to the whole-file scan's.  Prints one JSON line.
 
-  python tools/split_bench.py --gb 2 --parts 2 4 8
+  python tools/split_bench.py --gb 5 --parts 2 4 8
 """
 import argparse
 import ctypes
@@ -26,7 +26,7 @@ import numpy as np  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gb", type=float, default=2.0)  # the match search covers files below 2 GiB
+    ap.add_argument("--gb", type=float, default=5.0)
     ap.add_argument("--parts", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
@@ -35,7 +35,7 @@ def main():
     import trivy_amd._native as N
     import trivy_amd.secret as S
     dev = torch.device("cuda", 0)
-    size = min(int(a.gb * 1e9), 2 ** 31 - 1)
+    size = int(a.gb * 1e9)
     chunk = N.gen.tsg_gen_chunk_bytes()
     nch = (size + chunk - 1) // chunk
     ids = np.arange(nch, dtype=np.uint64)  # file 0, chunk k

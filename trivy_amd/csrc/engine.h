@@ -63,6 +63,12 @@ struct RuleDev {
   // side; grp_fast = 0 -> the capture search (k_captures)
   uint32_t grp_fast;
   int32_t grp_pre, grp_len, grp_suf;
+  // else, by byte runs (gre::group_run; one group, ASCII matches): ge = me
+  // minus the run of grp_s bytes ending at me, gs = ge minus the run of grp_b
+  // bytes ending at ge; grp_run = 0 -> the capture search
+  uint32_t grp_run;
+  int32_t grp_run_len;  // >= 0: a group of fixed length (gs = ge - len)
+  uint32_t grp_s[4], grp_b[4];
   uint32_t id_rank;  // position of the rule ID in sorted (ID, index) order: findings sort (scanner.go:441-446)
   uint32_t no_nl;    // no instruction of the program consumes '\n': every match lies inside one line
   uint32_t nfa_off;  // bit-parallel NFA (nfa.cpp): byte offset of its NfaDev record (kNoFollow = none)
@@ -239,6 +245,7 @@ struct RuleHost {
   NfaHost nfa;       // MODE_ANCHORED without a verify DFA
   bool gate_implied = false;  // every anchor literal contains one of the keywords
   gre::GroupSpan grp;         // secret-group span rule (valid: k_verify skips the capture search)
+  gre::GroupRun grun;         // else the byte-run rule (valid: likewise)
   bool fold_gate = false;     // an anchor literal has a case-free k / s: K/ſ spellings of it
                               // (k_fold_windows) are gated exactly, so its keyword bits are kept
 };

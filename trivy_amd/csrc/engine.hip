@@ -71,9 +71,10 @@ constexpr int kKeyPosBits = 40;
 constexpr uint64_t kKeyPosMask = (1ull << kKeyPosBits) - 1;
 constexpr uint64_t kMaxFileBytes = 1ull << kKeyPosBits;
 constexpr uint64_t kMaxBatchFiles = 1ull << (64 - kKeyPosBits);
-// The match search runs on 32-bit file-relative positions (verify DFA, Pike
-// VM) and signed 32-bit capture slots (backtracker): a file longer than this
-// is rejected with TSG_ERR_UNSUPPORTED by every entry point that verifies.
+// The match search runs on 32-bit file-relative positions (verify DFA, NFA
+// walk, Pike VM) with signed 32-bit capture slots for files up to this length;
+// the jobs of longer files run the same kernels instantiated on 64-bit
+// positions and slots (a second launch, only when the batch holds such a file).
 constexpr uint64_t kMaxVerifyFile = 0x7FFFFFFFull;
 
 // k_scan geometry: 256 threads = 4 waves; each lane owns a 128-byte chunk,
@@ -1523,20 +1524,22 @@ __device__ inline gre::VmScratch make_scratch(uint8_t* base, const RuleSetDev& r
   sc.sparse[1] = (uint16_t*)take(2ull * P);
   sc.dense[0] = (uint16_t*)take(2ull * P);
   sc.dense[1] = (uint16_t*)take(2ull * P);
-  sc.start[0] = (uint32_t*)take(4ull * P);
-  sc.start[1] = (uint32_t*)take(4ull * P);
+  // position / capture-slot arrays sized for the 64-bit instantiation (files
+  // of 4 GiB and more); the 32-bit one uses the first half of each
+  sc.start[0] = take(8ull * P);
+  sc.start[1] = take(8ull * P);
   sc.stack = (uint16_t*)take(2ull * (P + 1));
-  sc.cur = (int32_t*)take(4ull * ncap);
-  sc.capstack = (int32_t*)take(8ull * (P + 1));
-  sc.caps[0] = (int32_t*)take(4ull * PC * ncap);  // capture VM runs only group rules
-  sc.caps[1] = (int32_t*)take(4ull * PC * ncap);
+  sc.cur = take(8ull * ncap);
+  sc.capstack = take(16ull * (P + 1));
+  sc.caps[0] = take(8ull * PC * ncap);  // capture VM runs only group rules
+  sc.caps[1] = take(8ull * PC * ncap);
   return sc;
 }
 
 __host__ inline uint64_t scratch_bytes(uint32_t P, uint32_t ncap, uint32_t PC) {
   auto r = [](uint64_t b) { return (b + 15) & ~15ull; };
-  return r(2ull * P) * 4 + r(4ull * P) * 2 + r(2ull * (P + 1)) + r(4ull * ncap) + r(8ull * (P + 1)) +
-         r(4ull * PC * ncap) * 2 + 256;
+  return r(2ull * P) * 4 + r(8ull * P) * 2 + r(2ull * (P + 1)) + r(8ull * ncap) + r(16ull * (P + 1)) +
+         r(8ull * PC * ncap) * 2 + 256;
 }
 
 __device__ inline bool match_string(const gre::ProgView& pv, const uint8_t* s, uint32_t n,
@@ -1944,37 +1947,39 @@ struct VerifyParams {
 
 // Candidate start windows of one (file, rule) job, in increasing order
 // (DESIGN.md "anchor windows").
+// (Pos: uint32_t, or uint64_t for the jobs of files of 4 GiB and more)
+template <class Pos>
 struct IvIter {
   const uint64_t* keys;
   uint64_t ci, c1;
   uint64_t fstart;
   const uint8_t* text;
-  uint32_t n;
+  Pos n;
   uint32_t a, b;
   const uint64_t* alpha;
-  uint32_t h_prev, p_prev;
+  Pos h_prev, p_prev;
   bool have_prev;
   // current merged view
   bool have;
-  uint32_t cs, ce;
+  Pos cs, ce;
 
   __device__ bool in_alpha(uint8_t c) const { return (alpha[c >> 6] >> (c & 63)) & 1; }
 
-  __device__ bool next_raw(uint32_t* ws, uint32_t* we) {
+  __device__ bool next_raw(Pos* ws, Pos* we) {
     while (ci < c1) {
-      const uint32_t h = (uint32_t)((keys[ci++] & kPosMask) - fstart);
+      const Pos h = (Pos)((keys[ci++] & kPosMask) - fstart);
       if (h < a) continue;
-      const uint32_t lo = (b == gre::kInf || h < b) ? 0u : h - b;
+      const Pos lo = (b == gre::kInf || h < b) ? (Pos)0 : h - b;
       // window start: the alpha run before h, never walked below lo = h - b
       // (a run reaching the previous hit joins that hit's window).  Walking to
       // the previous hit when it lies below lo re-read whole minified lines.
-      uint32_t p;
+      Pos p;
       if (have_prev && h_prev <= h && h_prev >= lo) {
-        uint32_t q = h;
+        Pos q = h;
         while (q > h_prev && in_alpha(text[q - 1])) --q;
         p = (q == h_prev) ? (p_prev > lo ? p_prev : lo) : q;
       } else {
-        uint32_t q = h;
+        Pos q = h;
         while (q > lo && in_alpha(text[q - 1])) --q;
         p = q;
       }
@@ -1982,7 +1987,7 @@ struct IvIter {
       have_prev = true;
       h_prev = h;
       p_prev = p;
-      const uint32_t wend = h - a;
+      const Pos wend = h - a;
       while (p <= wend && !gre::is_rune_start(text, n, p)) ++p;
       if (p > wend) continue;
       *ws = p;
@@ -1993,59 +1998,61 @@ struct IvIter {
   }
   __device__ void advance() { have = next_raw(&cs, &ce); }
   // Start-permission protocol used by vm_search_starts.
-  __device__ bool skip_to(uint32_t pos, uint32_t* np) {
+  __device__ bool skip_to(Pos pos, Pos* np) {
     while (have && ce < pos) advance();
     if (!have) return false;
     *np = pos < cs ? cs : pos;
     return true;
   }
-  __device__ bool allowed(uint32_t pos) {
+  __device__ bool allowed(Pos pos) {
     while (have && ce < pos) advance();
     return have && cs <= pos && pos <= ce;
   }
 };
 
 // Exactly one permitted start: an anchored leftmost-first match at s.
+template <class Pos>
 struct OneStart {
-  uint32_t s;
-  __device__ bool skip_to(uint32_t pos, uint32_t* np) {
+  Pos s;
+  __device__ bool skip_to(Pos pos, Pos* np) {
     if (pos > s) return false;
     *np = s;
     return true;
   }
-  __device__ bool allowed(uint32_t pos) { return pos == s; }
+  __device__ bool allowed(Pos pos) { return pos == s; }
 };
 
+template <class Pos>
 struct LimitStarts {
-  uint32_t limit;
-  __device__ bool skip_to(uint32_t pos, uint32_t* np) {
+  Pos limit;
+  __device__ bool skip_to(Pos pos, Pos* np) {
     if (pos > limit) return false;
     *np = pos;
     return true;
   }
-  __device__ bool allowed(uint32_t pos) { return pos <= limit; }
+  __device__ bool allowed(Pos pos) { return pos <= limit; }
 };
 
 // vm_search with a start-position oracle (anchor windows or a plain limit);
 // when no thread is alive the VM jumps to the next permitted start.
-template <class Starts>
-__device__ bool vm_search_starts(const gre::ProgView& p, const uint8_t* text, uint32_t n, uint32_t pos0,
-                                 Starts& S, gre::VmScratch& sc, uint32_t* ms, uint32_t* me) {
-  gre::Queue q[2] = {{sc.sparse[0], sc.dense[0], sc.start[0], nullptr, 0},
-                     {sc.sparse[1], sc.dense[1], sc.start[1], nullptr, 0}};
+template <class Pos, class Starts>
+__device__ bool vm_search_starts(const gre::ProgView& p, const uint8_t* text, Pos n, Pos pos0,
+                                 Starts& S, gre::VmScratch& sc, Pos* ms, Pos* me) {
+  gre::Queue<Pos> q[2] = {{sc.sparse[0], sc.dense[0], (Pos*)sc.start[0], nullptr, 0},
+                          {sc.sparse[1], sc.dense[1], (Pos*)sc.start[1], nullptr, 0}};
   int cur = 0;
   bool matched = false;
-  uint32_t pos = pos0;
+  Pos pos = pos0;
   uint32_t w = 0, w1 = 0;
   int r = gre::decode_rune(text, n, pos, &w);
   int r1 = r >= 0 ? gre::decode_rune(text, n, pos + w, &w1) : -1;
   uint8_t ctx = gre::empty_ctx(gre::prev_ctx_rune(text, pos), r);
   for (;;) {
-    gre::Queue& runq = q[cur];
-    gre::Queue& nextq = q[cur ^ 1];
+    gre::Queue<Pos>& runq = q[cur];
+    gre::Queue<Pos>& nextq = q[cur ^ 1];
     if (runq.n == 0) {
       if (matched) break;
-      uint32_t np;
+      Pos np;
       if (!S.skip_to(pos, &np)) break;
       if (np != pos) {
         pos = np;
@@ -2092,8 +2099,8 @@ struct DfaRef {
 
 
 // kLds: d.T / d.cls are the block's LDS copy (k_verify stages the wave's rule).
-template <bool kLds>
-__device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, uint32_t n, uint32_t s, uint32_t* me,
+template <bool kLds, class Pos>
+__device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, Pos n, Pos s, Pos* me,
                                        uint32_t* steps) {
   typedef __attribute__((address_space(3))) const uint16_t lu16;
   typedef __attribute__((address_space(3))) const uint8_t lu8;
@@ -2108,7 +2115,7 @@ __device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, uint
   // step cost a TLB lookup per lane per byte; the batch is padded past its
   // end, so a block holding a content byte never leaves the allocation)
   const uintptr_t base = reinterpret_cast<uintptr_t>(text);
-  uint32_t q = s;
+  Pos q = s;
   while (q < n && st) {
     const uintptr_t addr = (base + q) & ~(uintptr_t)15;
     const u32x4 v = *as_global<__attribute__((address_space(1))) const u32x4>(reinterpret_cast<const void*>(addr));
@@ -2142,7 +2149,7 @@ __device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, uint
     }
   }
   if (last < 0) return 0;
-  *me = (uint32_t)last;
+  *me = (Pos)last;
   return 1;
 }
 
@@ -2159,19 +2166,32 @@ constexpr uint32_t kBsWords = 560;        // k_verify: LDS words per lane (140 K
 constexpr uint32_t kCapActive = 8;        // k_captures: searching lanes per 64-lane block (8 blocks per CU)
 constexpr uint32_t kBigBsWords = 9216;    // and their arenas (36 KiB: P x W <= 294 K (pc, pos) bits)
 
-__device__ bool bitstate_captures(const gre::ProgView& p, const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me,
-                                  const uint32_t* gnum, uint32_t ng, uint32_t* area, uint32_t words, int32_t* gcap) {
+// Slots: the tracked capture slots' type (int32_t, int64_t for files of 4 GiB
+// and more); they take the arena's last kSlotWords words.
+template <class Pos>
+struct CapSlots {
+  typedef typename gre::SlotOf<Pos>::type Slot;
+  static constexpr uint32_t kWords = 8 * sizeof(Slot) / 4;
+};
+
+template <class Pos>
+__device__ bool bitstate_captures(const gre::ProgView& p, const uint8_t* text, Pos n, Pos ms, Pos me,
+                                  const uint32_t* gnum, uint32_t ng, uint32_t* area, uint32_t words,
+                                  typename gre::SlotOf<Pos>::type* gcap) {
+  typedef typename gre::SlotOf<Pos>::type Slot;
+  constexpr uint32_t kSlotWords = CapSlots<Pos>::kWords;
   // visited rows for the join points only (Inst::vis); a path that consumes
   // past me can never end at me, so positions stay in [ms, me]
   const uint32_t P = p.nvis;
-  const uint32_t end = me;
-  const uint32_t W = end - ms + 1;
+  const Pos end = me;
+  if (end - ms + 1 >= 0xFFFF) return false;
+  const uint32_t W = (uint32_t)(end - ms + 1);
   const uint32_t vis_words = (P * W + 31) / 32;
-  // arena: visited bits | job stack | the 8 tracked capture slots (gcap, the last 8 words)
-  if (2 * ng > 8 || P >= 0x4000 || W >= 0xFFFF || vis_words + 8 + 32 > words) return false;
+  // arena: visited bits | job stack | the 8 tracked capture slots (gcap, the last words)
+  if (2 * ng > 8 || P >= 0x4000 || vis_words + kSlotWords + 32 > words) return false;
   uint32_t* vis = area;
   uint32_t* stk = area + vis_words;
-  const uint32_t stk_cap = words - 8 - vis_words;
+  const uint32_t stk_cap = words - kSlotWords - vis_words;
   for (uint32_t i = 0; i < vis_words; ++i) vis[i] = 0;
   for (uint32_t k = 0; k < 2 * ng; ++k) gcap[k] = -1;
   auto local = [&](uint32_t slot) -> int {  // tracked index of capture slot, or -1
@@ -2186,22 +2206,22 @@ __device__ bool bitstate_captures(const gre::ProgView& p, const uint8_t* text, u
     const uint32_t kind = j >> 30, pc0 = (j >> 16) & 0x3FFFu, v = j & 0xFFFFu;
     if (kind == 2) {  // capture restore
       const int l = local(p.inst[pc0].arg);
-      if (l >= 0) gcap[l] = v == 0xFFFFu ? -1 : (int32_t)(ms + v);
+      if (l >= 0) gcap[l] = v == 0xFFFFu ? (Slot)-1 : (Slot)(ms + v);
       continue;
     }
-    uint32_t pos = ms + v;
+    Pos pos = ms + v;
     uint32_t pc = kind == 1 ? p.inst[pc0].arg : pc0;  // ALT: the second branch
     for (;;) {
       if (pc == 0 || pos > end) break;
       const gre::Inst in = p.inst[pc];
       if (in.vis != gre::kNoVis) {
-        const uint32_t bit = in.vis * W + (pos - ms);
+        const uint32_t bit = in.vis * W + (uint32_t)(pos - ms);
         if (vis[bit >> 5] & (1u << (bit & 31))) break;
         vis[bit >> 5] |= 1u << (bit & 31);
       }
       if (in.op == gre::I_ALT) {
         if (sp >= stk_cap) return false;
-        stk[sp++] = (1u << 30) | (pc << 16) | (pos - ms);
+        stk[sp++] = (1u << 30) | (pc << 16) | (uint32_t)(pos - ms);
         pc = in.out;
         continue;
       }
@@ -2209,9 +2229,9 @@ __device__ bool bitstate_captures(const gre::ProgView& p, const uint8_t* text, u
         const int l = local(in.arg);
         if (l >= 0) {
           if (sp >= stk_cap) return false;
-          const int32_t old = gcap[l];
-          stk[sp++] = (2u << 30) | (pc << 16) | (old < 0 ? 0xFFFFu : (uint32_t)(old - (int32_t)ms));
-          gcap[l] = (int32_t)pos;
+          const Slot old = gcap[l];
+          stk[sp++] = (2u << 30) | (pc << 16) | (old < 0 ? 0xFFFFu : (uint32_t)(old - (Slot)ms));
+          gcap[l] = (Slot)pos;
         }
         pc = in.out;
         continue;
@@ -2243,14 +2263,16 @@ __device__ bool bitstate_captures(const gre::ProgView& p, const uint8_t* text, u
 // of `words` words; a match too long for it goes on to the next stage's list
 // (`next`, k_captures -> k_captures_big), and only past the last arena does
 // the capture VM run.
+template <class Pos>
 __device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t rule, uint32_t fi, uint32_t job,
-                            const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me, gre::VmScratch& sc,
+                            const uint8_t* text, Pos n, Pos ms, Pos me, gre::VmScratch& sc,
                             uint32_t* bs_area, uint32_t words, CapJob* next, uint64_t next_cap,
                             unsigned long long* next_n) {
+  typedef typename gre::SlotOf<Pos>::type Slot;
   const gre::ProgView& pv = V.rs.progs[rd.prog];
   const uint32_t* gnum = V.rs.group_slots + rd.group_off;
-  int32_t* gcap = (int32_t*)(bs_area + words - 8);  // tracked slots (the arena's last 8 words)
-  const bool bs_ok = bitstate_captures(pv, text, n, ms, me, gnum, rd.group_n, bs_area, words, gcap);
+  Slot* gcap = (Slot*)(bs_area + words - CapSlots<Pos>::kWords);  // tracked slots (the arena's last words)
+  const bool bs_ok = bitstate_captures<Pos>(pv, text, n, ms, me, gnum, rd.group_n, bs_area, words, gcap);
   if (!bs_ok && next) {
     const unsigned long long idx = atomicAdd(next_n, 1ull);
     if (idx < next_cap) next[idx] = CapJob{fi, rule, job, 0, ms, me};
@@ -2258,7 +2280,7 @@ __device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t r
   }
   if (bs_ok) {
     for (uint32_t g = 0; g < rd.group_n; ++g) {
-      const int32_t s = gcap[2 * g], e = gcap[2 * g + 1];
+      const Slot s = gcap[2 * g], e = gcap[2 * g + 1];
       unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
       if (idx < V.loc_cap) {
         if (s < 0 || e < 0) V.locs[idx] = DevLoc{fi, rule, 0, 0, 0, 0, 1, job};
@@ -2267,12 +2289,12 @@ __device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t r
     }
     return;
   }
-  int32_t out[kMaxCap];  // ncap <= kMaxCap is enforced by the rule compiler
-  bool ok = gre::vm_captures(pv, text, n, ms, sc, out);
-  if (!ok || (uint32_t)out[1] != me) atomicOr(&V.ctrl->err, 1u);
+  Slot out[kMaxCap];  // ncap <= kMaxCap is enforced by the rule compiler
+  bool ok = gre::vm_captures<Pos>(pv, text, n, ms, sc, out);
+  if (!ok || (Pos)out[1] != me) atomicOr(&V.ctrl->err, 1u);
   for (uint32_t g = 0; g < rd.group_n; ++g) {
     const uint32_t slot = gnum[g];
-    const int32_t s = out[2 * slot], e = out[2 * slot + 1];
+    const Slot s = out[2 * slot], e = out[2 * slot + 1];
     unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
     if (idx < V.loc_cap) {
       if (s < 0 || e < 0) V.locs[idx] = DevLoc{fi, rule, 0, 0, 0, 0, 1, job};
@@ -2284,26 +2306,31 @@ __device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t r
 // A match k_verify found: allow rules, then the whole-match location or, for
 // rules with a secret group, a capture job for k_captures (whose bit-state
 // arenas take LDS that would cap the search at one wave per CU).
+template <class Pos>
 __device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, uint32_t fi, uint32_t job,
-                                        const uint8_t* text, uint32_t n, uint32_t ms, uint32_t me, gre::VmScratch& sc,
+                                        const uint8_t* text, Pos n, Pos ms, Pos me, gre::VmScratch& sc,
                                         uint32_t* tck = nullptr) {
   const uint64_t t0 = tck ? __builtin_amdgcn_s_memrealtime() : 0;
   const RuleDev& rd = V.rs.rules[rule];
+  if (sizeof(Pos) > 4 && me - ms > (Pos)0xFFFFFFFFu) {  // allow regexes run on 32-bit match strings
+    atomicOr(&V.ctrl->err, 2u);
+    return;
+  }
   // AllowLocation (scanner.go:145-148): global then rule allow regexes on the whole match
   for (uint32_t k = 0; k < V.rs.n_global_allow; ++k) {
-    const bool al = match_string_pf(V.rs, V.rs.global_allow[k], text + ms, me - ms, sc);
+    const bool al = match_string_pf(V.rs, V.rs.global_allow[k], text + ms, (uint32_t)(me - ms), sc);
     if (tck) tck[2] += (uint32_t)(__builtin_amdgcn_s_memrealtime() - t0);
     if (al) return;
   }
   const uint32_t allow_off = rd.allow_off, allow_n = rd.allow_n;
   for (uint32_t k = 0; k < allow_n; ++k)
-    if (match_string_pf(V.rs, V.rs.allow_progs[allow_off + k], text + ms, me - ms, sc)) return;
+    if (match_string_pf(V.rs, V.rs.allow_progs[allow_off + k], text + ms, (uint32_t)(me - ms), sc)) return;
   if (!rd.use_groups) {
     unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
     if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, ms, me, 0, 0, 0, job};
     return;
   }
-  if (rd.grp_fast) {  // the group's span follows from [ms, me) on ASCII text (gre::group_span)
+  if (rd.grp_fast || rd.grp_run) {  // the group's span follows from [ms, me) on ASCII text (gre::group_span / group_run)
     // ASCII: the scan's per-4 KiB-span flags, byte by byte only in a flagged span
     bool ascii = true;
     if (V.span_hi && me > ms) {  // (an empty match holds no byte: nothing to check)
@@ -2312,9 +2339,9 @@ __device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, ui
     }
     if (!ascii || (!V.span_hi && me > ms)) {
       ascii = true;
-      for (uint32_t q = ms; q < me && ascii; ++q) ascii = as_global<gu8>(text)[q] < 0x80;
+      for (Pos q = ms; q < me && ascii; ++q) ascii = as_global<gu8>(text)[q] < 0x80;
     }
-    if (ascii) {
+    if (ascii && rd.grp_fast) {
       const int64_t gs = rd.grp_pre >= 0 ? (int64_t)ms + rd.grp_pre : (int64_t)me - rd.grp_suf - rd.grp_len;
       const int64_t ge = rd.grp_suf >= 0 ? (int64_t)me - rd.grp_suf : gs + rd.grp_len;
       if (gs >= (int64_t)ms && gs <= ge && ge <= (int64_t)me) {
@@ -2323,6 +2350,18 @@ __device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, ui
         return;
       }
       // (unreachable for a real match of the rule; the capture search decides)
+    } else if (ascii) {  // byte runs back from the match end (gre::group_run)
+      gu8* t = as_global<gu8>(text);
+      auto in = [](const uint32_t* m, uint32_t c) { return (m[c >> 5] >> (c & 31)) & 1u; };
+      Pos ge = me;
+      while (ge > ms && in(rd.grp_s, t[ge - 1])) --ge;
+      Pos gs = ge;
+      if (rd.grp_run_len >= 0) gs = ge - (Pos)rd.grp_run_len;
+      else
+        while (gs > ms && in(rd.grp_b, t[gs - 1])) --gs;
+      unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
+      if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, (uint64_t)gs, (uint64_t)ge, 0, 0, 0, job};
+      return;
     }
   }
   unsigned long long idx = atomicAdd(&V.ctrl->n_caps, 1ull);
@@ -2335,7 +2374,12 @@ __device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, ui
 // the backtracker's control flow differs per job, so jobs sharing a wave run
 // one after another; few active lanes per wave and many waves per CU keep
 // each wave to about one job and let the CU overlap their load latencies.
-template <uint32_t kLanes, uint32_t kActive, uint32_t kWords, bool kLast>
+// Files of 4 GiB and more: true when the job / location of file fi belongs to
+// the 64-bit instantiation of the search kernels (each kernel is launched
+// twice when the batch holds such a file; every lane skips the other's work).
+__device__ inline bool is_long_file(const uint64_t* off, uint32_t fi) { return off[fi + 1] - 1 - off[fi] > kMaxVerifyFile; }
+
+template <uint32_t kLanes, uint32_t kActive, uint32_t kWords, bool kLast, class Pos>
 __global__ __launch_bounds__(kLanes) void k_captures(VerifyParams V) {
   __shared__ uint32_t bs_lds[kActive * kWords];
   if (threadIdx.x >= kActive) return;
@@ -2352,11 +2396,12 @@ __global__ __launch_bounds__(kLanes) void k_captures(VerifyParams V) {
   for (uint64_t i = blockIdx.x + (uint64_t)threadIdx.x * gridDim.x; i < n_caps; i += nthreads) {
     const CapJob c = list[i];
     if (!(c.job & kJobRedo) && V.job_bad[c.job]) continue;  // a conflicting speculative job's match
+    if (is_long_file(V.off, c.file) != (sizeof(Pos) > 4)) continue;
     const RuleDev rd = V.rs.rules[c.rule];
     const uint64_t fstart = V.off[c.file];
-    const uint32_t n = (uint32_t)(V.off[c.file + 1] - 1 - fstart);
-    emit_groups(V, rd, c.rule, c.file, c.job, V.data + fstart, n, (uint32_t)c.ms, (uint32_t)c.me, sc, bs_area, kWords,
-                kLast ? nullptr : V.caps_big, V.cap_big_cap, &V.ctrl->n_caps_big);
+    const Pos n = (Pos)(V.off[c.file + 1] - 1 - fstart);
+    emit_groups<Pos>(V, rd, c.rule, c.file, c.job, V.data + fstart, n, (Pos)c.ms, (Pos)c.me, sc, bs_area, kWords,
+                     kLast ? nullptr : V.caps_big, V.cap_big_cap, &V.ctrl->n_caps_big);
   }
 }
 
@@ -2398,13 +2443,14 @@ constexpr uint32_t kVerifyBlock = 64;
 constexpr uint32_t kVerifyBlockWide = 256;
 
 // regexp.go allMatches over the whole file (rules without an anchor)
+template <class Pos>
 __device__ __noinline__ void verify_full_job(const VerifyParams& V, uint32_t rule, uint32_t fi, uint32_t job,
-                                             const uint8_t* text, uint32_t n, gre::VmScratch& sc) {
+                                             const uint8_t* text, Pos n, gre::VmScratch& sc) {
   const gre::ProgView& pv = V.rs.progs[V.rs.rules[rule].prog];
-  uint32_t pos = 0, ms, me;
+  Pos pos = 0, ms, me;
   int64_t prev_end = -1;
   while (pos <= n) {
-    LimitStarts ls{n};
+    LimitStarts<Pos> ls{n};
     if (!vm_search_starts(pv, text, n, pos, ls, sc, &ms, &me)) break;
     bool accept = true;
     if (me == pos) {
@@ -2423,14 +2469,17 @@ __device__ __noinline__ void verify_full_job(const VerifyParams& V, uint32_t rul
 // A job's first match start and last match end (every match FindAll took,
 // allow-listed ones included: they move its position all the same), for
 // k_chain_fix; a re-run chain (kJobRedo) records nothing.
-__device__ inline void job_record(const VerifyParams& V, uint32_t job, uint32_t fms, uint32_t lme) {
+// (fms == ~Pos(0): the job found no match)
+template <class Pos>
+__device__ inline void job_record(const VerifyParams& V, uint32_t job, Pos fms, Pos lme) {
   if (job & kJobRedo) return;
-  V.job_fms[job] = fms == 0xFFFFFFFFu ? ~0ull : (uint64_t)fms;
+  V.job_fms[job] = fms == ~(Pos)0 ? ~0ull : (uint64_t)fms;
   V.job_lme[job] = lme;
 }
 
-__device__ inline void iv_init(IvIter& it, const VerifyParams& V, uint32_t rule, uint64_t c0, uint64_t c1,
-                               uint64_t fstart, const uint8_t* text, uint32_t n) {
+template <class Pos>
+__device__ inline void iv_init(IvIter<Pos>& it, const VerifyParams& V, uint32_t rule, uint64_t c0, uint64_t c1,
+                               uint64_t fstart, const uint8_t* text, Pos n) {
   const RuleDev& rd = V.rs.rules[rule];
   it.keys = V.keys;
   it.ci = c0;
@@ -2449,10 +2498,10 @@ __device__ inline void iv_init(IvIter& it, const VerifyParams& V, uint32_t rule,
 // FindAll over the anchor windows with the verify DFA: the first permitted
 // start (>= pos) that matches is Go's leftmost match; a start the DFA cannot
 // decide (byte >= 0x80) is decided by the Pike VM alone, anchored there.
-template <bool kLds>
+template <bool kLds, class Pos>
 __device__ __noinline__ uint32_t verify_dfa_job(const VerifyParams& V, uint32_t rule, uint32_t fi, uint32_t job,
-                                                uint32_t pos0, uint64_t c0, uint64_t c1, uint64_t fstart,
-                                                const uint8_t* text, uint32_t n, gre::VmScratch& sc,
+                                                Pos pos0, uint64_t c0, uint64_t c1, uint64_t fstart,
+                                                const uint8_t* text, Pos n, gre::VmScratch& sc,
                                                 const uint16_t* lds_T, const uint8_t* lds_cls, uint32_t* tck) {
   uint32_t steps = 0;  // DFA transitions taken (diagnostics)
   uint32_t tck_dfa = 0, tck_emit = 0;
@@ -2461,30 +2510,30 @@ __device__ __noinline__ uint32_t verify_dfa_job(const VerifyParams& V, uint32_t 
                     rd.dfa_ncls, rd.dfa_start0, rd.dfa_start1, rd.dfa_smatch, rd.dfa_sym};
   const uint32_t fm0 = rd.dfa_first[0], fm1 = rd.dfa_first[1], fm2 = rd.dfa_first[2], fm3 = rd.dfa_first[3];
   const uint32_t prog = rd.prog;
-  IvIter it;
+  IvIter<Pos> it;
   iv_init(it, V, rule, c0, c1, fstart, text, n);
-  uint32_t pos = pos0, ms, me, fms = 0xFFFFFFFFu, lme = 0;
+  Pos pos = pos0, ms, me, fms = ~(Pos)0, lme = 0;
   while (it.have && it.ce < pos) it.advance();
   while (it.have) {
     bool found = false;
-    const uint32_t s0 = it.cs > pos ? it.cs : pos;
-    for (uint32_t sp = s0; sp <= it.ce && sp < n; ++sp) {
+    const Pos s0 = it.cs > pos ? it.cs : pos;
+    for (Pos sp = s0; sp <= it.ce && sp < n; ++sp) {
       if (!gre::is_rune_start(text, n, sp)) continue;
       const uint32_t b0 = as_global<gu8>(text)[sp];  // first-byte skip (no dependent table loads)
       const uint32_t fw = b0 < 32 ? fm0 : b0 < 64 ? fm1 : b0 < 96 ? fm2 : fm3;
       if (b0 < 0x80 && !((fw >> (b0 & 31)) & 1)) continue;
       const uint64_t ta = tck ? __builtin_amdgcn_s_memrealtime() : 0;
-      int r = dfa_anchored_dev<kLds>(dref, text, n, sp, &me, &steps);
+      int r = dfa_anchored_dev<kLds, Pos>(dref, text, n, sp, &me, &steps);
       if (tck) tck_dfa += (uint32_t)(__builtin_amdgcn_s_memrealtime() - ta);
       if (r == 2) {
-        OneStart one{sp};
-        r = vm_search_starts(V.rs.progs[prog], text, n, sp, one, sc, &ms, &me) ? 1 : 0;
+        OneStart<Pos> one{sp};
+        r = vm_search_starts<Pos>(V.rs.progs[prog], text, n, sp, one, sc, &ms, &me) ? 1 : 0;
       }
       if (r == 1) {
         const uint64_t tb = tck ? __builtin_amdgcn_s_memrealtime() : 0;
-        emit_match(V, rule, fi, job, text, n, sp, me, sc, tck);
+        emit_match<Pos>(V, rule, fi, job, text, n, sp, me, sc, tck);
         if (tck) tck_emit += (uint32_t)(__builtin_amdgcn_s_memrealtime() - tb);
-        if (fms == 0xFFFFFFFFu) fms = sp;
+        if (fms == ~(Pos)0) fms = sp;
         lme = me;
         pos = me;
         found = true;
@@ -2500,17 +2549,18 @@ __device__ __noinline__ uint32_t verify_dfa_job(const VerifyParams& V, uint32_t 
 }
 
 // The same FindAll with the Pike VM (rules without a verify DFA)
+template <class Pos>
 __device__ __noinline__ void verify_vm_job(const VerifyParams& V, uint32_t rule, uint32_t fi, uint32_t job,
-                                           uint32_t pos0, uint64_t c0, uint64_t c1, uint64_t fstart,
-                                           const uint8_t* text, uint32_t n, gre::VmScratch& sc) {
+                                           Pos pos0, uint64_t c0, uint64_t c1, uint64_t fstart,
+                                           const uint8_t* text, Pos n, gre::VmScratch& sc) {
   const gre::ProgView& pv = V.rs.progs[V.rs.rules[rule].prog];
-  IvIter it;
+  IvIter<Pos> it;
   iv_init(it, V, rule, c0, c1, fstart, text, n);
-  uint32_t pos = pos0, ms, me, fms = 0xFFFFFFFFu, lme = 0;
+  Pos pos = pos0, ms, me, fms = ~(Pos)0, lme = 0;
   while (it.have) {
-    if (!vm_search_starts(pv, text, n, pos, it, sc, &ms, &me)) break;
-    emit_match(V, rule, fi, job, text, n, ms, me, sc);
-    if (fms == 0xFFFFFFFFu) fms = ms;
+    if (!vm_search_starts<Pos>(pv, text, n, pos, it, sc, &ms, &me)) break;
+    emit_match<Pos>(V, rule, fi, job, text, n, ms, me, sc);
+    if (fms == ~(Pos)0) fms = ms;
     lme = me;
     if (me == ms) break;  // cannot happen for anchored rules (non-empty literal)
     pos = me;
@@ -2525,7 +2575,8 @@ struct VecText {
   uintptr_t blk;
   u32x4 v;
   __device__ explicit VecText(const uint8_t* b) : base(b), blk(~(uintptr_t)0), v{0, 0, 0, 0} {}
-  __device__ uint32_t operator[](uint32_t i) {
+  template <class Pos>
+  __device__ uint32_t operator[](Pos i) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(base) + i;
     const uintptr_t b = a & ~(uintptr_t)15;
     if (b != blk) {
@@ -2547,42 +2598,42 @@ struct VecText {
 // can have.  A start the walk cannot decide (a byte >= 0x80, two possible
 // ends -- Go's priorities choose -- or a walk past kNfaWalkMax) is decided by
 // the Pike VM anchored there.
-template <bool kWide>
+template <bool kWide, class Pos>
 __device__ __noinline__ uint32_t verify_nfa_job(const VerifyParams& V, uint32_t rule, uint32_t fi, uint32_t job,
-                                                uint32_t pos0, uint64_t c0, uint64_t c1, uint64_t fstart,
-                                                const uint8_t* text, uint32_t n, gre::VmScratch& sc,
+                                                Pos pos0, uint64_t c0, uint64_t c1, uint64_t fstart,
+                                                const uint8_t* text, Pos n, gre::VmScratch& sc,
                                                 const uint8_t* nfa) {
   const NfaDev& N = *(const NfaDev*)nfa;
   const U128* reach = (const U128*)(nfa + N.o_reach);
   const NfaExc* exc = (const NfaExc*)(nfa + N.o_exc);
   const uint32_t prog = V.rs.rules[rule].prog;
   uint32_t steps = 0;
-  IvIter it;
+  IvIter<Pos> it;
   iv_init(it, V, rule, c0, c1, fstart, text, n);
-  uint32_t pos = pos0, ms, me, fms = 0xFFFFFFFFu, lme = 0;
+  Pos pos = pos0, ms, me, fms = ~(Pos)0, lme = 0;
   while (it.have && it.ce < pos) it.advance();
   while (it.have) {
     bool found = false;
-    const uint32_t s0 = it.cs > pos ? it.cs : pos;
-    const uint32_t s1 = it.ce < n ? it.ce : n;
+    const Pos s0 = it.cs > pos ? it.cs : pos;
+    const Pos s1 = it.ce < n ? it.ce : n;
     int any = 0;
     if (s0 <= s1) {
       VecText T(text);
       any = nfa_walk<kWide>(N, reach, exc, T, n, s0, s1, &me, &steps);
     }
-    for (uint32_t sp = s0; any && sp <= s1 && sp < n; ++sp) {
+    for (Pos sp = s0; any && sp <= s1 && sp < n; ++sp) {
       if (!gre::is_rune_start(text, n, sp)) continue;
       const uint32_t b0 = as_global<gu8>(text)[sp];
       if (b0 < 0x80 && !nfa_first_ok(N, reach, b0)) continue;  // first-byte skip
       VecText T(text);
       int r = nfa_walk<kWide>(N, reach, exc, T, n, sp, sp, &me, &steps);
       if (r == 2) {
-        OneStart one{sp};
-        r = vm_search_starts(V.rs.progs[prog], text, n, sp, one, sc, &ms, &me) ? 1 : 0;
+        OneStart<Pos> one{sp};
+        r = vm_search_starts<Pos>(V.rs.progs[prog], text, n, sp, one, sc, &ms, &me) ? 1 : 0;
       }
       if (r == 1) {
-        emit_match(V, rule, fi, job, text, n, sp, me, sc);
-        if (fms == 0xFFFFFFFFu) fms = sp;
+        emit_match<Pos>(V, rule, fi, job, text, n, sp, me, sc);
+        if (fms == ~(Pos)0) fms = sp;
         lme = me;
         pos = me;
         found = true;
@@ -2606,7 +2657,8 @@ constexpr uint32_t kVerifyDfaLds = 64 * 1024;
 // the rule's verify DFA, else its NFA, else the Pike VM; full-scan jobs run
 // the VM over the whole file.  lds_dfa / lds_nfa: the block's staged table
 // when this job's rule is the one staged (else null: global tables).
-__device__ inline uint32_t run_job(const VerifyParams& V, uint32_t job, uint32_t pos0, uint64_t c0, uint64_t c1,
+template <class Pos>
+__device__ inline uint32_t run_job(const VerifyParams& V, uint32_t job, Pos pos0, uint64_t c0, uint64_t c1,
                                    gre::VmScratch& sc, const uint16_t* lds_dfa, const uint8_t* lds_cls,
                                    const uint8_t* lds_nfa, bool* full_out) {
   const uint32_t rule = (uint32_t)(V.keys[c0] >> kPosBits);
@@ -2616,26 +2668,28 @@ __device__ inline uint32_t run_job(const VerifyParams& V, uint32_t job, uint32_t
   *full_out = full;
   const uint64_t fstart = V.off[fi];
   const uint8_t* text = V.data + fstart;
-  const uint32_t n = (uint32_t)(V.off[fi + 1] - 1 - fstart);  // NUL separator excluded
+  const Pos n = (Pos)(V.off[fi + 1] - 1 - fstart);  // NUL separator excluded
   uint32_t* tck = V.tck && !(job & kJobRedo) ? V.tck + 4 * job : nullptr;
   const RuleDev& rd = V.rs.rules[rule];
   if (full) {
-    verify_full_job(V, rule, fi, job, text, n, sc);
+    verify_full_job<Pos>(V, rule, fi, job, text, n, sc);
     return 0;
   }
-  if (lds_dfa) return verify_dfa_job<true>(V, rule, fi, job, pos0, c0, c1, fstart, text, n, sc, lds_dfa, lds_cls, tck);
+  if (lds_dfa)
+    return verify_dfa_job<true, Pos>(V, rule, fi, job, pos0, c0, c1, fstart, text, n, sc, lds_dfa, lds_cls, tck);
   if (rd.dfa_off != kNoFollow)
-    return verify_dfa_job<false>(V, rule, fi, job, pos0, c0, c1, fstart, text, n, sc, nullptr, nullptr, tck);
+    return verify_dfa_job<false, Pos>(V, rule, fi, job, pos0, c0, c1, fstart, text, n, sc, nullptr, nullptr, tck);
   if (rd.nfa_off != kNoFollow) {
     const uint8_t* nfa = lds_nfa ? lds_nfa : V.rs.nfa_bytes + rd.nfa_off;
-    return ((const NfaDev*)nfa)->npos > 64 ? verify_nfa_job<true>(V, rule, fi, job, pos0, c0, c1, fstart, text, n, sc, nfa)
-                                           : verify_nfa_job<false>(V, rule, fi, job, pos0, c0, c1, fstart, text, n, sc, nfa);
+    return ((const NfaDev*)nfa)->npos > 64
+               ? verify_nfa_job<true, Pos>(V, rule, fi, job, pos0, c0, c1, fstart, text, n, sc, nfa)
+               : verify_nfa_job<false, Pos>(V, rule, fi, job, pos0, c0, c1, fstart, text, n, sc, nfa);
   }
-  verify_vm_job(V, rule, fi, job, pos0, c0, c1, fstart, text, n, sc);
+  verify_vm_job<Pos>(V, rule, fi, job, pos0, c0, c1, fstart, text, n, sc);
   return 0;
 }
 
-template <uint32_t kBlock>
+template <uint32_t kBlock, class Pos>
 __global__ __launch_bounds__(kBlock) void k_verify(VerifyParams V) {
   __shared__ __align__(16) uint16_t dfa_lds[kVerifyDfaLds / 2];
   __shared__ __align__(16) uint8_t cls_lds[128];
@@ -2664,10 +2718,11 @@ __global__ __launch_bounds__(kBlock) void k_verify(VerifyParams V) {
     const uint64_t t0 = V.prof ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz wall clock
     const uint64_t c0 = V.job_start[j];
     const uint64_t c1 = (j + 1 < n_jobs) ? V.job_start[j + 1] : V.n_cands;
+    if (is_long_file(V.off, V.vals[c0] & ~kFullFlag) != (sizeof(Pos) > 4)) continue;
     const uint32_t rule = (uint32_t)(V.keys[c0] >> kPosBits);
     bool full = false;
-    const uint32_t steps = run_job(V, j, 0, c0, c1, sc, staged && rule == r0 ? dfa_lds : nullptr, cls_lds,
-                                   staged_nfa && rule == r0 ? (const uint8_t*)dfa_lds : nullptr, &full);
+    const uint32_t steps = run_job<Pos>(V, j, 0, c0, c1, sc, staged && rule == r0 ? dfa_lds : nullptr, cls_lds,
+                                        staged_nfa && rule == r0 ? (const uint8_t*)dfa_lds : nullptr, &full);
     if (V.prof) {  // diagnostics (TSG_PROFILE_VERIFY): duration | end, rule | full
       const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
       V.prof[2 * j] = (t1 - t0) | ((t1 & 0xFFFFFFFFull) << 32);
@@ -2704,6 +2759,7 @@ __global__ void k_chain_fix(VerifyParams V) {
 
 // One lane per conflict: the chain's remaining jobs in order, as ONE job
 // (their candidates are consecutive), from the conflict's search position.
+template <class Pos>
 __global__ __launch_bounds__(64) void k_verify_redo(VerifyParams V) {
   const uint64_t n = V.ctrl->n_redo < V.redo_cap ? V.ctrl->n_redo : V.redo_cap;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2713,8 +2769,9 @@ __global__ __launch_bounds__(64) void k_verify_redo(VerifyParams V) {
     const RedoRec R = V.redo[i];
     const uint64_t c0 = V.job_start[R.job];
     const uint64_t c1 = R.last + 1 < n_jobs ? V.job_start[R.last + 1] : V.n_cands;
+    if (is_long_file(V.off, V.vals[c0] & ~kFullFlag) != (sizeof(Pos) > 4)) continue;
     bool full;
-    run_job(V, kJobRedo | R.job, (uint32_t)R.pos, c0, c1, sc, nullptr, nullptr, nullptr, &full);
+    run_job<Pos>(V, kJobRedo | R.job, (Pos)R.pos, c0, c1, sc, nullptr, nullptr, nullptr, &full);
   }
 }
 
@@ -2790,12 +2847,12 @@ __global__ __launch_bounds__(256) void k_exclude_tags(const uint8_t* data, const
     if (k >= nx) continue;
     const uint32_t prog = scope == 0 ? X.gx[k] : X.xprog[X.xoff[scope - 1] + k];
     const uint8_t* text = data + off[file];
-    const uint32_t n = (uint32_t)(off[file + 1] - 1 - off[file]);
+    const uint64_t n = off[file + 1] - 1 - off[file];  // (rare path: 64-bit positions for every file)
     const gre::ProgView& pv = rs.progs[prog];
-    uint32_t pos = 0, ms, me;
+    uint64_t pos = 0, ms, me;
     int64_t prev_end = -1;
     while (pos <= n) {  // FindAllIndex iteration (regexp.go allMatches)
-      LimitStarts ls{n};
+      LimitStarts<uint64_t> ls{n};
       if (!vm_search_starts(pv, text, n, pos, ls, sc, &ms, &me)) break;
       bool accept = true;
       if (me == pos) {
@@ -3867,6 +3924,13 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
         d.grp_pre = r.grp.pre;
         d.grp_len = r.grp.len;
         d.grp_suf = r.grp.suf;
+      } else if (d.use_groups && r.grun.valid) {  // else gre::group_run
+        d.grp_run = 1;
+        d.grp_run_len = r.grun.len;
+        for (int k = 0; k < 4; ++k) {
+          d.grp_s[k] = r.grun.s_alpha[k];
+          d.grp_b[k] = r.grun.b_alpha[k];
+        }
       }
     }
     d.gate_implied = r.gate_implied;  // ruleset.cpp: every anchor literal contains a keyword
@@ -4995,10 +5059,9 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   const uint64_t n_outputs = c.outputs;
   const uint64_t n_events = scan_overflow + c.events;
   if (sp && sp->mode == 1) return export_part(e, rs, P, n_hits, *sp);
-  if (c.long_files) {
-    set_last_error("a file of 2 GiB or more: the match search runs on 31-bit file positions");
-    return TSG_ERR_UNSUPPORTED;
-  }
+  // files past kMaxVerifyFile: their jobs run the 64-bit instantiations of the
+  // search kernels (launched only then)
+  const bool any_long = c.long_files != 0 || (merge && sp->file_len > kMaxVerifyFile);
   // ---- 3. candidates
   uint64_t cand_cap = std::max<uint64_t>(1 << 16, n_hits * 2 + nf / 4);
   ExpandParams E{};
@@ -5145,22 +5208,35 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     if (n_cands > (uint64_t)e->num_cus * kVerifyBlockWide * 4) {
       const uint32_t blocks = (uint32_t)std::min<uint64_t>((n_cands + kVerifyBlockWide - 1) / kVerifyBlockWide,
                                                            e->vm_threads / kVerifyBlockWide);  // (VM scratch per lane)
-      hipLaunchKernelGGL(k_verify<kVerifyBlockWide>, dim3(std::max(1u, blocks)), dim3(kVerifyBlockWide), 0, s, V);
+      hipLaunchKernelGGL((k_verify<kVerifyBlockWide, uint32_t>), dim3(std::max(1u, blocks)), dim3(kVerifyBlockWide), 0,
+                         s, V);
+      if (any_long)
+        hipLaunchKernelGGL((k_verify<kVerifyBlockWide, uint64_t>), dim3(std::max(1u, blocks)), dim3(kVerifyBlockWide),
+                           0, s, V);
     } else {
       const uint32_t blocks = (uint32_t)std::min<uint64_t>((n_cands + kVerifyBlock - 1) / kVerifyBlock, e->vm_threads / kVerifyBlock);
-      hipLaunchKernelGGL(k_verify<kVerifyBlock>, dim3(std::max(1u, blocks)), dim3(kVerifyBlock), 0, s, V);
+      hipLaunchKernelGGL((k_verify<kVerifyBlock, uint32_t>), dim3(std::max(1u, blocks)), dim3(kVerifyBlock), 0, s, V);
+      if (any_long)
+        hipLaunchKernelGGL((k_verify<kVerifyBlock, uint64_t>), dim3(std::max(1u, blocks)), dim3(kVerifyBlock), 0, s,
+                           V);
     }
     // speculative chains: conflicts re-run in order (grid: one lane per job
     // start at most; the re-run grid keeps every lane's VM scratch slot below
     // vm_threads)
     hipLaunchKernelGGL(k_chain_fix, dim3((uint32_t)((n_cands + 255) / 256)), dim3(256), 0, s, V);
-    hipLaunchKernelGGL(k_verify_redo, dim3(e->num_cus * 2), dim3(64), 0, s, V);
+    hipLaunchKernelGGL(k_verify_redo<uint32_t>, dim3(e->num_cus * 2), dim3(64), 0, s, V);
+    if (any_long) hipLaunchKernelGGL(k_verify_redo<uint64_t>, dim3(e->num_cus * 2), dim3(64), 0, s, V);
     HIP_TRY(hipGetLastError());
     // capture stages over the device-side lists: 8 searching lanes per wave with
     // 560-word arenas, then one lane per wave with 36 KiB for what does not fit
     // (grids keep every lane's VM scratch slot below vm_threads: 512 / 256 per CU)
-    hipLaunchKernelGGL((k_captures<64, kCapActive, kBsWords, false>), dim3(e->num_cus * 8), dim3(64), 0, s, V);
-    hipLaunchKernelGGL((k_captures<64, 1, kBigBsWords, true>), dim3(e->num_cus * 4), dim3(64), 0, s, V);
+    hipLaunchKernelGGL((k_captures<64, kCapActive, kBsWords, false, uint32_t>), dim3(e->num_cus * 8), dim3(64), 0, s, V);
+    if (any_long)
+      hipLaunchKernelGGL((k_captures<64, kCapActive, kBsWords, false, uint64_t>), dim3(e->num_cus * 8), dim3(64), 0, s,
+                         V);
+    hipLaunchKernelGGL((k_captures<64, 1, kBigBsWords, true, uint32_t>), dim3(e->num_cus * 4), dim3(64), 0, s, V);
+    if (any_long)
+      hipLaunchKernelGGL((k_captures<64, 1, kBigBsWords, true, uint64_t>), dim3(e->num_cus * 4), dim3(64), 0, s, V);
     hipLaunchKernelGGL(k_drop_spec, dim3(e->num_cus * 4), dim3(256), 0, s, V);
     HIP_TRY(hipGetLastError());
     if (prof) {  // the jobs that end last (their waves set k_verify's length), per-rule totals
@@ -5248,6 +5324,10 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   if (!verified) {
     set_last_error("internal: location buffers still overflowed after regrowing them");
     return TSG_ERR_INTERNAL;
+  }
+  if (c.err & 2u) {
+    set_last_error("a match of 4 GiB or more: its allow regexes would run past 32-bit match strings");
+    return TSG_ERR_UNSUPPORTED;
   }
   if (c.err) {
     set_last_error("internal: capture re-run disagreed with the whole-match run");
@@ -5651,10 +5731,6 @@ static int scan_merge_impl(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* 
                            tsg_result** out) {
   if (!e || !rs || !out || !d_file || (n_parts && (!blobs || !blob_lens))) return TSG_ERR_INVALID_ARG;
   *out = nullptr;
-  if (file_len > kMaxVerifyFile) {
-    set_last_error("split: the merged file must be below 2 GiB (31-bit positions in the match search)");
-    return TSG_ERR_UNSUPPORTED;
-  }
   std::lock_guard<std::mutex> lk(e->mu);
   HIP_TRY(hipSetDevice(e->device));
   uint8_t sep = 1;
@@ -5702,10 +5778,6 @@ int tsg_scan_merge_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d
 static int stage_host_batch(tsg_engine* e, const tsg_file* files, size_t n_files, uint64_t* nbytes_out) {
   std::vector<uint64_t> off(n_files + 1, 0), poff(n_files + 1, 0);
   for (size_t i = 0; i < n_files; ++i) {
-    if (files[i].len > kMaxVerifyFile) {
-      set_last_error("files of 2 GiB or more are outside this engine's coverage (31-bit match-search positions)");
-      return TSG_ERR_UNSUPPORTED;
-    }
     off[i + 1] = off[i] + files[i].len + 1;
     poff[i + 1] = poff[i] + (files[i].path ? strlen(files[i].path) : 0);
   }

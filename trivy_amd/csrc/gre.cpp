@@ -1313,6 +1313,128 @@ GroupSpan group_span(const Prog& p, uint32_t slot) {
   return g;
 }
 
+// Capture-group span by byte runs (see gre.h GroupRun).  With A the part of
+// the program before the group's CAP pair, B the group and S the rest: on
+// ASCII text, if no byte S can consume can be B's last byte, the match's
+// trailing run of S-bytes is exactly S's text (the byte before it was consumed
+// last by B); if no byte B can consume can be A's last byte, the run of
+// B-bytes before that is exactly the group (the byte before it, if any, was
+// consumed last by A).  Every parse of the match has these boundaries, so the
+// leftmost-first one does too.  Sets are supersets from graph reachability.
+GroupRun group_run(const Prog& p, uint32_t slot, int fixed_len) {
+  GroupRun g;
+  const int n = (int)p.inst.size();
+  int open = -1, close = -1;
+  for (int pc = 0; pc < n; ++pc) {
+    const Inst& in = p.inst[pc];
+    if (in.op != I_CAP) continue;
+    if (in.arg == 2 * slot) {
+      if (open >= 0) return g;
+      open = pc;
+    } else if (in.arg == 2 * slot + 1) {
+      if (close >= 0) return g;
+      close = pc;
+    }
+  }
+  if (open < 0 || close < 0) return g;
+  auto succ = [&](int pc, int* out) -> int {
+    const Inst& in = p.inst[pc];
+    switch (in.op) {
+      case I_FAIL:
+      case I_MATCH: return 0;
+      case I_ALT: out[0] = (int)in.out; out[1] = (int)in.arg; return 2;
+      default: out[0] = (int)in.out; return 1;
+    }
+  };
+  auto consumes = [&](int pc) {
+    const uint8_t op = p.inst[pc].op;
+    return op == I_RUNE || op == I_RUNE1 || op == I_ANY || op == I_ANYNL;
+  };
+  auto bytes_of = [&](int pc, uint32_t* m) {  // ASCII bytes the instruction consumes
+    const Inst& in = p.inst[pc];
+    switch (in.op) {
+      case I_RUNE:
+        for (int k = 0; k < 4; ++k) m[k] |= p.classes[in.arg].ascii[k];
+        break;
+      case I_RUNE1:
+        if (in.arg < 128) m[in.arg >> 5] |= 1u << (in.arg & 31);
+        break;
+      case I_ANY:
+        for (int k = 0; k < 4; ++k) m[k] = ~0u;
+        break;
+      case I_ANYNL:
+        for (int k = 0; k < 4; ++k) m[k] = ~0u;
+        m['\n' >> 5] &= ~(1u << ('\n' & 31));
+        break;
+    }
+  };
+  // forward reachability from `from` (over every edge), never entering `stop`
+  auto reach = [&](int from, int stop) {
+    std::vector<uint8_t> seen(n, 0);
+    std::vector<int> st{from};
+    while (!st.empty()) {
+      const int pc = st.back();
+      st.pop_back();
+      if (pc <= 0 || pc >= n || pc == stop || seen[pc]) continue;
+      seen[pc] = 1;
+      int o[2];
+      for (int k = succ(pc, o); k-- > 0;) st.push_back(o[k]);
+    }
+    return seen;
+  };
+  // the empty-width closure of `from` (no consuming instruction passed) meets `target`
+  auto eps_reaches = [&](int from, int target) {
+    std::vector<uint8_t> seen(n, 0);
+    std::vector<int> st{from};
+    while (!st.empty()) {
+      const int pc = st.back();
+      st.pop_back();
+      if (pc <= 0 || pc >= n || seen[pc]) continue;
+      if (pc == target) return true;
+      seen[pc] = 1;
+      if (consumes(pc) || p.inst[pc].op == I_MATCH) continue;
+      int o[2];
+      for (int k = succ(pc, o); k-- > 0;) st.push_back(o[k]);
+    }
+    return false;
+  };
+  // the group takes part in every match: MATCH unreachable around open / close
+  {
+    auto around = [&](int cut) {
+      const std::vector<uint8_t> r = reach((int)p.start, cut);
+      for (int pc = 1; pc < n; ++pc)
+        if (r[pc] && p.inst[pc].op == I_MATCH) return true;
+      return false;
+    };
+    if (around(open) || around(close)) return g;
+  }
+  if (eps_reaches((int)p.inst[open].out, close)) return g;  // the group may be empty
+  const std::vector<uint8_t> from_start = reach((int)p.start, -1);
+  const std::vector<uint8_t> in_group = reach((int)p.inst[open].out, close);  // B (and what loops back)
+  const std::vector<uint8_t> after = reach((int)p.inst[close].out, -1);       // S
+  uint32_t s_alpha[4] = {0, 0, 0, 0}, b_alpha[4] = {0, 0, 0, 0}, b_last[4] = {0, 0, 0, 0}, a_last[4] = {0, 0, 0, 0};
+  for (int pc = 1; pc < n; ++pc) {
+    if (!consumes(pc)) continue;
+    if (after[pc]) bytes_of(pc, s_alpha);
+    if (in_group[pc]) {
+      bytes_of(pc, b_alpha);
+      if (eps_reaches((int)p.inst[pc].out, close)) bytes_of(pc, b_last);
+    }
+    if (from_start[pc] && eps_reaches((int)p.inst[pc].out, open)) bytes_of(pc, a_last);
+  }
+  // (a group of fixed length starts len bytes before its end on ASCII text:
+  // what A ends with does not matter then)
+  for (int k = 0; k < 4; ++k)
+    if ((s_alpha[k] & b_last[k]) || (fixed_len < 0 && (b_alpha[k] & a_last[k]))) return g;
+  g.valid = true;
+  g.len = fixed_len;
+  for (int k = 0; k < 4; ++k) {
+    g.s_alpha[k] = s_alpha[k];
+    g.b_alpha[k] = b_alpha[k];
+  }
+  return g;
+}
+
 // Inst::vis rows: the start plus every instruction with >= 2 predecessors
 // among the instructions reachable from the start.
 static void assign_vis_rows(Prog* p) {

@@ -82,6 +82,21 @@ struct GroupSpan {
 };
 GroupSpan group_span(const Prog& p, uint32_t slot);
 
+// Capture-group span from byte runs at the match's end (the secret-group
+// shortcut for groups between variable-length parts, gitleaks' shape
+// `kw[..]{0,25}(=|:).{0,5}['"](?P<secret>[0-9a-f]{32})['"]?(\s|$)`): on an
+// ASCII match [ms, me), ge = me minus the run of s_alpha bytes ending at me,
+// gs = ge minus the run of b_alpha bytes ending at ge (not below ms), or
+// ge - len for a group of fixed length len (fixed_len: group_span's len, or
+// -1).  Valid when that is exact for every parse (gre.cpp group_run).
+struct GroupRun {
+  bool valid = false;
+  int len = -1;
+  uint32_t s_alpha[4] = {0, 0, 0, 0};  // ASCII bytes the program can consume after the group
+  uint32_t b_alpha[4] = {0, 0, 0, 0};  // ASCII bytes the group can consume
+};
+GroupRun group_run(const Prog& p, uint32_t slot, int fixed_len);
+
 // Unicode simple-fold orbit lookup (next member, or r itself when trivial).
 uint32_t simple_fold(uint32_t r);
 

@@ -70,8 +70,8 @@ __host__ __device__ inline int nfa_ctx_rune(uint32_t b) { return b < 0x80 ? (int
 
 // utf8.DecodeRune at i (text[i] >= 0x80) through the walk's byte accessor:
 // the rune symbol (0 K, 1 ſ, 2 İ, 3 U+FFFD, 4 any other rune) and its width.
-template <class Text>
-__host__ __device__ inline uint32_t nfa_rune_sym(Text& t, uint32_t n, uint32_t i, uint32_t* w) {
+template <class Text, class Pos>
+__host__ __device__ inline uint32_t nfa_rune_sym(Text& t, Pos n, Pos i, uint32_t* w) {
   const uint32_t c0 = t[i];
   uint32_t need, lo = 0x80, hi = 0xBF;
   *w = 1;
@@ -115,14 +115,17 @@ __host__ __device__ inline uint32_t nfa_rune_sym(Text& t, uint32_t n, uint32_t i
 // rune the symbols do not cover, a second match end -- Go's priorities pick
 // among them -- or kNfaWalkMax).  Unanchored: 1 = some thread reaches a match
 // (*me = the first end), 0 = none, 2 = undecidable.
-template <bool kWide, class Text>
-__host__ __device__ inline int nfa_walk(const NfaDev& N, const U128* reach, const NfaExc* exc, Text text, uint32_t n,
-                                        uint32_t s, uint32_t inj_hi, uint32_t* me, uint32_t* steps) {
+// (Pos: the text's position type, uint32_t or uint64_t; see pikevm.h)
+template <bool kWide, class Text, class Pos>
+__host__ __device__ inline int nfa_walk(const NfaDev& N, const U128* reach, const NfaExc* exc, Text text, Pos n,
+                                        typename gre::Ident<Pos>::type s, typename gre::Ident<Pos>::type inj_hi,
+                                        Pos* me, uint32_t* steps) {
   U128 D{0, 0};
-  uint32_t nacc = 0, e = 0;
+  uint32_t nacc = 0;
+  Pos e = 0;
   const bool anchored = inj_hi == s;
   int prev = s ? nfa_ctx_rune(text[s - 1]) : -1;
-  for (uint32_t q = s;;) {
+  for (Pos q = s;;) {
     const uint32_t c = q < n ? (uint32_t)text[q] : 0u;
     const int next = q < n ? nfa_ctx_rune(c) : -1;
     const uint32_t ctx = N.has_cond ? gre::empty_ctx(prev, next) : 0u;
@@ -148,7 +151,7 @@ __host__ __device__ inline int nfa_walk(const NfaDev& N, const U128* reach, cons
     if (c < 0x80) {
       R = reach[N.cls[c]];
     } else {  // a decoded rune: one of the symbols (the context sees a non-word, non-newline rune)
-      const uint32_t j = nfa_rune_sym(text, n, q, &w);
+      const uint32_t j = nfa_rune_sym<Text, Pos>(text, n, q, &w);
       if (j == kDfaRuneSyms - 1 && !N.na_ok) return 2;
       R = N.reach_sym[j];
     }

@@ -18,12 +18,33 @@
 
 namespace gre {
 
+// Positions: uint32_t for files below 4 GiB (every hot path), uint64_t for the
+// jobs of longer files (the engine instantiates the search twice).  Only the
+// text length fixes the type; the other positions convert to it.
+template <class T>
+struct Ident {
+  typedef T type;
+};
+template <class Pos>
+struct SlotOf {  // signed capture slot of a position type (-1 = unset)
+  typedef int32_t type;
+};
+template <>
+struct SlotOf<uint64_t> {
+  typedef int64_t type;
+};
+template <>
+struct SlotOf<unsigned long long> {
+  typedef int64_t type;
+};
+
 __host__ __device__ inline int is_word_rune(int r) {
   return (r >= '0' && r <= '9') || (r >= 'A' && r <= 'Z') || (r >= 'a' && r <= 'z') || r == '_';
 }
 
 // utf8.DecodeRune. Returns rune, sets *w (0 at end of text -> rune -1).
-__host__ __device__ inline int decode_rune(const uint8_t* s, uint32_t n, uint32_t i, uint32_t* w) {
+template <class Pos>
+__host__ __device__ inline int decode_rune(const uint8_t* s, Pos n, typename Ident<Pos>::type i, uint32_t* w) {
   if (i >= n) {
     *w = 0;
     return -1;
@@ -81,11 +102,12 @@ __host__ __device__ inline int decode_rune(const uint8_t* s, uint32_t n, uint32_
 
 // True if byte offset i is the start of a rune in the canonical decoding
 // from offset 0 (i.e. not inside a valid multi-byte sequence).
-__host__ __device__ inline bool is_rune_start(const uint8_t* s, uint32_t n, uint32_t i) {
+template <class Pos>
+__host__ __device__ inline bool is_rune_start(const uint8_t* s, Pos n, typename Ident<Pos>::type i) {
   if (i == 0 || i >= n) return true;
   if ((s[i] & 0xC0) != 0x80) return true;
-  uint32_t lim = i >= 3 ? i - 3 : 0;
-  for (uint32_t q = i; q-- > lim;) {
+  Pos lim = i >= 3 ? i - 3 : 0;
+  for (Pos q = i; q-- > lim;) {
     if ((s[q] & 0xC0) != 0x80) {
       uint32_t w;
       decode_rune(s, n, q, &w);
@@ -108,7 +130,8 @@ __host__ __device__ inline uint8_t empty_ctx(int r1, int r2) {
 // Context rune before position i for empty-width ops: only '\n' and ASCII
 // word-ness matter, and DecodeLastRune yields a non-ASCII rune (or
 // RuneError) whenever the previous byte is >= 0x80.
-__host__ __device__ inline int prev_ctx_rune(const uint8_t* s, uint32_t i) {
+template <class Pos>
+__host__ __device__ inline int prev_ctx_rune(const uint8_t* s, Pos i) {
   if (i == 0) return -1;
   uint8_t b = s[i - 1];
   return b < 0x80 ? (int)b : 0xFFFD;
@@ -137,34 +160,40 @@ __host__ __device__ inline bool inst_consumes(const Inst& in, const ProgView& p,
   return false;
 }
 
-// Scratch for one VM: sized by ninst (and ncap for the capture VM).
+// Scratch for one VM: sized by ninst (and ncap for the capture VM).  The
+// position arrays hold Pos / SlotOf<Pos> entries: sized for the widest
+// instantiation the owner runs (8 bytes on the device, 4 in the host VM).
 struct VmScratch {
   uint16_t* sparse[2];  // [ninst]
   uint16_t* dense[2];   // [ninst] visited pcs in priority order
-  uint32_t* start[2];   // [ninst] thread start offset (whole-match VM)
+  void* start[2];       // Pos [ninst] thread start offset (whole-match VM)
   uint16_t* stack;      // [ninst + 1]
-  int32_t* caps[2];     // [ninst * ncap]  (capture VM only)
-  int32_t* cur;         // [ncap]          (capture VM only)
-  int32_t* capstack;    // [2 * ninst + 2] (capture VM only)
+  void* caps[2];        // Slot [ninst * ncap]  (capture VM only)
+  void* cur;            // Slot [ncap]          (capture VM only)
+  void* capstack;       // Slot [2 * ninst + 2] (capture VM only)
 };
 
+template <class Pos>
 struct Queue {
+  typedef typename SlotOf<Pos>::type Slot;
   uint16_t* sparse;
   uint16_t* dense;
-  uint32_t* start;
-  int32_t* caps;
+  Pos* start;
+  Slot* caps;
   uint32_t n;
 };
 
-__host__ __device__ inline bool q_has(const Queue& q, uint32_t pc) {
+template <class Pos>
+__host__ __device__ inline bool q_has(const Queue<Pos>& q, uint32_t pc) {
   uint32_t j = q.sparse[pc];
   return j < q.n && q.dense[j] == pc;
 }
 
 // Go's machine.add for the whole-match VM: follow empty transitions from pc
 // in priority order, recording every visited pc.
-__host__ __device__ inline void vm_add(const ProgView& p, Queue& q, uint16_t* stack, uint32_t pc0,
-                                       uint32_t st, uint8_t ctx) {
+template <class Pos>
+__host__ __device__ inline void vm_add(const ProgView& p, Queue<Pos>& q, uint16_t* stack, uint32_t pc0,
+                                       Pos st, uint8_t ctx) {
   uint32_t sp = 0;
   stack[sp++] = (uint16_t)pc0;
   while (sp) {
@@ -201,11 +230,12 @@ __host__ __device__ inline void vm_add(const ProgView& p, Queue& q, uint16_t* st
 // start threads are only added at positions <= start_limit.  On success sets
 // [*ms, *me) and returns true.  If first_only, returns at the first MATCH
 // reached (MatchString semantics: any match).
-__host__ __device__ inline bool vm_search(const ProgView& p, const uint8_t* text, uint32_t n,
-                                          uint32_t pos0, uint32_t start_limit, bool first_only,
-                                          VmScratch& sc, uint32_t* ms, uint32_t* me) {
-  Queue q[2] = {{sc.sparse[0], sc.dense[0], sc.start[0], nullptr, 0},
-                {sc.sparse[1], sc.dense[1], sc.start[1], nullptr, 0}};
+template <class Pos>
+__host__ __device__ inline bool vm_search(const ProgView& p, const uint8_t* text, Pos n,
+                                          typename Ident<Pos>::type pos0, typename Ident<Pos>::type start_limit,
+                                          bool first_only, VmScratch& sc, Pos* ms, Pos* me) {
+  Queue<Pos> q[2] = {{sc.sparse[0], sc.dense[0], (Pos*)sc.start[0], nullptr, 0},
+                     {sc.sparse[1], sc.dense[1], (Pos*)sc.start[1], nullptr, 0}};
   int cur = 0;
   bool matched = false;
   uint32_t w = 0, w1 = 0;
@@ -213,10 +243,10 @@ __host__ __device__ inline bool vm_search(const ProgView& p, const uint8_t* text
   int r1 = -1;
   if (r >= 0) r1 = decode_rune(text, n, pos0 + w, &w1);
   uint8_t ctx = empty_ctx(prev_ctx_rune(text, pos0), r);
-  uint32_t pos = pos0;
+  Pos pos = pos0;
   for (;;) {
-    Queue& runq = q[cur];
-    Queue& nextq = q[cur ^ 1];
+    Queue<Pos>& runq = q[cur];
+    Queue<Pos>& nextq = q[cur ^ 1];
     if (runq.n == 0) {
       if (matched || pos > start_limit) break;
     }
@@ -249,19 +279,22 @@ __host__ __device__ inline bool vm_search(const ProgView& p, const uint8_t* text
 
 // ---- capture VM (FindAllSubmatchIndex) -----------------------------------
 
-__host__ __device__ inline void vmc_add(const ProgView& p, Queue& q, VmScratch& sc, uint32_t pc0,
-                                        uint32_t pos, uint8_t ctx) {
+template <class Pos>
+__host__ __device__ inline void vmc_add(const ProgView& p, Queue<Pos>& q, VmScratch& sc, uint32_t pc0,
+                                        Pos pos, uint8_t ctx) {
+  typedef typename SlotOf<Pos>::type Slot;
   // stack entries: pc (tag 0) or capture restore (slot, old) (tag 1)
   const uint32_t ncap = p.ncap;
-  int32_t* cs = sc.capstack;
+  Slot* cs = (Slot*)sc.capstack;
+  Slot* scur = (Slot*)sc.cur;
   uint32_t sp = 0;
-  cs[sp++] = (int32_t)pc0;
+  cs[sp++] = (Slot)pc0;
   cs[sp++] = -1;  // tag -1 = pc entry
   while (sp) {
-    int32_t tag = cs[--sp];
-    int32_t val = cs[--sp];
+    Slot tag = cs[--sp];
+    Slot val = cs[--sp];
     if (tag >= 0) {  // restore cap[tag] = val
-      sc.cur[tag] = val;
+      scur[tag] = val;
       continue;
     }
     uint32_t pc = (uint32_t)val;
@@ -272,7 +305,7 @@ __host__ __device__ inline void vmc_add(const ProgView& p, Queue& q, VmScratch& 
       q.dense[j] = (uint16_t)pc;
       const Inst in = p.inst[pc];
       if (in.op == I_ALT) {
-        cs[sp++] = (int32_t)in.arg;
+        cs[sp++] = (Slot)in.arg;
         cs[sp++] = -1;
         pc = in.out;
         continue;
@@ -290,15 +323,15 @@ __host__ __device__ inline void vmc_add(const ProgView& p, Queue& q, VmScratch& 
       }
       if (in.op == I_CAP) {
         if (in.arg < ncap) {
-          cs[sp++] = sc.cur[in.arg];
-          cs[sp++] = (int32_t)in.arg;  // restore after the subtree
-          sc.cur[in.arg] = (int32_t)pos;
+          cs[sp++] = scur[in.arg];
+          cs[sp++] = (Slot)in.arg;  // restore after the subtree
+          scur[in.arg] = (Slot)pos;
         }
         pc = in.out;
         continue;
       }
-      int32_t* dst = q.caps + (size_t)j * ncap;
-      for (uint32_t k = 0; k < ncap; ++k) dst[k] = sc.cur[k];
+      Slot* dst = q.caps + (size_t)j * ncap;
+      for (uint32_t k = 0; k < ncap; ++k) dst[k] = scur[k];
       break;
     }
   }
@@ -306,11 +339,15 @@ __host__ __device__ inline void vmc_add(const ProgView& p, Queue& q, VmScratch& 
 
 // Anchored capture run at position s (must be a rune boundary): returns the
 // leftmost-first match starting at s with all capture slots in caps_out.
-__host__ __device__ inline bool vm_captures(const ProgView& p, const uint8_t* text, uint32_t n,
-                                            uint32_t s, VmScratch& sc, int32_t* caps_out) {
+template <class Pos>
+__host__ __device__ inline bool vm_captures(const ProgView& p, const uint8_t* text, Pos n,
+                                            typename Ident<Pos>::type s, VmScratch& sc,
+                                            typename SlotOf<Pos>::type* caps_out) {
+  typedef typename SlotOf<Pos>::type Slot;
   const uint32_t ncap = p.ncap;
-  Queue q[2] = {{sc.sparse[0], sc.dense[0], nullptr, sc.caps[0], 0},
-                {sc.sparse[1], sc.dense[1], nullptr, sc.caps[1], 0}};
+  Slot* scur = (Slot*)sc.cur;
+  Queue<Pos> q[2] = {{sc.sparse[0], sc.dense[0], nullptr, (Slot*)sc.caps[0], 0},
+                     {sc.sparse[1], sc.dense[1], nullptr, (Slot*)sc.caps[1], 0}};
   int cur = 0;
   bool matched = false;
   uint32_t w = 0, w1 = 0;
@@ -318,16 +355,16 @@ __host__ __device__ inline bool vm_captures(const ProgView& p, const uint8_t* te
   int r1 = -1;
   if (r >= 0) r1 = decode_rune(text, n, s + w, &w1);
   uint8_t ctx = empty_ctx(prev_ctx_rune(text, s), r);
-  uint32_t pos = s;
+  Pos pos = s;
   for (uint32_t k = 0; k < ncap; ++k) caps_out[k] = -1;
   bool first = true;
   for (;;) {
-    Queue& runq = q[cur];
-    Queue& nextq = q[cur ^ 1];
+    Queue<Pos>& runq = q[cur];
+    Queue<Pos>& nextq = q[cur ^ 1];
     if (runq.n == 0 && !first) break;
     if (first) {
-      for (uint32_t k = 0; k < ncap; ++k) sc.cur[k] = -1;
-      sc.cur[0] = (int32_t)pos;
+      for (uint32_t k = 0; k < ncap; ++k) scur[k] = -1;
+      scur[0] = (Slot)pos;
       vmc_add(p, runq, sc, p.start, pos, ctx);
       first = false;
     }
@@ -335,15 +372,15 @@ __host__ __device__ inline bool vm_captures(const ProgView& p, const uint8_t* te
     nextq.n = 0;
     for (uint32_t j = 0; j < runq.n; ++j) {
       const Inst in = p.inst[runq.dense[j]];
-      int32_t* tc = runq.caps + (size_t)j * ncap;
+      Slot* tc = runq.caps + (size_t)j * ncap;
       if (in.op == I_MATCH) {
         for (uint32_t k = 0; k < ncap; ++k) caps_out[k] = tc[k];
-        caps_out[1] = (int32_t)pos;
+        caps_out[1] = (Slot)pos;
         matched = true;
         break;
       }
       if (inst_consumes(in, p, r)) {
-        for (uint32_t k = 0; k < ncap; ++k) sc.cur[k] = tc[k];
+        for (uint32_t k = 0; k < ncap; ++k) scur[k] = tc[k];
         vmc_add(p, nextq, sc, in.out, pos + w, nctx);
       }
     }

@@ -489,6 +489,7 @@ int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_r
         for (size_t k = 0; k < c.prog.cap_names.size(); ++k)
           if (c.prog.cap_names[k] == r.group_name) slot = (int)k, ++count;
         if (count == 1) r.grp = gre::group_span(c.prog, (uint32_t)slot);
+        if (count == 1 && !r.grp.valid) r.grun = gre::group_run(c.prog, (uint32_t)slot, r.grp.len);
       }
       // no group of that name => getMatchSubgroupsLocations yields nothing
       if (!has_group) r.mode = MODE_NEVER;
@@ -681,6 +682,21 @@ int tsg_ruleset_group_span(const tsg_ruleset* rs, size_t i, int* valid, int* pre
   if (pre) *pre = g.pre;
   if (len) *len = g.len;
   if (suf) *suf = g.suf;
+  return TSG_OK;
+}
+
+// Byte-run group rule of rule i (gre::group_run, used when group_span is not
+// valid): *valid = 0 when neither shortcut applies; masks = 4 u32 words each.
+int tsg_ruleset_group_run(const tsg_ruleset* rs, size_t i, int* valid, int* len, uint32_t* s_alpha,
+                          uint32_t* b_alpha) {
+  if (!rs || i >= rs->rules.size() || !valid) return TSG_ERR_INVALID_ARG;
+  const gre::GroupRun& g = rs->rules[i].grun;  // exactly what upload_ruleset hands the device
+  *valid = g.valid ? 1 : 0;
+  if (len) *len = g.len;
+  for (int k = 0; k < 4; ++k) {
+    if (s_alpha) s_alpha[k] = g.s_alpha[k];
+    if (b_alpha) b_alpha[k] = g.b_alpha[k];
+  }
   return TSG_OK;
 }
 
