@@ -1718,14 +1718,24 @@ __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
       }
       return memo_res;
     };
+    // path_rules ascend: a mask word is gathered in a register and stored once
+    // (a read-modify-write per skipped rule cost 1.7 ms for 1000 rules x 0.5 M files)
+    uint32_t cur_w = 0xFFFFFFFFu, bits = 0;
     for (uint32_t q = 0; q < G.n_path_rules; ++q) {  // only rules a path can skip
       const uint32_t r = G.path_rules[q];
       bool skip = false;
       if (G.rule_path[r] >= 0) skip = !path_match((uint32_t)G.rule_path[r]);
       for (uint32_t k = G.rule_apath_off[r]; k < G.rule_apath_off[r + 1] && !skip; ++k)
         skip = path_match(G.rule_apath[k]);
-      if (skip) G.path_mask[(size_t)f * G.rule_words + (r >> 5)] |= 1u << (r & 31);
+      if (!skip) continue;
+      if ((r >> 5) != cur_w) {
+        if (bits) G.path_mask[(size_t)f * G.rule_words + cur_w] = bits;
+        cur_w = r >> 5;
+        bits = 0;
+      }
+      bits |= 1u << (r & 31);
     }
+    if (bits) G.path_mask[(size_t)f * G.rule_words + cur_w] = bits;
   }
 }
 
@@ -2303,6 +2313,25 @@ __device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t r
   }
 }
 
+// Start of the run of bytes in the ASCII set m that ends at e (never below lo):
+// aligned 16-byte loads backwards, the bytes tested in registers.
+template <class Pos>
+__device__ inline Pos run_back(const uint8_t* text, Pos lo, Pos e, const uint32_t (&m)[4]) {
+  Pos q = e;
+  while (q > lo) {
+    const uintptr_t last = reinterpret_cast<uintptr_t>(text) + (q - 1);
+    const uintptr_t blk = last & ~(uintptr_t)15;
+    const u32x4 v = *as_global<__attribute__((address_space(1))) const u32x4>(reinterpret_cast<const void*>(blk));
+    for (int i = (int)(last - blk); i >= 0 && q > lo; --i, --q) {
+      const uint32_t wd = i < 8 ? (i < 4 ? v.x : v.y) : (i < 12 ? v.z : v.w);
+      const uint32_t c = (wd >> (8 * (i & 3))) & 0xFFu;
+      const uint32_t mw = c < 64 ? (c < 32 ? m[0] : m[1]) : (c < 96 ? m[2] : m[3]);  // (no dynamic index)
+      if (c >= 0x80 || !((mw >> (c & 31)) & 1u)) return q;
+    }
+  }
+  return q;
+}
+
 // A match k_verify found: allow rules, then the whole-match location or, for
 // rules with a secret group, a capture job for k_captures (whose bit-state
 // arenas take LDS that would cap the search at one wave per CU).
@@ -2351,14 +2380,15 @@ __device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, ui
       }
       // (unreachable for a real match of the rule; the capture search decides)
     } else if (ascii) {  // byte runs back from the match end (gre::group_run)
-      gu8* t = as_global<gu8>(text);
-      auto in = [](const uint32_t* m, uint32_t c) { return (m[c >> 5] >> (c & 31)) & 1u; };
-      Pos ge = me;
-      while (ge > ms && in(rd.grp_s, t[ge - 1])) --ge;
-      Pos gs = ge;
-      if (rd.grp_run_len >= 0) gs = ge - (Pos)rd.grp_run_len;
-      else
-        while (gs > ms && in(rd.grp_b, t[gs - 1])) --gs;
+      const uint32_t sm[4] = {rd.grp_s[0], rd.grp_s[1], rd.grp_s[2], rd.grp_s[3]};
+      const Pos ge = run_back<Pos>(text, ms, me, sm);
+      Pos gs;
+      if (rd.grp_run_len >= 0) {
+        gs = ge - (Pos)rd.grp_run_len;
+      } else {
+        const uint32_t bm[4] = {rd.grp_b[0], rd.grp_b[1], rd.grp_b[2], rd.grp_b[3]};
+        gs = run_back<Pos>(text, ms, ge, bm);
+      }
       unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
       if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, (uint64_t)gs, (uint64_t)ge, 0, 0, 0, job};
       return;
@@ -3066,10 +3096,20 @@ __device__ inline uint32_t wave_incl_sum32(uint32_t v, uint32_t lane) {
 // location of one interval shares it; EndLine == StartLine).  Scratch:
 // sort_key / sort_idx hold P(a) / P(b) per interval slot, line_uid the
 // location's interval, line_head the prefix (all reused later).
+// Files with kCensorBig or more locations (a minified line full of rule
+// instances) are merged by k_censor_big, a 1024-lane block per file, instead:
+// one wave would walk them 64 locations at a time.
+constexpr uint32_t kCensorBig = 4096;
+
+__device__ inline bool censor_big_group(const FindParams& F, uint64_t i) {
+  return i + kCensorBig - 1 < F.n_locs && F.locs[i + kCensorBig - 1].file == F.locs[i].file;
+}
+
 __global__ __launch_bounds__(256) void k_censor(FindParams F) {
   const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63;
   if (i >= F.n_locs || (i > 0 && F.locs[i - 1].file == F.locs[i].file)) return;  // wave-uniform
+  if (censor_big_group(F, i)) return;  // k_censor_big's
   const uint32_t file = F.locs[i].file;
   uint64_t j = i + 1;  // group end: wave-wide probe 64 at a time
   for (;;) {
@@ -3134,6 +3174,141 @@ __global__ __launch_bounds__(256) void k_censor(FindParams F) {
     run += __shfl(inc, 63);
   }
   for (uint64_t k = i + lane; k < j; k += 64) {
+    F.grp[k] = make_uint2((uint32_t)i, m_cnt);
+    DevLoc& L = F.locs[k];
+    if (L.flags) continue;
+    const uint32_t id = F.line_uid[k];
+    const uint32_t line = (uint32_t)F.sort_key[i + id] - F.line_head[i + id] + 1;
+    L.start_line = line;
+    L.end_line = line;
+  }
+}
+
+// Block-wide inclusive scans over 1024 lanes (16 waves): wave scans, then
+// the wave totals through LDS.  `tot` receives the block total.
+__device__ inline uint64_t block_incl_max64(uint64_t v, uint64_t* lds16, uint64_t* tot) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  v = wave_incl_max64(v, lane);
+  if (lane == 63) lds16[wv] = v;
+  __syncthreads();
+  uint64_t before = 0, all = 0;
+  for (uint32_t k = 0; k < blockDim.x / 64; ++k) {
+    const uint64_t x = lds16[k];
+    if (k < wv) before = before > x ? before : x;
+    all = all > x ? all : x;
+  }
+  __syncthreads();
+  *tot = all;
+  return v > before ? v : before;
+}
+__device__ inline uint32_t block_incl_sum32(uint32_t v, uint32_t* lds16, uint32_t* tot) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  v = wave_incl_sum32(v, lane);
+  if (lane == 63) lds16[wv] = v;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+  for (uint32_t k = 0; k < blockDim.x / 64; ++k) {
+    if (k < wv) before += lds16[k];
+    all += lds16[k];
+  }
+  __syncthreads();
+  *tot = all;
+  return v + before;
+}
+
+// k_censor for one file group of >= kCensorBig locations per 1024-lane block
+// (block b takes the big group whose first location lies in [b, b + 1) x
+// kCensorBig: two big groups cannot start that close).  Same results as
+// k_censor; an interval's end is the running maximum just before the location
+// that opens the next one (the maxima are monotone), the last one's the final
+// maximum.
+__global__ __launch_bounds__(1024) void k_censor_big(FindParams F) {
+  __shared__ uint64_t s64[16], s64b[16];
+  __shared__ uint32_t s32[16];
+  __shared__ unsigned long long first;
+  __shared__ unsigned long long gend;
+  __shared__ uint64_t prev_incl[1024], prev_incl_p[1024];
+  const uint32_t t = threadIdx.x;
+  const uint64_t w0 = (uint64_t)blockIdx.x * kCensorBig;
+  if (t == 0) {
+    first = ~0ull;
+    gend = ~0ull;
+  }
+  __syncthreads();
+  for (uint64_t k = w0 + t; k < w0 + kCensorBig && k < F.n_locs; k += blockDim.x)
+    if ((k == 0 || F.locs[k - 1].file != F.locs[k].file) && censor_big_group(F, k)) atomicMin(&first, k);
+  __syncthreads();
+  if (first == ~0ull) return;  // block-uniform
+  const uint64_t i = first;
+  const uint32_t file = F.locs[i].file;
+  for (uint64_t j0 = i + kCensorBig;; j0 += blockDim.x) {  // group end
+    const uint64_t k = j0 + t;
+    if (k >= F.n_locs || F.locs[k].file != file) atomicMin(&gend, k);
+    __syncthreads();
+    if (gend != ~0ull) break;
+    __syncthreads();
+  }
+  const uint64_t j = gend;
+  uint64_t carry = 0, carry_p = 0;
+  uint32_t m_cnt = 0, n_valid = 0;
+  for (uint64_t k0 = i; k0 < j; k0 += blockDim.x) {
+    const uint64_t k = k0 + t;
+    DevLoc L{};
+    if (k < j) L = F.locs[k];
+    const bool valid = k < j && !L.flags;
+    uint64_t tot, tot_p;
+    uint64_t incl = block_incl_max64(valid ? L.end : 0, s64, &tot);
+    uint64_t incl_p = block_incl_max64(valid ? (uint64_t)L.end_line : 0, s64b, &tot_p);
+    incl = incl > carry ? incl : carry;
+    incl_p = incl_p > carry_p ? incl_p : carry_p;
+    prev_incl[t] = incl;
+    prev_incl_p[t] = incl_p;
+    uint32_t vtot;
+    const uint32_t vincl = block_incl_sum32(valid ? 1u : 0u, s32, &vtot);
+    // (block_incl_sum32's barriers order the prev_incl writes before these reads)
+    const uint64_t excl = t ? prev_incl[t - 1] : carry;
+    const uint64_t excl_p = t ? prev_incl_p[t - 1] : carry_p;
+    const bool before = n_valid + vincl - (valid ? 1u : 0u) > 0;
+    const bool opens = valid && (!before || L.start > excl);
+    uint32_t otot;
+    const uint32_t oincl = block_incl_sum32(opens ? 1u : 0u, s32, &otot);
+    const uint32_t id = m_cnt + oincl - 1;  // (valid locations only)
+    if (valid) {
+      F.line_uid[k] = id;
+      if (opens) {
+        F.iv[2 * (i + id)] = L.start;
+        F.sort_key[i + id] = L.start_line;  // P(a)
+        if (id > 0) {  // the previous interval ends at the running maximum before this one
+          F.iv[2 * (i + id - 1) + 1] = excl;
+          F.sort_idx[i + id - 1] = (uint32_t)excl_p;  // P(b)
+        }
+      }
+    }
+    carry = carry > tot ? carry : tot;
+    carry_p = carry_p > tot_p ? carry_p : tot_p;
+    m_cnt += otot;
+    n_valid += vtot;
+    __syncthreads();  // prev_incl reused by the next step
+  }
+  if (t == 0 && m_cnt) {
+    F.iv[2 * (i + m_cnt - 1) + 1] = carry;
+    F.sort_idx[i + m_cnt - 1] = (uint32_t)carry_p;
+  }
+  __threadfence_block();
+  __syncthreads();
+  // exclusive prefix of censored newlines over the intervals
+  uint32_t run = 0;
+  for (uint32_t q0 = 0; q0 < m_cnt; q0 += blockDim.x) {
+    const uint32_t q = q0 + t;
+    const uint32_t d = q < m_cnt ? F.sort_idx[i + q] - (uint32_t)F.sort_key[i + q] : 0u;
+    uint32_t tot;
+    const uint32_t inc = block_incl_sum32(d, s32, &tot);
+    if (q < m_cnt) F.line_head[i + q] = run + inc - d;
+    run += tot;
+  }
+  __threadfence_block();
+  __syncthreads();
+  for (uint64_t k = i + t; k < j; k += blockDim.x) {
     F.grp[k] = make_uint2((uint32_t)i, m_cnt);
     DevLoc& L = F.locs[k];
     if (L.flags) continue;
@@ -3308,8 +3483,12 @@ __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
   if (!L.flags && L.start <= L.end && L.end <= n) {
     const uint2 g = F.grp[w];
     // match window (scanner.go:484-502)
-    uint64_t ls = cens_line_begin(F, fs, g.x, g.y, L.start, lane);
-    uint64_t le = cens_next_nl(F, fs, n, g.x, g.y, L.start, lane);
+    // the (censored) line holding the start: the Match window's and the first
+    // cause Code line's bounds, searched once (a search on a multi-MiB line
+    // costs a binary search over the newline prefix)
+    const uint64_t ls0 = cens_line_begin(F, fs, g.x, g.y, L.start, lane);
+    const uint64_t le0 = cens_next_nl(F, fs, n, g.x, g.y, L.start, lane);
+    uint64_t ls = ls0, le = le0;
     if (le - ls > 100) {
       ls = L.start >= 30 ? L.start - 30 : 0;
       le = L.end + 20 > n ? n : L.end + 20;
@@ -3319,12 +3498,12 @@ __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
     // code lines (scanner.go:505-534), 0-based numbers [sl - 2, el + 2)
     const uint32_t sl = L.start_line - 1, el = L.end_line - 1;
     const uint32_t cs = sl >= 2 ? sl - 2 : 0, ce = el + 2;
-    uint64_t p = cens_line_begin(F, fs, g.x, g.y, L.start, lane);
+    uint64_t p = ls0;
     for (uint32_t cur = sl; cur > cs && p > 0; --cur) p = cens_line_begin(F, fs, g.x, g.y, p - 1, lane);
     uint32_t k = 0;
     bool found_first = false;
     for (uint32_t ln = cs; ln < ce && p <= n && k < kCodeLines; ++ln, ++k) {
-      const uint64_t q = cens_next_nl(F, fs, n, g.x, g.y, p, lane);
+      const uint64_t q = p == ls0 ? le0 : cens_next_nl(F, fs, n, g.x, g.y, p, lane);
       const bool cause = ln >= sl && ln <= el;
       if (lane == 0) {
         CodeRec c{};
@@ -3392,6 +3571,42 @@ __global__ __launch_bounds__(256) void k_arena_fill(FindParams F) {
       else hi = mid;
     }
     uint64_t k = lo;
+    if (a + 16 <= total && a + 16 <= F.seg_off[k] + F.seg_len[k]) {
+      // fast path: the 16 bytes lie in one segment and outside every censor
+      // interval -- two aligned 16-byte loads, a funnel shift, one store
+      const uint64_t x = F.seg_src[k] + (a - F.seg_off[k]);
+      const uint32_t g0 = F.seg_grp[k].x, gm = F.seg_grp[k].y;
+      uint32_t l2 = 0, h2 = gm;  // first interval ending after x
+      while (l2 < h2) {
+        const uint32_t mid = (l2 + h2) >> 1;
+        if (F.iv[2 * (g0 + mid) + 1] <= x) l2 = mid + 1;
+        else h2 = mid;
+      }
+      if (l2 >= gm || F.iv[2 * (g0 + l2)] >= x + 16) {
+        const uint64_t src = F.off[F.seg_file[k]] + x;
+        const uint64_t b0 = src & ~15ull;
+        const uint32_t sh = (uint32_t)(src - b0);
+        const uint4 u = *(const uint4*)(F.data + b0);
+        uint4 o;
+        if (sh == 0) {
+          o = u;
+        } else {
+          const uint4 v = ld16_guard(F.data, b0 + 16, F.data_end);
+          const uint32_t d[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+          uint32_t r[4];
+          const uint32_t q = sh >> 2, bs = 8 * (sh & 3);
+#pragma unroll
+          for (int z = 0; z < 4; ++z) {
+            const uint32_t lo32 = q == 0 ? d[z] : q == 1 ? d[z + 1] : q == 2 ? d[z + 2] : d[z + 3];
+            const uint32_t hi32 = q == 0 ? d[z + 1] : q == 1 ? d[z + 2] : q == 2 ? d[z + 3] : d[z + 4];
+            r[z] = bs ? (lo32 >> bs) | (hi32 << (32 - bs)) : lo32;
+          }
+          o = make_uint4(r[0], r[1], r[2], r[3]);
+        }
+        *(uint4*)(F.arena + a) = o;
+        continue;
+      }
+    }
     uint32_t w[4] = {0, 0, 0, 0};
     uint64_t kk = ~0ull, fbase = 0;
     uint32_t g0 = 0, gm = 0, t = 0;  // the segment's file intervals, t = first one ending after x
@@ -4593,6 +4808,8 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   const uint32_t slot_blocks = (uint32_t)((n_slots + 255) / 256);
   HIP_TRY(hipMemsetAsync(e->f_slen.p, 0, n_seg * 8, s));  // unused line segments stay empty
   hipLaunchKernelGGL(k_censor, dim3(wave_blocks), dim3(256), 0, s, F);
+  if (n_locs >= kCensorBig)
+    hipLaunchKernelGGL(k_censor_big, dim3((uint32_t)((n_locs + kCensorBig - 1) / kCensorBig)), dim3(1024), 0, s, F);
   hipLaunchKernelGGL(k_find_spans, dim3(wave_blocks), dim3(256), 0, s, F);
   HIP_TRY(hipGetLastError());
   // distinct Code lines: sort the slots by (file, line start), number the runs
@@ -4722,10 +4939,19 @@ void order_finding_ties(ResultImpl& R, bool all_runs) {
     }
   }
   auto sort_run = [&](const std::pair<size_t, size_t>& r) {
+    if (r.second - r.first <= 16) {  // short runs (most): stable insertion sort, no temporary buffer
+      for (size_t a = r.first + 1; a < r.second; ++a) {
+        const FindRec x = R.frec[a];
+        size_t b = a;
+        for (; b > r.first && less(x, R.frec[b - 1]); --b) R.frec[b] = R.frec[b - 1];
+        R.frec[b] = x;
+      }
+      return;
+    }
     std::stable_sort(R.frec.begin() + r.first, R.frec.begin() + r.second, less);
   };
   const unsigned nt = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-  if (work < (1u << 16) || nt == 1 || runs.size() < 2) {
+  if (work < (1u << 13) || nt == 1 || runs.size() < 2) {
     for (auto& r : runs) sort_run(r);
     return;
   }
