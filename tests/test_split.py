@@ -203,6 +203,15 @@ def test_gpu_split_edges_and_errors():
         with pytest.raises(N.EngineError) as ei:
             sc.scan_merge(args, bad)
         assert ei.value.code == N.TSG_ERR_INVALID_ARG
+    # a forged hit outside its part's owned range (the device checks every hit)
+    import struct
+    own_lo, own_hi, n_hits = struct.unpack_from("<QQQ", parts[2], 24)
+    assert n_hits >= 1 and own_lo > 0
+    forged = bytearray(parts[2])
+    struct.pack_into("<Q", forged, len(forged) - 8, ((own_lo - 1) << 16) | 1)
+    with pytest.raises(N.EngineError) as ei:
+        sc.scan_merge(args, [parts[0], parts[1], bytes(forged)])
+    assert ei.value.code == N.TSG_ERR_INVALID_ARG
     other = S.new_scanner(S.Config(enable_builtin_rule_ids=["github-pat"]), device=0)
     with pytest.raises(N.EngineError):
         other.scan_merge(args, parts)

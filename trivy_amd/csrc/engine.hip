@@ -106,6 +106,7 @@ struct Ctrl {
   unsigned long long n_ties;     // findings whose (file, RuleID, Match prefix) equals the previous one's
   unsigned long long n_redo;     // speculative job chains re-run from a conflict (k_chain_fix)
   unsigned long long n_dropped;  // locations of the conflicting speculative jobs (k_drop_spec)
+  unsigned long long n_caps_run; // matches whose secret group k_group_runs cuts by byte runs
 };
 
 struct DevLoc {
@@ -1943,6 +1944,8 @@ struct VerifyParams {
   uint64_t cap_cap;
   CapJob* caps_big; // those too long for its arenas, for k_captures_big
   uint64_t cap_big_cap;
+  CapJob* caps_run; // ASCII matches of byte-run group rules (gre::group_run), for k_group_runs
+  uint64_t cap_run_cap;
   const uint8_t* span_hi;  // k_scan_fast's per-span ">= 0x80 occurs" flags (nullptr: not computed)
   // speculative jobs: per job the first match start / last match end
   // (file-relative; ~0 / 0 = no match), the split kind at each job start
@@ -2379,18 +2382,9 @@ __device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, ui
         return;
       }
       // (unreachable for a real match of the rule; the capture search decides)
-    } else if (ascii) {  // byte runs back from the match end (gre::group_run)
-      const uint32_t sm[4] = {rd.grp_s[0], rd.grp_s[1], rd.grp_s[2], rd.grp_s[3]};
-      const Pos ge = run_back<Pos>(text, ms, me, sm);
-      Pos gs;
-      if (rd.grp_run_len >= 0) {
-        gs = ge - (Pos)rd.grp_run_len;
-      } else {
-        const uint32_t bm[4] = {rd.grp_b[0], rd.grp_b[1], rd.grp_b[2], rd.grp_b[3]};
-        gs = run_back<Pos>(text, ms, ge, bm);
-      }
-      unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
-      if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, (uint64_t)gs, (uint64_t)ge, 0, 0, 0, job};
+    } else if (ascii) {  // byte runs back from the match end (gre::group_run): k_group_runs
+      const unsigned long long idx = atomicAdd(&V.ctrl->n_caps_run, 1ull);
+      if (idx < V.cap_run_cap) V.caps_run[idx] = CapJob{fi, rule, job, 0, (uint64_t)ms, (uint64_t)me};
       return;
     }
   }
@@ -2404,6 +2398,12 @@ __device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, ui
 // the backtracker's control flow differs per job, so jobs sharing a wave run
 // one after another; few active lanes per wave and many waves per CU keep
 // each wave to about one job and let the CU overlap their load latencies.
+// Secret groups by byte runs (gre::group_run), one lane per match: the
+// group ends where the trailing run of the rule's after-group bytes begins and
+// starts at its fixed length or the run of group bytes before that.
+template <class Pos>
+__global__ __launch_bounds__(256) void k_group_runs(VerifyParams V);
+
 // Files of 4 GiB and more: true when the job / location of file fi belongs to
 // the 64-bit instantiation of the search kernels (each kernel is launched
 // twice when the batch holds such a file; every lane skips the other's work).
@@ -2432,6 +2432,31 @@ __global__ __launch_bounds__(kLanes) void k_captures(VerifyParams V) {
     const Pos n = (Pos)(V.off[c.file + 1] - 1 - fstart);
     emit_groups<Pos>(V, rd, c.rule, c.file, c.job, V.data + fstart, n, (Pos)c.ms, (Pos)c.me, sc, bs_area, kWords,
                      kLast ? nullptr : V.caps_big, V.cap_big_cap, &V.ctrl->n_caps_big);
+  }
+}
+
+template <class Pos>
+__global__ __launch_bounds__(256) void k_group_runs(VerifyParams V) {
+  const unsigned long long cnt = V.ctrl->n_caps_run;
+  const uint64_t n = cnt < V.cap_run_cap ? cnt : V.cap_run_cap;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const CapJob c = V.caps_run[i];
+    if (!(c.job & kJobRedo) && V.job_bad[c.job]) continue;  // a conflicting speculative job's match
+    if (is_long_file(V.off, c.file) != (sizeof(Pos) > 4)) continue;
+    const RuleDev& rd = V.rs.rules[c.rule];
+    const uint8_t* text = V.data + V.off[c.file];
+    const Pos ms = (Pos)c.ms, me = (Pos)c.me;
+    const uint32_t sm[4] = {rd.grp_s[0], rd.grp_s[1], rd.grp_s[2], rd.grp_s[3]};
+    const Pos ge = run_back<Pos>(text, ms, me, sm);
+    Pos gs;
+    if (rd.grp_run_len >= 0) {
+      gs = ge - (Pos)rd.grp_run_len;
+    } else {
+      const uint32_t bm[4] = {rd.grp_b[0], rd.grp_b[1], rd.grp_b[2], rd.grp_b[3]};
+      gs = run_back<Pos>(text, ms, ge, bm);
+    }
+    const unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
+    if (idx < V.loc_cap) V.locs[idx] = DevLoc{c.file, c.rule, (uint64_t)gs, (uint64_t)ge, 0, 0, 0, c.job};
   }
 }
 
@@ -3572,8 +3597,9 @@ __global__ __launch_bounds__(256) void k_arena_fill(FindParams F) {
     }
     uint64_t k = lo;
     if (a + 16 <= total && a + 16 <= F.seg_off[k] + F.seg_len[k]) {
-      // fast path: the 16 bytes lie in one segment and outside every censor
-      // interval -- two aligned 16-byte loads, a funnel shift, one store
+      // fast path: the 16 bytes lie in one segment -- two aligned 16-byte
+      // loads and a funnel shift, the censor intervals overlapping them (0-2,
+      // sorted) applied as a byte mask, one store
       const uint64_t x = F.seg_src[k] + (a - F.seg_off[k]);
       const uint32_t g0 = F.seg_grp[k].x, gm = F.seg_grp[k].y;
       uint32_t l2 = 0, h2 = gm;  // first interval ending after x
@@ -3582,30 +3608,38 @@ __global__ __launch_bounds__(256) void k_arena_fill(FindParams F) {
         if (F.iv[2 * (g0 + mid) + 1] <= x) l2 = mid + 1;
         else h2 = mid;
       }
-      if (l2 >= gm || F.iv[2 * (g0 + l2)] >= x + 16) {
-        const uint64_t src = F.off[F.seg_file[k]] + x;
-        const uint64_t b0 = src & ~15ull;
-        const uint32_t sh = (uint32_t)(src - b0);
-        const uint4 u = *(const uint4*)(F.data + b0);
-        uint4 o;
-        if (sh == 0) {
-          o = u;
-        } else {
-          const uint4 v = ld16_guard(F.data, b0 + 16, F.data_end);
-          const uint32_t d[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-          uint32_t r[4];
-          const uint32_t q = sh >> 2, bs = 8 * (sh & 3);
-#pragma unroll
-          for (int z = 0; z < 4; ++z) {
-            const uint32_t lo32 = q == 0 ? d[z] : q == 1 ? d[z + 1] : q == 2 ? d[z + 2] : d[z + 3];
-            const uint32_t hi32 = q == 0 ? d[z + 1] : q == 1 ? d[z + 2] : q == 2 ? d[z + 3] : d[z + 4];
-            r[z] = bs ? (lo32 >> bs) | (hi32 << (32 - bs)) : lo32;
-          }
-          o = make_uint4(r[0], r[1], r[2], r[3]);
-        }
-        *(uint4*)(F.arena + a) = o;
-        continue;
+      uint32_t cmask = 0;  // bit j: byte x + j is censored
+      for (uint32_t t2 = l2; t2 < gm; ++t2) {
+        const uint64_t is = F.iv[2 * (g0 + t2)], ie = F.iv[2 * (g0 + t2) + 1];
+        if (is >= x + 16) break;
+        const uint32_t b = is > x ? (uint32_t)(is - x) : 0u, e2 = ie < x + 16 ? (uint32_t)(ie - x) : 16u;
+        if (e2 > b) cmask |= ((1u << (e2 - b)) - 1u) << b;
       }
+      const uint64_t src = F.off[F.seg_file[k]] + x;
+      const uint64_t b0 = src & ~15ull;
+      const uint32_t sh = (uint32_t)(src - b0);
+      const uint4 u = *(const uint4*)(F.data + b0);
+      uint32_t r[4] = {u.x, u.y, u.z, u.w};
+      if (sh) {
+        const uint4 v = ld16_guard(F.data, b0 + 16, F.data_end);
+        const uint32_t d[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+        const uint32_t q = sh >> 2, bs = 8 * (sh & 3);
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+          const uint32_t lo32 = q == 0 ? d[z] : q == 1 ? d[z + 1] : q == 2 ? d[z + 2] : d[z + 3];
+          const uint32_t hi32 = q == 0 ? d[z + 1] : q == 1 ? d[z + 2] : q == 2 ? d[z + 3] : d[z + 4];
+          r[z] = bs ? (lo32 >> bs) | (hi32 << (32 - bs)) : lo32;
+        }
+      }
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        const uint32_t m4 = (cmask >> (4 * z)) & 0xFu;
+        const uint32_t bm = ((m4 & 1u) ? 0xFFu : 0u) | ((m4 & 2u) ? 0xFF00u : 0u) | ((m4 & 4u) ? 0xFF0000u : 0u) |
+                            ((m4 & 8u) ? 0xFF000000u : 0u);
+        r[z] = (r[z] & ~bm) | (0x2A2A2A2Au & bm);  // '*'
+      }
+      *(uint4*)(F.arena + a) = make_uint4(r[0], r[1], r[2], r[3]);
+      continue;
     }
     uint32_t w[4] = {0, 0, 0, 0};
     uint64_t kk = ~0ull, fbase = 0;
@@ -3920,7 +3954,7 @@ struct tsg_engine {
   DBuf<uint8_t> span_hi;
   DBuf<uint64_t> fold_pos;    // fold-special rune occurrences (k_fold_windows)
   uint64_t fold_need = 0;     // fold-position capacity learnt from a lost scan
-  DBuf<CapJob> caps, caps_big;
+  DBuf<CapJob> caps, caps_big, caps_run;
   DBuf<uint64_t> job_fms, job_lme;  // speculative jobs (k_chain_fix)
   DBuf<uint8_t> job_bad;
   DBuf<RedoRec> redo;
@@ -3930,6 +3964,7 @@ struct tsg_engine {
   DBuf<uint8_t> fflags8;     // per-file result flags, u8
   uint32_t num_cus = 0;
   DBuf<ExclRange> excl_out;
+  DBuf<uint8_t> part_buf;  // byte-range split: a part's packed scan state (export / import)
   uint32_t vm_threads = 0;
   uint64_t scratch_stride = 0;
   hipEvent_t ev[12];
@@ -4972,7 +5007,87 @@ void order_finding_ties(ResultImpl& R, bool all_runs) {
 // whole file, so the result is the single-GPU result by construction.  The
 // scan state is position-local: keyword bits (OR), anchor hits owned by their
 // literal start, and per-4 KiB-span newline counts and >= 0x80 flags.
-constexpr uint64_t kPartMagic = 0x3174726170677374ull;  // "tsgpart1"
+constexpr uint64_t kPartMagic = 0x3274726170677374ull;  // "tsgpart2"
+// Blob body after the header, packed and unpacked on the device: kw_words u32
+// keyword words | n_spans u16 newline counts | ceil(n_spans / 8) bytes of
+// ">= 0x80" span bits | n_hits u64 owned anchor hits (file-relative starts).
+__host__ __device__ inline uint64_t part_fixed_bytes(uint32_t kw_words, uint64_t n_spans) {
+  return (uint64_t)kw_words * 4 + n_spans * 2 + (n_spans + 7) / 8;
+}
+// Part export on the device: the owned anchor hits compacted (any order: the
+// candidates are sorted later) with file-relative starts, the keyword words,
+// per-span newline counts as u16 (<= 4096 per 4 KiB span) and the >= 0x80
+// flags as bits -- one buffer, one D2H.  out[0] (u64) counts the kept hits.
+struct PartPack {
+  const uint64_t* hits;
+  uint64_t n_hits;
+  const uint32_t* kw;
+  uint32_t kw_words;
+  const uint32_t* nl;
+  const uint8_t* span_hi;  // may be null
+  uint64_t sp0, n_spans;
+  uint64_t base, own_lo, own_hi;  // view base, owned range (file-relative)
+  uint8_t* out;                   // u64 count | fixed body | hits
+};
+
+__global__ void k_part_pack(PartPack K) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (uint64_t)gridDim.x * blockDim.x;
+  uint8_t* body = K.out + 8;
+  uint32_t* kw = (uint32_t*)body;
+  uint16_t* nl = (uint16_t*)(body + (uint64_t)K.kw_words * 4);
+  uint8_t* hib = body + (uint64_t)K.kw_words * 4 + K.n_spans * 2;
+  uint64_t* hits = (uint64_t*)(K.out + 8 + ((part_fixed_bytes(K.kw_words, K.n_spans) + 7) & ~7ull));
+  for (uint64_t i = t; i < K.kw_words; i += nt) kw[i] = K.kw[i];
+  for (uint64_t i = t; i < K.n_spans; i += nt) nl[i] = (uint16_t)K.nl[K.sp0 + i];
+  for (uint64_t i = t; i < (K.n_spans + 7) / 8; i += nt) {
+    uint32_t b = 0;
+    if (K.span_hi)
+      for (uint32_t k = 0; k < 8 && 8 * i + k < K.n_spans; ++k) b |= (K.span_hi[K.sp0 + 8 * i + k] ? 1u : 0u) << k;
+    hib[i] = (uint8_t)b;
+  }
+  for (uint64_t i = t; i < K.n_hits; i += nt) {
+    const uint64_t h = K.hits[i];
+    const uint64_t start = ((h & ~kFoldHit) >> 16) + K.base;
+    if (start < K.own_lo || start >= K.own_hi) continue;
+    const unsigned long long k = atomicAdd((unsigned long long*)K.out, 1ull);
+    hits[k] = (start << 16) | (h & (kFoldHit | 0xFFFFull));
+  }
+}
+
+// Part import on the device: one blob body (already in device memory) into
+// the merge's scan state; a hit outside the part's owned range sets *bad.
+struct PartUnpack {
+  const uint8_t* body;
+  uint32_t kw_words;
+  uint64_t n_spans, s0, n_hits;
+  uint64_t own_lo, own_hi;
+  uint32_t* kw;
+  uint32_t* nl;
+  uint8_t* span_hi;
+  uint64_t* hits;  // at this part's offset
+  unsigned int* bad;
+};
+
+__global__ void k_part_unpack(PartUnpack U) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (uint64_t)gridDim.x * blockDim.x;
+  const uint32_t* kw = (const uint32_t*)U.body;
+  const uint16_t* nl = (const uint16_t*)(U.body + (uint64_t)U.kw_words * 4);
+  const uint8_t* hib = U.body + (uint64_t)U.kw_words * 4 + U.n_spans * 2;
+  const uint64_t* hits = (const uint64_t*)(U.body + ((part_fixed_bytes(U.kw_words, U.n_spans) + 7) & ~7ull));
+  for (uint64_t i = t; i < U.kw_words; i += nt)
+    if (kw[i]) atomicOr(&U.kw[i], kw[i]);
+  for (uint64_t i = t; i < U.n_spans; i += nt) {
+    U.nl[U.s0 + i] = nl[i];
+    U.span_hi[U.s0 + i] = (hib[i >> 3] >> (i & 7)) & 1u;
+  }
+  for (uint64_t i = t; i < U.n_hits; i += nt) {
+    const uint64_t h = hits[i];
+    const uint64_t start = (h & ~kFoldHit) >> 16;
+    if (start < U.own_lo || start >= U.own_hi) atomicOr(U.bad, 1u);
+    U.hits[i] = h;
+  }
+}
+
 struct PartHeader {
   uint64_t magic, ruleset_id, file_len, own_lo, own_hi, n_hits;
   uint32_t kw_words, flags, n_spans, has_span_hi;
@@ -4980,7 +5095,8 @@ struct PartHeader {
 struct SplitIo {
   int mode = 0;  // 1: export the part [own_lo, own_hi) of a view; 2: merge parts
   uint64_t text_base = 0, own_lo = 0, own_hi = 0, file_len = 0;
-  std::vector<uint8_t>* blob = nullptr;                        // mode 1 output
+  uint8_t** blob_out = nullptr;                                // mode 1 output (page-locked, tsg_part_free)
+  size_t* blob_len = nullptr;
   const std::vector<std::pair<const uint8_t*, size_t>>* parts = nullptr;  // mode 2 input
 };
 
@@ -4996,38 +5112,35 @@ int export_part(tsg_engine* e, const tsg_ruleset* rs, const ScanParams& P, uint6
   hipStream_t s = e->stream;
   const uint64_t base = sp.text_base;
   const uint64_t sp0 = (sp.own_lo - base) / kNlBlock, sp1 = (sp.own_hi - base + kNlBlock - 1) / kNlBlock;
-  const uint32_t n_spans = (uint32_t)(sp1 - sp0);
+  const uint64_t n_spans = sp1 - sp0;
   const bool has_hi = P.span_hi != nullptr;
-  std::vector<uint64_t> h(n_hits);
-  std::vector<uint32_t> kw(P.rs.kw_words + 1), nl(n_spans + 1);
-  std::vector<uint8_t> hi(n_spans + 1, 0);
+  const uint64_t fixed = part_fixed_bytes(P.rs.kw_words, n_spans);
+  const uint64_t cap = 8 + ((fixed + 7) & ~7ull) + n_hits * 8;
+  HIP_TRY(e->part_buf.ensure(cap));
+  HIP_TRY(hipMemsetAsync(e->part_buf.p, 0, 8, s));
+  PartPack K{e->hits.p, n_hits, e->file_kw.p, P.rs.kw_words, e->nl_blocks.p, has_hi ? P.span_hi : nullptr,
+             sp0, n_spans, base, sp.own_lo, sp.own_hi, e->part_buf.p};
+  const uint64_t work = std::max<uint64_t>(std::max<uint64_t>(n_hits, n_spans), 1);
+  hipLaunchKernelGGL(k_part_pack, dim3((uint32_t)std::min<uint64_t>((work + 255) / 256, e->num_cus * 8ull)), dim3(256),
+                     0, s, K);
+  HIP_TRY(hipGetLastError());
+  // one D2H of the packed buffer into page-locked memory (the blob itself)
+  uint8_t* blob = nullptr;
+  if (hipHostMalloc((void**)&blob, sizeof(PartHeader) + cap, hipHostMallocDefault) != hipSuccess) {
+    set_last_error("hipHostMalloc failed for a part blob");
+    return TSG_ERR_DEVICE;
+  }
   uint32_t flags = 0;
-  if (n_hits) HIP_TRY(hipMemcpyAsync(h.data(), e->hits.p, n_hits * 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(kw.data(), e->file_kw.p, P.rs.kw_words * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(blob + sizeof(PartHeader) - 8, e->part_buf.p, cap, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(&flags, e->file_flags.p, 4, hipMemcpyDeviceToHost, s));
-  if (n_spans) HIP_TRY(hipMemcpyAsync(nl.data(), e->nl_blocks.p + sp0, n_spans * 4, hipMemcpyDeviceToHost, s));
-  if (n_spans && has_hi) HIP_TRY(hipMemcpyAsync(hi.data(), P.span_hi + sp0, n_spans, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   uint64_t kept = 0;
-  for (uint64_t i = 0; i < n_hits; ++i) {
-    const uint64_t start = ((h[i] & ~kFoldHit) >> 16) + base;
-    if (start < sp.own_lo || start >= sp.own_hi) continue;
-    h[kept++] = (start << 16) | (h[i] & (kFoldHit | 0xFFFFull));
-  }
-  PartHeader H{kPartMagic, rs->id, sp.file_len, sp.own_lo, sp.own_hi, kept, P.rs.kw_words, flags, n_spans,
+  memcpy(&kept, blob + sizeof(PartHeader) - 8, 8);  // (the count sits where the header's tail goes)
+  PartHeader H{kPartMagic, rs->id, sp.file_len, sp.own_lo, sp.own_hi, kept, P.rs.kw_words, flags, (uint32_t)n_spans,
                has_hi ? 1u : 0u};
-  auto& b = *sp.blob;
-  b.resize(sizeof(H) + kept * 8 + P.rs.kw_words * 4 + n_spans * 4 + n_spans);
-  uint8_t* w = b.data();
-  memcpy(w, &H, sizeof(H));
-  w += sizeof(H);
-  memcpy(w, h.data(), kept * 8);
-  w += kept * 8;
-  memcpy(w, kw.data(), P.rs.kw_words * 4);
-  w += P.rs.kw_words * 4;
-  memcpy(w, nl.data(), n_spans * 4);
-  w += n_spans * 4;
-  memcpy(w, hi.data(), n_spans);
+  memcpy(blob, &H, sizeof(H));
+  *sp.blob_out = blob;
+  *sp.blob_len = sizeof(PartHeader) + ((fixed + 7) & ~7ull) + kept * 8;
   return TSG_OK;
 }
 
@@ -5049,16 +5162,9 @@ int import_parts(tsg_engine* e, const tsg_ruleset* rs, ScanParams& P, const Spli
               H->file_len == sp.file_len && H->own_lo < H->own_hi && H->own_hi <= sp.file_len &&
               H->own_lo % kNlBlock == 0 && (H->own_hi % kNlBlock == 0 || H->own_hi == sp.file_len) &&
               H->n_spans == (H->own_hi - H->own_lo + kNlBlock - 1) / kNlBlock && H->n_hits <= body / 8;
-    if (ok) {
-      const size_t need = (size_t)H->n_hits * 8 + (size_t)H->kw_words * 4 + (size_t)H->n_spans * 5;
-      ok = body == need;
-    }
-    if (ok) {  // every hit's literal starts inside the part's own range
-      const uint64_t* hp = (const uint64_t*)(H + 1);
-      for (uint64_t i = 0; i < H->n_hits && ok; ++i) {
-        const uint64_t start = (hp[i] & ~kFoldHit) >> 16;
-        ok = start >= H->own_lo && start < H->own_hi;
-      }
+    if (ok) {  // (every hit's start is checked on the device: k_part_unpack)
+      const uint64_t fixed = (part_fixed_bytes(H->kw_words, H->n_spans) + 7) & ~7ull;
+      ok = body == fixed + (size_t)H->n_hits * 8;
     }
     if (!ok) {
       set_last_error("split: a part blob belongs to another file or ruleset, or is corrupt");
@@ -5083,44 +5189,50 @@ int import_parts(tsg_engine* e, const tsg_ruleset* rs, ScanParams& P, const Spli
     return TSG_ERR_INVALID_ARG;
   }
   const uint64_t n_nlb = P.nbytes / kNlBlock + 2, n_spans = (P.nbytes + kNlBlock - 1) / kNlBlock;
-  std::vector<uint64_t> hits;
-  hits.reserve(total);
-  std::vector<uint32_t> kw(P.rs.kw_words + 1, 0), nl(n_nlb, 0);
-  std::vector<uint8_t> hi(n_spans + 1, 0);
+  // every body to the device (one H2D each, straight from the caller's
+  // blob), then unpacked there: keyword words OR'd, newline counts and span
+  // bits at their spans, hits appended part after part
+  uint64_t body_total = 0;
+  for (size_t i : order) body_total += parts[i].second - sizeof(PartHeader);
+  HIP_TRY(e->part_buf.ensure(body_total + 8));
+  HIP_TRY(e->hits.ensure(std::max<uint64_t>(total, 1)));
+  HIP_TRY(e->nl_blocks.ensure(n_nlb));
+  HIP_TRY(e->span_hi.ensure(n_spans + 1));
+  HIP_TRY(hipMemsetAsync(e->nl_blocks.p, 0, n_nlb * 4, s));
+  HIP_TRY(hipMemsetAsync(e->span_hi.p, 0, n_spans + 1, s));
+  HIP_TRY(hipMemsetAsync(&e->ctrl.p->err, 0, 4, s));
   uint32_t flags = 0;
   bool all_hi = true;
+  uint64_t at_body = 0, at_hit = 0;
   for (size_t i : order) {
     const PartHeader* H = hs[i];
-    const uint8_t* r = (const uint8_t*)(H + 1);
-    const uint64_t* hp = (const uint64_t*)r;
-    hits.insert(hits.end(), hp, hp + H->n_hits);
-    r += H->n_hits * 8;
-    const uint32_t* kp = (const uint32_t*)r;
-    for (uint32_t k = 0; k < H->kw_words; ++k) kw[k] |= kp[k];
-    r += (size_t)H->kw_words * 4;
-    const uint64_t s0 = H->own_lo / kNlBlock;
-    memcpy(nl.data() + s0, r, (size_t)H->n_spans * 4);
-    r += (size_t)H->n_spans * 4;
-    memcpy(hi.data() + s0, r, H->n_spans);
+    const size_t blen = parts[i].second - sizeof(PartHeader);
+    HIP_TRY(hipMemcpyAsync(e->part_buf.p + at_body, (const uint8_t*)(H + 1), blen, hipMemcpyHostToDevice, s));
+    PartUnpack U{e->part_buf.p + at_body, H->kw_words, H->n_spans, H->own_lo / kNlBlock, H->n_hits, H->own_lo,
+                 H->own_hi, e->file_kw.p, e->nl_blocks.p, e->span_hi.p, e->hits.p + at_hit, &e->ctrl.p->err};
+    const uint64_t work = std::max<uint64_t>(std::max<uint64_t>(H->n_hits, H->n_spans), 1);
+    hipLaunchKernelGGL(k_part_unpack, dim3((uint32_t)std::min<uint64_t>((work + 255) / 256, e->num_cus * 8ull)),
+                       dim3(256), 0, s, U);
+    HIP_TRY(hipGetLastError());
+    at_body += (blen + 15) & ~(size_t)15;
+    at_hit += H->n_hits;
     flags |= H->flags & ~kFileAllowed;  // the owner's path gate decides AllowPath
     all_hi = all_hi && H->has_span_hi;
   }
-  HIP_TRY(e->hits.ensure(std::max<uint64_t>(total, 1)));
-  if (total) HIP_TRY(hipMemcpyAsync(e->hits.p, hits.data(), total * 8, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(e->file_kw.p, kw.data(), P.rs.kw_words * 4, hipMemcpyHostToDevice, s));
-  HIP_TRY(e->nl_blocks.ensure(n_nlb));
-  HIP_TRY(hipMemcpyAsync(e->nl_blocks.p, nl.data(), n_nlb * 4, hipMemcpyHostToDevice, s));
-  HIP_TRY(e->span_hi.ensure(n_spans + 1));
-  HIP_TRY(hipMemcpyAsync(e->span_hi.p, hi.data(), n_spans + 1, hipMemcpyHostToDevice, s));
   P.span_hi = all_hi ? e->span_hi.p : nullptr;  // (no flags: k_uni_keywords searches every span)
   const uint64_t n_regions = P.nbytes / kNlBlock + 1;
   HIP_TRY(e->region_file.ensure(n_regions + 1));
   HIP_TRY(hipMemsetAsync(e->region_file.p, 0, (n_regions + 1) * 4, s));  // one file
   P.n_regions = n_regions;  // (k_uni_keywords' file lookup reads them through P)
   P.region_file = e->region_file.p;
-  uint32_t f0 = 0;
+  uint32_t f0 = 0, bad = 0;
   HIP_TRY(hipMemcpyAsync(&f0, e->file_flags.p, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&bad, &e->ctrl.p->err, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  if (bad) {
+    set_last_error("split: a part blob belongs to another file or ruleset, or is corrupt");
+    return TSG_ERR_INVALID_ARG;
+  }
   f0 |= flags;
   HIP_TRY(hipMemcpy(e->file_flags.p, &f0, 4, hipMemcpyHostToDevice));
   *n_hits_out = total;
@@ -5361,6 +5473,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   // ---- 5. verify
   uint64_t loc_cap = std::max<uint64_t>(1 << 16, n_cands);
   uint64_t caps_cap = std::max<uint64_t>(1 << 14, n_cands / 2), caps_big_cap = std::max<uint64_t>(1 << 12, n_cands / 16);
+  uint64_t caps_run_cap = std::max<uint64_t>(1 << 14, n_cands);
   uint64_t redo_cap = std::max<uint64_t>(1 << 12, n_cands / 64);
   uint64_t n_locs = 0, n_dropped = 0;
   bool verified = n_cands == 0;
@@ -5368,6 +5481,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(e->locs.ensure(loc_cap));
     HIP_TRY(e->caps.ensure(caps_cap));
     HIP_TRY(e->caps_big.ensure(caps_big_cap));
+    HIP_TRY(e->caps_run.ensure(caps_run_cap));
     HIP_TRY(e->job_fms.ensure(n_cands));
     HIP_TRY(e->job_lme.ensure(n_cands));
     HIP_TRY(e->job_bad.ensure(n_cands));
@@ -5375,7 +5489,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(hipMemsetAsync(e->job_bad.p, 0, n_cands, s));
     HIP_TRY(hipMemsetAsync(&e->ctrl.p->locs, 0, 8, s));
     HIP_TRY(hipMemsetAsync(&e->ctrl.p->n_caps, 0, 16, s));  // n_caps, n_caps_big
-    HIP_TRY(hipMemsetAsync(&e->ctrl.p->n_redo, 0, 16, s));  // n_redo, n_dropped
+    HIP_TRY(hipMemsetAsync(&e->ctrl.p->n_redo, 0, 24, s));  // n_redo, n_dropped, n_caps_run
     VerifyParams V{};
     V.data = d_data;
     V.off = d_off;
@@ -5394,6 +5508,8 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     V.cap_cap = e->caps.n;
     V.caps_big = e->caps_big.p;
     V.cap_big_cap = e->caps_big.n;
+    V.caps_run = e->caps_run.p;
+    V.cap_run_cap = e->caps_run.n;
     V.job_fms = e->job_fms.p;
     V.job_lme = e->job_lme.p;
     V.split = e->flags8.p;
@@ -5456,6 +5572,8 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     // capture stages over the device-side lists: 8 searching lanes per wave with
     // 560-word arenas, then one lane per wave with 36 KiB for what does not fit
     // (grids keep every lane's VM scratch slot below vm_threads: 512 / 256 per CU)
+    hipLaunchKernelGGL(k_group_runs<uint32_t>, dim3(e->num_cus * 4), dim3(256), 0, s, V);
+    if (any_long) hipLaunchKernelGGL(k_group_runs<uint64_t>, dim3(e->num_cus * 4), dim3(256), 0, s, V);
     hipLaunchKernelGGL((k_captures<64, kCapActive, kBsWords, false, uint32_t>), dim3(e->num_cus * 8), dim3(64), 0, s, V);
     if (any_long)
       hipLaunchKernelGGL((k_captures<64, kCapActive, kBsWords, false, uint64_t>), dim3(e->num_cus * 8), dim3(64), 0, s,
@@ -5537,7 +5655,8 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     if ((rc = read_ctrl(e, &c))) return rc;
     n_locs = c.locs;
     n_dropped = c.n_dropped;
-    if (n_locs <= e->locs.n && c.n_caps <= e->caps.n && c.n_caps_big <= e->caps_big.n && c.n_redo <= e->redo.n) {
+    if (n_locs <= e->locs.n && c.n_caps <= e->caps.n && c.n_caps_big <= e->caps_big.n && c.n_redo <= e->redo.n &&
+        c.n_caps_run <= e->caps_run.n) {
       verified = true;
       break;
     }
@@ -5546,6 +5665,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     caps_cap = std::max<uint64_t>(caps_cap, c.n_caps);
     caps_big_cap = std::max<uint64_t>(caps_big_cap, c.n_caps_big);
     redo_cap = std::max<uint64_t>(redo_cap, c.n_redo);
+    caps_run_cap = std::max<uint64_t>(caps_run_cap, c.n_caps_run);
   }
   if (!verified) {
     set_last_error("internal: location buffers still overflowed after regrowing them");
@@ -5829,7 +5949,7 @@ void tsg_engine_free(tsg_engine* e) {
   e->file_kw.release(); e->file_flags.release(); e->path_mask.release(); e->hits.release();
   e->keys.release(); e->keys2.release(); e->vals.release(); e->vals2.release(); e->flags8.release();
   e->job_start.release(); e->nsel.release(); e->cub_tmp.release(); e->locs.release(); e->locs2.release();
-  e->scratch.release(); e->ctrl.release(); e->excl_out.release();
+  e->scratch.release(); e->ctrl.release(); e->excl_out.release(); e->part_buf.release(); e->caps_run.release();
   e->nl_blocks.release(); e->nl_pre.release(); e->tail.release(); e->region_file.release(); e->region_tmp.release();
   e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->fold_pos.release(); e->caps.release(); e->caps_big.release();
   e->job_fms.release(); e->job_lme.release(); e->job_bad.release(); e->redo.release(); e->vprof.release(); e->fflags8.release();
@@ -5922,21 +6042,16 @@ static int scan_part_impl(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d
   }
   int rc = stage_one_file(e, text_len, path);
   if (rc) return rc;
-  std::vector<uint8_t> out;
   SplitIo sp;
   sp.mode = 1;
   sp.text_base = text_base;
   sp.own_lo = own_lo;
   sp.own_hi = own_hi;
   sp.file_len = file_len;
-  sp.blob = &out;
+  sp.blob_out = blob;
+  sp.blob_len = blob_len;
   tsg_result tmp;
-  if ((rc = run_pipeline(e, rs, d_text, e->off.p, e->paths.p, e->path_off.p, 1, text_len + 1, &tmp, &sp))) return rc;
-  *blob = (uint8_t*)malloc(out.size());
-  if (!*blob) return TSG_ERR_INTERNAL;
-  memcpy(*blob, out.data(), out.size());
-  *blob_len = out.size();
-  return TSG_OK;
+  return run_pipeline(e, rs, d_text, e->off.p, e->paths.p, e->path_off.p, 1, text_len + 1, &tmp, &sp);
 }
 
 int tsg_scan_part_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_text, uint64_t text_base,
@@ -5950,7 +6065,9 @@ int tsg_scan_part_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_
   }
 }
 
-void tsg_part_free(uint8_t* blob) { free(blob); }
+void tsg_part_free(uint8_t* blob) {
+  if (blob) (void)hipHostFree(blob);
+}
 
 static int scan_merge_impl(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_file, uint64_t file_len,
                            const char* path, const uint8_t* const* blobs, const size_t* blob_lens, size_t n_parts,
