@@ -151,6 +151,14 @@ int tsg_ruleset_group_span(const tsg_ruleset* rs, size_t i, int* valid, int* pre
  * rules. */
 int tsg_ruleset_group_run(const tsg_ruleset* rs, size_t i, int* valid, int* len, uint32_t* s_alpha,
                           uint32_t* b_alpha);
+/* MatchString of rule i's path regex (which = 0), its first allow-path regex
+ * (which = 1) or the i-th global allow path (which = 2) through the DFA the
+ * path gate walks (diagnostics / tests):
+ * *result 1 = match, 0 = none, 2 = no DFA or undecidable (the Pike VM
+ * decides).  Replaces regexp.MatchString in Rule.MatchPath / AllowPath
+ * (pkg/fanal/secret/scanner.go:391,397). */
+int tsg_ruleset_path_dfa_check(const tsg_ruleset* rs, size_t i, int which, const uint8_t* path, size_t len,
+                               int* result);
 
 /* Candidate filter of rule i, run on host text from anchor position h:
  * *accept = 0 only when no match of the rule can contain an anchor hit at h

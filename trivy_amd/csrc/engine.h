@@ -284,6 +284,9 @@ struct PatternHost {
 struct tsg_ruleset {
   std::vector<tsg::RegexHost> regexes;
   std::map<std::string, int> regex_ids;  // source -> regexes index
+  // MatchString DFAs of the path regexes (k_path_gate): the DFA of
+  // (?s:.)*?(?:src), anchored at 0, per regexes index (invalid: Pike VM)
+  std::vector<tsg::DfaHost> path_dfa;
   std::vector<tsg::RuleHost> rules;
   std::vector<int> global_allow_regex;  // AllowRules with Regex
   std::vector<int> global_allow_path;   // AllowRules with Path

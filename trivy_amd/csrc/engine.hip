@@ -1485,6 +1485,70 @@ __global__ __launch_bounds__(256) void k_fold_windows(ScanParams P, FoldItems F)
 }
 
 // ---------------------------------------------------------------- gating --
+constexpr uint32_t kPathDfaRec = 8;  // u32 per program: off, ncls, cls_off, start0, start1, smatch, sym, valid
+
+struct DfaRef {
+  const uint16_t* T;
+  const uint8_t* cls;
+  uint32_t K, start0, start1, smatch, sym;
+};
+
+
+// kLds: d.T / d.cls are the block's LDS copy (k_verify stages the wave's rule).
+template <bool kLds, class Pos>
+__device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, Pos n, Pos s, Pos* me,
+                                       uint32_t* steps) {
+  typedef __attribute__((address_space(3))) const uint16_t lu16;
+  typedef __attribute__((address_space(3))) const uint8_t lu8;
+  gu16* Tg = as_global<gu16>(d.T);
+  gu8* cg = as_global<gu8>(d.cls);
+  lu16* Tl = (lu16*)d.T;  // addrspacecast: only meaningful (and only read) when kLds
+  lu8* cl = (lu8*)d.cls;
+  uint32_t st = s == 0 ? d.start1 : d.start0;
+  int64_t last = ((d.smatch >> (s == 0 ? 1 : 0)) & 1) ? (int64_t)s : -1;
+  const uint32_t K = d.K;
+  // the text in aligned 16-byte blocks, one dwordx4 load each (a byte load per
+  // step cost a TLB lookup per lane per byte; the batch is padded past its
+  // end, so a block holding a content byte never leaves the allocation)
+  const uintptr_t base = reinterpret_cast<uintptr_t>(text);
+  Pos q = s;
+  while (q < n && st) {
+    const uintptr_t addr = (base + q) & ~(uintptr_t)15;
+    const u32x4 v = *as_global<__attribute__((address_space(1))) const u32x4>(reinterpret_cast<const void*>(addr));
+    uint32_t i = (uint32_t)((base + q) & 15);
+    while (i < 16 && q < n && st) {
+      const uint32_t wd = i < 8 ? (i < 4 ? v.x : v.y) : (i < 12 ? v.z : v.w);  // no dynamically indexed array
+      const uint32_t c = (wd >> (8 * (i & 3))) & 0xFFu;
+      uint32_t k, w = 1;
+      if (c < 0x80) {
+        k = kLds ? cl[c] : cg[c];
+      } else {
+        // a decoded rune: K, ſ, İ, U+FFFD or any other non-ASCII rune (dfa.cpp
+        // symbols after the ASCII classes); the VM decides only when this
+        // program tells other non-ASCII runes apart
+        const int r = gre::decode_rune(text, n, q, &w);
+        const uint32_t j = r == 0x212A ? 0u : r == 0x17F ? 1u : r == 0x130 ? 2u : r == 0xFFFD ? 3u : 4u;
+        if (j == 4 && !(d.sym >> 31)) return 2;
+        k = (d.sym & 0x7FFFFFFFu) + j;
+      }
+      const uint32_t e = kLds ? Tl[st * K + k] : Tg[st * K + k];
+      ++*steps;
+      if (q + w == n) {
+        if (e & 0x8000u) last = n;
+        st = 0;
+        break;
+      }
+      st = e & kDfaStateMask;
+      q += w;
+      i += w;
+      if (e & 0x4000u) last = q;
+    }
+  }
+  if (last < 0) return 0;
+  *me = (Pos)last;
+  return 1;
+}
+
 struct GateParams {
   const uint64_t* off;
   const uint8_t* paths;
@@ -1510,6 +1574,7 @@ struct GateParams {
   uint32_t o_pac_cls, o_pac_out_off, o_pac_out, o_pac_lits, o_pac_req, o_pac_bit;
   uint64_t pac_always;  // path progs without a literal filter
   uint32_t n_progs;
+  const uint32_t* pdfa;  // per program: its MatchString DFA record (kPathDfaRec u32; valid flag last)
 };
 
 __device__ inline gre::VmScratch make_scratch(uint8_t* base, const RuleSetDev& rs) {
@@ -1700,9 +1765,21 @@ __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
       const uint32_t b = prog < G.n_progs ? pbit[prog] : 0xFFu;
       return b == 0xFFu || ((mask >> b) & 1);
     };
+    // MatchString: the program's (?s:.)*?(?:re) DFA walked once over the path
+    // (ruleset.cpp path_dfa), the Pike VM when there is none or a rune the DFA
+    // cannot decide
+    auto path_matches = [&](uint32_t prog) {
+      const uint32_t* q = G.pdfa + (size_t)prog * kPathDfaRec;
+      if (q[7]) {
+        const DfaRef d{G.rs.dfa_delta + q[0], G.rs.dfa_bytes + q[2], q[1], q[3], q[4], q[5], q[6]};
+        uint32_t me = 0, steps = 0;
+        const int r = dfa_anchored_dev<false, uint32_t>(d, path, plen, 0u, &me, &steps);
+        if (r != 2) return r == 1;
+      }
+      return match_string(G.rs.progs[prog], path, plen, sc);
+    };
     bool allowed = false;
-    for (uint32_t k = 0; k < G.n_gpath && !allowed; ++k)
-      allowed = may(G.gpath[k]) && match_string(G.rs.progs[G.gpath[k]], path, plen, sc);
+    for (uint32_t k = 0; k < G.n_gpath && !allowed; ++k) allowed = may(G.gpath[k]) && path_matches(G.gpath[k]);
     if (allowed) {
       atomicOr(&G.file_flags[f], kFileAllowed);  // the scan flags files concurrently (side stream)
       continue;
@@ -1715,7 +1792,7 @@ __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
     auto path_match = [&](uint32_t prog) {
       if (prog != memo_prog) {
         memo_prog = prog;
-        memo_res = may(prog) && match_string(G.rs.progs[prog], path, plen, sc);
+        memo_res = may(prog) && path_matches(prog);
       }
       return memo_res;
     };
@@ -2104,68 +2181,6 @@ __device__ bool vm_search_starts(const gre::ProgView& p, const uint8_t* text, Po
 // T / cls: the rule's table and class map, in global memory or staged in LDS.
 // Plain scalars (no RuleDev reference: a by-reference struct lands in scratch
 // and its fields get reloaded inside the walk).
-struct DfaRef {
-  const uint16_t* T;
-  const uint8_t* cls;
-  uint32_t K, start0, start1, smatch, sym;
-};
-
-
-// kLds: d.T / d.cls are the block's LDS copy (k_verify stages the wave's rule).
-template <bool kLds, class Pos>
-__device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, Pos n, Pos s, Pos* me,
-                                       uint32_t* steps) {
-  typedef __attribute__((address_space(3))) const uint16_t lu16;
-  typedef __attribute__((address_space(3))) const uint8_t lu8;
-  gu16* Tg = as_global<gu16>(d.T);
-  gu8* cg = as_global<gu8>(d.cls);
-  lu16* Tl = (lu16*)d.T;  // addrspacecast: only meaningful (and only read) when kLds
-  lu8* cl = (lu8*)d.cls;
-  uint32_t st = s == 0 ? d.start1 : d.start0;
-  int64_t last = ((d.smatch >> (s == 0 ? 1 : 0)) & 1) ? (int64_t)s : -1;
-  const uint32_t K = d.K;
-  // the text in aligned 16-byte blocks, one dwordx4 load each (a byte load per
-  // step cost a TLB lookup per lane per byte; the batch is padded past its
-  // end, so a block holding a content byte never leaves the allocation)
-  const uintptr_t base = reinterpret_cast<uintptr_t>(text);
-  Pos q = s;
-  while (q < n && st) {
-    const uintptr_t addr = (base + q) & ~(uintptr_t)15;
-    const u32x4 v = *as_global<__attribute__((address_space(1))) const u32x4>(reinterpret_cast<const void*>(addr));
-    uint32_t i = (uint32_t)((base + q) & 15);
-    while (i < 16 && q < n && st) {
-      const uint32_t wd = i < 8 ? (i < 4 ? v.x : v.y) : (i < 12 ? v.z : v.w);  // no dynamically indexed array
-      const uint32_t c = (wd >> (8 * (i & 3))) & 0xFFu;
-      uint32_t k, w = 1;
-      if (c < 0x80) {
-        k = kLds ? cl[c] : cg[c];
-      } else {
-        // a decoded rune: K, ſ, İ, U+FFFD or any other non-ASCII rune (dfa.cpp
-        // symbols after the ASCII classes); the VM decides only when this
-        // program tells other non-ASCII runes apart
-        const int r = gre::decode_rune(text, n, q, &w);
-        const uint32_t j = r == 0x212A ? 0u : r == 0x17F ? 1u : r == 0x130 ? 2u : r == 0xFFFD ? 3u : 4u;
-        if (j == 4 && !(d.sym >> 31)) return 2;
-        k = (d.sym & 0x7FFFFFFFu) + j;
-      }
-      const uint32_t e = kLds ? Tl[st * K + k] : Tg[st * K + k];
-      ++*steps;
-      if (q + w == n) {
-        if (e & 0x8000u) last = n;
-        st = 0;
-        break;
-      }
-      st = e & kDfaStateMask;
-      q += w;
-      i += w;
-      if (e & 0x4000u) last = q;
-    }
-  }
-  if (last < 0) return 0;
-  *me = (Pos)last;
-  return 1;
-}
-
 // Bit-state backtracker (go1.22 regexp/backtrack.go semantics: depth-first in
 // priority order, each (pc, pos) visited once, so the first MATCH reached is
 // the leftmost-first match and its captures are Go's) for the secret-group
@@ -3914,6 +3929,7 @@ struct DevImage {
   uint32_t o_gpath = 0, n_gpath = 0, o_apoff = 0, o_ap = 0, o_full = 0, n_full = 0, o_prules = 0, n_prules = 0;
   uint32_t o_fold = 0, n_fold_items = 0;  // k_fold_windows work items
   uint32_t o_xoff = 0, o_xprog = 0, o_gx = 0, n_gx = 0, max_x = 0;  // exclude blocks (ExclDev)
+  uint32_t o_pdfa = 0;  // path-regex MatchString DFA records (kPathDfaRec u32 per program)
   void release() {
     big.release();
     inst.release(); classes.release(); ranges.release(); progs.release(); rules.release();
@@ -4246,6 +4262,28 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
     }
     im.o_fold = append(fold);
     im.n_fold_items = (uint32_t)fold.size();
+  }
+  {  // path-regex MatchString DFAs (k_path_gate): kPathDfaRec u32 per program
+    std::vector<uint32_t> pd(rs->regexes.size() * kPathDfaRec, 0);
+    for (size_t x = 0; x < rs->path_dfa.size(); ++x) {
+      const DfaHost& D = rs->path_dfa[x];
+      if (!D.valid) continue;
+      if (ddelta.size() & 1) ddelta.push_back(0);
+      uint32_t* q = pd.data() + x * kPathDfaRec;
+      q[0] = (uint32_t)ddelta.size();
+      q[1] = D.ncls;
+      q[2] = (uint32_t)dbytes.size();
+      dbytes.insert(dbytes.end(), D.cls, D.cls + 128);
+      dbytes.insert(dbytes.end(), D.match.begin(), D.match.end());
+      q[3] = D.start[0];
+      q[4] = D.start[1];
+      q[5] = (D.match[D.start[0]] ? 1u : 0u) | (D.match[D.start[1]] ? 2u : 0u);
+      q[6] = D.sym_base | (D.na_ok ? 0x80000000u : 0u);
+      q[7] = 1;
+      ddelta.insert(ddelta.end(), D.delta.begin(), D.delta.end());
+    }
+    im.o_pdfa = (uint32_t)u32.size();
+    u32.insert(u32.end(), pd.begin(), pd.end());
   }
   HIP_TRY(im.u32.ensure(u32.size() + 1));
   if (!u32.empty()) HIP_TRY(hipMemcpy(im.u32.p, u32.data(), u32.size() * 4, hipMemcpyHostToDevice));
@@ -5313,6 +5351,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     G.o_pac_bit = im.o_pac_bit;
     G.pac_always = im.pac_always;
     G.n_progs = (uint32_t)rs->regexes.size();
+    G.pdfa = im.u32.p + im.o_pdfa;
     uint32_t blocks = std::min<uint32_t>((nf + 255) / 256, e->vm_threads / 256);
     hipLaunchKernelGGL(k_path_gate, dim3(std::max(1u, blocks)), dim3(256), 0, s, G);
     HIP_TRY(hipGetLastError());

@@ -593,6 +593,20 @@ int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_r
     }
   }
   if (!build_ac(rs, &e)) return fail(TSG_ERR_UNSUPPORTED);
+  {  // path regexes: MatchString as one anchored DFA walk over the path
+    rs->path_dfa.assign(rs->regexes.size(), DfaHost{});
+    std::vector<int> pr(rs->global_allow_path.begin(), rs->global_allow_path.end());
+    for (auto& r : rs->rules) {
+      if (r.path >= 0) pr.push_back(r.path);
+      pr.insert(pr.end(), r.allow_path.begin(), r.allow_path.end());
+    }
+    for (int x : pr) {
+      if (rs->path_dfa[x].valid) continue;
+      gre::Compiled any;
+      std::string err2;
+      if (gre::compile("(?s:.)*?(?:" + rs->regexes[x].src + ")", &any, &err2)) build_dfa(any, &rs->path_dfa[x]);
+    }
+  }
   *out = rs;
   return TSG_OK;
 }
@@ -710,6 +724,29 @@ int tsg_ruleset_dfa_check(const tsg_ruleset* rs, size_t i, const uint8_t* text, 
   size_t e = 0;
   *result = dfa_anchored(d, text, len, s, &e);
   if (me) *me = e;
+  return TSG_OK;
+}
+
+// MatchString of rule i's path regex (which = 0), its first allow-path regex
+// (which = 1) or the i-th global allow path (which = 2) through the path DFA
+// k_path_gate walks (ruleset path_dfa):
+// *result 1 = match, 0 = none, 2 = no DFA / undecidable (the Pike VM decides).
+int tsg_ruleset_path_dfa_check(const tsg_ruleset* rs, size_t i, int which, const uint8_t* path, size_t len,
+                               int* result) {
+  if (!rs || !result || (len && !path)) return TSG_ERR_INVALID_ARG;
+  int x = -1;
+  if (which == 2) {  // i-th global allow path
+    if (i >= rs->global_allow_path.size()) return TSG_ERR_INVALID_ARG;
+    x = rs->global_allow_path[i];
+  } else {
+    if (i >= rs->rules.size()) return TSG_ERR_INVALID_ARG;
+    const RuleHost& r = rs->rules[i];
+    x = which == 0 ? r.path : (r.allow_path.empty() ? -1 : r.allow_path[0]);
+  }
+  *result = 2;
+  if (x < 0 || (size_t)x >= rs->path_dfa.size() || !rs->path_dfa[x].valid) return TSG_OK;
+  size_t e = 0;
+  *result = dfa_anchored(rs->path_dfa[x], path, len, 0, &e);
   return TSG_OK;
 }
 
