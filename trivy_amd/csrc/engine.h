@@ -109,6 +109,7 @@ struct AcDev {
   // k_report's LDS blob = fast image | out_off | out_pat | pats | pat_bytes
   // (fast_lds is its start; offsets in bytes)
   uint32_t rep_bytes, o_out_off, o_out_pat, o_pats, o_pat_bytes;
+  uint32_t o_pair;  // the pair table's offset in the blob (0: none)
 };
 
 constexpr uint32_t kLitRec = 36;  // prefilter literal record: len, lower[16], req[16], exact, pad
@@ -266,6 +267,9 @@ struct AcHost {
   std::vector<uint16_t> fast_out_pat;
   std::vector<uint8_t> fast_ext;
   uint32_t fast_states = 0;
+  // k_scan_fast pair table: the state two bytes after the root, per column
+  // pair (64 x 64 u16); empty when a state one byte from the root has outputs
+  std::vector<uint16_t> fast_pair;
 };
 
 struct PatternHost {

@@ -414,6 +414,28 @@ __device__ inline uint32_t fstep(const uint8_t* T, uint32_t e, uint32_t w, int j
 }
 
 
+// Two bytes (j, j + 1 of the folded dword w, j even) from entry e: a lane at
+// the root reads the state after both from the pair table (at kFastImgMax in
+// LDS), the others walk two rows (the root lanes sit the second read out, so
+// the LDS serves fewer lanes).  Returns the larger of the states passed; the
+// skipped middle state of a root pair is never an output (ruleset.cpp).
+__device__ inline uint32_t fstep2(const uint8_t* T, uint32_t& e, uint32_t w, int j) {
+  uint32_t c1, c2;
+  if (j == 0) c1 = w & 0xFFu;
+  else asm("v_bfe_u32 %0, %1, %2, 8" : "=v"(c1) : "v"(w), "i"(8 * j));
+  if (j + 1 == 3) c2 = w >> 24;
+  else asm("v_bfe_u32 %0, %1, %2, 8" : "=v"(c2) : "v"(w), "i"(8 * (j + 1)));
+  const uint32_t a = e == 0 ? kFastImgMax + c1 * 64u + c2 : e * kFastRowBytes + c1;
+  uint32_t x = *(const uint16_t*)(T + a);
+  uint32_t m = x;
+  if (e != 0) {
+    x = *(const uint16_t*)(T + (x * kFastRowBytes + c2));
+    m = m > x ? m : x;
+  }
+  e = x;
+  return m;
+}
+
 // `src` for a position: the batch, or for the final partial unit the
 // zero-padded copy addressed with the same offsets (ScanParams::tail).
 __device__ inline const uint8_t* fast_src(const ScanParams& P, uint64_t pos) {
@@ -524,7 +546,7 @@ __device__ inline void fast_group2(const ScanParams& P, const uint8_t* T, uint32
 // output state anywhere in the window (rare: ~one group in 10^3) are the
 // groups' events appended in order.  Cuts the compare / ballot / branch per
 // group that otherwise sits on every chain step.
-template <int V, int kMode, int G>
+template <int V, int kMode, int G, bool kPair = false>
 __device__ inline void fast_window(const ScanParams& P, const uint8_t* T, uint32_t out_e, FastChain<V>& C,
                                    const uint32_t (&d)[2 * G], uint64_t gpos, bool live, uint64_t lanes_lt,
                                    FastEvent* ev_seg, uint32_t* ev_count) {
@@ -537,10 +559,18 @@ __device__ inline void fast_window(const ScanParams& P, const uint8_t* T, uint32
     const uint32_t f0 = fold6(d0), f1 = fold6(d1);
     gs[g] = C.e;
     uint32_t mm = 0;
+    if (kPair) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      C.e = fstep(T, C.e, j < 4 ? f0 : f1, j & 3);
-      mm = mm > C.e ? mm : C.e;
+      for (int j = 0; j < 8; j += 2) {
+        const uint32_t x = fstep2(T, C.e, j < 4 ? f0 : f1, j & 3);
+        mm = mm > x ? mm : x;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        C.e = fstep(T, C.e, j < 4 ? f0 : f1, j & 3);
+        mm = mm > C.e ? mm : C.e;
+      }
     }
     m[g] = mm;
   }
@@ -559,17 +589,23 @@ __device__ inline void fast_window(const ScanParams& P, const uint8_t* T, uint32
   C.prev = make_uint2(d[2 * G - 2], d[2 * G - 1]);
 }
 
-template <int CH, int V, int kFastThreads, int kMode = 0, int kWin = 1>
+template <int CH, int V, int kFastThreads, int kMode = 0, int kWin = 1, bool kPair = false>
 __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
   constexpr uint32_t kUnit = CH * kNlBlock;          // bytes per lane per work unit
   constexpr int kStep = V * 16;                      // bytes per chain step
   constexpr int kSteps = kNlBlock / kStep;           // steps per span
-  __shared__ __align__(16) uint8_t smem[kFastImgMax];  // static: LDS base folds to 0 in the step
+  // static: LDS base folds to 0 in the step (kPair: the pair table follows the image)
+  __shared__ __align__(16) uint8_t smem[kFastImgMax + (kPair ? kFastCols * kFastCols * 2 : 0)];
   const AcDev& ac = P.rs.ac;
   {
     const uint32_t words = ac.fast_bytes / 4;
     const uint32_t* src = (const uint32_t*)ac.fast_lds;
     for (uint32_t i = threadIdx.x; i < words; i += kFastThreads) ((uint32_t*)smem)[i] = src[i];
+    if (kPair) {
+      const uint32_t* ps = (const uint32_t*)(ac.fast_lds + ac.o_pair);
+      for (uint32_t i = threadIdx.x; i < kFastCols * kFastCols / 2; i += kFastThreads)
+        ((uint32_t*)(smem + kFastImgMax))[i] = ps[i];
+    }
   }
   __syncthreads();
   const uint8_t* T = smem;
@@ -654,7 +690,8 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
           if (k % 2 == 0) {
             const uint4 v = C[0].cur[k], w = C[0].cur[k + 1 < V ? k + 1 : k];
             const uint32_t d[8] = {v.x, v.y, v.z, v.w, w.x, w.y, w.z, w.w};
-            fast_window<V, kMode, 4>(P, T, out_e, C[0], d, C[0].pos + 16 * k, live, lanes_lt, ev_seg, &ev_count);
+            fast_window<V, kMode, 4, kPair>(P, T, out_e, C[0], d, C[0].pos + 16 * k, live, lanes_lt, ev_seg,
+                                            &ev_count);
           }
         } else {
           const uint4 v = C[0].cur[k];
@@ -4551,7 +4588,7 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   v.max_ncap = max_ncap;
   v.max_ninst_cap = max_ninst_cap;
   const uint8_t* fast = nullptr;
-  uint32_t o_out_off = 0, o_out_pat = 0, o_pats = 0, o_pbytes = 0, rep_bytes = 0;
+  uint32_t o_out_off = 0, o_out_pat = 0, o_pats = 0, o_pbytes = 0, rep_bytes = 0, o_pair = 0;
   if (!ac.fast.empty()) {
     // k_report blob: the scan image followed by the small output tables
     std::vector<uint8_t> blob(ac.fast.begin(), ac.fast.end());
@@ -4566,14 +4603,15 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
     o_pats = put(pats.data(), pats.size() * sizeof(PatDev));
     o_pbytes = put(pbytes.data(), pbytes.size());
     blob.resize((blob.size() + 15) & ~(size_t)15);
-    rep_bytes = (uint32_t)blob.size();
+    rep_bytes = (uint32_t)blob.size();  // (k_report stages [0, rep_bytes); the pair table follows)
+    if (!ac.fast_pair.empty()) o_pair = put(ac.fast_pair.data(), ac.fast_pair.size() * 2);
     HIP_TRY(im.fast.ensure(blob.size() + 16));
     HIP_TRY(hipMemcpy(im.fast.p, blob.data(), blob.size(), hipMemcpyHostToDevice));
     fast = im.fast.p;
   }
   v.ac = AcDev{im.delta.p, im.cls.p, im.out_off.p, im.out_pat.p, im.pats.p, im.pat_bytes.p, im.pat_rules.p,
                ac.nstates, ac.nclasses, fast, (uint32_t)ac.fast.size(), ac.fast_out_entry, ac.depth,
-               rep_bytes, o_out_off, o_out_pat, o_pats, o_pbytes};
+               rep_bytes, o_out_off, o_out_pat, o_pats, o_pbytes, o_pair};
   // keywords whose lowercase holds a non-ASCII rune (k_uni_keywords)
   {
     std::vector<uint8_t> ub;
@@ -4665,8 +4703,11 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     if (const char* m = getenv("TSG_SCAN_MODE")) mode = atoi(m);
     int win = kFastEventWin;     // groups per event check (fast_window; A/B via TSG_EVENT_WIN)
     if (const char* w = getenv("TSG_EVENT_WIN")) win = atoi(w);
+    bool pair = false;  // TSG_FAST_VARIANT=pair: root pair table (fstep2)
     if (const char* v = getenv("TSG_FAST_VARIANT")) {
-      if (sscanf(v, "d%dx%d", &deep_v, &deep_d) != 2) {
+      pair = strcmp(v, "pair") == 0;
+      if (pair) {
+      } else if (sscanf(v, "d%dx%d", &deep_v, &deep_d) != 2) {
         deep_v = 0;
         ring = sscanf(v, "%dx%d", &chains, &vecs) != 2;
       }
@@ -4720,6 +4761,8 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
 #undef TSG_MODE
     else if (chains == 1 && vecs == 8 && win == 2) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 2>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1 && vecs == 8 && win == 8) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 8>), dim3(blocks), dim3(nt), 0, s, P);
+    else if (chains == 1 && vecs == 8 && win == 4 && pair && P.rs.ac.o_pair)
+      hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 4, true>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1 && vecs == 8 && win == 4) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 4>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1 && vecs == 8) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1) hipLaunchKernelGGL((k_scan_fast<1, 4, 1024>), dim3(blocks), dim3(nt), 0, s, P);

@@ -226,6 +226,7 @@ static bool build_fast(tsg_ruleset* rs, int depth, const std::vector<uint8_t>& p
   ac.fast_states = 0;
   ac.fast_out_entry = 0;
   ac.fast_ext.assign(rs->patterns.size(), 0);
+  ac.fast_pair.clear();
   for (auto& p : rs->patterns)
     if (!p.special)
       for (unsigned char c : p.lower)
@@ -311,6 +312,14 @@ static bool build_fast(tsg_ruleset* rs, int depth, const std::vector<uint8_t>& p
   ac.fast_out_off[S] = (uint32_t)ac.fast_out_pat.size();
   ac.fast_out_entry = (uint32_t)first_out;
   ac.fast_states = (uint32_t)S;
+  ac.fast_pair.clear();
+  bool one_step_out = false;  // (a pair step skips the middle state: it must never be an output)
+  for (uint32_t v = 0; v < kFastCols; ++v) one_step_out |= perm[go[0][v]] >= first_out;
+  if (!one_step_out) {
+    ac.fast_pair.assign(kFastCols * kFastCols, 0);
+    for (uint32_t v1 = 0; v1 < kFastCols; ++v1)
+      for (uint32_t v2 = 0; v2 < kFastCols; ++v2) ac.fast_pair[v1 * kFastCols + v2] = (uint16_t)perm[go[go[0][v1]][v2]];
+  }
   return true;
 }
 
