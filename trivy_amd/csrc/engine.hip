@@ -2072,6 +2072,27 @@ struct VerifyParams {
   uint64_t redo_cap;
 };
 
+// The text of a job read in aligned 16-byte blocks (one dwordx4 load per
+// block; the batch is padded past its end), for the NFA walk's byte stream.
+struct VecText {
+  const uint8_t* base;
+  uintptr_t blk;
+  u32x4 v;
+  __device__ explicit VecText(const uint8_t* b) : base(b), blk(~(uintptr_t)0), v{0, 0, 0, 0} {}
+  template <class Pos>
+  __device__ uint32_t operator[](Pos i) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(base) + i;
+    const uintptr_t b = a & ~(uintptr_t)15;
+    if (b != blk) {
+      blk = b;
+      v = *as_global<__attribute__((address_space(1))) const u32x4>(reinterpret_cast<const void*>(b));
+    }
+    const uint32_t o = (uint32_t)(a & 15);
+    const uint32_t wd = o < 8 ? (o < 4 ? v.x : v.y) : (o < 12 ? v.z : v.w);  // no dynamically indexed array
+    return (wd >> (8 * (o & 3))) & 0xFFu;
+  }
+};
+
 // Candidate start windows of one (file, rule) job, in increasing order
 // (DESIGN.md "anchor windows").
 // (Pos: uint32_t, or uint64_t for the jobs of files of 4 GiB and more)
@@ -2083,14 +2104,32 @@ struct IvIter {
   const uint8_t* text;
   Pos n;
   uint32_t a, b;
-  const uint64_t* alpha;
+  uint64_t al0, al1, al2, al3;  // the anchor prefix alphabet, in registers
   Pos h_prev, p_prev;
   bool have_prev;
   // current merged view
   bool have;
   Pos cs, ce;
 
-  __device__ bool in_alpha(uint8_t c) const { return (alpha[c >> 6] >> (c & 63)) & 1; }
+  __device__ bool in_alpha(uint32_t c) const {
+    const uint64_t w = c < 128 ? (c < 64 ? al0 : al1) : (c < 192 ? al2 : al3);  // (no dynamic index)
+    return (w >> (c & 63)) & 1;
+  }
+  // Start of the run of alphabet bytes ending at h, never below lo: aligned
+  // 16-byte loads backwards (a byte load per step was a dependent global read)
+  __device__ Pos alpha_back(Pos lo, Pos h) const {
+    Pos q = h;
+    while (q > lo) {
+      const uintptr_t last = reinterpret_cast<uintptr_t>(text) + (q - 1);
+      const uintptr_t blk = last & ~(uintptr_t)15;
+      const u32x4 v = *as_global<__attribute__((address_space(1))) const u32x4>(reinterpret_cast<const void*>(blk));
+      for (int i = (int)(last - blk); i >= 0 && q > lo; --i, --q) {
+        const uint32_t wd = i < 8 ? (i < 4 ? v.x : v.y) : (i < 12 ? v.z : v.w);
+        if (!in_alpha((wd >> (8 * (i & 3))) & 0xFFu)) return q;
+      }
+    }
+    return q;
+  }
 
   __device__ bool next_raw(Pos* ws, Pos* we) {
     while (ci < c1) {
@@ -2102,13 +2141,10 @@ struct IvIter {
       // the previous hit when it lies below lo re-read whole minified lines.
       Pos p;
       if (have_prev && h_prev <= h && h_prev >= lo) {
-        Pos q = h;
-        while (q > h_prev && in_alpha(text[q - 1])) --q;
+        const Pos q = alpha_back(h_prev, h);
         p = (q == h_prev) ? (p_prev > lo ? p_prev : lo) : q;
       } else {
-        Pos q = h;
-        while (q > lo && in_alpha(text[q - 1])) --q;
-        p = q;
+        p = alpha_back(lo, h);
       }
       if (p < lo) p = lo;
       have_prev = true;
@@ -2596,7 +2632,10 @@ __device__ inline void iv_init(IvIter<Pos>& it, const VerifyParams& V, uint32_t 
   it.n = n;
   it.a = rd.off_min;
   it.b = rd.off_max;
-  it.alpha = rd.alpha;
+  it.al0 = rd.alpha[0];
+  it.al1 = rd.alpha[1];
+  it.al2 = rd.alpha[2];
+  it.al3 = rd.alpha[3];
   it.have_prev = false;
   it.h_prev = it.p_prev = 0;
   it.advance();
@@ -2624,9 +2663,10 @@ __device__ __noinline__ uint32_t verify_dfa_job(const VerifyParams& V, uint32_t 
   while (it.have) {
     bool found = false;
     const Pos s0 = it.cs > pos ? it.cs : pos;
+    VecText TS(text);  // the window's bytes, one 16-byte load per block
     for (Pos sp = s0; sp <= it.ce && sp < n; ++sp) {
-      if (!gre::is_rune_start(text, n, sp)) continue;
-      const uint32_t b0 = as_global<gu8>(text)[sp];  // first-byte skip (no dependent table loads)
+      const uint32_t b0 = TS[sp];  // first-byte skip (no dependent table loads)
+      if (b0 >= 0x80 && !gre::is_rune_start(text, n, sp)) continue;  // (an ASCII byte starts a rune)
       const uint32_t fw = b0 < 32 ? fm0 : b0 < 64 ? fm1 : b0 < 96 ? fm2 : fm3;
       if (b0 < 0x80 && !((fw >> (b0 & 31)) & 1)) continue;
       const uint64_t ta = tck ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -2674,27 +2714,6 @@ __device__ __noinline__ void verify_vm_job(const VerifyParams& V, uint32_t rule,
   }
   job_record(V, job, fms, lme);
 }
-
-// The text of a job read in aligned 16-byte blocks (one dwordx4 load per
-// block; the batch is padded past its end), for the NFA walk's byte stream.
-struct VecText {
-  const uint8_t* base;
-  uintptr_t blk;
-  u32x4 v;
-  __device__ explicit VecText(const uint8_t* b) : base(b), blk(~(uintptr_t)0), v{0, 0, 0, 0} {}
-  template <class Pos>
-  __device__ uint32_t operator[](Pos i) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(base) + i;
-    const uintptr_t b = a & ~(uintptr_t)15;
-    if (b != blk) {
-      blk = b;
-      v = *as_global<__attribute__((address_space(1))) const u32x4>(reinterpret_cast<const void*>(b));
-    }
-    const uint32_t o = (uint32_t)(a & 15);
-    const uint32_t wd = o < 8 ? (o < 4 ? v.x : v.y) : (o < 12 ? v.z : v.w);  // no dynamically indexed array
-    return (wd >> (8 * (o & 3))) & 0xFFu;
-  }
-};
 
 // FindAll over the anchor windows with the bit-parallel NFA (nfa.cpp; rules
 // whose verify DFA exploded or that use \b / (?m) assertions): one walk
@@ -3078,6 +3097,62 @@ __device__ inline uint32_t wave_nl_prefix(const uint8_t* data, const uint32_t* n
   return nl_pre[x / kNlBlock] + c;
 }
 
+// bit k set <=> byte k of the 16 is '\n'
+__device__ inline uint32_t nl_mask16(uint4 v) {
+  const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t t = d[k] ^ 0x0A0A0A0Au;
+    const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);  // 0x80 per '\n' byte
+    m |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * k);
+  }
+  return m;
+}
+
+// wave_nl_prefix of x0 <= x1 <= x2 with one read of each distinct 4 KiB
+// block (the lane's 64-byte slice: whole 16-byte vectors before the block's
+// largest x, bytes for the partial one -- nothing at or past it is read).
+__device__ inline void wave_nl_prefix3(const uint8_t* data, const uint32_t* nl_pre, uint64_t x0, uint64_t x1,
+                                       uint64_t x2, uint32_t lane, uint32_t* out) {
+  constexpr uint32_t kPer = kNlBlock / 64;  // bytes per lane
+  const uint64_t xs[3] = {x0, x1, x2};
+  uint64_t packed = 0;  // 21 bits per count (<= 4096 per block)
+  int k = 0;
+  while (k < 3) {
+    const uint64_t b0 = xs[k] & ~(uint64_t)(kNlBlock - 1);
+    int e = k;  // xs[k..e] share this block; xs[e] is the largest
+    while (e + 1 < 3 && (xs[e + 1] & ~(uint64_t)(kNlBlock - 1)) == b0) ++e;
+    const uint64_t xmax = xs[e];
+    const uint64_t s0 = b0 + (uint64_t)lane * kPer;
+    uint32_t m[kPer / 16];  // '\n' bit masks of the slice's vectors (bytes before xmax)
+#pragma unroll
+    for (uint32_t v = 0; v < kPer / 16; ++v) {
+      const uint64_t p = s0 + 16 * v;
+      if (p + 16 <= xmax) {
+        m[v] = nl_mask16(*(const uint4*)(data + p));
+      } else {
+        uint32_t mm = 0;
+        for (uint64_t i = p; i < xmax && i < p + 16; ++i) mm |= (data[i] == '\n' ? 1u : 0u) << (uint32_t)(i - p);
+        m[v] = mm;
+      }
+    }
+    for (int q = k; q <= e; ++q) {
+      uint32_t c = 0;
+#pragma unroll
+      for (uint32_t v = 0; v < kPer / 16; ++v) {
+        const uint64_t p = s0 + 16 * v;
+        const uint32_t keep = p + 16 <= xs[q] ? 0xFFFFu : (xs[q] > p ? (1u << (uint32_t)(xs[q] - p)) - 1u : 0u);
+        c += __builtin_popcount(m[v] & keep);
+      }
+      packed |= (uint64_t)c << (21 * q);
+    }
+    k = e + 1;
+  }
+  for (int d = 32; d > 0; d >>= 1) packed += __shfl_xor(packed, d);
+  for (int q = 0; q < 3; ++q) out[q] = nl_pre[xs[q] / kNlBlock] + (uint32_t)((packed >> (21 * q)) & 0x1FFFFFu);
+}
+
 // One wave per location: P(start), P(end) relative to the file start on the
 // uncensored content; censored_lines() turns them into findLocation's numbers.
 __global__ __launch_bounds__(256) void k_lines(const uint8_t* data, const uint64_t* off, const uint32_t* nl_pre,
@@ -3089,12 +3164,13 @@ __global__ __launch_bounds__(256) void k_lines(const uint8_t* data, const uint64
   if (L.flags) return;
   const uint64_t fs = off[L.file];
   if (L.start > L.end || fs + L.end >= off[L.file + 1]) return;  // never read outside the file
-  const uint32_t g0 = wave_nl_prefix(data, nl_pre, fs, lane);
-  const uint32_t g1 = wave_nl_prefix(data, nl_pre, fs + L.start, lane);
-  const uint32_t g2 = wave_nl_prefix(data, nl_pre, fs + L.end, lane);
+  // the three prefixes in one wave pass: a 4 KiB block shared by two of
+  // them is read once (the location and its file start usually share one)
+  uint32_t g[3];
+  wave_nl_prefix3(data, nl_pre, fs, fs + L.start, fs + L.end, lane, g);
   if (lane == 0) {  // raw prefix counts P(start), P(end); see censored_lines()
-    locs[w].start_line = g1 - g0;
-    locs[w].end_line = g2 - g0;
+    locs[w].start_line = g[1] - g[0];
+    locs[w].end_line = g[2] - g[0];
   }
 }
 
@@ -3414,19 +3490,6 @@ __device__ inline uint4 ld16_guard(const uint8_t* data, uint64_t p, uint64_t end
   uint32_t w[4] = {0, 0, 0, 0};
   for (uint32_t k = 0; k < 16 && p + k < end; ++k) w[k >> 2] |= (uint32_t)data[p + k] << (8 * (k & 3));
   return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-// bit k set <=> byte k of the 16 is '\n'
-__device__ inline uint32_t nl_mask16(uint4 v) {
-  const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-  uint32_t m = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t t = d[k] ^ 0x0A0A0A0Au;
-    const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);  // 0x80 per '\n' byte
-    m |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * k);
-  }
-  return m;
 }
 
 // Block holding newline number k (0-based, whole batch): the largest b with
