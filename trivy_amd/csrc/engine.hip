@@ -219,9 +219,10 @@ struct GlobalHitSink {
 
 // kConfirm: the automaton ran on 7-bit aliased bytes (k_scan_fast), so each
 // reported pattern is re-checked on the real bytes first.
-template <bool kConfirm, class Sink>
-__device__ inline void report_t(const ScanParams& P, uint32_t st, uint64_t p, uint64_t* last_kw, Sink& sink) {
-  const AcDev& ac = P.rs.ac;
+// The file holding p, with a one-entry cache (*fc: file, [*fs, *fe) its
+// bytes incl. the separator) for the outputs of one event.
+__device__ inline uint32_t file_at(const ScanParams& P, uint64_t p, uint32_t* fc, uint64_t* fs, uint64_t* fe) {
+  if (*fc != 0xFFFFFFFFu && p >= *fs && p < *fe) return *fc;
   uint32_t lo = 0, hi = P.n_files;
   if (P.region_file) {
     const uint64_t r = p / kNlBlock;
@@ -230,6 +231,19 @@ __device__ inline void report_t(const ScanParams& P, uint32_t st, uint64_t p, ui
     if (hi > P.n_files) hi = P.n_files;
   }
   const uint32_t fi = find_file(P.off, lo, hi, p);
+  *fc = fi;
+  *fs = P.off[fi];
+  *fe = P.off[fi + 1];
+  return fi;
+}
+
+template <bool kConfirm, class Sink>
+__device__ inline void report_t(const ScanParams& P, uint32_t st, uint64_t p, uint64_t* last_kw, Sink& sink,
+                                uint32_t* fc = nullptr, uint64_t* fcs = nullptr, uint64_t* fce = nullptr) {
+  const AcDev& ac = P.rs.ac;
+  uint32_t fc0 = 0xFFFFFFFFu;
+  uint64_t fs0 = 0, fe0 = 0;
+  const uint32_t fi = fc ? file_at(P, p, fc, fcs, fce) : file_at(P, p, &fc0, &fs0, &fe0);
   const uint64_t fend = P.off[fi + 1] - 1;  // content end (separator excluded)
   uint32_t o0 = ac.out_off[st], o1 = ac.out_off[st + 1];
   for (uint32_t o = o0; o < o1; ++o) {
@@ -918,11 +932,13 @@ __global__ __launch_bounds__(1024) void k_big_report(ScanParams P, uint32_t n_wa
       if (i < n) {
         const FastEvent ev = seg[i];
         uint32_t e = ev.entry;
+        uint32_t fc = 0xFFFFFFFFu;  // the event's file, looked up once for all its outputs
+        uint64_t fcs = 0, fce = 0;
 #pragma unroll 1
         for (int j = 0; j < 8; ++j) {
           const uint32_t nx = big_next(L, e, L.cls[((j < 4 ? ev.cur.x : ev.cur.y) >> (8 * (j & 3))) & 0xFFu]);
           e = nx & 0x7FFFu;
-          if (nx & 0x8000u) report_t<false>(P, e, ev.pos + j, &last_kw, sink);
+          if (nx & 0x8000u) report_t<false>(P, e, ev.pos + j, &last_kw, sink, &fc, &fcs, &fce);
         }
       }
       __syncthreads();
@@ -4085,6 +4101,8 @@ struct tsg_engine {
   uint64_t scratch_stride = 0;
   hipEvent_t ev[12];
   bool events = false;
+  hipStream_t side = nullptr;  // D2H of the findings' Code records and strings under the last sorts
+  hipEvent_t ev_fill = nullptr, ev_side = nullptr;
   DBuf<uint32_t> gate_out, gate_rules;  // tsg_gate_device: rule gate words, rule -> keyword-id CSR
   // tsg_analyze: IsBinary flags, '\r'-stripped batch and its offsets, block sums, chunk positions
   DBuf<uint8_t> bin8, strip_out;
@@ -5017,38 +5035,11 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   if (int rc = read_ctrl(e, &c)) return rc;  // the arena size
   HIP_TRY(e->f_arena.ensure(c.find_bytes + 16));
   F.arena = e->f_arena.p;
-  if (c.find_bytes)
-    hipLaunchKernelGGL(k_arena_fill, dim3((uint32_t)std::min<uint64_t>((c.find_bytes / 16 + 255) / 256 + 1, 8192)),
-                       dim3(256), 0, s, F);
-  HIP_TRY(hipGetLastError());
-  // order: (file, RuleID rank) major, Match prefix minor -- two stable radix
-  // sorts, least significant key first (f_lkey / f_lkey2 / f_lslot* are free now)
-  hipLaunchKernelGGL(k_match_prefix, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->f_arena.p, n_locs, e->f_lkey.p,
-                     e->f_lslot.p);
-  size_t tmp2 = 0;
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p, e->f_lslot2.p,
-                                             (int)n_locs, 0, 64, s));
-  HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p,
-                                             e->f_lslot2.p, (int)n_locs, 0, 64, s));
-  hipLaunchKernelGGL(k_gather_u64, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lslot2.p, n_locs, e->keys2.p);
-  tmp2 = 0;
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->keys2.p, e->keys.p, e->f_lslot2.p, e->vals2.p,
-                                             (int)n_locs, 0, key_bits, s));
-  HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys2.p, e->keys.p, e->f_lslot2.p, e->vals2.p,
-                                             (int)n_locs, 0, key_bits, s));
-  hipLaunchKernelGGL(k_find_gather, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->vals2.p, n_locs, e->f_rec2.p);
-  const uint64_t tie_cap = std::max<uint64_t>(1024, n_locs / 8);
-  HIP_TRY(e->f_ties.ensure(tie_cap));
-  hipLaunchKernelGGL(k_tie_list, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lkey.p, e->vals2.p, n_locs,
-                     e->f_ties.p, tie_cap, e->ctrl.p);
-  HIP_TRY(hipGetLastError());
-  // the kept locations as tsg_loc records
-  HIP_TRY(e->out_locs.ensure(n_locs));
-  hipLaunchKernelGGL(k_out_locs, dim3(lane_blocks), dim3(256), 0, s, e->locs2.p, n_locs, e->out_locs.p, e->ctrl.p);
-  HIP_TRY(hipGetLastError());
+  // the result's page-locked block, laid out now: the Code records and the
+  // string arena are final once k_arena_fill ends, so their D2H (most of the
+  // bytes) runs on a side stream under the Match sorts below
   auto& R = res->impl;
+  const uint64_t tie_cap = std::max<uint64_t>(1024, n_locs / 8);
   const size_t rec_bytes = n_locs * sizeof(FindRec), code_bytes = n_slots * sizeof(CodeRec);
   const size_t o_locs = (rec_bytes + code_bytes + c.find_bytes + 15) & ~(size_t)15;
   const size_t o_flags = o_locs + n_locs * sizeof(tsg_loc);
@@ -5067,12 +5058,51 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   R.file_flags = {base + o_flags, n_files};
   R.ties = {(uint32_t*)(base + o_ties), 0};
   R.ctrl_off = o_ctrl;
-  HIP_TRY(hipMemcpyAsync(R.frec.p, e->f_rec2.p, rec_bytes, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(R.code.p, e->f_code.p, code_bytes, hipMemcpyDeviceToHost, s));
   if (c.find_bytes)
-    HIP_TRY(hipMemcpyAsync(base + rec_bytes + code_bytes, e->f_arena.p, c.find_bytes, hipMemcpyDeviceToHost, s));
+    hipLaunchKernelGGL(k_arena_fill, dim3((uint32_t)std::min<uint64_t>((c.find_bytes / 16 + 255) / 256 + 1, 8192)),
+                       dim3(256), 0, s, F);
+  HIP_TRY(hipGetLastError());
+  if (!e->side) {
+    HIP_TRY(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&e->ev_fill, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&e->ev_side, hipEventDisableTiming));
+  }
+  HIP_TRY(hipEventRecord(e->ev_fill, s));
+  HIP_TRY(hipStreamWaitEvent(e->side, e->ev_fill, 0));
+  HIP_TRY(hipMemcpyAsync(R.code.p, e->f_code.p, code_bytes, hipMemcpyDeviceToHost, e->side));
+  if (c.find_bytes)
+    HIP_TRY(hipMemcpyAsync(base + rec_bytes + code_bytes, e->f_arena.p, c.find_bytes, hipMemcpyDeviceToHost, e->side));
+  HIP_TRY(hipEventRecord(e->ev_side, e->side));
+  // order: (file, RuleID rank) major, Match prefix minor -- two stable radix
+  // sorts, least significant key first (f_lkey / f_lkey2 / f_lslot* are free now)
+  hipLaunchKernelGGL(k_match_prefix, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->f_arena.p, n_locs, e->f_lkey.p,
+                     e->f_lslot.p);
+  size_t tmp2 = 0;
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p, e->f_lslot2.p,
+                                             (int)n_locs, 0, 64, s));
+  HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p,
+                                             e->f_lslot2.p, (int)n_locs, 0, 64, s));
+  hipLaunchKernelGGL(k_gather_u64, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lslot2.p, n_locs, e->keys2.p);
+  tmp2 = 0;
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->keys2.p, e->keys.p, e->f_lslot2.p, e->vals2.p,
+                                             (int)n_locs, 0, key_bits, s));
+  HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys2.p, e->keys.p, e->f_lslot2.p, e->vals2.p,
+                                             (int)n_locs, 0, key_bits, s));
+  hipLaunchKernelGGL(k_find_gather, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->vals2.p, n_locs, e->f_rec2.p);
+  HIP_TRY(e->f_ties.ensure(tie_cap));
+  hipLaunchKernelGGL(k_tie_list, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lkey.p, e->vals2.p, n_locs,
+                     e->f_ties.p, tie_cap, e->ctrl.p);
+  HIP_TRY(hipGetLastError());
+  // the kept locations as tsg_loc records
+  HIP_TRY(e->out_locs.ensure(n_locs));
+  hipLaunchKernelGGL(k_out_locs, dim3(lane_blocks), dim3(256), 0, s, e->locs2.p, n_locs, e->out_locs.p, e->ctrl.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(R.frec.p, e->f_rec2.p, rec_bytes, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(R.locs.p, e->out_locs.p, n_locs * sizeof(tsg_loc), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(R.ties.p, e->f_ties.p, tie_cap * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamWaitEvent(s, e->ev_side, 0));  // the caller's final synchronisation covers the side copies
   R.ties_cap = tie_cap;
   return TSG_OK;
 }
@@ -5846,6 +5876,10 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     // containment filter; the host reads two counts)
     ExclDev X{im.u32.p + im.o_xoff, im.u32.p + im.o_xprog, im.u32.p + im.o_gx, im.n_gx, std::max(1u, im.max_x)};
     const uint64_t nk = 2 * n_locs;
+    if (nk >= (1ull << (64 - kKeyPosBits))) {  // group ids share the range sort key with 40-bit starts
+      set_last_error("exclude blocks: more than 2^23 locations in one batch");
+      return TSG_ERR_UNSUPPORTED;
+    }
     HIP_TRY(e->keys.ensure(nk));
     HIP_TRY(e->keys2.ensure(nk));
     HIP_TRY(e->vals.ensure(nk));
@@ -5956,7 +5990,10 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
                        e->vals2.p, n_locs, e->locs2.p);
     HIP_TRY(hipGetLastError());
     // ---- 8. findings (censored lines, Match, Code, order) on the device
-    if ((rc = build_findings_dev(e, d_data, d_off, nbytes, nf, n_locs, res))) return rc;
+    if ((rc = build_findings_dev(e, d_data, d_off, nbytes, nf, n_locs, res))) {
+      if (e->side) (void)hipStreamSynchronize(e->side);  // no side copy may outlive the result block
+      return rc;
+    }
   }
   HIP_TRY(hipEventRecord(e->ev[7], s));
   auto& R = res->impl;
@@ -6108,6 +6145,12 @@ void tsg_engine_free(tsg_engine* e) {
   e->f_ties.release(); e->out_locs.release();
   if (e->events)
     for (auto& ev : e->ev) (void)hipEventDestroy(ev);
+  if (e->side) {
+    (void)hipStreamSynchronize(e->side);
+    (void)hipEventDestroy(e->ev_fill);
+    (void)hipEventDestroy(e->ev_side);
+    (void)hipStreamDestroy(e->side);
+  }
   (void)hipStreamDestroy(e->stream);
   delete e;
 }
