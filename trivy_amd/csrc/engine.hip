@@ -122,11 +122,37 @@ struct DevLoc {
 // class map, dense rows of the n_dense shallowest states, and for every
 // deeper ("cold") state only the classes on which it differs from its
 // failure state, plus the failure link -- delta(s, c) = its own entry, else
-// delta(fail(s), c), ending in a dense row.
+// delta(fail(s), c), ending in a dense row.  A cold state is one 8-byte
+// record (one ds_read_b64): classes c1, c2 (kBigNone = unused), their entries
+// and the failure link; a state with more than two own classes has
+// c1 = c2 = kBigMore and its list (u32 class << 16 | entry, ended by
+// 0xFFFFFFFF) at the 32-bit offset held in the entry fields.  Most cold
+// states are trie nodes whose only own class is the next literal byte.
+constexpr uint32_t kBigNone = 0xFF, kBigMore = 0xFE;  // (classes < kBigMore)
+
+// Text byte model that orders k_scan_big's states (relative weights: English
+// letter frequencies, lowercase ten times uppercase; space, newline, digits
+// and the punctuation of code and config files).
+static double big_byte_weight(uint8_t b) {
+  static const double kLetter[26] = {8.2, 1.5, 2.8, 4.3, 12.7, 2.2, 2.0, 6.1, 7.0, 0.15, 0.8, 4.0, 2.4,
+                                     6.7, 7.5, 1.9, 0.1, 6.0, 6.3, 9.1, 2.8, 1.0, 2.4, 0.15, 2.0, 0.07};
+  if (b >= 'a' && b <= 'z') return 0.6 * kLetter[b - 'a'];
+  if (b >= 'A' && b <= 'Z') return 0.06 * kLetter[b - 'A'];
+  if (b >= '0' && b <= '9') return 0.5;
+  switch (b) {
+    case ' ': return 15.0;
+    case '\n': return 3.0;
+    case '_': case '.': case '=': case '"': case '-': case '/': case ',': case ':': case '\'':
+    case '(': case ')': case ';': return 0.8;
+    default: return b >= 0x20 && b < 0x7F ? 0.1 : 0.02;
+  }
+}
+inline const char* experiment_env(const char* name);
 struct BigDev {
   const uint8_t* blob;  // global copy
   uint32_t blob_bytes, n_dense, n_cold;
-  uint32_t o_eoff, o_eval, o_fail;  // byte offsets: u32 [n_cold + 1], u32 (class << 16 | entry), u16 [n_cold]
+  uint32_t o_cold, o_eval;  // byte offsets: uint2 [n_cold], u32 lists
+  const uint16_t* ac_of;    // blob state id -> the automaton's (AcDev) state id
 };
 
 struct ScanParams {
@@ -142,6 +168,8 @@ struct ScanParams {
   uint32_t* file_flags;  // n_files
   uint64_t* hits;
   uint64_t hit_cap;
+  uint64_t* big_outs;  // k_big_walk -> k_big_resolve: output records (position << 16 | state)
+  uint64_t big_out_cap;
   Ctrl* ctrl;
   uint32_t* nl_blocks;  // newline count per kNlBlock bytes of the batch
   const uint8_t* tail;  // virtual base of a zero-padded copy of data[tail_base-8, nbytes)
@@ -257,12 +285,18 @@ __device__ inline void report_t(const ScanParams& P, uint32_t st, uint64_t p, ui
       for (uint32_t k = 0; k < tl && ok; ++k) ok = lower_ascii(P.data[start + k]) == pb[k];
       if (!ok) continue;
     }
+    // (the byte checks below have no early exit: each chunk of 8 loads is
+    // issued before any compare, one memory latency instead of a chain)
     if (pd.trunc) {
       if (start + pd.len > fend) continue;
-      bool ok = true;
+      uint32_t bad = 0;
       const uint8_t* pb = ac.pat_bytes + pd.bytes_off;
-      for (uint32_t k = ac.depth; k < pd.len && ok; ++k) ok = lower_ascii(P.data[start + k]) == pb[k];
-      if (!ok) continue;
+      for (uint32_t k0 = ac.depth; k0 < pd.len && !bad; k0 += 8) {
+#pragma unroll
+        for (uint32_t k = k0; k < k0 + 8; ++k)
+          if (k < pd.len) bad |= lower_ascii(P.data[start + k]) ^ pb[k];
+      }
+      if (bad) continue;
     }
     if (pd.special) {
       mark_special(P, fi);
@@ -281,9 +315,16 @@ __device__ inline void report_t(const ScanParams& P, uint32_t st, uint64_t p, ui
     if (pd.rule_n) {
       if (pd.confirm) {
         const uint8_t* rq = ac.pat_bytes + pd.req_off;
-        bool ok = true;
-        for (uint32_t k = 0; k < pd.len && ok; ++k) ok = rq[k] == 0 || P.data[start + k] == rq[k];
-        if (!ok) continue;
+        bool bad = false;
+        for (uint32_t k0 = 0; k0 < pd.len && !bad; k0 += 8) {
+#pragma unroll
+          for (uint32_t k = k0; k < k0 + 8; ++k)
+            if (k < pd.len) {
+              const uint8_t r = rq[k], d = P.data[start + k];
+              bad |= (r != 0) & (d != r);
+            }
+        }
+        if (bad) continue;
       }
       sink.push(P, (start << 16) | pid);
     }
@@ -742,52 +783,106 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
 // wave's segment) that k_big_report replays -- no per-byte output branch, no
 // global atomics, newlines counted SWAR and stored once per span.
 constexpr uint32_t kBigThreads = 1024;
+constexpr int kBigMode = 0, kBigChains = 1;  // k_scan_big's product shape
 constexpr uint32_t kBigLdsMax = 152 * 1024;
 
 struct BigLds {
   const uint8_t* cls;
   const uint16_t* dense;
-  const uint32_t* eoff;
+  const uint2* cold;
   const uint32_t* eval;
-  const uint16_t* fl;
   uint32_t K, ND;
 };
 
 __device__ inline BigLds big_lds(const BigDev& B, const uint8_t* smem, uint32_t K) {
-  return BigLds{smem, (const uint16_t*)(smem + 256), (const uint32_t*)(smem + B.o_eoff),
-                (const uint32_t*)(smem + B.o_eval), (const uint16_t*)(smem + B.o_fail), K, B.n_dense};
+  return BigLds{smem, (const uint16_t*)(smem + 256), (const uint2*)(smem + B.o_cold),
+                (const uint32_t*)(smem + B.o_eval), K, B.n_dense};
 }
 
 // delta(st, c): own entry of a cold state, else its failure state's (the
 // chain ends in a dense row).  Entry bit 15 = output state.
 __device__ inline uint32_t big_next(const BigLds& L, uint32_t st, uint32_t c) {
   while (st >= L.ND) {
-    const uint32_t j = st - L.ND;
-    for (uint32_t k = L.eoff[j]; k < L.eoff[j + 1]; ++k) {
-      const uint32_t v = L.eval[k];
-      if ((v >> 16) == c) return v & 0xFFFFu;
+    const uint2 r = L.cold[st - L.ND];  // x: c1 | c2 << 8 | entry1 << 16, y: entry2 | fail << 16
+    if (c == (r.x & 0xFFu)) return r.x >> 16;
+    if (c == ((r.x >> 8) & 0xFFu)) return r.y & 0xFFFFu;
+    if ((r.x & 0xFFu) == kBigMore) {
+      for (uint32_t k = (r.x >> 16) | (r.y << 16);; ++k) {
+        const uint32_t v = L.eval[k];
+        if (v == 0xFFFFFFFFu) break;
+        if ((v >> 16) == c) return v & 0xFFFFu;
+      }
     }
-    st = L.fl[j];
+    st = r.y >> 16;
   }
   return L.dense[st * L.K + c];
 }
 
-// 8 bytes (two dwords) through the automaton from entry e; returns the OR of
-// the entries (bit 15 = some output state was reached).
-__device__ inline uint32_t big_group(const BigLds& L, uint32_t& e, uint32_t d0, uint32_t d1) {
-  uint32_t c[8];
+// 8 bytes (two dwords) of each of CH chains through the automaton from their
+// entries e[c]; acc[c] = the OR of a chain's entries (bit 15 = some output
+// state was reached).  The chains are independent, so their row lookups
+// overlap in one lane.  kMode != 0 only in the -DTSG_EXPERIMENTS build
+// (TSG_BIG_VARIANT; bits 0/1 are timing bounds with wrong results): bit 0 =
+// class from ALU instead of LDS, bit 1 = dense rows only, bit 3 = every
+// chain's dense row read issued before any cold walk.
+template <int kMode, int CH>
+__device__ inline void big_group(const BigLds& L, uint32_t (&e)[CH], const uint32_t (&d)[2 * CH],
+                                 uint32_t (&acc)[CH]) {
+  uint32_t c[CH][8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) c[j] = L.cls[((j < 4 ? d0 : d1) >> (8 * (j & 3))) & 0xFFu];
-  uint32_t acc = 0;
+  for (int h = 0; h < CH; ++h)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t b = (d[2 * h + (j >> 2)] >> (8 * (j & 3))) & 0xFFu;
+      c[h][j] = (kMode & 1) ? (b & 31u) : L.cls[b];
+    }
+#pragma unroll
+  for (int h = 0; h < CH; ++h) acc[h] = 0;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const uint32_t nx = big_next(L, e, c[j]);
-    acc |= nx;
-    e = nx & 0x7FFFu;
+    uint32_t nx[CH];
+    if (kMode & 10) {
+#pragma unroll
+      for (int h = 0; h < CH; ++h) nx[h] = L.dense[min(e[h], L.ND - 1) * L.K + c[h][j]];
+    }
+    if (!(kMode & 2)) {
+#pragma unroll
+      for (int h = 0; h < CH; ++h)
+        if (!(kMode & 8) || e[h] >= L.ND) nx[h] = big_next(L, e[h], c[h][j]);
+    }
+#pragma unroll
+    for (int h = 0; h < CH; ++h) {
+      acc[h] |= nx[h];
+      e[h] = nx[h] & 0x7FFFu;
+    }
   }
-  return acc;
 }
 
+__device__ inline void big_event(const ScanParams& P, uint64_t b, uint32_t lane, uint64_t lanes_lt, uint64_t pos,
+                                 uint32_t entry, uint2 prev, uint32_t d0, uint32_t d1, FastEvent* ev_seg,
+                                 uint32_t ev_count) {
+  if ((b >> lane) & 1) {
+    FastEvent r;
+    r.pos = pos;
+    r.entry = entry;
+    r.pad = 0;
+    r.prev = prev;
+    r.cur = make_uint2(d0, d1);
+    const uint32_t slot = ev_count + (uint32_t)__popcll(b & lanes_lt);
+    if (slot < P.ev_cap_per_wave) {
+      ev_seg[slot] = r;
+    } else {
+      unsigned long long ov = atomicAdd(&P.ctrl->ev_overflow, 1ull);
+      if (ov < P.ev_overflow_cap) P.ev_overflow[ov] = r;
+    }
+  }
+}
+
+// CH chains per lane: lane unit u covers the CH consecutive 4 KiB spans
+// u * CH .. u * CH + CH - 1, each walked by its own chain (kBigRing bytes of
+// register ring per chain).  Bit 2 of kMode: one event ballot per 16 bytes
+// (both groups of a dword quad) instead of per group.
+template <int kMode = 0, int CH = 1, int V = 8 / CH>
 __global__ __launch_bounds__(kBigThreads) void k_scan_big(ScanParams P) {
   extern __shared__ __align__(16) uint8_t smem[];
   const BigDev& B = P.big;
@@ -795,102 +890,138 @@ __global__ __launch_bounds__(kBigThreads) void k_scan_big(ScanParams P) {
     ((uint32_t*)smem)[i] = ((const uint32_t*)B.blob)[i];
   __syncthreads();
   const BigLds L = big_lds(B, smem, P.rs.ac.nclasses);
-  constexpr int V = 8;
   constexpr int kStep = V * 16;
   constexpr int kSteps = kNlBlock / kStep;
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t lanes_lt = (1ull << lane) - 1;
   const uint32_t wave = blockIdx.x * (kBigThreads / 64) + (threadIdx.x >> 6);
   const uint64_t nlanes = (uint64_t)gridDim.x * kBigThreads;
-  const uint64_t units = (P.nbytes + kNlBlock - 1) / kNlBlock;
+  const uint64_t spans = (P.nbytes + kNlBlock - 1) / kNlBlock;
+  const uint64_t units = (spans + CH - 1) / CH;
   FastEvent* ev_seg = P.events + (uint64_t)wave * P.ev_cap_per_wave;
   uint32_t ev_count = 0;  // wave-uniform
   uint64_t u = (uint64_t)blockIdx.x * kBigThreads + threadIdx.x;
-  uint4 cur[V], nxt[V];
-  uint64_t pos = u * kNlBlock;
-  if (u < units) {
-    const uint8_t* src = fast_src(P, pos);
+  uint4 cur[CH][V], nxt[CH][V];
+  uint64_t pos[CH];
+  bool live[CH];
 #pragma unroll
-    for (int k = 0; k < V; ++k) nxt[k] = *(const uint4*)(src + pos + 16 * k);
+  for (int h = 0; h < CH; ++h) {
+    pos[h] = (u * CH + h) * kNlBlock;
+    live[h] = u * CH + h < spans;
+    if (live[h]) {
+      const uint8_t* src = fast_src(P, pos[h]);
+#pragma unroll
+      for (int k = 0; k < V; ++k) nxt[h][k] = *(const uint4*)(src + pos[h] + 16 * k);
+    }
   }
   while (__ballot(u < units)) {
-    const bool live = u < units;
     const uint64_t un = u + nlanes;
-    const uint64_t s0 = pos;
-    const uint2 h = live && s0 >= 8 ? *(const uint2*)(fast_src(P, s0 - 8) + s0 - 8) : make_uint2(0, 0);
-    uint32_t e = 0;
-    {  // warm-up: the 7 bytes before the span (automaton depth <= kAcMaxLit)
+    uint64_t s0[CH];
+    uint32_t e[CH], nl[CH], hi[CH];
+    uint2 prev[CH];
 #pragma unroll
-      for (int j = 1; j < 8; ++j) e = big_next(L, e, L.cls[((j < 4 ? h.x : h.y) >> (8 * (j & 3))) & 0xFFu]) & 0x7FFFu;
+    for (int h = 0; h < CH; ++h) {
+      s0[h] = pos[h];
+      live[h] = u * CH + h < spans;
+      const uint2 w = live[h] && s0[h] >= 8 ? *(const uint2*)(fast_src(P, s0[h] - 8) + s0[h] - 8) : make_uint2(0, 0);
+      e[h] = 0;
+      // warm-up: the 7 bytes before the span (automaton depth <= kAcMaxLit)
+#pragma unroll
+      for (int j = 1; j < 8; ++j)
+        e[h] = big_next(L, e[h], L.cls[((j < 4 ? w.x : w.y) >> (8 * (j & 3))) & 0xFFu]) & 0x7FFFu;
+      prev[h] = w;
+      nl[h] = 0;
+      hi[h] = 0;
     }
-    uint2 prev = h;
-    uint32_t nl = 0, hi = 0;
     for (int step = 0; step < kSteps; ++step) {
+      uint64_t np[CH];
 #pragma unroll
-      for (int k = 0; k < V; ++k) cur[k] = nxt[k];
-      const uint64_t np = step + 1 < kSteps ? pos + kStep : un * kNlBlock;
-      if (live && (step + 1 < kSteps || un < units)) {
-        const uint8_t* src = fast_src(P, np);
+      for (int h = 0; h < CH; ++h) {
 #pragma unroll
-        for (int k = 0; k < V; ++k) nxt[k] = *(const uint4*)(src + np + 16 * k);
+        for (int k = 0; k < V; ++k) cur[h][k] = nxt[h][k];
+        np[h] = step + 1 < kSteps ? pos[h] + kStep : (un * CH + h) * kNlBlock;
+        if (live[h] && (step + 1 < kSteps || un * CH + h < spans)) {
+          const uint8_t* src = fast_src(P, np[h]);
+#pragma unroll
+          for (int k = 0; k < V; ++k) nxt[h][k] = *(const uint4*)(src + np[h] + 16 * k);
+        }
       }
 #pragma unroll
       for (int k = 0; k < V; ++k) {
-        const uint32_t d[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
+        uint32_t gs[2][CH], acc[2][CH];
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
-          const uint32_t d0 = d[2 * g], d1 = d[2 * g + 1];
-          nl += nl_count_dword(d0) + nl_count_dword(d1);
-          hi |= d0 | d1;
-          const uint32_t gs = e;
-          const uint32_t acc = big_group(L, e, d0, d1);
-          const uint64_t b = __ballot(live && (acc & 0x8000u));
-          if (b) {
-            if ((b >> lane) & 1) {
-              FastEvent r;
-              r.pos = pos + 16 * k + 8 * g;
-              r.entry = gs;
-              r.pad = 0;
-              r.prev = prev;
-              r.cur = make_uint2(d0, d1);
-              const uint32_t slot = ev_count + (uint32_t)__popcll(b & lanes_lt);
-              if (slot < P.ev_cap_per_wave) {
-                ev_seg[slot] = r;
-              } else {
-                unsigned long long ov = atomicAdd(&P.ctrl->ev_overflow, 1ull);
-                if (ov < P.ev_overflow_cap) P.ev_overflow[ov] = r;
-              }
-            }
-            ev_count += (uint32_t)__popcll(b);
+          uint32_t d[2 * CH];
+#pragma unroll
+          for (int h = 0; h < CH; ++h) {
+            d[2 * h] = g ? cur[h][k].z : cur[h][k].x;
+            d[2 * h + 1] = g ? cur[h][k].w : cur[h][k].y;
+            nl[h] += nl_count_dword(d[2 * h]) + nl_count_dword(d[2 * h + 1]);
+            hi[h] |= d[2 * h] | d[2 * h + 1];
+            gs[g][h] = e[h];
           }
-          prev = make_uint2(d0, d1);
+          big_group<kMode, CH>(L, e, d, acc[g]);
+          if (!(kMode & 4)) {
+#pragma unroll
+            for (int h = 0; h < CH; ++h) {
+              const uint64_t b = __ballot(live[h] && (acc[g][h] & 0x8000u));
+              if (b) {
+                big_event(P, b, lane, lanes_lt, pos[h] + 16 * k + 8 * g, gs[g][h], prev[h], d[2 * h], d[2 * h + 1],
+                          ev_seg, ev_count);
+                ev_count += (uint32_t)__popcll(b);
+              }
+              prev[h] = make_uint2(d[2 * h], d[2 * h + 1]);
+            }
+          }
+        }
+        if (kMode & 4) {
+          uint32_t any = 0;
+#pragma unroll
+          for (int h = 0; h < CH; ++h) any |= live[h] ? (acc[0][h] | acc[1][h]) : 0u;
+          if (__ballot(any & 0x8000u)) {
+#pragma unroll
+            for (int h = 0; h < CH; ++h)
+#pragma unroll
+              for (int g = 0; g < 2; ++g) {
+                const uint32_t d0 = g ? cur[h][k].z : cur[h][k].x, d1 = g ? cur[h][k].w : cur[h][k].y;
+                const uint64_t b = __ballot(live[h] && (acc[g][h] & 0x8000u));
+                if (b) {
+                  big_event(P, b, lane, lanes_lt, pos[h] + 16 * k + 8 * g, gs[g][h], prev[h], d0, d1, ev_seg,
+                            ev_count);
+                  ev_count += (uint32_t)__popcll(b);
+                }
+                prev[h] = make_uint2(d0, d1);
+              }
+          }
+#pragma unroll
+          for (int h = 0; h < CH; ++h) prev[h] = make_uint2(cur[h][k].z, cur[h][k].w);
         }
       }
-      pos = np;
+#pragma unroll
+      for (int h = 0; h < CH; ++h) pos[h] = np[h];
     }
-    if (live) {
-      P.nl_blocks[s0 / kNlBlock] = nl;
-      P.span_hi[s0 / kNlBlock] = (hi & 0x80808080u) ? 1 : 0;
-    }
+#pragma unroll
+    for (int h = 0; h < CH; ++h)
+      if (live[h]) {
+        P.nl_blocks[s0[h] / kNlBlock] = nl[h];
+        P.span_hi[s0[h] / kNlBlock] = (hi[h] & 0x80808080u) ? 1 : 0;
+      }
     u = un;
   }
   if (lane == 0) P.ev_counts[wave] = ev_count < P.ev_cap_per_wave ? ev_count : P.ev_cap_per_wave;
 }
 
-// k_scan_big's events: each flagged 8-byte group is replayed from its entry
-// state with the big automaton (blob in LDS) and every output state reached
-// is resolved by report_t (file lookup, confirm on the real bytes, keyword
-// gate bits, anchor hits).  Anchor hits are staged in LDS and appended to
-// P.hits with one global atomic per block (a global atomic per hit on the one
+// Anchor hits of k_big_resolve are staged in LDS and appended to P.hits with
+// one global atomic per block round (a global atomic per hit on the one
 // counter serialised at L2: 2.3 M hits cost 27 ms on configs[4]); overflow
 // past the stage goes straight to global.
-constexpr uint32_t kBigHitStage = 512;  // (blob <= kBigLdsMax + this stage fits the 160 KiB LDS)
-struct LdsHitSink {
+template <uint32_t kCap>
+struct LdsStageSink {
   uint64_t* buf;
   uint32_t* cnt;
   __device__ void push(const ScanParams& P, uint64_t rec) {
     const uint32_t i = atomicAdd(cnt, 1u);
-    if (i < kBigHitStage) {
+    if (i < kCap) {
       buf[i] = rec;
     } else {
       GlobalHitSink g;
@@ -899,19 +1030,46 @@ struct LdsHitSink {
   }
 };
 
-__global__ __launch_bounds__(1024) void k_big_report(ScanParams P, uint32_t n_waves) {
-  extern __shared__ __align__(16) uint8_t smem[];  // blob, then the hit stage
+__device__ inline uint32_t wave_incl_sum32(uint32_t v, uint32_t lane) {
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(v, d);
+    if (lane >= d) v += o;
+  }
+  return v;
+}
+__device__ inline uint32_t block_incl_sum32(uint32_t v, uint32_t* lds16, uint32_t* tot) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  v = wave_incl_sum32(v, lane);
+  if (lane == 63) lds16[wv] = v;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+  for (uint32_t k = 0; k < blockDim.x / 64; ++k) {
+    if (k < wv) before += lds16[k];
+    all += lds16[k];
+  }
+  __syncthreads();
+  *tot = all;
+  return v + before;
+}
+
+// k_big_report, part 1: each event's 8-byte group is replayed from its entry
+// state (blob in LDS) and every output state reached becomes one record
+// (position << 16 | state) in P.big_outs -- one block-wide prefix sum and one
+// global reservation (Ctrl::outputs) per 1024 events.  Only LDS work: the
+// outputs' global lookups are left to k_big_resolve, which runs without the
+// blob at full occupancy (resolving them here, one event per lane in
+// lock-step rounds, left the block waiting on each round's slowest chain of
+// dependent global reads: 3.0 ms on configs[4]).
+__global__ __launch_bounds__(1024) void k_big_walk(ScanParams P, uint32_t n_waves) {
+  extern __shared__ __align__(16) uint8_t smem[];
   const BigDev& B = P.big;
   for (uint32_t i = threadIdx.x; i < B.blob_bytes / 4; i += blockDim.x)
     ((uint32_t*)smem)[i] = ((const uint32_t*)B.blob)[i];
-  uint64_t* stage = (uint64_t*)(smem + ((B.blob_bytes + 15) & ~15u));
-  __shared__ uint32_t n_stage;
-  __shared__ unsigned long long base;
+  __shared__ uint32_t s32[16];
+  __shared__ unsigned long long obase;
+  __syncthreads();
   const BigLds L = big_lds(B, smem, P.rs.ac.nclasses);
-  uint64_t last_kw = ~0ull;
   for (uint32_t w = blockIdx.x; w < n_waves + 1; w += gridDim.x) {
-    if (threadIdx.x == 0) n_stage = 0;
-    __syncthreads();
     const FastEvent* seg;
     uint64_t n;
     if (w < n_waves) {
@@ -922,35 +1080,69 @@ __global__ __launch_bounds__(1024) void k_big_report(ScanParams P, uint32_t n_wa
       seg = P.ev_overflow;
       n = P.ctrl->ev_overflow < P.ev_overflow_cap ? P.ctrl->ev_overflow : P.ev_overflow_cap;
     }
-    LdsHitSink sink{stage, &n_stage};
-    // one event per thread per round, the stage flushed after every round (a
-    // segment of a hit-dense stretch -- a minified line full of rule
-    // instances -- holds thousands of hits: beyond the stage they would go
-    // through the one global counter, which serialises at L2)
     for (uint64_t r0 = 0; r0 < n; r0 += blockDim.x) {
       const uint64_t i = r0 + threadIdx.x;
+      uint32_t st[8], cnt = 0;
+      uint64_t pos = 0;
       if (i < n) {
         const FastEvent ev = seg[i];
+        pos = ev.pos;
         uint32_t e = ev.entry;
-        uint32_t fc = 0xFFFFFFFFu;  // the event's file, looked up once for all its outputs
-        uint64_t fcs = 0, fce = 0;
-#pragma unroll 1
+#pragma unroll
         for (int j = 0; j < 8; ++j) {
           const uint32_t nx = big_next(L, e, L.cls[((j < 4 ? ev.cur.x : ev.cur.y) >> (8 * (j & 3))) & 0xFFu]);
           e = nx & 0x7FFFu;
-          if (nx & 0x8000u) report_t<false>(P, e, ev.pos + j, &last_kw, sink, &fc, &fcs, &fce);
+          st[j] = (nx & 0x8000u) ? e : 0xFFFFu;
+          cnt += nx >> 15;
         }
       }
-      __syncthreads();
-      const uint32_t m = n_stage < kBigHitStage ? n_stage : kBigHitStage;
-      if (threadIdx.x == 0) base = m ? atomicAdd(&P.ctrl->hits, (unsigned long long)m) : 0ull;
-      __syncthreads();
-      for (uint32_t k = threadIdx.x; k < m; k += blockDim.x)
-        if (base + k < P.hit_cap) P.hits[base + k] = stage[k];
-      __syncthreads();
-      if (threadIdx.x == 0) n_stage = 0;
-      __syncthreads();
+      uint32_t tot;
+      const uint32_t incl = block_incl_sum32(cnt, s32, &tot);
+      if (threadIdx.x == 0) obase = atomicAdd(&P.ctrl->outputs, (unsigned long long)tot);
+      __syncthreads();  // (the next round's scan barriers order this read before obase's next write)
+      if (cnt) {
+        uint64_t k = obase + incl - cnt;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (st[j] != 0xFFFFu) {
+            if (k < P.big_out_cap) P.big_outs[k] = ((pos + j) << 16) | B.ac_of[st[j]];
+            ++k;
+          }
+      }
     }
+  }
+}
+
+// k_big_report, part 2: one output record per lane (grid-stride), resolved by
+// report_t (file lookup, truncated-literal and case checks on the real bytes,
+// keyword gate bits, anchor hits); hits staged in LDS, one global
+// reservation per block round.
+constexpr uint32_t kResolveThreads = 256, kResolveStage = 2048;
+__global__ __launch_bounds__(kResolveThreads) void k_big_resolve(ScanParams P) {
+  __shared__ uint64_t stage[kResolveStage];
+  __shared__ uint32_t n_stage;
+  __shared__ unsigned long long base;
+  const uint64_t n = P.ctrl->outputs < P.big_out_cap ? P.ctrl->outputs : P.big_out_cap;
+  uint64_t last_kw = ~0ull;
+  const uint64_t stride = (uint64_t)gridDim.x * kResolveThreads;
+  if (threadIdx.x == 0) n_stage = 0;
+  __syncthreads();
+  for (uint64_t r0 = (uint64_t)blockIdx.x * kResolveThreads; r0 < n; r0 += stride) {
+    const uint64_t i = r0 + threadIdx.x;
+    LdsStageSink<kResolveStage> sink{stage, &n_stage};
+    if (i < n) {
+      const uint64_t rec = P.big_outs[i];
+      report_t<false>(P, (uint32_t)(rec & 0xFFFFu), rec >> 16, &last_kw, sink);
+    }
+    __syncthreads();
+    const uint32_t m = n_stage < kResolveStage ? n_stage : kResolveStage;
+    if (threadIdx.x == 0) base = m ? atomicAdd(&P.ctrl->hits, (unsigned long long)m) : 0ull;
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < m; k += kResolveThreads)
+      if (base + k < P.hit_cap) P.hits[base + k] = stage[k];
+    __syncthreads();
+    if (threadIdx.x == 0) n_stage = 0;
+    __syncthreads();
   }
 }
 
@@ -3232,6 +3424,12 @@ struct FindParams {
   uint64_t* seg_len;   // then, after the exclusive scan, seg_off
   uint64_t* seg_off;
   uint64_t n_seg_cap;  // n_locs + kCodeLines * n_locs
+  // arena granules (kArenaGran bytes): gran_seg[g] = the segment covering
+  // byte g * kArenaGran after k_arena_gran_scan, up to the maximum carried in
+  // from earlier blocks of 1024 granules (gran_carry)
+  uint32_t* gran_seg;
+  uint32_t* gran_carry;
+  uint64_t n_gran;
   uint8_t* arena;
   uint64_t* sort_key;
   uint32_t* sort_idx;
@@ -3244,13 +3442,6 @@ __device__ inline uint64_t wave_incl_max64(uint64_t v, uint32_t lane) {
   for (uint32_t d = 1; d < 64; d <<= 1) {
     const uint64_t o = __shfl_up(v, d);
     if (lane >= d) v = v > o ? v : o;
-  }
-  return v;
-}
-__device__ inline uint32_t wave_incl_sum32(uint32_t v, uint32_t lane) {
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(v, d);
-    if (lane >= d) v += o;
   }
   return v;
 }
@@ -3369,20 +3560,6 @@ __device__ inline uint64_t block_incl_max64(uint64_t v, uint64_t* lds16, uint64_
   __syncthreads();
   *tot = all;
   return v > before ? v : before;
-}
-__device__ inline uint32_t block_incl_sum32(uint32_t v, uint32_t* lds16, uint32_t* tot) {
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  v = wave_incl_sum32(v, lane);
-  if (lane == 63) lds16[wv] = v;
-  __syncthreads();
-  uint32_t before = 0, all = 0;
-  for (uint32_t k = 0; k < blockDim.x / 64; ++k) {
-    if (k < wv) before += lds16[k];
-    all += lds16[k];
-  }
-  __syncthreads();
-  *tot = all;
-  return v + before;
 }
 
 // k_censor for one file group of >= kCensorBig locations per 1024-lane block
@@ -3713,14 +3890,59 @@ __global__ void k_seg_total(FindParams F) {
     F.ctrl->find_bytes = F.seg_off[F.n_seg_cap - 1] + F.seg_len[F.n_seg_cap - 1];
 }
 
+// Arena granule index: a non-empty segment k records itself at the first
+// granule whose start byte it covers (at most one segment covers a byte), and
+// an inclusive max-scan spreads it over the later granules it covers --
+// segments ascend with their offsets.  Per block of 1024 granules here, the
+// blocks' maxima carried by k_arena_gran_carry.
+constexpr uint32_t kArenaGran = 256;
+__global__ void k_arena_gran_mark(FindParams F) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= F.n_seg_cap) return;
+  const uint64_t o = F.seg_off[k], len = F.seg_len[k];
+  if (!len) return;
+  const uint64_t g = (o + kArenaGran - 1) / kArenaGran;
+  if (g * kArenaGran < o + len && g < F.n_gran) F.gran_seg[g] = (uint32_t)k;
+}
+__global__ __launch_bounds__(1024) void k_arena_gran_scan(FindParams F) {
+  __shared__ uint64_t s64[16];
+  const uint64_t g = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+  const uint32_t v = g < F.n_gran ? F.gran_seg[g] : 0u;
+  uint64_t tot;
+  const uint64_t incl = block_incl_max64(v, s64, &tot);
+  if (g < F.n_gran) F.gran_seg[g] = (uint32_t)incl;
+  if (threadIdx.x == 0) F.gran_carry[blockIdx.x + 1] = (uint32_t)tot;  // (exclusive carries after the next pass)
+}
+__global__ __launch_bounds__(1024) void k_arena_gran_carry(FindParams F, uint32_t n_blocks) {
+  __shared__ uint64_t s64[16];
+  uint64_t carry = 0;
+  for (uint32_t b0 = 0; b0 < n_blocks; b0 += 1024) {
+    const uint32_t b = b0 + threadIdx.x;
+    const uint32_t v = b < n_blocks ? F.gran_carry[b + 1] : 0u;
+    uint64_t tot;
+    uint64_t incl = block_incl_max64(v, s64, &tot);
+    incl = incl > carry ? incl : carry;
+    if (b < n_blocks) F.gran_carry[b + 1] = (uint32_t)incl;  // carry into block b + 1
+    carry = carry > tot ? carry : tot;
+  }
+  if (threadIdx.x == 0) F.gran_carry[0] = 0;
+}
+__device__ inline uint64_t arena_gran_seg(const FindParams& F, uint64_t g, uint64_t total) {
+  if (g >= F.n_gran || g * kArenaGran >= total) return F.n_seg_cap - 1;
+  const uint32_t a = F.gran_seg[g], c = F.gran_carry[g >> 10];
+  return a > c ? a : c;
+}
+
 // The string arena, 16 bytes per lane over all segments (a multi-MiB line is
-// spread over the whole grid): the segment by binary search over seg_off,
+// spread over the whole grid): the segment by binary search over seg_off
+// between the covering segments of the chunk's granule and the next one,
 // source bytes from the batch, bytes inside the file's censor intervals as '*'.
 __global__ __launch_bounds__(256) void k_arena_fill(FindParams F) {
   const uint64_t total = F.ctrl->find_bytes;
   for (uint64_t a = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; a < total;
        a += (uint64_t)gridDim.x * blockDim.x * 16) {
-    uint64_t lo = 0, hi = F.n_seg_cap;  // last segment with seg_off <= a
+    // last segment with seg_off <= a: in [covering(g), covering(g + 1)]
+    uint64_t lo = arena_gran_seg(F, a / kArenaGran, total), hi = arena_gran_seg(F, a / kArenaGran + 1, total) + 1;
     while (hi - lo > 1) {
       const uint64_t mid = (lo + hi) >> 1;
       if (F.seg_off[mid] <= a) lo = mid;
@@ -3823,17 +4045,22 @@ __global__ void k_find_gather(const FindRec* in, const uint32_t* idx, uint64_t n
   if (i < n) out[i] = in[idx[i]];
 }
 
-// Scan's sort (scanner.go:441-446) is by (RuleID, Match): the first 8 bytes
+// Scan's sort (scanner.go:441-446) is by (RuleID, Match): the first 16 bytes
 // of each Match window (from the filled arena, zero-padded, big-endian) are
-// a sort key, so the device orders (file, RuleID rank, Match prefix) and the
-// host only breaks ties of equal prefixes.
-__global__ void k_match_prefix(const FindRec* rec, const uint8_t* arena, uint64_t n, uint64_t* key, uint32_t* idx) {
+// two sort keys, so the device orders (file, RuleID rank, Match prefix) and
+// the host only breaks ties of equal prefixes.  (8 bytes left 19 k ties on
+// configs[4] -- lines opening with the same assignment -- and 2.7 ms of host
+// sorting.)
+__global__ void k_match_prefix(const FindRec* rec, const uint8_t* arena, uint64_t n, uint64_t* key, uint64_t* key_b,
+                               uint32_t* idx) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const FindRec& r = rec[i];
-  uint64_t k = 0;
+  uint64_t k = 0, kb = 0;
   for (uint32_t j = 0; j < 8; ++j) k = (k << 8) | (j < r.m_len ? arena[r.m_off + j] : 0u);
+  for (uint32_t j = 8; j < 16; ++j) kb = (kb << 8) | (j < r.m_len ? arena[r.m_off + j] : 0u);
   key[i] = k;
+  key_b[i] = kb;
   idx[i] = (uint32_t)i;
 }
 
@@ -3845,11 +4072,12 @@ __global__ void k_gather_u64(const uint64_t* in, const uint32_t* idx, uint64_t n
 // Positions i (> 0) of the ordered findings whose (file, rank) key AND Match
 // prefix equal those of i - 1: the only places the host has to compare whole
 // Match strings (appended unordered; the host sorts the short list).
-__global__ void k_tie_list(const uint64_t* fr_key, const uint64_t* prefix, const uint32_t* order, uint64_t n,
-                           uint32_t* ties, uint64_t cap, Ctrl* ctrl) {
+__global__ void k_tie_list(const uint64_t* fr_key, const uint64_t* prefix, const uint64_t* prefix_b,
+                           const uint32_t* order, uint64_t n, uint32_t* ties, uint64_t cap, Ctrl* ctrl) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0 || i >= n) return;
-  if (fr_key[i] != fr_key[i - 1] || prefix[order[i]] != prefix[order[i - 1]]) return;
+  const uint32_t a = order[i], b = order[i - 1];
+  if (fr_key[i] != fr_key[i - 1] || prefix[a] != prefix[b] || prefix_b[a] != prefix_b[b]) return;
   const unsigned long long k = atomicAdd(&ctrl->n_ties, 1ull);
   if (k < cap) ties[k] = (uint32_t)i;
 }
@@ -4009,6 +4237,7 @@ struct DBuf {
 struct DevImage {
   uint64_t rs_id = 0;
   DBuf<uint8_t> big;  // k_scan_big blob (empty unless the automaton needs it)
+  DBuf<uint16_t> big_ac_of;  // its state numbering -> the automaton's
   BigDev big_view{};
   DBuf<gre::Inst> inst;
   DBuf<gre::ClassDesc> classes;
@@ -4092,6 +4321,8 @@ struct tsg_engine {
   DBuf<RedoRec> redo;
   DBuf<uint32_t> ev_counts;
   uint64_t ev_ovf_need = 0;  // overflow-event capacity learnt from a lost scan
+  DBuf<uint64_t> big_outs;   // k_big_walk's output records
+  uint64_t big_out_need = 0;  // their capacity learnt from a lost scan
   bool fast_timed = false;   // ev[10..11] bracket the last k_scan_fast launch
   DBuf<uint8_t> fflags8;     // per-file result flags, u8
   uint32_t num_cus = 0;
@@ -4122,6 +4353,8 @@ struct tsg_engine {
   DBuf<tsg_loc> out_locs;  // k_out_locs
   DBuf<CodeRec> f_code;
   DBuf<uint8_t> f_arena;
+  DBuf<uint32_t> f_gran, f_gcarry;  // arena granule index (k_arena_gran_*)
+  DBuf<uint64_t> f_lkeyb;            // Match bytes 8..15 (k_match_prefix)
   std::shared_ptr<PinnedPool> pinned = std::make_shared<PinnedPool>();
 };
 
@@ -4432,22 +4665,54 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   // k_scan_big blob: only for an automaton that neither k_scan_fast's image
   // nor an LDS table holds (see BigDev); the most dense rows that fit
   im.big_view = BigDev{};
-  if (ac.fast.empty() && (size_t)ac.nstates * ac.nclasses * 2 > (size_t)kLdsTableMax && ac.fail.size() == ac.nstates) {
+  if (ac.fast.empty() && (size_t)ac.nstates * ac.nclasses * 2 > (size_t)kLdsTableMax && ac.fail.size() == ac.nstates &&
+      ac.nclasses <= kBigMore && ac.nstates <= 0x8000u) {
     const uint32_t S = ac.nstates, K = ac.nclasses;
-    std::vector<uint32_t> ecount(S + 1, 0);  // differing classes per state
-    std::vector<std::vector<uint32_t>> edges(S);
-    for (uint32_t st = 1; st < S; ++st) {
-      const uint32_t f = ac.fail[st];
-      for (uint32_t c = 0; c < K; ++c)
-        if (ac.delta[(size_t)st * K + c] != ac.delta[(size_t)f * K + c])
-          edges[st].push_back((c << 16) | ac.delta[(size_t)st * K + c]);
+    // blob numbering: the states text is likeliest to hold first (they get the
+    // dense rows).  A state's weight is the probability of its label under
+    // independent bytes of a text byte model (big_byte_weight); the label
+    // probability is the parent's times the edge class's, walked breadth
+    // first (a state is first reached from its trie parent).  The automaton's
+    // own numbering (breadth first, output states last) left the output and
+    // deep-but-common states cold.
+    std::vector<uint32_t> order(S), at(S);  // blob id -> automaton id, and back
+    for (uint32_t k = 0; k < S; ++k) order[k] = k;
+    if (!experiment_env("TSG_BIG_BFS")) {
+      std::vector<double> pc(K, 0.0);
+      for (int b = 0; b < 256; ++b) pc[ac.cls[b]] += big_byte_weight((uint8_t)b);
+      std::vector<double> P(S, -1.0);
+      std::vector<uint32_t> q{0};
+      P[0] = 2.0;  // (the root first)
+      for (size_t h = 0; h < q.size(); ++h) {
+        const uint32_t st = q[h];
+        for (uint32_t c = 0; c < K; ++c) {
+          const uint32_t t = ac.delta[(size_t)st * K + c] & 0x7FFFu;
+          if (P[t] < 0) {
+            P[t] = (st ? P[st] : 1.0) * pc[c];
+            q.push_back(t);
+          }
+        }
+      }
+      for (uint32_t k = 0; k < S; ++k)
+        if (P[k] < 0) P[k] = 0;  // (unreachable: none)
+      std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return P[a] > P[b]; });
     }
-    std::vector<uint64_t> suffix(S + 1, 0);  // edges of states >= s
-    for (uint32_t st = S; st-- > 0;) suffix[st] = suffix[st + 1] + edges[st].size();
-    auto a4 = [](uint64_t x) { return (x + 3) & ~3ull; };
+    for (uint32_t k = 0; k < S; ++k) at[order[k]] = k;
+    auto entry = [&](uint32_t st, uint32_t c) {  // delta in blob ids (bit 15 kept)
+      const uint16_t v = ac.delta[(size_t)st * K + c];
+      return (uint32_t)((v & 0x8000u) | at[v & 0x7FFFu]);
+    };
+    std::vector<std::vector<uint32_t>> edges(S);  // per blob state: class << 16 | entry where it differs from fail
+    for (uint32_t n = 1; n < S; ++n) {
+      const uint32_t st = order[n], f = ac.fail[st];
+      for (uint32_t c = 0; c < K; ++c)
+        if (ac.delta[(size_t)st * K + c] != ac.delta[(size_t)f * K + c]) edges[n].push_back((c << 16) | entry(st, c));
+    }
+    std::vector<uint64_t> suffix(S + 1, 0);  // list words of cold states >= s
+    for (uint32_t st = S; st-- > 0;) suffix[st] = suffix[st + 1] + (edges[st].size() > 2 ? edges[st].size() + 1 : 0);
+    auto a8 = [](uint64_t x) { return (x + 7) & ~7ull; };
     auto bytes_for = [&](uint32_t nd) {
-      const uint64_t cold = S - nd;
-      return 256 + a4((uint64_t)nd * K * 2) + (cold + 1) * 4 + suffix[nd] * 4 + a4(cold * 2);
+      return a8(256 + (uint64_t)nd * K * 2) + (uint64_t)(S - nd) * 8 + suffix[nd] * 4;
     };
     uint32_t lo = 1, hi = S;  // largest nd with bytes_for(nd) <= kBigLdsMax (bytes grow with nd)
     if (bytes_for(1) <= kBigLdsMax) {
@@ -4459,23 +4724,36 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
       const uint32_t nd = lo, cold = S - nd;
       std::vector<uint8_t> blob(bytes_for(nd), 0);
       memcpy(blob.data(), ac.cls, 256);
-      memcpy(blob.data() + 256, ac.delta.data(), (size_t)nd * K * 2);
-      const uint32_t o_eoff = (uint32_t)(256 + a4((uint64_t)nd * K * 2));
-      const uint32_t o_eval = o_eoff + (cold + 1) * 4;
-      const uint32_t o_fail = (uint32_t)(o_eval + suffix[nd] * 4);
-      uint32_t* eo = (uint32_t*)(blob.data() + o_eoff);
+      uint16_t* dense = (uint16_t*)(blob.data() + 256);
+      for (uint32_t n = 0; n < nd; ++n)
+        for (uint32_t c = 0; c < K; ++c) dense[(size_t)n * K + c] = (uint16_t)entry(order[n], c);
+      const uint32_t o_cold = (uint32_t)a8(256 + (uint64_t)nd * K * 2);
+      const uint32_t o_eval = o_cold + cold * 8;
+      uint32_t* rec = (uint32_t*)(blob.data() + o_cold);
       uint32_t* ev = (uint32_t*)(blob.data() + o_eval);
-      uint16_t* fl = (uint16_t*)(blob.data() + o_fail);
       uint32_t k = 0;
       for (uint32_t j = 0; j < cold; ++j) {
-        eo[j] = k;
-        for (uint32_t v : edges[nd + j]) ev[k++] = v;
-        fl[j] = ac.fail[nd + j];
+        const std::vector<uint32_t>& E = edges[nd + j];
+        const uint32_t fl = at[ac.fail[order[nd + j]]];
+        if (E.size() <= 2) {
+          const uint32_t c1 = E.size() > 0 ? E[0] >> 16 : kBigNone, c2 = E.size() > 1 ? E[1] >> 16 : kBigNone;
+          const uint32_t n1 = E.size() > 0 ? E[0] & 0xFFFFu : 0, n2 = E.size() > 1 ? E[1] & 0xFFFFu : 0;
+          rec[2 * j] = c1 | c2 << 8 | n1 << 16;
+          rec[2 * j + 1] = n2 | fl << 16;
+        } else {
+          rec[2 * j] = kBigMore | kBigMore << 8 | (k & 0xFFFFu) << 16;
+          rec[2 * j + 1] = (k >> 16) | fl << 16;
+          for (uint32_t v : E) ev[k++] = v;
+          ev[k++] = 0xFFFFFFFFu;
+        }
       }
-      eo[cold] = k;
+      std::vector<uint16_t> ac_of(S);
+      for (uint32_t n = 0; n < S; ++n) ac_of[n] = (uint16_t)order[n];
       HIP_TRY(im.big.ensure(blob.size()));
       HIP_TRY(hipMemcpy(im.big.p, blob.data(), blob.size(), hipMemcpyHostToDevice));
-      im.big_view = BigDev{im.big.p, (uint32_t)blob.size(), nd, cold, o_eoff, o_eval, o_fail};
+      HIP_TRY(im.big_ac_of.ensure(S));
+      HIP_TRY(hipMemcpy(im.big_ac_of.p, ac_of.data(), S * 2, hipMemcpyHostToDevice));
+      im.big_view = BigDev{im.big.p, (uint32_t)blob.size(), nd, cold, o_cold, o_eval, im.big_ac_of.p};
     }
   }
   HIP_TRY(im.out_off.ensure(ac.out_off.size()));
@@ -4874,7 +5152,34 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     const uint64_t units = (P.nbytes + kNlBlock - 1) / kNlBlock;
     HIP_TRY(e->span_hi.ensure(units + 1));
     P.span_hi = e->span_hi.p;
-    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((units + nt - 1) / nt, e->num_cus));
+    // one unit per lane: CH spans (kBigChains)
+    const void* big_fn = (const void*)k_scan_big<kBigMode, kBigChains>;
+    int big_mode = kBigMode, big_ch = kBigChains;
+#ifdef TSG_EXPERIMENTS
+    int big_v = 8;
+    if (const char* v = getenv("TSG_BIG_VARIANT")) {  // "<mode>[x<chains>][v<ring uint4s>]"
+      big_mode = atoi(v);
+      big_ch = strchr(v, 'x') ? atoi(strchr(v, 'x') + 1) : 1;
+      big_v = strchr(v, 'v') ? atoi(strchr(v, 'v') + 1) : 8 / big_ch;
+    }
+    using BigFn = void (*)(ScanParams);
+    struct BigV { int mode, ch, v; BigFn fn; };
+    static const BigV kBigVariants[] = {
+        {0, 1, 8, k_scan_big<0, 1>},     {1, 1, 8, k_scan_big<1, 1>},     {2, 1, 8, k_scan_big<2, 1>},
+        {3, 1, 8, k_scan_big<3, 1>},     {4, 1, 8, k_scan_big<4, 1>},     {0, 2, 4, k_scan_big<0, 2>},
+        {8, 2, 4, k_scan_big<8, 2>},     {0, 2, 2, k_scan_big<0, 2, 2>},  {8, 2, 2, k_scan_big<8, 2, 2>},
+        {12, 2, 2, k_scan_big<12, 2, 2>}, {2, 2, 2, k_scan_big<2, 2, 2>}, {4, 1, 4, k_scan_big<4, 1, 4>}};
+    BigFn pick = nullptr;
+    for (const BigV& x : kBigVariants)
+      if (x.mode == big_mode && x.ch == big_ch && x.v == big_v) pick = x.fn;
+    if (!pick) {
+      set_last_error("TSG_BIG_VARIANT: no such k_scan_big instantiation");
+      return TSG_ERR_INVALID_ARG;
+    }
+    big_fn = (const void*)pick;
+#endif
+    const uint64_t big_units = (units + big_ch - 1) / big_ch;
+    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((big_units + nt - 1) / nt, e->num_cus));
     const uint64_t n_waves = (uint64_t)blocks * (nt / 64);
     P.ev_cap_per_wave = std::max<uint64_t>(1024, (P.nbytes / 256) / n_waves + 256);
     HIP_TRY(e->ev_buf.ensure(n_waves * P.ev_cap_per_wave));
@@ -4885,17 +5190,22 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     P.ev_overflow = e->ev_overflow.p;
     P.ev_overflow_cap = e->ev_overflow.n;
     HIP_TRY(hipMemsetAsync(&P.ctrl->ev_overflow, 0, 8, s));
-    HIP_TRY(hipFuncSetAttribute((const void*)k_scan_big, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)P.big.blob_bytes));
+    HIP_TRY(hipFuncSetAttribute(big_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.big.blob_bytes));
     if (e->events) HIP_TRY(hipEventRecord(e->ev[10], s));
-    hipLaunchKernelGGL(k_scan_big, dim3(blocks), dim3(nt), P.big.blob_bytes, s, P);
+    (void)big_mode;
+    void* big_args[] = {&P};
+    HIP_TRY(hipLaunchKernel(big_fn, dim3(blocks), dim3(nt), big_args, P.big.blob_bytes, s));
     HIP_TRY(hipGetLastError());
     if (e->events) HIP_TRY(hipEventRecord(e->ev[11], s));
     e->fast_timed = e->events;
-    const uint32_t rep_lds = ((P.big.blob_bytes + 15) & ~15u) + kBigHitStage * 8;
-    HIP_TRY(hipFuncSetAttribute((const void*)k_big_report, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rep_lds));
-    hipLaunchKernelGGL(k_big_report, dim3((uint32_t)std::min<uint64_t>(n_waves + 1, e->num_cus)), dim3(1024), rep_lds, s,
-                       P, (uint32_t)n_waves);
+    HIP_TRY(e->big_outs.ensure(std::max<uint64_t>({1 << 20, P.nbytes / 256, e->big_out_need})));
+    P.big_outs = e->big_outs.p;
+    P.big_out_cap = e->big_outs.n;
+    HIP_TRY(hipFuncSetAttribute((const void*)k_big_walk, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)P.big.blob_bytes));
+    hipLaunchKernelGGL(k_big_walk, dim3((uint32_t)std::min<uint64_t>(n_waves + 1, e->num_cus)), dim3(1024),
+                       P.big.blob_bytes, s, P, (uint32_t)n_waves);
+    hipLaunchKernelGGL(k_big_resolve, dim3(e->num_cus * 8), dim3(kResolveThreads), 0, s, P);
     HIP_TRY(hipGetLastError());
   } else {
     const size_t table_bytes = (size_t)ac.nstates * ac.nclasses * 2;
@@ -5035,6 +5345,18 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   if (int rc = read_ctrl(e, &c)) return rc;  // the arena size
   HIP_TRY(e->f_arena.ensure(c.find_bytes + 16));
   F.arena = e->f_arena.p;
+  F.n_gran = c.find_bytes / kArenaGran + 2;
+  const uint32_t gran_blocks = (uint32_t)((F.n_gran + 1023) / 1024);
+  HIP_TRY(e->f_gran.ensure(F.n_gran));
+  HIP_TRY(e->f_gcarry.ensure(gran_blocks + 1));
+  F.gran_seg = e->f_gran.p;
+  F.gran_carry = e->f_gcarry.p;
+  if (c.find_bytes) {
+    HIP_TRY(hipMemsetAsync(F.gran_seg, 0, F.n_gran * 4, s));
+    hipLaunchKernelGGL(k_arena_gran_mark, dim3((uint32_t)((n_seg + 255) / 256)), dim3(256), 0, s, F);
+    hipLaunchKernelGGL(k_arena_gran_scan, dim3(gran_blocks), dim3(1024), 0, s, F);
+    hipLaunchKernelGGL(k_arena_gran_carry, dim3(1), dim3(1024), 0, s, F, gran_blocks);
+  }
   // the result's page-locked block, laid out now: the Code records and the
   // string arena are final once k_arena_fill ends, so their D2H (most of the
   // bytes) runs on a side stream under the Match sorts below
@@ -5075,25 +5397,30 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   HIP_TRY(hipEventRecord(e->ev_side, e->side));
   // order: (file, RuleID rank) major, Match prefix minor -- two stable radix
   // sorts, least significant key first (f_lkey / f_lkey2 / f_lslot* are free now)
+  HIP_TRY(e->f_lkeyb.ensure(n_locs));
   hipLaunchKernelGGL(k_match_prefix, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->f_arena.p, n_locs, e->f_lkey.p,
-                     e->f_lslot.p);
+                     e->f_lkeyb.p, e->f_lslot.p);
   size_t tmp2 = 0;
   HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p, e->f_lslot2.p,
                                              (int)n_locs, 0, 64, s));
   HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p,
+  // Match bytes 8..15, then (stable) bytes 0..7, then (file, RuleID rank)
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->f_lkeyb.p, e->f_lkey2.p, e->f_lslot.p,
                                              e->f_lslot2.p, (int)n_locs, 0, 64, s));
-  hipLaunchKernelGGL(k_gather_u64, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lslot2.p, n_locs, e->keys2.p);
+  hipLaunchKernelGGL(k_gather_u64, dim3(lane_blocks), dim3(256), 0, s, e->f_lkey.p, e->f_lslot2.p, n_locs, e->keys2.p);
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys2.p, e->f_lkey2.p, e->f_lslot2.p,
+                                             e->f_lslot.p, (int)n_locs, 0, 64, s));
+  hipLaunchKernelGGL(k_gather_u64, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lslot.p, n_locs, e->keys2.p);
   tmp2 = 0;
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->keys2.p, e->keys.p, e->f_lslot2.p, e->vals2.p,
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->keys2.p, e->keys.p, e->f_lslot.p, e->vals2.p,
                                              (int)n_locs, 0, key_bits, s));
   HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys2.p, e->keys.p, e->f_lslot2.p, e->vals2.p,
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys2.p, e->keys.p, e->f_lslot.p, e->vals2.p,
                                              (int)n_locs, 0, key_bits, s));
   hipLaunchKernelGGL(k_find_gather, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->vals2.p, n_locs, e->f_rec2.p);
   HIP_TRY(e->f_ties.ensure(tie_cap));
-  hipLaunchKernelGGL(k_tie_list, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lkey.p, e->vals2.p, n_locs,
-                     e->f_ties.p, tie_cap, e->ctrl.p);
+  hipLaunchKernelGGL(k_tie_list, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lkey.p, e->f_lkeyb.p, e->vals2.p,
+                     n_locs, e->f_ties.p, tie_cap, e->ctrl.p);
   HIP_TRY(hipGetLastError());
   // the kept locations as tsg_loc records
   HIP_TRY(e->out_locs.ensure(n_locs));
@@ -5509,6 +5836,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   P.hits = e->hits.p;
   P.hit_cap = hit_cap;
   P.ctrl = e->ctrl.p;
+
   HIP_TRY(e->fold_pos.ensure(std::max<uint64_t>(1 << 16, e->fold_need)));
   P.fold_pos = e->fold_pos.p;
   P.fold_cap = e->fold_pos.n;
@@ -5540,12 +5868,14 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     if ((rc = read_ctrl(e, &c))) return rc;
     const bool ev_lost = (rs->ac.fast.size() || P.big.blob) && c.ev_overflow > e->ev_overflow.n;
     const bool fold_lost = c.n_fold > P.fold_cap;
-    if (c.hits <= hit_cap && !ev_lost && !fold_lost) {
+    const bool outs_lost = P.big.blob && c.outputs > P.big_out_cap;  // (k_big_walk's records)
+    if (c.hits <= hit_cap && !ev_lost && !fold_lost && !outs_lost) {
       scanned = true;
       break;
     }
     // overflow: grow and rescan (keyword bits are idempotent)
     if (ev_lost) e->ev_ovf_need = c.ev_overflow + (c.ev_overflow >> 2);
+    if (outs_lost) e->big_out_need = c.outputs + (c.outputs >> 2);
     if (fold_lost) {
       e->fold_need = c.n_fold + (c.n_fold >> 2);
       HIP_TRY(e->fold_pos.ensure(e->fold_need));
@@ -6142,6 +6472,7 @@ void tsg_engine_free(tsg_engine* e) {
   e->f_soff.release(); e->f_lslot.release(); e->f_lslot2.release(); e->f_lhead.release(); e->f_lscan.release();
   e->f_luid.release(); e->f_sfile.release(); e->f_sgrp.release(); e->f_grp.release();
   e->f_rec.release(); e->f_rec2.release(); e->f_code.release(); e->f_arena.release();
+  e->f_gran.release(); e->f_gcarry.release(); e->big_outs.release(); e->f_lkeyb.release();
   e->f_ties.release(); e->out_locs.release();
   if (e->events)
     for (auto& ev : e->ev) (void)hipEventDestroy(ev);
@@ -6569,7 +6900,9 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
     Ctrl c;
     if ((rc = read_ctrl(e, &c))) return rc;
     const bool ev_lost = (rs->ac.fast.size() || P.big.blob) && c.ev_overflow > e->ev_overflow.n;
-    if (!ev_lost && c.n_fold <= P.fold_cap) {
+    const bool outs_lost = P.big.blob && c.outputs > P.big_out_cap;  // (k_big_walk's records)
+    if (outs_lost) e->big_out_need = c.outputs + (c.outputs >> 2);
+    if (!ev_lost && !outs_lost && c.n_fold <= P.fold_cap) {
       if ((rc = launch_fold_windows(e, P, false))) return rc;
       if ((rc = launch_uni_keywords(e, P))) return rc;
       scanned = true;
