@@ -160,6 +160,15 @@ int tsg_ruleset_group_run(const tsg_ruleset* rs, size_t i, int* valid, int* len,
 int tsg_ruleset_path_dfa_check(const tsg_ruleset* rs, size_t i, int which, const uint8_t* path, size_t len,
                                int* result);
 
+/* k_scan_big's LDS blob replayed on the CPU (diagnostics / tests): the text
+ * walked through the keyword/anchor automaton's table and through the blob
+ * (dense rows + cold-state records, frequency or, bfs != 0, breadth-first
+ * state numbering); *mismatches = steps where they disagree (state or output
+ * bit), *cold_hops = cold records read, *n_dense = dense rows.
+ * TSG_ERR_UNSUPPORTED when the automaton has no blob shape. */
+int tsg_ruleset_big_check(const tsg_ruleset* rs, const uint8_t* text, size_t len, int bfs, uint64_t* mismatches,
+                          uint64_t* cold_hops, uint32_t* n_dense);
+
 /* Candidate filter of rule i, run on host text from anchor position h:
  * *accept = 0 only when no match of the rule can contain an anchor hit at h
  * (k_expand drops such hits); *n_states = its DFA size (0 = no filter). */

@@ -3665,9 +3665,40 @@ __global__ __launch_bounds__(1024) void k_censor_big(FindParams F) {
   }
 }
 
-// The censor interval holding file-relative byte x, or -1 (binary search).
-__device__ inline int64_t censor_holder(const uint64_t* iv, uint32_t g0, uint32_t m, uint64_t x) {
-  uint32_t lo = 0, hi = m;  // first interval with a > x
+
+// The censor interval holding file-relative byte x, or -1, for x near
+// interval h of the group (relative): a galloping search out from h, then a binary search of the bracket -- the
+// line breaks k_find_spans looks up lie a few lines from the location, whose
+// own interval is h, so a file with thousands of intervals costs ~2 loads a
+// lookup instead of a full-depth binary search.
+__device__ inline int64_t censor_holder_near(const uint64_t* iv, uint32_t g0, uint32_t m, uint64_t x, uint32_t h) {
+  if (m == 0) return -1;
+  if (h >= m) h = m - 1;
+  uint32_t lo, hi;  // the first interval with a > x lies in [lo, hi]
+  if (iv[2 * (g0 + h)] <= x) {
+    lo = h + 1;
+    hi = m;
+    for (uint32_t d = 1;; d <<= 1) {
+      const uint32_t t = lo - 1 + d;
+      if (t >= m) break;
+      if (iv[2 * (g0 + t)] > x) {
+        hi = t;
+        break;
+      }
+      lo = t + 1;
+    }
+  } else {
+    lo = 0;
+    hi = h;
+    for (uint32_t d = 1; hi >= d; d <<= 1) {
+      const uint32_t t = hi - d;
+      if (iv[2 * (g0 + t)] <= x) {
+        lo = t + 1;
+        break;
+      }
+      hi = t;
+    }
+  }
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
     if (iv[2 * (g0 + mid)] <= x) lo = mid + 1;
@@ -3774,27 +3805,27 @@ __device__ int64_t wave_nl_bwd(const FindParams& F, uint64_t S, uint64_t B, uint
 
 // Censored-buffer line breaks of file [fs, fs + n) with intervals (g0, m):
 // first '\n' at or after `from` (n if none) / start of the line holding pos.
-__device__ uint64_t cens_next_nl(const FindParams& F, uint64_t fs, uint64_t n, uint32_t g0, uint32_t m, uint64_t from,
-                                 uint32_t lane) {
+__device__ uint64_t cens_next_nl(const FindParams& F, uint64_t fs, uint64_t n, uint32_t g0, uint32_t m, uint32_t h,
+                                 uint64_t from, uint32_t lane) {
   while (from < n) {
     const uint64_t i = wave_nl_fwd(F, fs + from, fs + n, lane) - fs;
     if (i >= n) return n;
-    const int64_t h = censor_holder(F.iv, g0, m, i);
-    if (h < 0) return i;
-    from = F.iv[2 * h + 1];
+    const int64_t hold = censor_holder_near(F.iv, g0, m, i, h);
+    if (hold < 0) return i;
+    from = F.iv[2 * hold + 1];
   }
   return n;
 }
 
-__device__ uint64_t cens_line_begin(const FindParams& F, uint64_t fs, uint32_t g0, uint32_t m, uint64_t pos,
+__device__ uint64_t cens_line_begin(const FindParams& F, uint64_t fs, uint32_t g0, uint32_t m, uint32_t h, uint64_t pos,
                                     uint32_t lane) {
   while (pos) {
     const int64_t a = wave_nl_bwd(F, fs, fs + pos, lane);
     if (a < 0) return 0;
     const uint64_t i = (uint64_t)a - fs;
-    const int64_t h = censor_holder(F.iv, g0, m, i);
-    if (h < 0) return i + 1;
-    pos = F.iv[2 * h];
+    const int64_t hold = censor_holder_near(F.iv, g0, m, i, h);
+    if (hold < 0) return i + 1;
+    pos = F.iv[2 * hold];
   }
   return 0;
 }
@@ -3819,8 +3850,9 @@ __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
     // the (censored) line holding the start: the Match window's and the first
     // cause Code line's bounds, searched once (a search on a multi-MiB line
     // costs a binary search over the newline prefix)
-    const uint64_t ls0 = cens_line_begin(F, fs, g.x, g.y, L.start, lane);
-    const uint64_t le0 = cens_next_nl(F, fs, n, g.x, g.y, L.start, lane);
+    const uint32_t h = F.line_uid[w];  // the location's own interval (k_censor)
+    const uint64_t ls0 = cens_line_begin(F, fs, g.x, g.y, h, L.start, lane);
+    const uint64_t le0 = cens_next_nl(F, fs, n, g.x, g.y, h, L.start, lane);
     uint64_t ls = ls0, le = le0;
     if (le - ls > 100) {
       ls = L.start >= 30 ? L.start - 30 : 0;
@@ -3832,11 +3864,11 @@ __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
     const uint32_t sl = L.start_line - 1, el = L.end_line - 1;
     const uint32_t cs = sl >= 2 ? sl - 2 : 0, ce = el + 2;
     uint64_t p = ls0;
-    for (uint32_t cur = sl; cur > cs && p > 0; --cur) p = cens_line_begin(F, fs, g.x, g.y, p - 1, lane);
+    for (uint32_t cur = sl; cur > cs && p > 0; --cur) p = cens_line_begin(F, fs, g.x, g.y, h, p - 1, lane);
     uint32_t k = 0;
     bool found_first = false;
     for (uint32_t ln = cs; ln < ce && p <= n && k < kCodeLines; ++ln, ++k) {
-      const uint64_t q = p == ls0 ? le0 : cens_next_nl(F, fs, n, g.x, g.y, p, lane);
+      const uint64_t q = p == ls0 ? le0 : cens_next_nl(F, fs, n, g.x, g.y, h, p, lane);
       const bool cause = ln >= sl && ln <= el;
       if (lane == 0) {
         CodeRec c{};
@@ -4233,6 +4265,139 @@ struct DBuf {
     n = 0;
   }
 };
+
+// k_scan_big's LDS blob for automaton `ac` (BigDev layout) and its state
+// numbering; false when even one dense row does not fit.  Host only, so
+// tsg_ruleset_big_check can replay it on the CPU.
+struct BigBlobHost {
+  std::vector<uint8_t> blob;
+  std::vector<uint16_t> ac_of;  // blob state id -> automaton state id
+  uint32_t nd = 0, cold = 0, o_cold = 0, o_eval = 0;
+};
+static bool build_big_blob(const AcHost& ac, bool bfs, BigBlobHost* out) {
+  if (ac.fail.size() != ac.nstates || ac.nclasses > kBigMore || ac.nstates > 0x8000u || !ac.nstates) return false;
+  const uint32_t S = ac.nstates, K = ac.nclasses;
+  // blob numbering (the first nd states get the dense rows): breadth first,
+  // output states in place (the automaton's own numbering puts them last),
+  // and inside a depth the likelier labels first -- a label's probability
+  // under independent bytes of a text byte model (big_byte_weight), the
+  // parent's times the edge class's (a state is first reached from its trie
+  // parent).  Cold records read per byte, CPU replay of the stress corpora
+  // (tests/test_big_blob.py): 0.0149 / 0.0084 -> 0.0140 / 0.0072; by
+  // probability alone, 0.0181 / 0.0128.
+  std::vector<uint32_t> order(S), at(S);  // blob id -> automaton id, and back
+  for (uint32_t k = 0; k < S; ++k) order[k] = k;
+  if (!bfs) {
+    double wsum = 0;
+    for (int b = 0; b < 256; ++b) wsum += big_byte_weight((uint8_t)b);
+    std::vector<double> pc(K, 0.0);
+    for (int b = 0; b < 256; ++b) pc[ac.cls[b]] += big_byte_weight((uint8_t)b) / wsum;
+    std::vector<double> prob(S, -1.0);
+    std::vector<int> depth(S, 0);
+    std::vector<uint32_t> q{0};
+    prob[0] = 1.0;
+    for (size_t h = 0; h < q.size(); ++h) {
+      const uint32_t st = q[h];
+      for (uint32_t c = 0; c < K; ++c) {
+        const uint32_t t = ac.delta[(size_t)st * K + c] & 0x7FFFu;
+        if (prob[t] < 0) {
+          prob[t] = prob[st] * pc[c];
+          depth[t] = depth[st] + 1;
+          q.push_back(t);
+        }
+      }
+    }
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+      return depth[a] != depth[b] ? depth[a] < depth[b] : prob[a] > prob[b];
+    });
+    if (order[0] != 0) return false;  // (k_scan_big starts every lane in blob state 0)
+  }
+  for (uint32_t k = 0; k < S; ++k) at[order[k]] = k;
+  auto entry = [&](uint32_t st, uint32_t c) {  // delta in blob ids (bit 15 kept)
+    const uint16_t v = ac.delta[(size_t)st * K + c];
+    return (uint32_t)((v & 0x8000u) | at[v & 0x7FFFu]);
+  };
+  std::vector<std::vector<uint32_t>> edges(S);  // per blob state: class << 16 | entry where it differs from fail
+  for (uint32_t n = 1; n < S; ++n) {
+    const uint32_t st = order[n], f = ac.fail[st];
+    for (uint32_t c = 0; c < K; ++c)
+      if (ac.delta[(size_t)st * K + c] != ac.delta[(size_t)f * K + c]) edges[n].push_back((c << 16) | entry(st, c));
+  }
+  std::vector<uint64_t> suffix(S + 1, 0);  // list words of cold states >= s
+  for (uint32_t st = S; st-- > 0;) suffix[st] = suffix[st + 1] + (edges[st].size() > 2 ? edges[st].size() + 1 : 0);
+  auto a8 = [](uint64_t x) { return (x + 7) & ~7ull; };
+  auto bytes_for = [&](uint32_t nd) {
+    return a8(256 + (uint64_t)nd * K * 2) + (uint64_t)(S - nd) * 8 + suffix[nd] * 4;
+  };
+  if (bytes_for(1) > kBigLdsMax) return false;
+  uint32_t lo = 1, hi = S;  // a large nd with bytes_for(nd) <= kBigLdsMax (bytes mostly grow with nd)
+  {
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) / 2;
+      if (bytes_for(mid) <= kBigLdsMax) lo = mid;
+      else hi = mid - 1;
+    }
+    const uint32_t nd = lo, cold = S - nd;
+    std::vector<uint8_t> blob(bytes_for(nd), 0);
+    memcpy(blob.data(), ac.cls, 256);
+    uint16_t* dense = (uint16_t*)(blob.data() + 256);
+    for (uint32_t n = 0; n < nd; ++n)
+      for (uint32_t c = 0; c < K; ++c) dense[(size_t)n * K + c] = (uint16_t)entry(order[n], c);
+    const uint32_t o_cold = (uint32_t)a8(256 + (uint64_t)nd * K * 2);
+    const uint32_t o_eval = o_cold + cold * 8;
+    uint32_t* rec = (uint32_t*)(blob.data() + o_cold);
+    uint32_t* ev = (uint32_t*)(blob.data() + o_eval);
+    uint32_t k = 0;
+    for (uint32_t j = 0; j < cold; ++j) {
+      const std::vector<uint32_t>& E = edges[nd + j];
+      const uint32_t fl = at[ac.fail[order[nd + j]]];
+      if (E.size() <= 2) {
+        const uint32_t c1 = E.size() > 0 ? E[0] >> 16 : kBigNone, c2 = E.size() > 1 ? E[1] >> 16 : kBigNone;
+        const uint32_t n1 = E.size() > 0 ? E[0] & 0xFFFFu : 0, n2 = E.size() > 1 ? E[1] & 0xFFFFu : 0;
+        rec[2 * j] = c1 | c2 << 8 | n1 << 16;
+        rec[2 * j + 1] = n2 | fl << 16;
+      } else {
+        rec[2 * j] = kBigMore | kBigMore << 8 | (k & 0xFFFFu) << 16;
+        rec[2 * j + 1] = (k >> 16) | fl << 16;
+        for (uint32_t v : E) ev[k++] = v;
+        ev[k++] = 0xFFFFFFFFu;
+      }
+    }
+    out->ac_of.assign(S, 0);
+    for (uint32_t n = 0; n < S; ++n) out->ac_of[n] = (uint16_t)order[n];
+    out->blob.swap(blob);
+    out->nd = nd;
+    out->cold = cold;
+    out->o_cold = o_cold;
+    out->o_eval = o_eval;
+  }
+  return true;
+}
+
+// big_next on the host copy of the blob (the device walk, for the CPU check);
+// *hops = cold records read.
+static uint32_t big_next_host(const BigBlobHost& bb, uint32_t K, uint32_t st, uint32_t c, uint32_t* hops) {
+  const uint16_t* dense = (const uint16_t*)(bb.blob.data() + 256);
+  const uint32_t* rec = (const uint32_t*)(bb.blob.data() + bb.o_cold);
+  const uint32_t* ev = (const uint32_t*)(bb.blob.data() + bb.o_eval);
+  const size_t n_ev = (bb.blob.size() - bb.o_eval) / 4;
+  while (st >= bb.nd) {
+    if (++*hops > 64) return 0xFFFFFFFFu;  // (a cycle: the device would hang)
+    const uint32_t x = rec[2 * (st - bb.nd)], y = rec[2 * (st - bb.nd) + 1];
+    if (c == (x & 0xFFu)) return x >> 16;
+    if (c == ((x >> 8) & 0xFFu)) return y & 0xFFFFu;
+    if ((x & 0xFFu) == kBigMore) {
+      for (size_t k = (x >> 16) | (y << 16);; ++k) {
+        if (k >= n_ev) return 0xFFFFFFFEu;  // (list runs off the blob)
+        const uint32_t v = ev[k];
+        if (v == 0xFFFFFFFFu) break;
+        if ((v >> 16) == c) return v & 0xFFFFu;
+      }
+    }
+    st = y >> 16;
+  }
+  return dense[st * K + c];
+}
 
 struct DevImage {
   uint64_t rs_id = 0;
@@ -4665,95 +4830,14 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   // k_scan_big blob: only for an automaton that neither k_scan_fast's image
   // nor an LDS table holds (see BigDev); the most dense rows that fit
   im.big_view = BigDev{};
-  if (ac.fast.empty() && (size_t)ac.nstates * ac.nclasses * 2 > (size_t)kLdsTableMax && ac.fail.size() == ac.nstates &&
-      ac.nclasses <= kBigMore && ac.nstates <= 0x8000u) {
-    const uint32_t S = ac.nstates, K = ac.nclasses;
-    // blob numbering: the states text is likeliest to hold first (they get the
-    // dense rows).  A state's weight is the probability of its label under
-    // independent bytes of a text byte model (big_byte_weight); the label
-    // probability is the parent's times the edge class's, walked breadth
-    // first (a state is first reached from its trie parent).  The automaton's
-    // own numbering (breadth first, output states last) left the output and
-    // deep-but-common states cold.
-    std::vector<uint32_t> order(S), at(S);  // blob id -> automaton id, and back
-    for (uint32_t k = 0; k < S; ++k) order[k] = k;
-    if (!experiment_env("TSG_BIG_BFS")) {
-      std::vector<double> pc(K, 0.0);
-      for (int b = 0; b < 256; ++b) pc[ac.cls[b]] += big_byte_weight((uint8_t)b);
-      std::vector<double> P(S, -1.0);
-      std::vector<uint32_t> q{0};
-      P[0] = 2.0;  // (the root first)
-      for (size_t h = 0; h < q.size(); ++h) {
-        const uint32_t st = q[h];
-        for (uint32_t c = 0; c < K; ++c) {
-          const uint32_t t = ac.delta[(size_t)st * K + c] & 0x7FFFu;
-          if (P[t] < 0) {
-            P[t] = (st ? P[st] : 1.0) * pc[c];
-            q.push_back(t);
-          }
-        }
-      }
-      for (uint32_t k = 0; k < S; ++k)
-        if (P[k] < 0) P[k] = 0;  // (unreachable: none)
-      std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return P[a] > P[b]; });
-    }
-    for (uint32_t k = 0; k < S; ++k) at[order[k]] = k;
-    auto entry = [&](uint32_t st, uint32_t c) {  // delta in blob ids (bit 15 kept)
-      const uint16_t v = ac.delta[(size_t)st * K + c];
-      return (uint32_t)((v & 0x8000u) | at[v & 0x7FFFu]);
-    };
-    std::vector<std::vector<uint32_t>> edges(S);  // per blob state: class << 16 | entry where it differs from fail
-    for (uint32_t n = 1; n < S; ++n) {
-      const uint32_t st = order[n], f = ac.fail[st];
-      for (uint32_t c = 0; c < K; ++c)
-        if (ac.delta[(size_t)st * K + c] != ac.delta[(size_t)f * K + c]) edges[n].push_back((c << 16) | entry(st, c));
-    }
-    std::vector<uint64_t> suffix(S + 1, 0);  // list words of cold states >= s
-    for (uint32_t st = S; st-- > 0;) suffix[st] = suffix[st + 1] + (edges[st].size() > 2 ? edges[st].size() + 1 : 0);
-    auto a8 = [](uint64_t x) { return (x + 7) & ~7ull; };
-    auto bytes_for = [&](uint32_t nd) {
-      return a8(256 + (uint64_t)nd * K * 2) + (uint64_t)(S - nd) * 8 + suffix[nd] * 4;
-    };
-    uint32_t lo = 1, hi = S;  // largest nd with bytes_for(nd) <= kBigLdsMax (bytes grow with nd)
-    if (bytes_for(1) <= kBigLdsMax) {
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) / 2;
-        if (bytes_for(mid) <= kBigLdsMax) lo = mid;
-        else hi = mid - 1;
-      }
-      const uint32_t nd = lo, cold = S - nd;
-      std::vector<uint8_t> blob(bytes_for(nd), 0);
-      memcpy(blob.data(), ac.cls, 256);
-      uint16_t* dense = (uint16_t*)(blob.data() + 256);
-      for (uint32_t n = 0; n < nd; ++n)
-        for (uint32_t c = 0; c < K; ++c) dense[(size_t)n * K + c] = (uint16_t)entry(order[n], c);
-      const uint32_t o_cold = (uint32_t)a8(256 + (uint64_t)nd * K * 2);
-      const uint32_t o_eval = o_cold + cold * 8;
-      uint32_t* rec = (uint32_t*)(blob.data() + o_cold);
-      uint32_t* ev = (uint32_t*)(blob.data() + o_eval);
-      uint32_t k = 0;
-      for (uint32_t j = 0; j < cold; ++j) {
-        const std::vector<uint32_t>& E = edges[nd + j];
-        const uint32_t fl = at[ac.fail[order[nd + j]]];
-        if (E.size() <= 2) {
-          const uint32_t c1 = E.size() > 0 ? E[0] >> 16 : kBigNone, c2 = E.size() > 1 ? E[1] >> 16 : kBigNone;
-          const uint32_t n1 = E.size() > 0 ? E[0] & 0xFFFFu : 0, n2 = E.size() > 1 ? E[1] & 0xFFFFu : 0;
-          rec[2 * j] = c1 | c2 << 8 | n1 << 16;
-          rec[2 * j + 1] = n2 | fl << 16;
-        } else {
-          rec[2 * j] = kBigMore | kBigMore << 8 | (k & 0xFFFFu) << 16;
-          rec[2 * j + 1] = (k >> 16) | fl << 16;
-          for (uint32_t v : E) ev[k++] = v;
-          ev[k++] = 0xFFFFFFFFu;
-        }
-      }
-      std::vector<uint16_t> ac_of(S);
-      for (uint32_t n = 0; n < S; ++n) ac_of[n] = (uint16_t)order[n];
-      HIP_TRY(im.big.ensure(blob.size()));
-      HIP_TRY(hipMemcpy(im.big.p, blob.data(), blob.size(), hipMemcpyHostToDevice));
-      HIP_TRY(im.big_ac_of.ensure(S));
-      HIP_TRY(hipMemcpy(im.big_ac_of.p, ac_of.data(), S * 2, hipMemcpyHostToDevice));
-      im.big_view = BigDev{im.big.p, (uint32_t)blob.size(), nd, cold, o_cold, o_eval, im.big_ac_of.p};
+  if (ac.fast.empty() && (size_t)ac.nstates * ac.nclasses * 2 > (size_t)kLdsTableMax) {
+    BigBlobHost bb;
+    if (build_big_blob(ac, experiment_env("TSG_BIG_BFS") != nullptr, &bb)) {
+      HIP_TRY(im.big.ensure(bb.blob.size()));
+      HIP_TRY(hipMemcpy(im.big.p, bb.blob.data(), bb.blob.size(), hipMemcpyHostToDevice));
+      HIP_TRY(im.big_ac_of.ensure(bb.ac_of.size()));
+      HIP_TRY(hipMemcpy(im.big_ac_of.p, bb.ac_of.data(), bb.ac_of.size() * 2, hipMemcpyHostToDevice));
+      im.big_view = BigDev{im.big.p, (uint32_t)bb.blob.size(), bb.nd, bb.cold, bb.o_cold, bb.o_eval, im.big_ac_of.p};
     }
   }
   HIP_TRY(im.out_off.ensure(ac.out_off.size()));
@@ -5498,6 +5582,38 @@ void order_finding_ties(ResultImpl& R, bool all_runs) {
       for (size_t k; (k = next.fetch_add(1)) < runs.size();) sort_run(runs[k]);
     });
   for (auto& t : th) t.join();
+}
+
+// CPU replay of k_scan_big's walk (test hook): the text through the
+// automaton's own table and through the LDS blob's dense rows / cold records
+// (breadth-first or frequency numbering) must visit the same states with the
+// same output bits.
+extern "C" int tsg_ruleset_big_check(const tsg_ruleset* rs, const uint8_t* text, size_t len, int bfs,
+                                     uint64_t* mismatches, uint64_t* cold_hops, uint32_t* n_dense) {
+  if (!rs || (!text && len) || !mismatches || !cold_hops || !n_dense) return TSG_ERR_INVALID_ARG;
+  const AcHost& ac = rs->ac;
+  BigBlobHost bb;
+  *mismatches = *cold_hops = 0;
+  *n_dense = 0;
+  if (!build_big_blob(ac, bfs != 0, &bb)) return TSG_ERR_UNSUPPORTED;
+  *n_dense = bb.nd;
+  const uint32_t K = ac.nclasses;
+  uint32_t a = 0, b = 0;  // automaton state, blob state
+  for (size_t i = 0; i < len; ++i) {
+    const uint32_t c = ac.cls[text[i]];
+    const uint32_t va = ac.delta[(size_t)a * K + c];
+    uint32_t hops = 0;
+    const uint32_t vb = big_next_host(bb, K, b, c, &hops);
+    *cold_hops += hops;
+    if (vb >= 0xFFFFFFFEu || (vb & 0x8000u) != (va & 0x8000u) || bb.ac_of[vb & 0x7FFFu] != (va & 0x7FFFu)) {
+      ++*mismatches;
+      a = b = 0;  // resynchronise
+      continue;
+    }
+    a = va & 0x7FFFu;
+    b = vb & 0x7FFFu;
+  }
+  return TSG_OK;
 }
 
 // ------------------------------------------------- byte-range split (§8(e)) --
