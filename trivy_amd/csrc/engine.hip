@@ -783,7 +783,10 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
 // wave's segment) that k_big_report replays -- no per-byte output branch, no
 // global atomics, newlines counted SWAR and stored once per span.
 constexpr uint32_t kBigThreads = 1024;
-constexpr int kBigMode = 0, kBigChains = 1;  // k_scan_big's product shape
+// k_scan_big's product shape (tools/big_ab.sh, profiles/r03l): two chains
+// per lane, each with a 2 x 16-byte ring, every chain's dense row read issued
+// before any cold walk -- 8.87 vs 9.63 ms (one chain, 8 x 16 B) on configs[4]
+constexpr int kBigMode = 8, kBigChains = 2, kBigRing = 2;
 constexpr uint32_t kBigLdsMax = 152 * 1024;
 
 struct BigLds {
@@ -4498,7 +4501,7 @@ struct tsg_engine {
   hipEvent_t ev[12];
   bool events = false;
   hipStream_t side = nullptr;  // D2H of the findings' Code records and strings under the last sorts
-  hipEvent_t ev_fill = nullptr, ev_side = nullptr;
+  hipEvent_t ev_code = nullptr, ev_fill = nullptr, ev_side = nullptr;
   DBuf<uint32_t> gate_out, gate_rules;  // tsg_gate_device: rule gate words, rule -> keyword-id CSR
   // tsg_analyze: IsBinary flags, '\r'-stripped batch and its offsets, block sums, chunk positions
   DBuf<uint8_t> bin8, strip_out;
@@ -5237,10 +5240,10 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     HIP_TRY(e->span_hi.ensure(units + 1));
     P.span_hi = e->span_hi.p;
     // one unit per lane: CH spans (kBigChains)
-    const void* big_fn = (const void*)k_scan_big<kBigMode, kBigChains>;
+    const void* big_fn = (const void*)k_scan_big<kBigMode, kBigChains, kBigRing>;
     int big_mode = kBigMode, big_ch = kBigChains;
 #ifdef TSG_EXPERIMENTS
-    int big_v = 8;
+    int big_v = kBigRing;
     if (const char* v = getenv("TSG_BIG_VARIANT")) {  // "<mode>[x<chains>][v<ring uint4s>]"
       big_mode = atoi(v);
       big_ch = strchr(v, 'x') ? atoi(strchr(v, 'x') + 1) : 1;
@@ -5435,15 +5438,10 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   HIP_TRY(e->f_gcarry.ensure(gran_blocks + 1));
   F.gran_seg = e->f_gran.p;
   F.gran_carry = e->f_gcarry.p;
-  if (c.find_bytes) {
-    HIP_TRY(hipMemsetAsync(F.gran_seg, 0, F.n_gran * 4, s));
-    hipLaunchKernelGGL(k_arena_gran_mark, dim3((uint32_t)((n_seg + 255) / 256)), dim3(256), 0, s, F);
-    hipLaunchKernelGGL(k_arena_gran_scan, dim3(gran_blocks), dim3(1024), 0, s, F);
-    hipLaunchKernelGGL(k_arena_gran_carry, dim3(1), dim3(1024), 0, s, F, gran_blocks);
-  }
-  // the result's page-locked block, laid out now: the Code records and the
-  // string arena are final once k_arena_fill ends, so their D2H (most of the
-  // bytes) runs on a side stream under the Match sorts below
+  // the result's page-locked block, laid out now.  The Code records and the
+  // kept locations are final already: their D2H starts on a side stream under
+  // the arena fill; the string arena's (most of the bytes) follows it there,
+  // under the Match sorts
   auto& R = res->impl;
   const uint64_t tie_cap = std::max<uint64_t>(1024, n_locs / 8);
   const size_t rec_bytes = n_locs * sizeof(FindRec), code_bytes = n_slots * sizeof(CodeRec);
@@ -5464,18 +5462,31 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   R.file_flags = {base + o_flags, n_files};
   R.ties = {(uint32_t*)(base + o_ties), 0};
   R.ctrl_off = o_ctrl;
-  if (c.find_bytes)
-    hipLaunchKernelGGL(k_arena_fill, dim3((uint32_t)std::min<uint64_t>((c.find_bytes / 16 + 255) / 256 + 1, 8192)),
-                       dim3(256), 0, s, F);
-  HIP_TRY(hipGetLastError());
   if (!e->side) {
     HIP_TRY(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&e->ev_code, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&e->ev_fill, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&e->ev_side, hipEventDisableTiming));
   }
+  // the kept locations as tsg_loc records
+  HIP_TRY(e->out_locs.ensure(n_locs));
+  hipLaunchKernelGGL(k_out_locs, dim3(lane_blocks), dim3(256), 0, s, e->locs2.p, n_locs, e->out_locs.p, e->ctrl.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(e->ev_code, s));
+  HIP_TRY(hipStreamWaitEvent(e->side, e->ev_code, 0));
+  HIP_TRY(hipMemcpyAsync(R.code.p, e->f_code.p, code_bytes, hipMemcpyDeviceToHost, e->side));
+  HIP_TRY(hipMemcpyAsync(R.locs.p, e->out_locs.p, n_locs * sizeof(tsg_loc), hipMemcpyDeviceToHost, e->side));
+  if (c.find_bytes) {
+    HIP_TRY(hipMemsetAsync(F.gran_seg, 0, F.n_gran * 4, s));
+    hipLaunchKernelGGL(k_arena_gran_mark, dim3((uint32_t)((n_seg + 255) / 256)), dim3(256), 0, s, F);
+    hipLaunchKernelGGL(k_arena_gran_scan, dim3(gran_blocks), dim3(1024), 0, s, F);
+    hipLaunchKernelGGL(k_arena_gran_carry, dim3(1), dim3(1024), 0, s, F, gran_blocks);
+    hipLaunchKernelGGL(k_arena_fill, dim3((uint32_t)std::min<uint64_t>((c.find_bytes / 16 + 255) / 256 + 1, 8192)),
+                       dim3(256), 0, s, F);
+  }
+  HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(e->ev_fill, s));
   HIP_TRY(hipStreamWaitEvent(e->side, e->ev_fill, 0));
-  HIP_TRY(hipMemcpyAsync(R.code.p, e->f_code.p, code_bytes, hipMemcpyDeviceToHost, e->side));
   if (c.find_bytes)
     HIP_TRY(hipMemcpyAsync(base + rec_bytes + code_bytes, e->f_arena.p, c.find_bytes, hipMemcpyDeviceToHost, e->side));
   HIP_TRY(hipEventRecord(e->ev_side, e->side));
@@ -5506,12 +5517,7 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   hipLaunchKernelGGL(k_tie_list, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lkey.p, e->f_lkeyb.p, e->vals2.p,
                      n_locs, e->f_ties.p, tie_cap, e->ctrl.p);
   HIP_TRY(hipGetLastError());
-  // the kept locations as tsg_loc records
-  HIP_TRY(e->out_locs.ensure(n_locs));
-  hipLaunchKernelGGL(k_out_locs, dim3(lane_blocks), dim3(256), 0, s, e->locs2.p, n_locs, e->out_locs.p, e->ctrl.p);
-  HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(R.frec.p, e->f_rec2.p, rec_bytes, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(R.locs.p, e->out_locs.p, n_locs * sizeof(tsg_loc), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(R.ties.p, e->f_ties.p, tie_cap * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamWaitEvent(s, e->ev_side, 0));  // the caller's final synchronisation covers the side copies
   R.ties_cap = tie_cap;
@@ -6218,6 +6224,19 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
       for (uint32_t q = 0; q < n_jobs; ++q) idx[q] = q;
       std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return end(a) > end(b); });
       fprintf(stderr, "[verify] kernel span %.3f ms\n", (end(idx[0]) - tmin) / 1e5);
+      {  // job end times and durations by percentile (a tail-bound kernel ends late for a few jobs)
+        std::vector<uint64_t> ends(n_jobs), durs(n_jobs);
+        for (uint32_t q = 0; q < n_jobs; ++q) {
+          ends[q] = end(q) - tmin;
+          durs[q] = dur(q);
+        }
+        std::sort(ends.begin(), ends.end());
+        std::sort(durs.begin(), durs.end());
+        auto pct = [&](const std::vector<uint64_t>& v, double f) { return v[std::min<size_t>(v.size() - 1, (size_t)(f * v.size()))] / 1e5; };
+        fprintf(stderr, "[verify] job ends p50 %.3f p90 %.3f p99 %.3f p99.9 %.3f max %.3f ms; durations p50 %.3f p90 %.3f p99 %.3f max %.3f ms\n",
+                pct(ends, 0.5), pct(ends, 0.9), pct(ends, 0.99), pct(ends, 0.999), ends.back() / 1e5, pct(durs, 0.5),
+                pct(durs, 0.9), pct(durs, 0.99), durs.back() / 1e5);
+      }
       for (uint32_t q = 0; q < std::min<uint32_t>(16, n_jobs); ++q) {
         const uint32_t jq = idx[q];
         const uint64_t c0 = hjs[jq], c1 = jq + 1 < n_jobs ? hjs[jq + 1] : n_cands;
@@ -6594,6 +6613,7 @@ void tsg_engine_free(tsg_engine* e) {
     for (auto& ev : e->ev) (void)hipEventDestroy(ev);
   if (e->side) {
     (void)hipStreamSynchronize(e->side);
+    (void)hipEventDestroy(e->ev_code);
     (void)hipEventDestroy(e->ev_fill);
     (void)hipEventDestroy(e->ev_side);
     (void)hipStreamDestroy(e->side);
