@@ -117,7 +117,7 @@ def test_stress_1000_rules_vs_oracle(stress_cfg):
 
 
 def test_stress_entry_points_agree(stress_cfg):
-    """The big-automaton path (k_scan_big + k_big_report) through the three
+    """The big-automaton path (k_scan_big + k_big_walk + k_big_resolve) through the three
     entry points -- host batch (tsg_scan), batch already in HBM
     (tsg_scan_device) and the analyzer front end on CR-free files
     (tsg_analyze) -- gives identical findings, Match and Code included, in

@@ -773,14 +773,14 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
 }
 
 // Scan with an automaton too large for k_scan_fast's image (configs[4]: 1000+
-// custom rules), in k_scan_fast's shape: one 4 KiB span per lane (7 bytes of
-// warm-up), the span streamed through a 128-byte register ring, 1024 threads
-// and ONE LDS copy of the automaton per CU (BigDev: byte classes, dense rows of
-// the shallowest states, sparse rows + failure links for the rest).  The byte
+// custom rules), in k_scan_fast's shape: 4 KiB spans (7 bytes of warm-up)
+// streamed through register rings, 1024 threads and ONE LDS copy of the
+// automaton per CU (BigDev: byte classes, dense rows of the first states,
+// 8-byte cold-state records + failure links for the rest).  The byte
 // class lookups do not depend on the state, so only the row lookup sits on the
 // dependent chain.  Outputs: entries carry bit 15; the OR over an 8-byte group
 // flags it, and a flagged group becomes a FastEvent (ballot/popcount into the
-// wave's segment) that k_big_report replays -- no per-byte output branch, no
+// wave's segment) that k_big_walk replays -- no per-byte output branch, no
 // global atomics, newlines counted SWAR and stored once per span.
 constexpr uint32_t kBigThreads = 1024;
 // k_scan_big's product shape (tools/big_ab.sh, profiles/r03l): two chains
@@ -1055,7 +1055,7 @@ __device__ inline uint32_t block_incl_sum32(uint32_t v, uint32_t* lds16, uint32_
   return v + before;
 }
 
-// k_big_report, part 1: each event's 8-byte group is replayed from its entry
+// Event resolution, part 1 (k_big_walk): each event's 8-byte group is replayed from its entry
 // state (blob in LDS) and every output state reached becomes one record
 // (position << 16 | state) in P.big_outs -- one block-wide prefix sum and one
 // global reservation (Ctrl::outputs) per 1024 events.  Only LDS work: the
@@ -1116,7 +1116,7 @@ __global__ __launch_bounds__(1024) void k_big_walk(ScanParams P, uint32_t n_wave
   }
 }
 
-// k_big_report, part 2: one output record per lane (grid-stride), resolved by
+// Event resolution, part 2 (k_big_resolve): one output record per lane (grid-stride), resolved by
 // report_t (file lookup, truncated-literal and case checks on the real bytes,
 // keyword gate bits, anchor hits); hits staged in LDS, one global
 // reservation per block round.
