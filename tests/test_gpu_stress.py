@@ -133,3 +133,27 @@ def test_stress_entry_points_agree(stress_cfg):
     assert [_plain(g) for g in dev] == [_plain(w) for w in want]
     assert [_plain(g) for g in ana if g is not None] == [_plain(w) for w, g in zip(want, ana) if g is not None]
     assert sum(len(w.Findings) for w in want) > 50
+
+
+@pytest.mark.parametrize("n_bytes", [0, 9, 4095, 4096, 4097, 3 * 4096 + 17, 5 * 4096, 9 * 4096 + 4095])
+def test_big_walk_span_counts_vs_oracle(stress_cfg, n_bytes):
+    """k_scan_big walks two consecutive 4 KiB spans per lane (the second chain
+    idle past the last span, the batch tail read from the padded copy):
+    batches of an odd and even span count, shorter than one span, and exactly
+    on span boundaries, with rule instances straddling each boundary, equal
+    the oracle's findings."""
+    path, rules = stress_cfg
+    rng = __import__("random").Random(n_bytes)
+    gens = [g for _, g in rules if g is not None]
+    body = bytearray()
+    while len(body) < n_bytes:
+        body += b"x" * rng.randrange(1, 40) + b" " + gens[rng.randrange(len(gens))](rng).encode() + b"\n"
+    body = bytes(body[:n_bytes])
+    # a second file so the boundary also falls inside a file; an empty file last
+    half = n_bytes // 2
+    files = [("a/one.env", body[:half]), ("b/two.txt", body[half:]), ("c/empty.cfg", b"")]
+    sc_o = o.Scanner(o.parse_config(path))
+    sc_g = S.new_scanner(S.parse_config(path), device=0)
+    got = sc_g.scan_batch_device([S.ScanArgs(p, d) for p, d in files])
+    for (p, d), g in zip(files, got):
+        assert _canon(_plain(g)) == _canon(_oracle_plain(sc_o.scan(p, d))), p
