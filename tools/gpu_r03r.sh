@@ -1,0 +1,15 @@
+#!/bin/bash
+# r03r: GPU suite (incl. the big-walk span-count cases), configs[2] line +
+# timeline (k_report segments claimed dynamically, follow/precede filters on 16-byte loads), configs[4] line.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread > gpurun_out/pytest_r03r.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_r03r.log; exit 1; }
+tail -2 gpurun_out/pytest_r03r.log
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > gpurun_out/bench_c2_r03r.log 2>&1 || { echo "bench c2 failed"; tail -20 gpurun_out/bench_c2_r03r.log; exit 1; }
+tail -1 gpurun_out/bench_c2_r03r.log | cut -c1-1500
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/c2r -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu --no-parity > gpurun_out/c2r.log 2>&1 || { echo "c2 trace failed"; tail -20 gpurun_out/c2r.log; exit 1; }
+python3 tools/timeline.py gpurun_out/c2r/run_kernel_trace.csv k_scan_fast 12 > gpurun_out/c2r/timeline.txt
+awk '$2>0.05 || $3>0.05' gpurun_out/c2r/timeline.txt
+timeout -k 10 300 python -u bench.py --config 4 --steps 5 --warmup 2 > gpurun_out/bench_c4_r03r.log 2>&1 || { echo "bench c4 failed"; tail -20 gpurun_out/bench_c4_r03r.log; exit 1; }
+tail -1 gpurun_out/bench_c4_r03r.log | cut -c1-900

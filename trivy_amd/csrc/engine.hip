@@ -99,6 +99,7 @@ struct Ctrl {
   unsigned long long n_fold;     // fold-special rune occurrences recorded (ScanParams::fold_pos)
   unsigned long long events;     // k_scan_fast events in the wave segments (diagnostics, summed by k_report)
   unsigned long long find_bytes; // string arena bytes of the findings (k_find_copy)
+  unsigned long long rep_next;   // k_report: next wave segment to claim
   unsigned long long n_caps;     // matches whose secret-group spans k_captures resolves
   unsigned long long n_caps_big; // ... and those too long for its arenas (k_captures_big)
   unsigned long long long_files; // files longer than kMaxVerifyFile (k_region_mark)
@@ -1386,7 +1387,16 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
   const uint32_t out_e = ac.fast_out_entry;
   uint32_t my_out = 0;
   uint64_t last_kw = ~0ull;
-  for (uint32_t w = blockIdx.x; w < n_waves + 1; w += gridDim.x) {
+  // wave segments claimed one at a time from a global counter: their event
+  // counts differ by text (a static block-strided assignment waits on the
+  // block that drew the keyword-dense segments)
+  __shared__ uint32_t s_w;
+  for (;;) {
+    if (threadIdx.x == 0) s_w = (uint32_t)atomicAdd(&P.ctrl->rep_next, 1ull);
+    __syncthreads();
+    const uint32_t w = s_w;
+    __syncthreads();
+    if (w >= n_waves + 1) break;
     const FastEvent* seg;
     uint64_t n;
     if (w < n_waves) {
@@ -1430,17 +1440,25 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
               if (fi == 0xFFFFFFFFu) fi = (P.report_mode & 1) ? (uint32_t)((pos >> 12) % P.n_files) : file_of_pos(P, pos);
               const uint64_t fend = P.off[fi + 1] - 1;
               if (start + pd.len > fend) continue;
-              bool ok = true;
+              // chunks of 8 batch bytes issued before any compare (one memory
+              // latency per chunk; a byte-by-byte early-exit loop was a chain of
+              // dependent loads that held the whole lock-step round)
+              uint32_t bad = 0, req_bad = 0;
               const uint8_t* pb = pbytes + pd.bytes_off;
-              for (uint32_t k = tl; k < pd.len && ok; ++k) {
-                const uint8_t b = P.data[start + k];
-                ok = lower_ascii(b) == pb[k];
-                if (want_hit && pd.confirm) {
-                  const uint8_t r = pbytes[pd.req_off + k];
-                  want_hit = r == 0 || b == r;
-                }
+              for (uint32_t k0 = tl; k0 < pd.len && !bad; k0 += 8) {
+#pragma unroll
+                for (uint32_t k = k0; k < k0 + 8; ++k)
+                  if (k < pd.len) {
+                    const uint8_t b = P.data[start + k];
+                    bad |= lower_ascii(b) ^ pb[k];
+                    if (want_hit && pd.confirm) {
+                      const uint8_t r = pbytes[pd.req_off + k];
+                      req_bad |= (r != 0) & (b != r);
+                    }
+                  }
               }
-              if (!ok) continue;
+              if (bad) continue;
+              if (req_bad) want_hit = false;
             }
             ++my_out;
             if (want_kw) {
@@ -2095,6 +2113,27 @@ __device__ inline bool rule_gate(const RuleSetDev& rs, const RuleDev& r, const u
   return false;
 }
 
+// The text of a job read in aligned 16-byte blocks (one dwordx4 load per
+// block; the batch is padded past its end), for the NFA walk's byte stream.
+struct VecText {
+  const uint8_t* base;
+  uintptr_t blk;
+  u32x4 v;
+  __device__ explicit VecText(const uint8_t* b) : base(b), blk(~(uintptr_t)0), v{0, 0, 0, 0} {}
+  template <class Pos>
+  __device__ uint32_t operator[](Pos i) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(base) + i;
+    const uintptr_t b = a & ~(uintptr_t)15;
+    if (b != blk) {
+      blk = b;
+      v = *as_global<__attribute__((address_space(1))) const u32x4>(reinterpret_cast<const void*>(b));
+    }
+    const uint32_t o = (uint32_t)(a & 15);
+    const uint32_t wd = o < 8 ? (o < 4 ? v.x : v.y) : (o < 12 ? v.z : v.w);  // no dynamically indexed array
+    return (wd >> (8 * (o & 3))) & 0xFFu;
+  }
+};
+
 // Candidate filter (follow.cpp): may a match of rule `rd` contain the anchor
 // hit at text[h]?  false only when provably not.
 __device__ inline bool follow_accepts_dev(const RuleSetDev& rs, const RuleDev& rd, const uint8_t* data, uint64_t h,
@@ -2104,9 +2143,10 @@ __device__ inline bool follow_accepts_dev(const RuleSetDev& rs, const RuleDev& r
   const uint8_t* cls = rs.follow_cls + rd.follow_cls_off;
   const uint32_t K = rd.follow_ncls;
   uint32_t st = 2;
+  VecText D(data);  // (16 bytes per load: only the table walk is a dependent chain)
   for (uint32_t i = 0; i < kFollowDepth; ++i) {
     if (h + i >= fend) return false;
-    const uint8_t c = data[h + i];
+    const uint32_t c = D[h + i];
     if (c >= 0x80) return true;
     st = T[st * K + cls[c]];
     if (st < 2) return st == 1;
@@ -2127,8 +2167,9 @@ __device__ inline bool precede_accepts_dev(const RuleDev& rd, const uint8_t* dat
   if (a == 0) return true;
   if (h - fstart < a) return false;
   const uint32_t k = a < kPrecedeMax ? a : kPrecedeMax;
+  VecText D(data);
   for (uint32_t i = 1; i <= k; ++i) {
-    const uint8_t c = data[h - i];
+    const uint32_t c = D[h - i];
     if (!((rd.alpha[c >> 6] >> (c & 63)) & 1)) return false;
   }
   return true;
@@ -2283,26 +2324,6 @@ struct VerifyParams {
   uint64_t redo_cap;
 };
 
-// The text of a job read in aligned 16-byte blocks (one dwordx4 load per
-// block; the batch is padded past its end), for the NFA walk's byte stream.
-struct VecText {
-  const uint8_t* base;
-  uintptr_t blk;
-  u32x4 v;
-  __device__ explicit VecText(const uint8_t* b) : base(b), blk(~(uintptr_t)0), v{0, 0, 0, 0} {}
-  template <class Pos>
-  __device__ uint32_t operator[](Pos i) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(base) + i;
-    const uintptr_t b = a & ~(uintptr_t)15;
-    if (b != blk) {
-      blk = b;
-      v = *as_global<__attribute__((address_space(1))) const u32x4>(reinterpret_cast<const void*>(b));
-    }
-    const uint32_t o = (uint32_t)(a & 15);
-    const uint32_t wd = o < 8 ? (o < 4 ? v.x : v.y) : (o < 12 ? v.z : v.w);  // no dynamically indexed array
-    return (wd >> (8 * (o & 3))) & 0xFFu;
-  }
-};
 
 // Candidate start windows of one (file, rule) job, in increasing order
 // (DESIGN.md "anchor windows").
