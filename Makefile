@@ -10,7 +10,7 @@ LIB      = trivy_amd/libtrivy_secret_gpu.so
 
 HOST_SRCS = $(SRC_DIR)/gre.cpp $(SRC_DIR)/ruleset.cpp $(SRC_DIR)/follow.cpp $(SRC_DIR)/dfa.cpp $(SRC_DIR)/nfa.cpp $(SRC_DIR)/layertar.cpp
 HIP_SRCS  = $(SRC_DIR)/engine.hip
-HDRS      = $(wildcard $(SRC_DIR)/*.h) include/trivy_secret_gpu.h
+HDRS      = $(wildcard $(SRC_DIR)/*.h) $(wildcard include/*.h)
 
 OBJS = $(patsubst $(SRC_DIR)/%.cpp,$(BUILD)/%.o,$(HOST_SRCS)) $(patsubst $(SRC_DIR)/%.hip,$(BUILD)/%.o,$(HIP_SRCS))
 

@@ -395,9 +395,9 @@ def traffic_bytes(content_bytes, kernel="k_scan_fast"):
     content bytes when the profiled corpus differs.  None without a profile."""
     p = os.path.join(ROOT, "profiles", f"traffic_{kernel}.json")
     if not os.path.exists(p):
-        return None
+        return None, None
     t = json.load(open(p))
-    return round(t["hbm_read_bytes_per_launch"] * content_bytes / t["algorithmic_bytes_per_launch"])
+    return round(t["hbm_read_bytes_per_launch"] * content_bytes / t["algorithmic_bytes_per_launch"]), t["source"]
 
 
 def physical_cores():
@@ -865,6 +865,7 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     value = total_all * args.steps / dt / 1e9
     scan_kernel_ms = float(np.mean(scan_ms))
+    traffic = traffic_bytes(c["total"], scan_kernel) if args.config in (2, 4) else (None, None)
     achieved = c["total"] / (scan_kernel_ms / 1e3) / 1e9
     parity = None
     if rank == 0 and not args.no_parity:
@@ -908,7 +909,7 @@ def main():
             "pct_hbm_peak": round(100.0 * value / (HBM_PEAK_GBPS * world), 2),
             "roofline": {"bound": "hbm", "kernel": scan_kernel, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic_bytes(c["total"], scan_kernel) if args.config in (2, 4) else None,
+                         "traffic": traffic[0], "traffic_source": traffic[1],
                          "algorithmic_bytes_per_launch": c["total"],
                          "avg_launch_ms": round(scan_kernel_ms, 3)},
             "stages_ms": ({"prefilter_total": round(stage[0], 3), "scan_kernel": round(scan_kernel_ms, 3)}

@@ -53,3 +53,19 @@ def test_big_blob_builtin_automaton():
     for bfs in (0, 1):
         mm, hops, nd = _check(sc, text, bfs)
         assert nd > 0 and mm == 0
+
+
+@pytest.mark.parametrize("kind", [1, 2, 3, 4])
+def test_forged_blob_is_rejected(stress_rs, kind):
+    """A malformed blob is an error, never a device walk that cannot end: the
+    validator the engine runs before every upload (and tsg_ruleset_compile
+    before handing out a ruleset) rejects a failure-link cycle, an
+    unterminated overflow list and out-of-range entries / classes, and
+    accepts the ruleset's real blob."""
+    sc, _ = stress_rs
+    rc = ctypes.c_int(-1)
+    N.check(N.lib.tsg_ruleset_big_forge_check(sc._rs.handle, 0, ctypes.byref(rc)))
+    assert rc.value == N.TSG_OK
+    rc = ctypes.c_int(-1)
+    N.check(N.lib.tsg_ruleset_big_forge_check(sc._rs.handle, kind, ctypes.byref(rc)))
+    assert rc.value == N.TSG_ERR_INTERNAL

@@ -17,13 +17,21 @@ N = pytest.importorskip("trivy_amd._native")
 import trivy_amd.secret as S  # noqa: E402
 
 
+def _decls(name):
+    return set(re.findall(r"\b(tsg_[a-z_]+)\s*\(", open(os.path.join(ROOT, "include", name)).read()))
+
+
 def test_header_symbols_exported():
-    hdr = open(os.path.join(ROOT, "include", "trivy_secret_gpu.h")).read()
-    decl = set(re.findall(r"\b(tsg_[a-z_]+)\s*\(", hdr))
-    assert decl, "no declarations found"
-    for name in decl:
+    """Every entry point of the drop-in ABI (trivy_secret_gpu.h) and of the
+    diagnostic header (trivy_secret_gpu_diag.h) is exported; the two are
+    disjoint, and the diagnostic hooks stay out of the drop-in header."""
+    abi, diag = _decls("trivy_secret_gpu.h"), _decls("trivy_secret_gpu_diag.h")
+    assert abi and diag and not abi & diag
+    for name in abi | diag:
         assert hasattr(N.lib, name), name
-    assert set(N.EXPORTED) <= decl
+    assert set(N.EXPORTED) <= abi | diag
+    assert not any(n.endswith("_check") or n in ("tsg_ruleset_scan_image", "tsg_ruleset_scan_pattern",
+                                                 "tsg_regex_find_all") for n in abi)
 
 
 def test_version():

@@ -68,6 +68,23 @@ def test_invalid_utf8_renders_as_go_does():
     out.encode("utf-8")  # no lone surrogate left
 
 
+def test_invalid_utf8_dicts_keep_the_bytes():
+    """secret_results' dicts keep invalid bytes as lone surrogates (report.py
+    contract): dumps() renders Go's escapes from them, a surrogateescape
+    encode gives back the scanned bytes, a strict encode refuses them."""
+    raw = b"k=\xff\xfe \xe2\x84\xaa"
+    s = raw.decode("utf-8", "surrogateescape")
+    f = T.SecretFinding(RuleID="r", Match=s, Code=T.Code(Lines=[T.Line(Number=1, Content=s, Highlighted=s)]))
+    d = R.secret_results([T.Secret(FilePath="p", Findings=[f])])
+    m = d[0]["Secrets"][0]["Match"]
+    assert m.encode("utf-8", "surrogateescape") == raw
+    with pytest.raises(UnicodeEncodeError):
+        m.encode("utf-8")
+    out = R.dumps(d)
+    assert out.count('k=\\ufffd\\ufffd \u212a') == 3
+    out.encode("utf-8")
+
+
 @pytest.mark.gpu
 def test_gpu_findings_render_the_golden_report():
     from trivy_amd.analyzer import SecretAnalyzer

@@ -272,3 +272,26 @@ def test_gpu_split_with_exclude_block_and_allow_rules_vs_oracle():
     # cut inside the exclude block and between the two tokens
     for n in (2, 3, 5, 9):
         assert _canon(_plain(scan_split(sc, args, n_parts=n))) == want, n
+
+
+@pytest.mark.gpu
+def test_gpu_split_many_small_parts_equal_whole_scan():
+    """64 one-span parts of a 256 KiB file (every part body padded to 16
+    bytes on the owner: the merge buffer is sized by the padded bodies) and
+    other many-part cuts, against the whole-file scan."""
+    import trivy_amd.secret as S
+
+    from . import corpus_gen
+    from .test_gpu_parity import _canon, _plain
+    rng = random.Random(64)
+    files = corpus_gen.make_corpus(6401, 400)
+    data = b"\n".join(d for _, d in files)
+    data = (data * (1 + (256 << 10) // max(1, len(data))))[: 256 << 10]
+    args = S.ScanArgs("many.txt", data)
+    sc = S.new_scanner(None, device=0)  # a fresh scanner: its merge buffer starts small
+    parts = scan_split(sc, args, n_parts=64)
+    want = _canon(_plain(S.new_scanner(None, device=0).scan_batch_device([args])[0]))
+    assert _canon(_plain(parts)) == want
+    for n in (63, 40, rng.randint(17, 60)):
+        assert _canon(_plain(scan_split(sc, args, n_parts=n))) == want, n
+    assert len(want["Findings"]) > 5

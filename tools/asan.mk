@@ -14,7 +14,7 @@ SRC_DIR  = trivy_amd/csrc
 SRCS     = gre.cpp ruleset.cpp follow.cpp dfa.cpp nfa.cpp layertar.cpp engine.hip
 OBJS     = $(patsubst %,build_asan/%.o,$(SRCS))
 LIB      = trivy_amd/libtrivy_secret_gpu_asan.so
-HDRS     = $(wildcard $(SRC_DIR)/*.h) include/trivy_secret_gpu.h
+HDRS     = $(wildcard $(SRC_DIR)/*.h) $(wildcard include/*.h)
 
 $(LIB): $(OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -shared-libsan $(SAN) -o $@ $(OBJS) -lamdhip64

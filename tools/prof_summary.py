@@ -25,6 +25,40 @@ def short(name):
     return n.split("::")[-1] if "::" in n else n[:80]
 
 
+CUS, SIMDS, XCDS = 256, 1024, 8
+
+
+def derive(e):
+    """Derived per-dispatch metrics (keys prefixed `d_`), each from counters
+    of ONE pass (tools/pmc.sh) and that pass's own average duration:
+    * d_lds_bank_conflict_rate = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
+      (extra conflict cycles over all LDS-array cycles)
+    * d_valu_per_lds = SQ_INSTS_VALU / SQ_INSTS_LDS
+    * d_clock_ghz = GRBM_GUI_ACTIVE / 8 XCDs / duration
+    * d_valu_busy = SQ_ACTIVE_INST_VALU x 4 (quad-cycles) / (1024 SIMDs x
+      GRBM_GUI_ACTIVE / 8): share of SIMD cycles issuing VALU
+    * d_lds_busy, d_issue_busy: the same for SQ_ACTIVE_INST_LDS / _ANY
+    * d_waves_per_simd = SQ_WAVE_CYCLES x 4 / (1024 SIMDs x cycles), cycles
+      from the sq pass's duration at the busy pass's clock (occupancy)
+    * d_hbm_read_GBps = FETCH_SIZE x 2 KiB / duration of the fetch pass"""
+    g = e.get("GRBM_GUI_ACTIVE")
+    if e.get("SQ_LDS_IDX_ACTIVE"):
+        e["d_lds_bank_conflict_rate"] = e.get("SQ_LDS_BANK_CONFLICT", 0.0) / e["SQ_LDS_IDX_ACTIVE"]
+    if e.get("SQ_INSTS_LDS"):
+        e["d_valu_per_lds"] = e.get("SQ_INSTS_VALU", 0.0) / e["SQ_INSTS_LDS"]
+    if g and e.get("avg_ms_busy"):
+        cyc = g / XCDS
+        e["d_clock_ghz"] = cyc / (e["avg_ms_busy"] * 1e6)
+        for c, n in (("SQ_ACTIVE_INST_VALU", "d_valu_busy"), ("SQ_ACTIVE_INST_LDS", "d_lds_busy"),
+                     ("SQ_ACTIVE_INST_ANY", "d_issue_busy")):
+            if c in e:
+                e[n] = e[c] * 4 / (SIMDS * cyc)
+        if "SQ_WAVE_CYCLES" in e and e.get("avg_ms_sq"):
+            e["d_waves_per_simd"] = e["SQ_WAVE_CYCLES"] * 4 / (SIMDS * e["d_clock_ghz"] * e["avg_ms_sq"] * 1e6)
+    if "FETCH_SIZE" in e and e.get("avg_ms_fetch"):
+        e["d_hbm_read_GBps"] = e["FETCH_SIZE"] * 2048 / (e["avg_ms_fetch"] * 1e6)
+
+
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
     st = os.path.join(src, "trace", "run_kernel_stats.csv")
@@ -48,6 +82,8 @@ def main(src, dst):
                 e["avg_ms_" + sub] = sum(t for _, t in l) / len(l)
             if "FETCH_SIZE" in e:
                 e["hbm_read_bytes_corrected"] = e["FETCH_SIZE"] * 1024 * 2
+    for k, e in out.items():
+        derive(e)
     json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1, sort_keys=True)
     # per-launch HBM read traffic of the scan kernel, for bench.py's roofline
     alg = os.environ.get("PROF_ALG_BYTES")

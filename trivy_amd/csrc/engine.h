@@ -10,7 +10,7 @@
 #include <vector>
 
 #include "gre.h"
-#include "trivy_secret_gpu.h"
+#include "trivy_secret_gpu_diag.h"  // (includes trivy_secret_gpu.h)
 
 namespace tsg {
 
@@ -312,6 +312,10 @@ struct tsg_ruleset {
 
 namespace tsg {
 bool build_ac(tsg_ruleset* rs, std::string* err);
+// k_scan_big's blob for this automaton (engine.hip), when the engine would use
+// one, built and checked against the invariants that make its device walk end:
+// TSG_OK, or TSG_ERR_INTERNAL with *err naming the violated invariant.
+int big_blob_precheck(const AcHost& ac, std::string* err);
 // The keyword-only shadow of rs (owned by rs), or nullptr with *err set.
 const tsg_ruleset* gate_ruleset(const tsg_ruleset* rs, std::string* err);
 }

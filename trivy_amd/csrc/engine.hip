@@ -2724,7 +2724,8 @@ __device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, ui
 template <class Pos>
 __global__ __launch_bounds__(256) void k_group_runs(VerifyParams V);
 
-// Files of 4 GiB and more: true when the job / location of file fi belongs to
+// Files longer than 2^31 - 1 bytes (kMaxVerifyFile: the 32-bit instantiations
+// keep capture slots in int32): true when the job / location of file fi belongs to
 // the 64-bit instantiation of the search kernels (each kernel is launched
 // twice when the batch holds such a file; every lane skips the other's work).
 __device__ inline bool is_long_file(const uint64_t* off, uint32_t fi) { return off[fi + 1] - 1 - off[fi] > kMaxVerifyFile; }
@@ -2770,6 +2771,11 @@ __global__ __launch_bounds__(256) void k_group_runs(VerifyParams V) {
     const Pos ge = run_back<Pos>(text, ms, me, sm);
     Pos gs;
     if (rd.grp_run_len >= 0) {
+      if (ge < ms || ge - ms < (Pos)rd.grp_run_len) {  // (not for a real match of the rule: the capture search decides)
+        const unsigned long long ci = atomicAdd(&V.ctrl->n_caps, 1ull);
+        if (ci < V.cap_cap) V.caps[ci] = c;
+        continue;
+      }
       gs = ge - (Pos)rd.grp_run_len;
     } else {
       const uint32_t bm[4] = {rd.grp_b[0], rd.grp_b[1], rd.grp_b[2], rd.grp_b[3]};
@@ -4398,6 +4404,71 @@ static bool build_big_blob(const AcHost& ac, bool bfs, BigBlobHost* out) {
   return true;
 }
 
+// Invariants that make big_next (and k_big_walk's replay) terminate, checked
+// on every blob before it is uploaded, and at tsg_ruleset_compile: state 0 is
+// the root and has a dense row; every class byte is < K; every entry (dense,
+// inline, listed) names a state < S; every cold state's failure link names a
+// strictly smaller blob id (the numbering is by depth, and a failure state is
+// strictly shallower), so a walk's cold hops strictly decrease and end in a
+// dense row; every overflow list lies inside the blob and is terminated.
+// Returns an empty string, or what is violated.
+static std::string validate_big_blob(const BigBlobHost& bb, uint32_t K, uint32_t S) {
+  if (K == 0 || K >= kBigMore || S == 0 || S > 0x8000u) return "class or state count out of range";
+  if (bb.nd == 0 || bb.nd + bb.cold != S || bb.ac_of.size() != S || bb.ac_of[0] != 0)
+    return "state 0 is not the dense root";
+  if (bb.o_cold < 256 + (uint64_t)bb.nd * K * 2 || bb.o_eval != bb.o_cold + (uint64_t)bb.cold * 8 ||
+      bb.o_eval > bb.blob.size() || bb.blob.size() > kBigLdsMax)
+    return "blob sections overlap or exceed the LDS budget";
+  for (int b = 0; b < 256; ++b)
+    if (bb.blob[b] >= K) return "byte class out of range";
+  const uint16_t* dense = (const uint16_t*)(bb.blob.data() + 256);
+  for (uint64_t i = 0; i < (uint64_t)bb.nd * K; ++i)
+    if ((dense[i] & 0x7FFFu) >= S) return "dense entry out of range";
+  const uint32_t* rec = (const uint32_t*)(bb.blob.data() + bb.o_cold);
+  const uint32_t* ev = (const uint32_t*)(bb.blob.data() + bb.o_eval);
+  const uint64_t n_ev = (bb.blob.size() - bb.o_eval) / 4;
+  for (uint32_t j = 0; j < bb.cold; ++j) {
+    const uint32_t st = bb.nd + j, x = rec[2 * j], y = rec[2 * j + 1];
+    if ((y >> 16) >= st) return "a cold state's failure link does not point to a shallower state";
+    const uint32_t c1 = x & 0xFFu, c2 = (x >> 8) & 0xFFu;
+    if (c1 == kBigMore) {
+      uint64_t k = (x >> 16) | ((uint64_t)(y & 0xFFFFu) << 16);
+      for (;; ++k) {
+        if (k >= n_ev) return "an overflow list is not terminated inside the blob";
+        const uint32_t v = ev[k];
+        if (v == 0xFFFFFFFFu) break;
+        if ((v >> 16) >= K || (v & 0x7FFFu) >= S) return "overflow list entry out of range";
+      }
+    } else {
+      if ((c1 != kBigNone && c1 >= K) || (c2 != kBigNone && c2 >= K)) return "cold record class out of range";
+      if ((c1 != kBigNone && ((x >> 16) & 0x7FFFu) >= S) || (c2 != kBigNone && (y & 0x7FFFu) >= S))
+        return "cold record entry out of range";
+    }
+  }
+  return std::string();
+}
+
+// The blob the engine would upload for this ruleset (none when k_scan_fast's
+// image or an LDS table holds the automaton), validated: TSG_ERR_INTERNAL with
+// the violated invariant rather than a device walk that could not end.
+static bool needs_big_blob(const AcHost& ac) {
+  return ac.fast.empty() && (size_t)ac.nstates * ac.nclasses * 2 > (size_t)kLdsTableMax;
+}
+
+}  // namespace
+
+int tsg::big_blob_precheck(const AcHost& ac, std::string* err) {
+  if (!needs_big_blob(ac)) return TSG_OK;
+  BigBlobHost bb;
+  if (!build_big_blob(ac, experiment_env("TSG_BIG_BFS") != nullptr, &bb)) return TSG_OK;  // (generic kernel)
+  const std::string why = validate_big_blob(bb, ac.nclasses, ac.nstates);
+  if (why.empty()) return TSG_OK;
+  *err = "k_scan_big automaton blob is malformed: " + why;
+  return TSG_ERR_INTERNAL;
+}
+
+namespace {
+
 // big_next on the host copy of the blob (the device walk, for the CPU check);
 // *hops = cold records read.
 static uint32_t big_next_host(const BigBlobHost& bb, uint32_t K, uint32_t st, uint32_t c, uint32_t* hops) {
@@ -4854,9 +4925,14 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   // k_scan_big blob: only for an automaton that neither k_scan_fast's image
   // nor an LDS table holds (see BigDev); the most dense rows that fit
   im.big_view = BigDev{};
-  if (ac.fast.empty() && (size_t)ac.nstates * ac.nclasses * 2 > (size_t)kLdsTableMax) {
+  if (needs_big_blob(ac)) {
     BigBlobHost bb;
     if (build_big_blob(ac, experiment_env("TSG_BIG_BFS") != nullptr, &bb)) {
+      const std::string why = validate_big_blob(bb, ac.nclasses, ac.nstates);
+      if (!why.empty()) {  // never launch a walk that might not end
+        set_last_error("k_scan_big automaton blob is malformed: " + why);
+        return TSG_ERR_INTERNAL;
+      }
       HIP_TRY(im.big.ensure(bb.blob.size()));
       HIP_TRY(hipMemcpy(im.big.p, bb.blob.data(), bb.blob.size(), hipMemcpyHostToDevice));
       HIP_TRY(im.big_ac_of.ensure(bb.ac_of.size()));
@@ -5645,6 +5721,43 @@ extern "C" int tsg_ruleset_big_check(const tsg_ruleset* rs, const uint8_t* text,
   return TSG_OK;
 }
 
+// The blob validator against forged blobs (tests): the ruleset's blob with
+// one invariant broken -- kind 1: a cold state's failure link pointed at
+// itself (a cycle), 2: an overflow list's terminator removed, 3: a dense
+// entry past the last state, 4: a cold record's class past the class count,
+// 0: unmodified.  *rc = what the validator (the product's pre-launch check)
+// returns for it: TSG_OK or TSG_ERR_INTERNAL.
+extern "C" int tsg_ruleset_big_forge_check(const tsg_ruleset* rs, int kind, int* rc) {
+  if (!rs || !rc || kind < 0 || kind > 4) return TSG_ERR_INVALID_ARG;
+  const AcHost& ac = rs->ac;
+  BigBlobHost bb;
+  if (!build_big_blob(ac, false, &bb)) return TSG_ERR_UNSUPPORTED;
+  uint32_t* rec = (uint32_t*)(bb.blob.data() + bb.o_cold);
+  uint32_t* ev = (uint32_t*)(bb.blob.data() + bb.o_eval);
+  const uint64_t n_ev = (bb.blob.size() - bb.o_eval) / 4;
+  if (kind == 1) {
+    if (!bb.cold) return TSG_ERR_UNSUPPORTED;
+    const uint32_t j = bb.cold / 2;
+    rec[2 * j + 1] = (rec[2 * j + 1] & 0xFFFFu) | ((bb.nd + j) << 16);
+  } else if (kind == 2) {
+    uint64_t last = n_ev;
+    for (uint64_t k = 0; k < n_ev; ++k)
+      if (ev[k] == 0xFFFFFFFFu) last = k;
+    if (last == n_ev) return TSG_ERR_UNSUPPORTED;
+    ev[last] = 0;  // the last list now runs off the blob's end
+  } else if (kind == 3) {
+    ((uint16_t*)(bb.blob.data() + 256))[1] = (uint16_t)ac.nstates;
+  } else if (kind == 4) {
+    if (!bb.cold) return TSG_ERR_UNSUPPORTED;
+    uint32_t j = 0;
+    while (j < bb.cold && (rec[2 * j] & 0xFFu) == kBigMore) ++j;
+    if (j == bb.cold) return TSG_ERR_UNSUPPORTED;
+    rec[2 * j] = (rec[2 * j] & ~0xFFu) | (ac.nclasses & 0xFFu);
+  }
+  *rc = validate_big_blob(bb, ac.nclasses, ac.nstates).empty() ? TSG_OK : TSG_ERR_INTERNAL;
+  return TSG_OK;
+}
+
 // ------------------------------------------------- byte-range split (§8(e)) --
 // One large file scanned by several GPUs: every rank runs the scan pass (the
 // HBM-bound part) over its byte range [own_lo, own_hi) and exports the scan
@@ -5777,9 +5890,14 @@ int export_part(tsg_engine* e, const tsg_ruleset* rs, const ScanParams& P, uint6
     return TSG_ERR_DEVICE;
   }
   uint32_t flags = 0;
-  HIP_TRY(hipMemcpyAsync(blob + sizeof(PartHeader) - 8, e->part_buf.p, cap, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(&flags, e->file_flags.p, 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  hipError_t he = hipMemcpyAsync(blob + sizeof(PartHeader) - 8, e->part_buf.p, cap, hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess) he = hipMemcpyAsync(&flags, e->file_flags.p, 4, hipMemcpyDeviceToHost, s);
+  if (he == hipSuccess) he = hipStreamSynchronize(s);
+  if (he != hipSuccess) {  // the blob is not handed out: free it here
+    (void)hipHostFree(blob);
+    set_last_error(std::string("HIP error in export_part: ") + hipGetErrorString(he));
+    return TSG_ERR_DEVICE;
+  }
   uint64_t kept = 0;
   memcpy(&kept, blob + sizeof(PartHeader) - 8, 8);  // (the count sits where the header's tail goes)
   PartHeader H{kPartMagic, rs->id, sp.file_len, sp.own_lo, sp.own_hi, kept, P.rs.kw_words, flags, (uint32_t)n_spans,
@@ -5838,8 +5956,8 @@ int import_parts(tsg_engine* e, const tsg_ruleset* rs, ScanParams& P, const Spli
   // every body to the device (one H2D each, straight from the caller's
   // blob), then unpacked there: keyword words OR'd, newline counts and span
   // bits at their spans, hits appended part after part
-  uint64_t body_total = 0;
-  for (size_t i : order) body_total += parts[i].second - sizeof(PartHeader);
+  uint64_t body_total = 0;  // each body starts 16-byte aligned (at_body below)
+  for (size_t i : order) body_total += (parts[i].second - sizeof(PartHeader) + 15) & ~(uint64_t)15;
   HIP_TRY(e->part_buf.ensure(body_total + 8));
   HIP_TRY(e->hits.ensure(std::max<uint64_t>(total, 1)));
   HIP_TRY(e->nl_blocks.ensure(n_nlb));

@@ -14,6 +14,15 @@ Restates what a Trivy user reads after a secret scan:
 
 The findings come from the engine (device-built Match / Code), so this module
 only formats; it never scans.
+
+Contract for invalid UTF-8: strings in findings carry each byte Go's decoder
+rejects as a lone surrogate (U+DC80-U+DCFF, Python's `surrogateescape`), and
+the dicts `line_json` / `finding_json` / `secret_results` return keep them so,
+because one dict string cannot tell Go's `\ufffd` escape text (an invalid
+byte) from a raw U+FFFD (a valid rune).  Only `dumps()` / `report_json()`
+produce Go's bytes; other serialisers of those dicts must either pass them
+through `dumps()` or encode with `surrogateescape` (which gives back the raw
+bytes, not Go's escapes).
 """
 from __future__ import annotations
 
@@ -31,15 +40,11 @@ _GO_ESCAPES = {"<": "\\u003c", ">": "\\u003e", "&": "\\u0026", " ": "\\u2028",
 _INVALID = re.compile("[\udc80-\udcff]")
 
 
-def _go_str(s: str) -> str:
-    return s
-
-
 def line_json(ln) -> dict:
-    d = {"Number": ln.Number, "Content": _go_str(ln.Content), "IsCause": ln.IsCause,
+    d = {"Number": ln.Number, "Content": ln.Content, "IsCause": ln.IsCause,
          "Annotation": ln.Annotation, "Truncated": ln.Truncated}
     if ln.Highlighted:
-        d["Highlighted"] = _go_str(ln.Highlighted)
+        d["Highlighted"] = ln.Highlighted
     d["FirstCause"] = ln.FirstCause
     d["LastCause"] = ln.LastCause
     return d
@@ -49,7 +54,7 @@ def finding_json(f) -> dict:
     return {"RuleID": f.RuleID, "Category": f.Category, "Severity": f.Severity, "Title": f.Title,
             "StartLine": f.StartLine, "EndLine": f.EndLine,
             "Code": {"Lines": [line_json(ln) for ln in f.Code.Lines] if f.Code.Lines else None},
-            "Match": _go_str(f.Match), "Layer": {}}
+            "Match": f.Match, "Layer": {}}
 
 
 def secret_results(secrets: Iterable[Optional[Secret]]) -> List[dict]:
