@@ -916,12 +916,14 @@ def main():
                           if args.config == 1 else {k: round(v, 3) for k, v in zip(
                               ["path_gate", "scan_total", "expand", "sort_jobs", "verify", "exclude", "lines",
                                "scan_kernels"], stage)}),
-            "counts": None if args.config == 1 else {k: int(v) for k, v in zip(
-                ["hits", "candidates", "jobs", "locs", "event_overflow", "events", "outputs"], stage[8:15])},
+            "counts": None if args.config == 1 else dict(zip(
+                ["hits", "candidates", "jobs", "locs", "event_overflow", "events", "outputs", "verify_deferred"],
+                [int(v) for v in stage[8:15] + stage[23:24]])),
             "host_ms": {"call_wall": round(stage[15], 3), "post": round(stage[16], 3),
-                        **({"pack": round(stage[18], 3), "h2d": round(stage[19], 3)} if len(stage) > 19 else {}),
+                        **({"pack": round(stage[18], 3), "h2d": round(stage[19], 3)}
+                           if len(stage) > 19 and args.config in (0, 3) else {}),
                         **({"front": round(stage[20], 3), "pipeline": round(stage[21], 3),
-                            "findings": round(stage[22], 3)} if len(stage) > 22 else {})},
+                            "findings": round(stage[22], 3)} if len(stage) > 22 and args.config in (0, 3) else {})},
             "cpu_baseline": cpu,
             "parity": parity,
         }

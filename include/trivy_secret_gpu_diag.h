@@ -90,6 +90,13 @@ int tsg_ruleset_follow_check(const tsg_ruleset* rs, size_t i, const uint8_t* tex
 int tsg_ruleset_dfa_check(const tsg_ruleset* rs, size_t i, const uint8_t* text, size_t len, size_t s,
                           int* result, size_t* me, uint32_t* n_states);
 
+/* The same anchored walk with k_verify's run acceleration (a state whose
+ * entry is the same on all but <= 3 ASCII bytes skips runs of the others with
+ * vector compares), restated on the host: *result / *me as
+ * tsg_ruleset_dfa_check's, *skipped = bytes stepped over by skips. */
+int tsg_ruleset_dfa_accel_check(const tsg_ruleset* rs, size_t i, const uint8_t* text, size_t len, size_t s,
+                                int* result, size_t* me, uint64_t* skipped);
+
 /* Bit-parallel Glushkov NFA of rule i (the verify fallback for rules whose
  * DFA state count explodes, or with \b / (?m) assertions), on host text with
  * threads started at every boundary in [s, inj_hi]: *result = 1 (anchored,
@@ -110,6 +117,11 @@ int tsg_regex_match(const char* pattern, const uint8_t* text, size_t len, int* m
  * up to cap (start,end) pairs. */
 int tsg_regex_find_all(const char* pattern, const uint8_t* text, size_t len, int64_t* pairs,
                        size_t cap, size_t* n_out);
+
+/* Route every verify job list through k_verify_fast / k_verify_slow /
+ * k_allow (on != 0), not only long lists (tests of the split on small
+ * batches); 0 restores the default. */
+int tsg_engine_force_verify_split(tsg_engine* e, int on);
 
 #ifdef __cplusplus
 }

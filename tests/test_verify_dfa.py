@@ -154,3 +154,40 @@ def test_verify_dfa_rune_symbols_equal_vm():
             decided += 1
             total += len(want)
     assert decided > 5000 and total > 100
+
+
+def test_accelerated_walk_equals_plain_walk():
+    """k_verify's run acceleration (engine.hip dfa_accel_skip: a state whose
+    entry is the same on all but <= 3 ASCII bytes skips runs of the others
+    with vector compares), restated on the host, gives the plain walk's
+    answer from every start of ASCII, non-ASCII and private-key texts, for
+    every builtin rule with a verify DFA; the private-key body is skipped."""
+    sc = S.new_scanner(None)
+    rs = sc._rs.handle
+    rng = random.Random(17)
+    texts = _ascii_texts()[:40]
+    body = "".join(rng.choice("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/\n") for _ in range(3000))
+    key = ("-----BEGIN RSA PRIVATE KEY-----\n" + body + "\n-----END RSA PRIVATE KEY-----\n").encode()
+    texts += [key, key[:-5], b"x = " + key + b" tail", "é ſ K ".encode() + key, key.replace(b"Q", "é".encode())]
+    res, me, ns = ctypes.c_int(), ctypes.c_size_t(), ctypes.c_uint32()
+    ares, ame, sk = ctypes.c_int(), ctypes.c_size_t(), ctypes.c_uint64()
+    skipped = checked = 0
+    for i in range(N.lib.tsg_ruleset_rule_count(rs)):
+        N.check(N.lib.tsg_ruleset_dfa_check(rs, i, b"x", 1, 0, ctypes.byref(res), ctypes.byref(me), ctypes.byref(ns)))
+        if not ns.value:
+            continue
+        for t in texts:
+            starts = range(len(t)) if len(t) < 400 else sorted(rng.sample(range(len(t)), 150) + [0, len(t) - 1])
+            for s in starts:
+                N.check(N.lib.tsg_ruleset_dfa_check(rs, i, t, len(t), s, ctypes.byref(res), ctypes.byref(me),
+                                                    ctypes.byref(ns)))
+                N.check(N.lib.tsg_ruleset_dfa_accel_check(rs, i, t, len(t), s, ctypes.byref(ares), ctypes.byref(ame),
+                                                          ctypes.byref(sk)))
+                assert ares.value == res.value and (res.value != 1 or ame.value == me.value), (i, s)
+                skipped += sk.value
+                checked += 1
+    assert checked > 10000 and skipped > 5000
+    pk = next(i for i in range(N.lib.tsg_ruleset_rule_count(rs)) if sc.rules[i].id == "private-key")
+    N.check(N.lib.tsg_ruleset_dfa_accel_check(rs, pk, key, len(key), 0, ctypes.byref(ares), ctypes.byref(ame),
+                                              ctypes.byref(sk)))
+    assert ares.value == 1 and ame.value == len(key) - 1 and sk.value > 2900  # the body: runs of base64 bytes

@@ -29,7 +29,8 @@ constexpr uint32_t kFollowMaxStates = 1024;  // follow-DFA subset-construction b
 constexpr uint32_t kFollowDepth = 96;        // bytes a candidate filter reads past the hit
 constexpr uint32_t kNoFollow = 0xFFFFFFFFu;
 constexpr uint32_t kDfaMaxStates = 4096;     // verify-DFA budget per rule (else the Pike VM)
-constexpr uint32_t kDfaStateMask = 0x3FFF;  // verify-DFA entry: bit15 end-match, bit14 match state
+constexpr uint32_t kDfaStateMask = 0x1FFF;  // verify-DFA entry: bit15 end-match, bit14 match state
+constexpr uint32_t kDfaAccel = 0x2000;      // (device copy) bit13: the entry's state is accelerable (dfa_accel_off)
 constexpr uint32_t kDfaRuneSyms = 5;        // verify-DFA rune symbols: K, ſ, İ, U+FFFD, other non-ASCII
 
 enum RuleMode : uint8_t { MODE_NEVER = 0, MODE_ANCHORED = 1, MODE_FULL = 2 };
@@ -53,6 +54,8 @@ struct RuleDev {
                                 // bytes a match implies the MatchKeywords gate (scanner.go:169-181)
   uint32_t dfa_off;             // verify DFA (dfa.cpp): first u16 of its table (kNoFollow = none)
   uint32_t dfa_ncls, dfa_cls_off, dfa_match_off;
+  uint32_t dfa_accel_off;   // per state u32 index of its run-acceleration record (~0: none), in dfa_bytes
+  uint32_t dfa_accel_recs;  // the 32-byte records (stay bitmap, stay class), 16-aligned in dfa_bytes
   uint32_t dfa_start0, dfa_start1;  // start state at s > 0 / s == 0 (BeginText)
   uint32_t dfa_first[4];        // ASCII bytes on which a start state does not die (k_verify start skip)
   uint32_t dfa_size;            // u16 entries of its table (k_verify stages it in LDS when it fits)
@@ -130,6 +133,7 @@ struct RuleSetDev {
   const uint32_t* group_slots;
   const uint32_t* allow_progs;   // per-rule allow lists
   const uint32_t* global_allow;  // global allow regex progs
+  const uint32_t* pdfa;          // per program: its MatchString DFA record (kPathDfaRec u32; valid flag last)
   uint32_t n_global_allow;
   uint32_t n_rules;
   uint32_t kw_words;       // uint32 words of keyword bits per file
@@ -172,6 +176,7 @@ struct DfaHost {
 };
 bool build_dfa(const gre::Compiled& c, DfaHost* out);
 int dfa_anchored(const DfaHost& d, const uint8_t* text, size_t n, size_t s, size_t* me);
+int dfa_rune_sym(const DfaHost& d, const uint8_t* text, size_t n, size_t q, uint32_t* w);
 bool follow_accepts(const FollowDfa& f, const uint8_t* text, size_t n, size_t h);
 
 // Bit-parallel Glushkov NFA (nfa.cpp), the fallback for rules whose verify

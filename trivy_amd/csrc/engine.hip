@@ -108,6 +108,8 @@ struct Ctrl {
   unsigned long long n_redo;     // speculative job chains re-run from a conflict (k_chain_fix)
   unsigned long long n_dropped;  // locations of the conflicting speculative jobs (k_drop_spec)
   unsigned long long n_caps_run; // matches whose secret group k_group_runs cuts by byte runs
+  unsigned long long n_defer;    // jobs k_verify_fast handed to k_verify_slow
+  unsigned long long n_match;    // matches k_verify_fast found (k_allow's list)
 };
 
 struct DevLoc {
@@ -1361,12 +1363,19 @@ __device__ inline uint64_t lower64(uint64_t x) {
   return x | (up >> 2);
 }
 
+// Each wave works on its own: it claims wave segments from a global counter
+// (their event counts differ by text), replays 64 events per round (one per
+// lane) and stages its anchor hits in its own LDS slots, flushed to P.hits
+// with one global reservation per wave when half full.  No block-wide
+// barrier after the image load: a lock-step block round lasted as long as
+// its slowest lane's chain of dependent global reads (file lookup, keyword
+// atomics) while the other 15 waves idled (0.69 ms on configs[2]).
+constexpr uint32_t kReportWaveHits = kReportHitCap / (kReportThreads / 64);
+
 __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_t n_waves) {
   __shared__ __align__(16) uint8_t L[kReportLds];
   __shared__ uint64_t hbuf[kReportHitCap];
-  __shared__ uint32_t hcnt;
-  __shared__ unsigned long long hbase;
-  __shared__ uint32_t nout;
+  __shared__ uint32_t hcnt[kReportThreads / 64];
   const AcDev& ac = P.rs.ac;
   const bool in_lds = ac.rep_bytes <= kReportLds;
   if (in_lds) {
@@ -1379,37 +1388,31 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
   const uint16_t* out_pat = (const uint16_t*)(B + ac.o_out_pat);
   const PatDev* pats = (const PatDev*)(B + ac.o_pats);
   const uint8_t* pbytes = B + ac.o_pat_bytes;
-  if (threadIdx.x == 0) {
-    hcnt = 0;
-    nout = 0;
-  }
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t* wbuf = hbuf + wv * kReportWaveHits;
+  if (lane == 0) hcnt[wv] = 0;
   __syncthreads();
   const uint32_t out_e = ac.fast_out_entry;
   uint32_t my_out = 0;
   uint64_t last_kw = ~0ull;
-  // wave segments claimed one at a time from a global counter: their event
-  // counts differ by text (a static block-strided assignment waits on the
-  // block that drew the keyword-dense segments)
-  __shared__ uint32_t s_w;
+  unsigned long long my_events = 0;
   for (;;) {
-    if (threadIdx.x == 0) s_w = (uint32_t)atomicAdd(&P.ctrl->rep_next, 1ull);
-    __syncthreads();
-    const uint32_t w = s_w;
-    __syncthreads();
+    uint32_t w = 0;
+    if (lane == 0) w = (uint32_t)atomicAdd(&P.ctrl->rep_next, 1ull);
+    w = __shfl(w, 0);
     if (w >= n_waves + 1) break;
     const FastEvent* seg;
     uint64_t n;
     if (w < n_waves) {
       seg = P.events + (uint64_t)w * P.ev_cap_per_wave;
       n = P.ev_counts[w];
-      if (threadIdx.x == 0 && n) atomicAdd(&P.ctrl->events, (unsigned long long)n);
+      my_events += n;
     } else {  // overflow bucket
       seg = P.ev_overflow;
       n = P.ctrl->ev_overflow < P.ev_overflow_cap ? P.ctrl->ev_overflow : P.ev_overflow_cap;
     }
-    const uint32_t rounds = (uint32_t)((n + blockDim.x - 1) / blockDim.x);
-    for (uint32_t rd_i = 0; rd_i < rounds; ++rd_i) {
-      const uint64_t i = (uint64_t)rd_i * blockDim.x + threadIdx.x;
+    for (uint64_t i0 = 0; i0 < n; i0 += 64) {
+      const uint64_t i = i0 + lane;
       if (i < n) {
         const FastEvent ev = seg[i];
         uint64_t hist = ((uint64_t)ev.prev.y << 32) | ev.prev.x;  // the 8 raw bytes before (oldest low)
@@ -1442,7 +1445,7 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
               if (start + pd.len > fend) continue;
               // chunks of 8 batch bytes issued before any compare (one memory
               // latency per chunk; a byte-by-byte early-exit loop was a chain of
-              // dependent loads that held the whole lock-step round)
+              // dependent loads)
               uint32_t bad = 0, req_bad = 0;
               const uint8_t* pb = pbytes + pd.bytes_off;
               for (uint32_t k0 = tl; k0 < pd.len && !bad; k0 += 8) {
@@ -1474,10 +1477,10 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
               }
             }
             if (want_hit) {
-              const uint32_t slot = atomicAdd(&hcnt, 1u);
+              const uint32_t slot = atomicAdd(&hcnt[wv], 1u);  // (this wave's slots only)
               const uint64_t hrec = (start << 16) | pid;
-              if (slot < kReportHitCap) {
-                hbuf[slot] = hrec;
+              if (slot < kReportWaveHits) {
+                wbuf[slot] = hrec;
               } else {
                 unsigned long long idx = atomicAdd(&P.ctrl->hits, 1ull);
                 if (idx < P.hit_cap) P.hits[idx] = hrec;
@@ -1486,23 +1489,29 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
           }
         }
       }
-      // stage -> global with one reservation per half-full buffer (uniform decision)
-      __syncthreads();
-      if (hcnt >= kReportHitCap / 2 || rd_i + 1 == rounds) {
-        const uint32_t nh = hcnt < kReportHitCap ? hcnt : kReportHitCap;
-        if (threadIdx.x == 0 && nh) hbase = atomicAdd(&P.ctrl->hits, (unsigned long long)nh);
-        __syncthreads();
-        for (uint32_t q = threadIdx.x; q < nh; q += blockDim.x)
-          if (hbase + q < P.hit_cap) P.hits[hbase + q] = hbuf[q];
-        __syncthreads();
-        if (threadIdx.x == 0) hcnt = 0;
-        __syncthreads();
+      // this wave's staged hits -> global, one reservation when half full (or at
+      // the segment's end); the fence orders the wave's LDS stores before the reads
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      const uint32_t hc = __shfl(atomicAdd(&hcnt[wv], 0u), 0);
+      if (hc >= kReportWaveHits / 2 || i0 + 64 >= n) {
+        const uint32_t nh = hc < kReportWaveHits ? hc : kReportWaveHits;
+        unsigned long long base = 0;
+        if (lane == 0 && nh) base = atomicAdd(&P.ctrl->hits, (unsigned long long)nh);
+        base = __shfl(base, 0);
+        for (uint32_t q = lane; q < nh; q += 64)
+          if (base + q < P.hit_cap) P.hits[base + q] = wbuf[q];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (lane == 0) hcnt[wv] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       }
     }
   }
-  atomicAdd(&nout, my_out);
-  __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(&P.ctrl->outputs, (unsigned long long)nout);
+  // per-wave totals: one atomic each
+  for (uint32_t d = 32; d; d >>= 1) my_out += __shfl_xor(my_out, d);
+  if (lane == 0) {
+    if (my_out) atomicAdd(&P.ctrl->outputs, (unsigned long long)my_out);
+    if (my_events) atomicAdd(&P.ctrl->events, my_events);
+  }
 }
 
 // Fold-special sequences (C4B0 U+0130, C5BF U+017F, E284AA U+212A) in the
@@ -1753,12 +1762,41 @@ __global__ __launch_bounds__(256) void k_fold_windows(ScanParams P, FoldItems F)
 // ---------------------------------------------------------------- gating --
 constexpr uint32_t kPathDfaRec = 8;  // u32 per program: off, ncls, cls_off, start0, start1, smatch, sym, valid
 
+__device__ inline uint32_t zero_bytes(uint32_t x) {  // 0x80 in every byte of x that is 0 (and maybe above one)
+  return (x - 0x01010101u) & ~x & 0x80808080u;
+}
+
 struct DfaRef {
   const uint16_t* T;
   const uint8_t* cls;
   uint32_t K, start0, start1, smatch, sym;
+  const uint32_t* accel = nullptr;  // per-state accel record index (entries flagged kDfaAccel), global memory
+  const uint4* accel_recs = nullptr;  // the 32-byte records: stay bitmap, stay class
 };
 
+// From q: the first position whose byte is not in the 128-bit stay set bm
+// (every byte >= 0x80 is not), else n -- 16 bytes per load, one bitmap test
+// per byte, no table lookups.  The batch is padded past every file end.
+constexpr uint32_t kAccelRun = 8;
+template <class Pos>
+__device__ inline Pos dfa_accel_skip(const uint8_t* text, Pos n, Pos q, const uint4 bm) {
+  const uintptr_t base = reinterpret_cast<uintptr_t>(text);
+  uintptr_t a = (base + q) & ~(uintptr_t)15;
+  uint32_t i = (uint32_t)((base + q) & 15);  // first byte of the first block
+  for (; a < base + n; a += 16, i = 0) {
+    const u32x4 v = *as_global<__attribute__((address_space(1))) const u32x4>(reinterpret_cast<const void*>(a));
+    for (; i < 16; ++i) {
+      const uint32_t wd = i < 8 ? (i < 4 ? v.x : v.y) : (i < 12 ? v.z : v.w);
+      const uint32_t c = (wd >> (8 * (i & 3))) & 0xFFu;
+      const uint32_t w = c < 64 ? (c < 32 ? bm.x : bm.y) : (c < 96 ? bm.z : bm.w);
+      if (c >= 0x80 || !((w >> (c & 31)) & 1)) {
+        const Pos p = (Pos)(a + i - base);
+        return p < n ? p : n;
+      }
+    }
+  }
+  return n;
+}
 
 // kLds: d.T / d.cls are the block's LDS copy (k_verify stages the wave's rule).
 template <bool kLds, class Pos>
@@ -1778,6 +1816,7 @@ __device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, Pos 
   // end, so a block holding a content byte never leaves the allocation)
   const uintptr_t base = reinterpret_cast<uintptr_t>(text);
   Pos q = s;
+  uint32_t same = 0;  // consecutive steps that kept the state (the skip engages only on a run)
   while (q < n && st) {
     const uintptr_t addr = (base + q) & ~(uintptr_t)15;
     const u32x4 v = *as_global<__attribute__((address_space(1))) const u32x4>(reinterpret_cast<const void*>(addr));
@@ -1804,10 +1843,35 @@ __device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, Pos 
         st = 0;
         break;
       }
+      const uint32_t prev_st = st;
       st = e & kDfaStateMask;
       q += w;
       i += w;
       if (e & 0x4000u) last = q;
+      same = st == prev_st ? same + 1 : 0;
+      // the record is a global read: taken only once the state has kept
+      // itself for kAccelRun steps (a short run costs less walked)
+      if (same >= kAccelRun && (e & kDfaAccel) && d.accel) {
+        same = 0;
+        // st keeps itself (same flags) on every byte of its stay set: skip
+        // the run as the byte steps would take it
+        const uint4* rec = d.accel_recs + 2 * d.accel[st];
+        const Pos q2 = dfa_accel_skip<Pos>(text, n, q, rec[0]);
+        if (q2 > q) {
+          const uint32_t sc = rec[1].x;
+          const uint32_t es = kLds ? Tl[st * K + sc] : Tg[st * K + sc];
+          *steps += (uint32_t)(q2 - q);
+          if (q2 == n) {  // the run reaches the end: bytes q .. n-2 as steps, n-1 as the last one
+            if (n - 1 > q && (es & 0x4000u)) last = n - 1;
+            if (es & 0x8000u) last = n;
+            st = 0;
+            break;
+          }
+          if (es & 0x4000u) last = q2;
+          q = q2;
+          break;  // reload the block at q
+        }
+      }
     }
   }
   if (last < 0) return 0;
@@ -1894,9 +1958,6 @@ __device__ inline bool match_string(const gre::ProgView& pv, const uint8_t* s, u
 constexpr uint32_t kMayLits = 4;  // literals whose first bytes stay in registers
 enum MayResult : uint32_t { kMayNo = 0, kMayHit = 1, kMayMaybe = 2 };
 
-__device__ inline uint32_t zero_bytes(uint32_t x) {  // 0x80 in every byte of x that is 0 (and maybe above one)
-  return (x - 0x01010101u) & ~x & 0x80808080u;
-}
 
 __device__ inline uint32_t may_match(const RuleSetDev& rs, uint32_t prog, const uint8_t* s, uint32_t n) {
   const uint32_t l0 = rs.prog_lit_off[prog], l1 = rs.prog_lit_off[prog + 1];
@@ -2285,6 +2346,15 @@ struct CapJob {
 // equals the sequential one (FindAll would have tested the same starts) --
 // and re-runs a chain sequentially from the first job where that fails.
 constexpr uint32_t kJobRedo = 0x80000000u;  // DevLoc::job / CapJob::job of a re-run chain's output
+constexpr uint32_t kJobFast = 0x40000000u;  // ... of k_verify_fast's output (void when the job was deferred)
+constexpr uint32_t kJobMask = 0x3FFFFFFFu;
+// Is an output of `job` void?  A re-run chain's never is; k_verify_fast's is
+// when its job was later deferred (bit 1) or conflicts (bit 0); the others'
+// when their job conflicts.
+__device__ inline bool job_void(const uint8_t* job_bad, uint32_t job) {
+  if (job & kJobRedo) return false;
+  return (job_bad[job & kJobMask] & ((job & kJobFast) ? 3u : 1u)) != 0;
+}
 struct RedoRec {
   uint32_t job, last;  // jobs [job, last] of one chain, re-run in order
   uint64_t pos;        // FindAll's search position at `job` (file-relative)
@@ -2319,9 +2389,12 @@ struct VerifyParams {
   uint64_t* job_fms;
   uint64_t* job_lme;
   const uint8_t* split;
-  uint8_t* job_bad;
+  uint8_t* job_bad;  // bit 0: a conflicting speculative job; bit 1: deferred by k_verify_fast
   RedoRec* redo;
   uint64_t redo_cap;
+  uint32_t* defer;   // jobs k_verify_fast handed to k_verify_slow (capacity >= jobs)
+  CapJob* matches;   // k_verify_fast's matches, for k_allow
+  uint64_t match_cap;
 };
 
 
@@ -2655,28 +2728,12 @@ __device__ inline Pos run_back(const uint8_t* text, Pos lo, Pos e, const uint32_
   return q;
 }
 
-// A match k_verify found: allow rules, then the whole-match location or, for
-// rules with a secret group, a capture job for k_captures (whose bit-state
-// arenas take LDS that would cap the search at one wave per CU).
+// A kept match: the whole-match location or, for rules with a secret group,
+// its span (ASCII shortcuts) or a capture job for k_captures (whose
+// bit-state arenas take LDS that would cap the search at one wave per CU).
 template <class Pos>
-__device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, uint32_t fi, uint32_t job,
-                                        const uint8_t* text, Pos n, Pos ms, Pos me, gre::VmScratch& sc,
-                                        uint32_t* tck = nullptr) {
-  const uint64_t t0 = tck ? __builtin_amdgcn_s_memrealtime() : 0;
-  const RuleDev& rd = V.rs.rules[rule];
-  if (sizeof(Pos) > 4 && me - ms > (Pos)0xFFFFFFFFu) {  // allow regexes run on 32-bit match strings
-    atomicOr(&V.ctrl->err, 2u);
-    return;
-  }
-  // AllowLocation (scanner.go:145-148): global then rule allow regexes on the whole match
-  for (uint32_t k = 0; k < V.rs.n_global_allow; ++k) {
-    const bool al = match_string_pf(V.rs, V.rs.global_allow[k], text + ms, (uint32_t)(me - ms), sc);
-    if (tck) tck[2] += (uint32_t)(__builtin_amdgcn_s_memrealtime() - t0);
-    if (al) return;
-  }
-  const uint32_t allow_off = rd.allow_off, allow_n = rd.allow_n;
-  for (uint32_t k = 0; k < allow_n; ++k)
-    if (match_string_pf(V.rs, V.rs.allow_progs[allow_off + k], text + ms, (uint32_t)(me - ms), sc)) return;
+__device__ inline void emit_kept(const VerifyParams& V, const RuleDev& rd, uint32_t rule, uint32_t fi, uint32_t job,
+                                 const uint8_t* text, Pos ms, Pos me) {
   if (!rd.use_groups) {
     unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
     if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, ms, me, 0, 0, 0, job};
@@ -2710,6 +2767,67 @@ __device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, ui
   }
   unsigned long long idx = atomicAdd(&V.ctrl->n_caps, 1ull);
   if (idx < V.cap_cap) V.caps[idx] = CapJob{fi, rule, job, 0, ms, me};
+}
+
+// A match k_verify found: allow rules (scanner.go:145-148), then emit_kept.
+template <class Pos>
+__device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, uint32_t fi, uint32_t job,
+                                        const uint8_t* text, Pos n, Pos ms, Pos me, gre::VmScratch& sc,
+                                        uint32_t* tck = nullptr) {
+  const uint64_t t0 = tck ? __builtin_amdgcn_s_memrealtime() : 0;
+  const RuleDev& rd = V.rs.rules[rule];
+  if (sizeof(Pos) > 4 && me - ms > (Pos)0xFFFFFFFFu) {  // allow regexes run on 32-bit match strings
+    atomicOr(&V.ctrl->err, 2u);
+    return;
+  }
+  // AllowLocation (scanner.go:145-148): global then rule allow regexes on the whole match
+  for (uint32_t k = 0; k < V.rs.n_global_allow; ++k) {
+    const bool al = match_string_pf(V.rs, V.rs.global_allow[k], text + ms, (uint32_t)(me - ms), sc);
+    if (tck) tck[2] += (uint32_t)(__builtin_amdgcn_s_memrealtime() - t0);
+    if (al) return;
+  }
+  const uint32_t allow_off = rd.allow_off, allow_n = rd.allow_n;
+  for (uint32_t k = 0; k < allow_n; ++k)
+    if (match_string_pf(V.rs, V.rs.allow_progs[allow_off + k], text + ms, (uint32_t)(me - ms), sc)) return;
+  emit_kept<Pos>(V, rd, rule, fi, job, text, ms, me);
+}
+
+// emit_match for k_verify_fast: the match goes to the raw match list; the
+// allow rules (which may need the Pike VM) run in k_allow, a kernel of its
+// own.  false (the job is deferred) only for a match of 4 GiB or more.
+template <class Pos>
+__device__ inline bool emit_match_fast(const VerifyParams& V, uint32_t rule, uint32_t fi, uint32_t job,
+                                       const uint8_t* text, Pos ms, Pos me) {
+  (void)text;
+  if (sizeof(Pos) > 4 && me - ms > (Pos)0xFFFFFFFFu) return false;  // (the slow kernel reports it)
+  const unsigned long long idx = atomicAdd(&V.ctrl->n_match, 1ull);
+  if (idx < V.match_cap) V.matches[idx] = CapJob{fi, rule, job | kJobFast, 0, (uint64_t)ms, (uint64_t)me};
+  return true;
+}
+
+// AllowLocation (scanner.go:145-148) for k_verify_fast's matches, one lane
+// per match (the Pike VM's registers stay out of the search kernel), then the
+// location / group stage as emit_match.  A match of a job deferred after it
+// was found is void (k_verify_slow re-finds it).
+__global__ __launch_bounds__(64) void k_allow(VerifyParams V) {
+  const unsigned long long cnt = V.ctrl->n_match;
+  const uint64_t n = cnt < V.match_cap ? cnt : V.match_cap;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  gre::VmScratch sc = make_scratch(V.scratch + (uint64_t)t * V.scratch_stride, V.rs);
+  for (uint64_t i = t; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const CapJob M = V.matches[i];
+    if (job_void(V.job_bad, M.job)) continue;
+    const RuleDev& rd = V.rs.rules[M.rule];
+    const uint8_t* text = V.data + V.off[M.file];
+    const uint8_t* m = text + M.ms;
+    const uint32_t len = (uint32_t)(M.me - M.ms);
+    bool allowed = false;
+    for (uint32_t k = 0; k < V.rs.n_global_allow && !allowed; ++k)
+      allowed = match_string_pf(V.rs, V.rs.global_allow[k], m, len, sc);
+    for (uint32_t k = 0; k < rd.allow_n && !allowed; ++k)
+      allowed = match_string_pf(V.rs, V.rs.allow_progs[rd.allow_off + k], m, len, sc);
+    if (!allowed) emit_kept<uint64_t>(V, rd, M.rule, M.file, M.job, text, M.ms, M.me);
+  }
 }
 
 // Capture stages: a fixed grid walks the list the previous stage filled,
@@ -2746,7 +2864,7 @@ __global__ __launch_bounds__(kLanes) void k_captures(VerifyParams V) {
   // (few divergent lanes per wave) instead of filling the first waves
   for (uint64_t i = blockIdx.x + (uint64_t)threadIdx.x * gridDim.x; i < n_caps; i += nthreads) {
     const CapJob c = list[i];
-    if (!(c.job & kJobRedo) && V.job_bad[c.job]) continue;  // a conflicting speculative job's match
+    if (job_void(V.job_bad, c.job)) continue;  // a conflicting speculative job's (or a deferred fast job's) match
     if (is_long_file(V.off, c.file) != (sizeof(Pos) > 4)) continue;
     const RuleDev rd = V.rs.rules[c.rule];
     const uint64_t fstart = V.off[c.file];
@@ -2762,7 +2880,7 @@ __global__ __launch_bounds__(256) void k_group_runs(VerifyParams V) {
   const uint64_t n = cnt < V.cap_run_cap ? cnt : V.cap_run_cap;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const CapJob c = V.caps_run[i];
-    if (!(c.job & kJobRedo) && V.job_bad[c.job]) continue;  // a conflicting speculative job's match
+    if (job_void(V.job_bad, c.job)) continue;  // a conflicting speculative job's (or a deferred fast job's) match
     if (is_long_file(V.off, c.file) != (sizeof(Pos) > 4)) continue;
     const RuleDev& rd = V.rs.rules[c.rule];
     const uint8_t* text = V.data + V.off[c.file];
@@ -2854,6 +2972,7 @@ __device__ __noinline__ void verify_full_job(const VerifyParams& V, uint32_t rul
 template <class Pos>
 __device__ inline void job_record(const VerifyParams& V, uint32_t job, Pos fms, Pos lme) {
   if (job & kJobRedo) return;
+  job &= kJobMask;
   V.job_fms[job] = fms == ~(Pos)0 ? ~0ull : (uint64_t)fms;
   V.job_lme[job] = lme;
 }
@@ -2891,7 +3010,9 @@ __device__ __noinline__ uint32_t verify_dfa_job(const VerifyParams& V, uint32_t 
   uint32_t tck_dfa = 0, tck_emit = 0;
   const RuleDev& rd = V.rs.rules[rule];
   const DfaRef dref{kLds ? lds_T : V.rs.dfa_delta + rd.dfa_off, kLds ? lds_cls : V.rs.dfa_bytes + rd.dfa_cls_off,
-                    rd.dfa_ncls, rd.dfa_start0, rd.dfa_start1, rd.dfa_smatch, rd.dfa_sym};
+                    rd.dfa_ncls, rd.dfa_start0, rd.dfa_start1, rd.dfa_smatch, rd.dfa_sym,
+                    (const uint32_t*)(V.rs.dfa_bytes + rd.dfa_accel_off),
+                    (const uint4*)(V.rs.dfa_bytes + rd.dfa_accel_recs)};
   const uint32_t fm0 = rd.dfa_first[0], fm1 = rd.dfa_first[1], fm2 = rd.dfa_first[2], fm3 = rd.dfa_first[3];
   const uint32_t prog = rd.prog;
   IvIter<Pos> it;
@@ -3011,6 +3132,116 @@ __device__ __noinline__ uint32_t verify_nfa_job(const VerifyParams& V, uint32_t 
   return steps;
 }
 
+// k_verify_fast's job paths: the verify DFA / NFA walks of verify_dfa_job /
+// verify_nfa_job with every Pike VM call replaced by a deferral (return 0):
+// a start the walk cannot decide, or an allow rule the DFA cannot decide.
+// Matches found before a deferral are tagged kJobFast and voided with the job.
+template <bool kLds, class Pos>
+__device__ __forceinline__ int fast_dfa_job(const VerifyParams& V, uint32_t rule, uint32_t fi, uint32_t job, uint64_t c0,
+                                         uint64_t c1, uint64_t fstart, const uint8_t* text, Pos n,
+                                         const uint16_t* lds_T, const uint8_t* lds_cls) {
+  uint32_t steps = 0;
+  const RuleDev& rd = V.rs.rules[rule];
+  const DfaRef dref{kLds ? lds_T : V.rs.dfa_delta + rd.dfa_off, kLds ? lds_cls : V.rs.dfa_bytes + rd.dfa_cls_off,
+                    rd.dfa_ncls, rd.dfa_start0, rd.dfa_start1, rd.dfa_smatch, rd.dfa_sym,
+                    (const uint32_t*)(V.rs.dfa_bytes + rd.dfa_accel_off),
+                    (const uint4*)(V.rs.dfa_bytes + rd.dfa_accel_recs)};
+  const uint32_t fm0 = rd.dfa_first[0], fm1 = rd.dfa_first[1], fm2 = rd.dfa_first[2], fm3 = rd.dfa_first[3];
+  IvIter<Pos> it;
+  iv_init(it, V, rule, c0, c1, fstart, text, n);
+  Pos pos = 0, me, fms = ~(Pos)0, lme = 0;
+  while (it.have) {
+    bool found = false;
+    const Pos s0 = it.cs > pos ? it.cs : pos;
+    VecText TS(text);
+    for (Pos sp = s0; sp <= it.ce && sp < n; ++sp) {
+      const uint32_t b0 = TS[sp];
+      if (b0 >= 0x80 && !gre::is_rune_start(text, n, sp)) continue;
+      const uint32_t fw = b0 < 32 ? fm0 : b0 < 64 ? fm1 : b0 < 96 ? fm2 : fm3;
+      if (b0 < 0x80 && !((fw >> (b0 & 31)) & 1)) continue;
+      const int r = dfa_anchored_dev<kLds, Pos>(dref, text, n, sp, &me, &steps);
+      if (r == 2) return 0;
+      if (r == 1) {
+        if (!emit_match_fast<Pos>(V, rule, fi, job, text, sp, me)) return 0;
+        if (fms == ~(Pos)0) fms = sp;
+        lme = me;
+        pos = me;
+        found = true;
+        break;
+      }
+    }
+    if (!found) it.advance();
+    else while (it.have && it.ce < pos) it.advance();
+  }
+  job_record(V, job, fms, lme);
+  return 1;
+}
+
+template <bool kWide, class Pos>
+__device__ __forceinline__ int fast_nfa_job(const VerifyParams& V, uint32_t rule, uint32_t fi, uint32_t job, uint64_t c0,
+                                         uint64_t c1, uint64_t fstart, const uint8_t* text, Pos n, const uint8_t* nfa) {
+  const NfaDev& N = *(const NfaDev*)nfa;
+  const U128* reach = (const U128*)(nfa + N.o_reach);
+  const NfaExc* exc = (const NfaExc*)(nfa + N.o_exc);
+  uint32_t steps = 0;
+  IvIter<Pos> it;
+  iv_init(it, V, rule, c0, c1, fstart, text, n);
+  Pos pos = 0, me, fms = ~(Pos)0, lme = 0;
+  while (it.have) {
+    bool found = false;
+    const Pos s0 = it.cs > pos ? it.cs : pos;
+    const Pos s1 = it.ce < n ? it.ce : n;
+    int any = 0;
+    if (s0 <= s1) {
+      VecText T(text);
+      any = nfa_walk<kWide>(N, reach, exc, T, n, s0, s1, &me, &steps);  // (2: the starts one by one decide)
+    }
+    for (Pos sp = s0; any && sp <= s1 && sp < n; ++sp) {
+      if (!gre::is_rune_start(text, n, sp)) continue;
+      const uint32_t b0 = as_global<gu8>(text)[sp];
+      if (b0 < 0x80 && !nfa_first_ok(N, reach, b0)) continue;
+      VecText T(text);
+      const int r = nfa_walk<kWide>(N, reach, exc, T, n, sp, sp, &me, &steps);
+      if (r == 2) return 0;
+      if (r == 1) {
+        if (!emit_match_fast<Pos>(V, rule, fi, job, text, sp, me)) return 0;
+        if (fms == ~(Pos)0) fms = sp;
+        lme = me;
+        pos = me;
+        found = true;
+        break;
+      }
+    }
+    if (!found) it.advance();
+    else while (it.have && it.ce < pos) it.advance();
+  }
+  job_record(V, job, fms, lme);
+  return 1;
+}
+
+// One job without the Pike VM: 1 = done, 0 = deferred to k_verify_slow
+// (full-scan jobs and rules with neither a verify DFA nor an NFA at once).
+template <class Pos>
+__device__ inline int run_job_fast(const VerifyParams& V, uint32_t job, uint64_t c0, uint64_t c1,
+                                   const uint16_t* lds_dfa, const uint8_t* lds_cls, const uint8_t* lds_nfa) {
+  const uint32_t rule = (uint32_t)(V.keys[c0] >> kPosBits);
+  const uint32_t fi = V.vals[c0] & ~kFullFlag;
+  for (uint64_t c = c0; c < c1; ++c)
+    if (V.vals[c] & kFullFlag) return 0;
+  const uint64_t fstart = V.off[fi];
+  const uint8_t* text = V.data + fstart;
+  const Pos n = (Pos)(V.off[fi + 1] - 1 - fstart);
+  const RuleDev& rd = V.rs.rules[rule];
+  if (lds_dfa) return fast_dfa_job<true, Pos>(V, rule, fi, job, c0, c1, fstart, text, n, lds_dfa, lds_cls);
+  if (rd.dfa_off != kNoFollow) return fast_dfa_job<false, Pos>(V, rule, fi, job, c0, c1, fstart, text, n, nullptr, nullptr);
+  if (rd.nfa_off != kNoFollow) {
+    const uint8_t* nfa = lds_nfa ? lds_nfa : V.rs.nfa_bytes + rd.nfa_off;
+    return ((const NfaDev*)nfa)->npos > 64 ? fast_nfa_job<true, Pos>(V, rule, fi, job, c0, c1, fstart, text, n, nfa)
+                                            : fast_nfa_job<false, Pos>(V, rule, fi, job, c0, c1, fstart, text, n, nfa);
+  }
+  return 0;
+}
+
 // The block (one wave) stages the verify DFA of its first job's rule in LDS:
 // jobs are sorted by rule, so nearly every lane walks that table, and an LDS
 // step costs no L2 round trip and no TLB lookup (the random text pages the
@@ -3095,6 +3326,68 @@ __global__ __launch_bounds__(kBlock) void k_verify(VerifyParams V) {
   }
 }
 
+// The match search in two kernels.  k_verify_fast runs every job on the
+// verify DFA / NFA paths, which never reach the Pike VM, so it compiles to a
+// register budget of its own (the VM's ~250 VGPRs and private stack capped
+// k_verify at two waves per SIMD); a job that needs the VM (a start the walk
+// cannot decide, an allow rule its DFA cannot decide, full-scan jobs, rules
+// with neither table) is flagged (job_bad bit 1, its fast output void) and
+// listed for k_verify_slow, which runs it whole with the VM-capable paths.
+constexpr uint32_t kVerifyFastLds = 32 * 1024;  // staged table: five 256-lane blocks per CU
+template <uint32_t kBlock, class Pos>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_verify_fast(VerifyParams V) {
+  __shared__ __align__(16) uint16_t dfa_lds[kVerifyFastLds / 2];
+  __shared__ __align__(16) uint8_t cls_lds[128];
+  const uint32_t nthreads = gridDim.x * blockDim.x;
+  const uint32_t n_jobs = *V.n_jobs_dev;
+  for (uint32_t jb = blockIdx.x * blockDim.x; jb < n_jobs; jb += nthreads) {  // block-uniform
+    const uint32_t r0 = (uint32_t)(V.keys[V.job_start[jb]] >> kPosBits);
+    const RuleDev& rd0 = V.rs.rules[r0];
+    const bool staged = rd0.dfa_off != kNoFollow && rd0.dfa_size * 2 <= kVerifyFastLds;
+    const bool staged_nfa = !staged && rd0.dfa_off == kNoFollow && rd0.nfa_off != kNoFollow &&
+                            rd0.nfa_bytes <= kVerifyFastLds;
+    __syncthreads();  // the previous group's walks are done with the table
+    if (staged) {
+      const uint32_t* src = (const uint32_t*)(V.rs.dfa_delta + rd0.dfa_off);
+      for (uint32_t i = threadIdx.x; i < (rd0.dfa_size + 1) / 2; i += blockDim.x) ((uint32_t*)dfa_lds)[i] = src[i];
+      for (uint32_t i = threadIdx.x; i < 128; i += blockDim.x) cls_lds[i] = V.rs.dfa_bytes[rd0.dfa_cls_off + i];
+    } else if (staged_nfa) {
+      const uint32_t* src = (const uint32_t*)(V.rs.nfa_bytes + rd0.nfa_off);
+      for (uint32_t i = threadIdx.x; i < rd0.nfa_bytes / 4; i += blockDim.x) ((uint32_t*)dfa_lds)[i] = src[i];
+    }
+    __syncthreads();
+    const uint32_t j = jb + threadIdx.x;
+    if (j >= n_jobs) continue;
+    const uint64_t c0 = V.job_start[j];
+    const uint64_t c1 = (j + 1 < n_jobs) ? V.job_start[j + 1] : V.n_cands;
+    if (is_long_file(V.off, V.vals[c0] & ~kFullFlag) != (sizeof(Pos) > 4)) continue;
+    const uint32_t rule = (uint32_t)(V.keys[c0] >> kPosBits);
+    if (!run_job_fast<Pos>(V, j, c0, c1, staged && rule == r0 ? dfa_lds : nullptr, cls_lds,
+                           staged_nfa && rule == r0 ? (const uint8_t*)dfa_lds : nullptr)) {
+      V.job_bad[j] |= 2;
+      const unsigned long long k = atomicAdd(&V.ctrl->n_defer, 1ull);
+      V.defer[k] = j;  // (capacity: every job)
+    }
+  }
+}
+
+template <class Pos>
+__global__ __launch_bounds__(64) void k_verify_slow(VerifyParams V) {
+  const uint64_t n = V.ctrl->n_defer;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  gre::VmScratch sc = make_scratch(V.scratch + (uint64_t)t * V.scratch_stride, V.rs);
+  const uint32_t n_jobs = *V.n_jobs_dev;
+  // job i -> block i % grid, lane i / grid: a short list spreads over every CU
+  for (uint64_t i = blockIdx.x + (uint64_t)threadIdx.x * gridDim.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t j = V.defer[i];
+    const uint64_t c0 = V.job_start[j];
+    const uint64_t c1 = (j + 1 < n_jobs) ? V.job_start[j + 1] : V.n_cands;
+    if (is_long_file(V.off, V.vals[c0] & ~kFullFlag) != (sizeof(Pos) > 4)) continue;
+    bool full;
+    run_job<Pos>(V, j, 0, c0, c1, sc, nullptr, nullptr, nullptr, &full);
+  }
+}
+
 // The speculative chains (one lane per chain head -- a job whose first
 // candidate starts a hard split -- over the soft-split jobs after it): the
 // first job whose first match starts before the previous match's end is a
@@ -3112,7 +3405,7 @@ __global__ void k_chain_fix(VerifyParams V) {
     const uint64_t f = V.job_fms[j];
     if (f == ~0ull) continue;
     if (f < end) {
-      for (uint32_t q = j; q <= last; ++q) V.job_bad[q] = 1;
+      for (uint32_t q = j; q <= last; ++q) V.job_bad[q] |= 1;
       const unsigned long long k = atomicAdd(&V.ctrl->n_redo, 1ull);
       if (k < V.redo_cap) V.redo[k] = RedoRec{j, last, end};
       return;
@@ -3145,7 +3438,7 @@ __global__ void k_drop_spec(VerifyParams V) {
   const uint64_t n_locs = V.ctrl->locs < V.loc_cap ? V.ctrl->locs : V.loc_cap;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_locs; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t job = V.locs[i].job;
-    if (!(job & kJobRedo) && V.job_bad[job]) {
+    if (job_void(V.job_bad, job)) {
       V.locs[i].flags |= 2;
       atomicAdd(&V.ctrl->n_dropped, 1ull);
     }
@@ -4494,6 +4787,44 @@ static uint32_t big_next_host(const BigBlobHost& bb, uint32_t K, uint32_t st, ui
   return dense[st * K + c];
 }
 
+// Run acceleration of a verify DFA: a state whose entry is the same on a
+// set of at least kAccelMinStay ASCII bytes (its "stay" set), and that entry
+// keeps the state with the same flags, steps over runs of stay bytes with a
+// bitmap test per byte and no table lookups (a private key's base64 body,
+// `[a-z0-9]{17,}` tails).  Records (32 B): the stay bitmap (4 u32), the class
+// of a stay byte, padding; per state a record index or ~0.
+constexpr int kAccelMinStay = 16;
+struct DfaAccel {
+  std::vector<uint32_t> idx;   // per state
+  std::vector<uint32_t> recs;  // 8 u32 per record
+};
+static DfaAccel dfa_accel_records(const DfaHost& D) {
+  const uint32_t K = std::max<uint32_t>(1, D.ncls), S = (uint32_t)(D.delta.size() / K);
+  DfaAccel A;
+  A.idx.assign(S, 0xFFFFFFFFu);
+  for (uint32_t st = 1; st < S; ++st) {
+    std::map<uint16_t, int> cnt;
+    for (int b = 0; b < 128; ++b) ++cnt[D.delta[(size_t)st * K + D.cls[b]]];
+    uint16_t self = 0;
+    int best = -1;
+    for (auto& kv : cnt)
+      if ((kv.first & kDfaStateMask) == st && kv.second > best) {
+        best = kv.second;
+        self = kv.first;
+      }
+    if (best < kAccelMinStay) continue;
+    uint32_t bm[4] = {0, 0, 0, 0}, scls = 0;
+    for (int b = 0; b < 128; ++b)
+      if (D.delta[(size_t)st * K + D.cls[b]] == self) {
+        bm[b >> 5] |= 1u << (b & 31);
+        scls = D.cls[b];
+      }
+    A.idx[st] = (uint32_t)(A.recs.size() / 8);
+    A.recs.insert(A.recs.end(), {bm[0], bm[1], bm[2], bm[3], scls, 0, 0, 0});
+  }
+  return A;
+}
+
 struct DevImage {
   uint64_t rs_id = 0;
   DBuf<uint8_t> big;  // k_scan_big blob (empty unless the automaton needs it)
@@ -4549,6 +4880,7 @@ struct DevImage {
 
 struct tsg_engine {
   int device = 0;
+  int verify_split = 0;  // 1: every job list through k_verify_fast (tests; tsg_engine_force_verify_split)
   hipStream_t stream = nullptr;
   std::mutex mu;
   DevImage img;
@@ -4579,6 +4911,8 @@ struct tsg_engine {
   DBuf<uint64_t> job_fms, job_lme;  // speculative jobs (k_chain_fix)
   DBuf<uint8_t> job_bad;
   DBuf<RedoRec> redo;
+  DBuf<uint32_t> defer;  // k_verify_fast -> k_verify_slow job list
+  DBuf<CapJob> matches;  // k_verify_fast -> k_allow
   DBuf<uint32_t> ev_counts;
   uint64_t ev_ovf_need = 0;  // overflow-event capacity learnt from a lost scan
   DBuf<uint64_t> big_outs;   // k_big_walk's output records
@@ -4752,7 +5086,20 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
       d.dfa_size = (uint32_t)r.dfa.delta.size();
       d.dfa_smatch = (r.dfa.match[r.dfa.start[0]] ? 1u : 0u) | (r.dfa.match[r.dfa.start[1]] ? 2u : 0u);
       d.dfa_sym = r.dfa.sym_base | (r.dfa.na_ok ? 0x80000000u : 0u);
+      // accelerable states (a private key's body, `.{0,N}` runs): the entry
+      // on all but <= 3 ASCII bytes keeps the state with the same flags, so
+      // the device skips such runs with vector compares (dfa_accel_skip)
+      const DfaAccel acc = dfa_accel_records(r.dfa);
+      while (dbytes.size() & 15) dbytes.push_back(0);
+      d.dfa_accel_off = (uint32_t)dbytes.size();  // per-state record index (u32), then the 32-byte records
+      dbytes.insert(dbytes.end(), (const uint8_t*)acc.idx.data(), (const uint8_t*)(acc.idx.data() + acc.idx.size()));
+      while (dbytes.size() & 15) dbytes.push_back(0);
+      d.dfa_accel_recs = (uint32_t)dbytes.size();
+      dbytes.insert(dbytes.end(), (const uint8_t*)acc.recs.data(), (const uint8_t*)(acc.recs.data() + acc.recs.size()));
+      const size_t at = ddelta.size();
       ddelta.insert(ddelta.end(), r.dfa.delta.begin(), r.dfa.delta.end());
+      for (size_t i = at; i < ddelta.size(); ++i)
+        if (acc.idx[ddelta[i] & kDfaStateMask] != 0xFFFFFFFFu) ddelta[i] |= kDfaAccel;
     }
     d.nfa_off = kNoFollow;
     if (r.nfa.valid) {  // (records are multiples of 16 bytes: every one stays 16-byte aligned)
@@ -5125,6 +5472,7 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   v.allow_progs = im.u32.p + o_ap;
   v.global_allow = im.u32.p + o_ga;
   v.n_global_allow = (uint32_t)gallow.size();
+  v.pdfa = im.u32.p + im.o_pdfa;
   v.n_rules = (uint32_t)rs->rules.size();
   v.kw_words = std::max<uint32_t>(1, ((uint32_t)rs->keywords.size() + 31) / 32);
   v.max_ninst = max_ninst;
@@ -5721,6 +6069,63 @@ extern "C" int tsg_ruleset_big_check(const tsg_ruleset* rs, const uint8_t* text,
   return TSG_OK;
 }
 
+// The verify DFA walk with k_verify's run acceleration (dfa_accel_skip),
+// restated on the host for tests: must give tsg_ruleset_dfa_check's answer
+// for every start; *skipped = bytes the accelerated runs stepped over.
+extern "C" int tsg_ruleset_dfa_accel_check(const tsg_ruleset* rs, size_t i, const uint8_t* text, size_t len, size_t s,
+                                           int* result, size_t* me, uint64_t* skipped) {
+  if (!rs || i >= rs->rules.size() || !result || !me || !skipped || (len && !text)) return TSG_ERR_INVALID_ARG;
+  const DfaHost& d = rs->rules[i].dfa;
+  *skipped = 0;
+  if (!d.valid || s >= len) {
+    *result = 2;
+    return TSG_OK;
+  }
+  const DfaAccel acc = dfa_accel_records(d);
+  const size_t n = len;
+  uint32_t st = d.start[s == 0 ? 1 : 0];
+  int64_t last = d.match[st] ? (int64_t)s : -1;
+  for (size_t q = s; q < n && st;) {
+    const uint8_t c = text[q];
+    uint32_t w = 1, k = d.cls[c & 0x7F];
+    if (c >= 0x80) {
+      const int sym = dfa_rune_sym(d, text, n, q, &w);
+      if (sym < 0) {
+        *result = 2;
+        return TSG_OK;
+      }
+      k = (uint32_t)sym;
+    }
+    const uint16_t e = d.delta[(size_t)st * d.ncls + k];
+    if (q + w == n) {
+      if (e & 0x8000) last = (int64_t)n;
+      break;
+    }
+    st = e & kDfaStateMask;
+    q += w;
+    if (e & 0x4000) last = (int64_t)q;
+    if (acc.idx[st] != 0xFFFFFFFFu) {
+      const uint32_t* rec = acc.recs.data() + 8 * (size_t)acc.idx[st];
+      size_t q2 = q;
+      while (q2 < n && text[q2] < 0x80 && ((rec[text[q2] >> 5] >> (text[q2] & 31)) & 1)) ++q2;
+      if (q2 > q) {
+        const uint16_t es = d.delta[(size_t)st * d.ncls + rec[4]];
+        *skipped += q2 - q;
+        if (q2 == n) {
+          if (n - 1 > q && (es & 0x4000)) last = (int64_t)n - 1;
+          if (es & 0x8000) last = (int64_t)n;
+          break;
+        }
+        if (es & 0x4000) last = (int64_t)q2;
+        q = q2;
+      }
+    }
+  }
+  *result = last < 0 ? 0 : 1;
+  if (last >= 0) *me = (size_t)last;
+  return TSG_OK;
+}
+
 // The blob validator against forged blobs (tests): the ruleset's blob with
 // one invariant broken -- kind 1: a cold state's failure link pointed at
 // itself (a cycle), 2: an overflow list's terminator removed, 3: a dense
@@ -6036,7 +6441,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   }
   HIP_TRY(e->scratch.ensure((size_t)e->vm_threads * e->scratch_stride));
   std::vector<double>& tm = res->impl.timings;
-  tm.assign(18, 0.0);
+  tm.assign(24, 0.0);  // [18..22]: tsg_analyze's host stages, [23]: jobs k_verify_fast deferred
   if (!e->events) {
     for (auto& ev : e->ev) HIP_TRY(hipEventCreate(&ev));
     e->events = true;
@@ -6243,7 +6648,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   uint64_t caps_cap = std::max<uint64_t>(1 << 14, n_cands / 2), caps_big_cap = std::max<uint64_t>(1 << 12, n_cands / 16);
   uint64_t caps_run_cap = std::max<uint64_t>(1 << 14, n_cands);
   uint64_t redo_cap = std::max<uint64_t>(1 << 12, n_cands / 64);
-  uint64_t n_locs = 0, n_dropped = 0;
+  uint64_t n_locs = 0, n_dropped = 0, n_deferred = 0;
   bool verified = n_cands == 0;
   for (int attempt = 0; attempt < 4 && !verified; ++attempt) {
     HIP_TRY(e->locs.ensure(loc_cap));
@@ -6254,6 +6659,9 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(e->job_lme.ensure(n_cands));
     HIP_TRY(e->job_bad.ensure(n_cands));
     HIP_TRY(e->redo.ensure(redo_cap));
+    HIP_TRY(e->defer.ensure(n_cands));
+    HIP_TRY(e->matches.ensure(loc_cap));
+    HIP_TRY(hipMemsetAsync(&e->ctrl.p->n_defer, 0, 16, s));  // n_defer, n_match
     HIP_TRY(hipMemsetAsync(e->job_bad.p, 0, n_cands, s));
     HIP_TRY(hipMemsetAsync(&e->ctrl.p->locs, 0, 8, s));
     HIP_TRY(hipMemsetAsync(&e->ctrl.p->n_caps, 0, 16, s));  // n_caps, n_caps_big
@@ -6284,6 +6692,9 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     V.job_bad = e->job_bad.p;
     V.redo = e->redo.p;
     V.redo_cap = e->redo.n;
+    V.defer = e->defer.p;
+    V.matches = e->matches.p;
+    V.match_cap = e->matches.n;
     V.span_hi = (rs->ac.fast.size() || P.big.blob) && nbytes ? e->span_hi.p : nullptr;
     const bool prof = experiment_env("TSG_PROFILE_VERIFY") != nullptr;
     if (prof) {  // diagnostics only: the job count on the host
@@ -6315,7 +6726,29 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
       hipLaunchKernelGGL(k_warm, dim3(8 * kWarmParts), dim3(256), 0, s, W, (uint32_t*)e->nsel.p);
       HIP_TRY(hipGetLastError());
     }
-    if (n_cands > (uint64_t)e->num_cus * kVerifyBlockWide * 4) {
+    // fast / slow split (k_verify_fast) for long job lists, where occupancy
+    // sets the time (configs[4]: 5.09 -> 1.07 ms).  A short list (a few jobs
+    // per lane of one wave per CU: configs[2]) ends with its slowest job, and
+    // there the single VM-capable kernel with its 64 KiB staged table is
+    // quicker (0.43 vs 0.62 ms, profiles/r04e); it also serves the per-job
+    // profile (TSG_PROFILE_VERIFY) and A/B (TSG_VERIFY_SINGLE).
+    const bool long_list = n_cands > (uint64_t)e->num_cus * kVerifyBlockWide * 4;
+    const bool single = (!long_list && !e->verify_split) || prof || experiment_env("TSG_VERIFY_SINGLE") != nullptr;
+    if (!single) {
+      {
+        const uint32_t blocks = (uint32_t)((n_cands + kVerifyBlockWide - 1) / kVerifyBlockWide);
+        hipLaunchKernelGGL((k_verify_fast<kVerifyBlockWide, uint32_t>), dim3(std::max(1u, blocks)),
+                           dim3(kVerifyBlockWide), 0, s, V);
+        if (any_long)
+          hipLaunchKernelGGL((k_verify_fast<kVerifyBlockWide, uint64_t>), dim3(std::max(1u, blocks)),
+                             dim3(kVerifyBlockWide), 0, s, V);
+      }
+      // the deferred jobs with the VM-capable paths, then the allow rules of
+      // the fast matches (grids: one VM scratch slot per lane)
+      hipLaunchKernelGGL(k_verify_slow<uint32_t>, dim3(e->vm_threads / 64), dim3(64), 0, s, V);
+      if (any_long) hipLaunchKernelGGL(k_verify_slow<uint64_t>, dim3(e->vm_threads / 64), dim3(64), 0, s, V);
+      hipLaunchKernelGGL(k_allow, dim3(e->vm_threads / 64), dim3(64), 0, s, V);
+    } else if (n_cands > (uint64_t)e->num_cus * kVerifyBlockWide * 4) {
       const uint32_t blocks = (uint32_t)std::min<uint64_t>((n_cands + kVerifyBlockWide - 1) / kVerifyBlockWide,
                                                            e->vm_threads / kVerifyBlockWide);  // (VM scratch per lane)
       hipLaunchKernelGGL((k_verify<kVerifyBlockWide, uint32_t>), dim3(std::max(1u, blocks)), dim3(kVerifyBlockWide), 0,
@@ -6436,13 +6869,14 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     if ((rc = read_ctrl(e, &c))) return rc;
     n_locs = c.locs;
     n_dropped = c.n_dropped;
+    n_deferred = c.n_defer;
     if (n_locs <= e->locs.n && c.n_caps <= e->caps.n && c.n_caps_big <= e->caps_big.n && c.n_redo <= e->redo.n &&
-        c.n_caps_run <= e->caps_run.n) {
+        c.n_caps_run <= e->caps_run.n && c.n_match <= e->matches.n) {
       verified = true;
       break;
     }
     // a list overflowed: grow it and re-run the search and the capture stages
-    loc_cap = std::max<uint64_t>(loc_cap, n_locs);
+    loc_cap = std::max<uint64_t>({loc_cap, n_locs, c.n_match});
     caps_cap = std::max<uint64_t>(caps_cap, c.n_caps);
     caps_big_cap = std::max<uint64_t>(caps_big_cap, c.n_caps_big);
     redo_cap = std::max<uint64_t>(redo_cap, c.n_redo);
@@ -6636,6 +7070,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   tm[12] = (double)scan_overflow;
   tm[13] = (double)n_events;
   tm[14] = (double)n_outputs;
+  tm[23] = (double)n_deferred;
   if (nbytes) {  // k_scan alone (the dominant, HBM-bound kernel)
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, e->ev[8], e->ev[9]));
@@ -6951,20 +7386,49 @@ static int stage_host_batch(tsg_engine* e, const tsg_file* files, size_t n_files
     }
   };
   const unsigned nt = nbytes < (64u << 20) ? 1u : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-  // chunks: packing chunk k+1 overlaps the DMA of chunk k
+  // chunks: the DMA of chunk k is issued as soon as every worker has packed
+  // its slice of it, while the workers go on to the next chunks (one set of
+  // threads per call: a spawn / join per 64 MiB chunk cost ~0.3 ms each)
   constexpr uint64_t kStageChunk = 64ull << 20;
+  const uint64_t n_chunks = (nbytes + kStageChunk - 1) / kStageChunk;
   bool ok = true;
-  for (uint64_t lo = 0; lo < nbytes && ok; lo += kStageChunk) {
-    const uint64_t hi = std::min(nbytes, lo + kStageChunk);
-    if (nt == 1) {
+  if (nt == 1 || n_chunks == 0) {
+    for (uint64_t lo = 0; lo < nbytes && ok; lo += kStageChunk) {
+      const uint64_t hi = std::min(nbytes, lo + kStageChunk);
       pack_range(lo, hi);
-    } else {
-      std::vector<std::thread> th;
-      for (unsigned t = 0; t < nt; ++t)
-        th.emplace_back(pack_range, lo + (hi - lo) * t / nt, lo + (hi - lo) * (t + 1) / nt);
-      for (auto& t : th) t.join();
+      ok = hipMemcpyAsync(e->data.p + lo, h + lo, hi - lo, hipMemcpyHostToDevice, s) == hipSuccess;
     }
-    ok = hipMemcpyAsync(e->data.p + lo, h + lo, hi - lo, hipMemcpyHostToDevice, s) == hipSuccess;
+  } else {
+    std::unique_ptr<std::atomic<unsigned>[]> done(new std::atomic<unsigned>[n_chunks]);
+    for (uint64_t c = 0; c < n_chunks; ++c) done[c].store(0, std::memory_order_relaxed);
+    std::atomic<bool> stop{false};
+    auto worker = [&](unsigned t) {
+      for (uint64_t c = 0; c < n_chunks && !stop.load(std::memory_order_relaxed); ++c) {
+        const uint64_t lo = c * kStageChunk, hi = std::min(nbytes, lo + kStageChunk);
+        pack_range(lo + (hi - lo) * t / nt, lo + (hi - lo) * (t + 1) / nt);
+        done[c].fetch_add(1, std::memory_order_release);
+      }
+    };
+    std::vector<std::thread> th;
+    unsigned started = 0;
+    try {
+      for (; started < nt; ++started) th.emplace_back(worker, started);
+    } catch (const std::system_error&) {
+    }
+    for (unsigned t = started; t < nt; ++t) {  // slices of threads that could not start: done here, up front
+      for (uint64_t c = 0; c < n_chunks; ++c) {
+        const uint64_t lo = c * kStageChunk, hi = std::min(nbytes, lo + kStageChunk);
+        pack_range(lo + (hi - lo) * t / nt, lo + (hi - lo) * (t + 1) / nt);
+        done[c].fetch_add(1, std::memory_order_release);
+      }
+    }
+    for (uint64_t c = 0; c < n_chunks && ok; ++c) {
+      while (done[c].load(std::memory_order_acquire) < nt) std::this_thread::yield();
+      const uint64_t lo = c * kStageChunk, hi = std::min(nbytes, lo + kStageChunk);
+      ok = hipMemcpyAsync(e->data.p + lo, h + lo, hi - lo, hipMemcpyHostToDevice, s) == hipSuccess;
+    }
+    if (!ok) stop.store(true);
+    for (auto& t : th) t.join();
   }
   for (size_t i = 0; i < n_files; ++i)
     if (files[i].path) memcpy(h + nbytes + poff[i], files[i].path, poff[i + 1] - poff[i]);
@@ -6999,7 +7463,7 @@ static int scan_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files
     delete res;
     return rc;
   }
-  res->impl.timings.resize(20, 0.0);
+  res->impl.timings.resize(std::max<size_t>(res->impl.timings.size(), 20), 0.0);
   res->impl.timings[18] = e->stage_ms[0];  // host pack into pinned staging
   res->impl.timings[19] = e->stage_ms[1];  // H2D
   *out = res;
@@ -7094,7 +7558,7 @@ static int analyze_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* fi
     if (bin[i]) R.file_flags[i] |= TSG_FILE_BINARY;
   // findings were built on the device from the CR-stripped batch Scan saw
 
-  res->impl.timings.resize(23, 0.0);
+  res->impl.timings.resize(std::max<size_t>(res->impl.timings.size(), 23), 0.0);
   res->impl.timings[18] = e->stage_ms[0];  // host pack into pinned staging
   res->impl.timings[19] = e->stage_ms[1];  // H2D
   {
@@ -7236,6 +7700,13 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
     }
   }
   e->gate_tm[15] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - wall0).count();
+  return TSG_OK;
+}
+
+int tsg_engine_force_verify_split(tsg_engine* e, int on) {
+  if (!e) return TSG_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(e->mu);
+  e->verify_split = on ? 1 : 0;
   return TSG_OK;
 }
 
