@@ -1816,7 +1816,9 @@ __device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, Pos 
   // end, so a block holding a content byte never leaves the allocation)
   const uintptr_t base = reinterpret_cast<uintptr_t>(text);
   Pos q = s;
+#ifdef TSG_EXPERIMENTS
   uint32_t same = 0;  // consecutive steps that kept the state (the skip engages only on a run)
+#endif
   while (q < n && st) {
     const uintptr_t addr = (base + q) & ~(uintptr_t)15;
     const u32x4 v = *as_global<__attribute__((address_space(1))) const u32x4>(reinterpret_cast<const void*>(addr));
@@ -1843,11 +1845,14 @@ __device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, Pos 
         st = 0;
         break;
       }
+#ifdef TSG_EXPERIMENTS
       const uint32_t prev_st = st;
+#endif
       st = e & kDfaStateMask;
       q += w;
       i += w;
       if (e & 0x4000u) last = q;
+#ifdef TSG_EXPERIMENTS
       same = st == prev_st ? same + 1 : 0;
       // the record is a global read: taken only once the state has kept
       // itself for kAccelRun steps (a short run costs less walked)
@@ -1872,6 +1877,7 @@ __device__ inline int dfa_anchored_dev(const DfaRef d, const uint8_t* text, Pos 
           break;  // reload the block at q
         }
       }
+#endif
     }
   }
   if (last < 0) return 0;
@@ -2395,6 +2401,7 @@ struct VerifyParams {
   uint32_t* defer;   // jobs k_verify_fast handed to k_verify_slow (capacity >= jobs)
   CapJob* matches;   // k_verify_fast's matches, for k_allow
   uint64_t match_cap;
+  uint32_t no_accel;  // 1 but in the exp build with TSG_ACCEL: DFA run acceleration (measured slower)
 };
 
 
@@ -3011,7 +3018,7 @@ __device__ __noinline__ uint32_t verify_dfa_job(const VerifyParams& V, uint32_t 
   const RuleDev& rd = V.rs.rules[rule];
   const DfaRef dref{kLds ? lds_T : V.rs.dfa_delta + rd.dfa_off, kLds ? lds_cls : V.rs.dfa_bytes + rd.dfa_cls_off,
                     rd.dfa_ncls, rd.dfa_start0, rd.dfa_start1, rd.dfa_smatch, rd.dfa_sym,
-                    (const uint32_t*)(V.rs.dfa_bytes + rd.dfa_accel_off),
+                    V.no_accel ? nullptr : (const uint32_t*)(V.rs.dfa_bytes + rd.dfa_accel_off),
                     (const uint4*)(V.rs.dfa_bytes + rd.dfa_accel_recs)};
   const uint32_t fm0 = rd.dfa_first[0], fm1 = rd.dfa_first[1], fm2 = rd.dfa_first[2], fm3 = rd.dfa_first[3];
   const uint32_t prog = rd.prog;
@@ -3144,7 +3151,7 @@ __device__ __forceinline__ int fast_dfa_job(const VerifyParams& V, uint32_t rule
   const RuleDev& rd = V.rs.rules[rule];
   const DfaRef dref{kLds ? lds_T : V.rs.dfa_delta + rd.dfa_off, kLds ? lds_cls : V.rs.dfa_bytes + rd.dfa_cls_off,
                     rd.dfa_ncls, rd.dfa_start0, rd.dfa_start1, rd.dfa_smatch, rd.dfa_sym,
-                    (const uint32_t*)(V.rs.dfa_bytes + rd.dfa_accel_off),
+                    V.no_accel ? nullptr : (const uint32_t*)(V.rs.dfa_bytes + rd.dfa_accel_off),
                     (const uint4*)(V.rs.dfa_bytes + rd.dfa_accel_recs)};
   const uint32_t fm0 = rd.dfa_first[0], fm1 = rd.dfa_first[1], fm2 = rd.dfa_first[2], fm3 = rd.dfa_first[3];
   IvIter<Pos> it;
@@ -5089,7 +5096,11 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
       // accelerable states (a private key's body, `.{0,N}` runs): the entry
       // on all but <= 3 ASCII bytes keeps the state with the same flags, so
       // the device skips such runs with vector compares (dfa_accel_skip)
+#ifdef TSG_EXPERIMENTS
       const DfaAccel acc = dfa_accel_records(r.dfa);
+#else
+      const DfaAccel acc{std::vector<uint32_t>(r.dfa.delta.size() / std::max<uint32_t>(1, r.dfa.ncls), 0xFFFFFFFFu), {}};
+#endif
       while (dbytes.size() & 15) dbytes.push_back(0);
       d.dfa_accel_off = (uint32_t)dbytes.size();  // per-state record index (u32), then the 32-byte records
       dbytes.insert(dbytes.end(), (const uint8_t*)acc.idx.data(), (const uint8_t*)(acc.idx.data() + acc.idx.size()));
@@ -6697,6 +6708,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     V.match_cap = e->matches.n;
     V.span_hi = (rs->ac.fast.size() || P.big.blob) && nbytes ? e->span_hi.p : nullptr;
     const bool prof = experiment_env("TSG_PROFILE_VERIFY") != nullptr;
+    V.no_accel = experiment_env("TSG_ACCEL") == nullptr;
     if (prof) {  // diagnostics only: the job count on the host
       HIP_TRY(hipMemcpyAsync(&n_jobs, e->nsel.p, 4, hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
