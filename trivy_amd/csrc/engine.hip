@@ -6535,6 +6535,8 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(hipMemcpyAsync(&e->ctrl.p->hits, &nh, 8, hipMemcpyHostToDevice, s));
     HIP_TRY(hipEventRecord(e->ev[9], s));
   }
+  Ctrl c_scan{};
+  bool have_c = false;  // c_scan holds the counters after the scan (k_uni_keywords changes none)
   for (int attempt = 0; attempt < 3 && !scanned; ++attempt) {
     HIP_TRY(hipMemsetAsync(e->nl_blocks.p, 0, n_nlb * 4, s));
     HIP_TRY(hipEventRecord(e->ev[8], s));
@@ -6543,8 +6545,9 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     // the fold-window pass reads the scan's rune count on the device; one
     // read of the counters afterwards checks every buffer of both passes
     if ((rc = launch_fold_windows(e, P, true))) return rc;
-    Ctrl c;
+    Ctrl& c = c_scan;
     if ((rc = read_ctrl(e, &c))) return rc;
+    have_c = true;
     const bool ev_lost = (rs->ac.fast.size() || P.big.blob) && c.ev_overflow > e->ev_overflow.n;
     const bool fold_lost = c.n_fold > P.fold_cap;
     const bool outs_lost = P.big.blob && c.outputs > P.big_out_cap;  // (k_big_walk's records)
@@ -6574,8 +6577,8 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   }
   if ((rc = launch_uni_keywords(e, P))) return rc;
   HIP_TRY(hipEventRecord(e->ev[2], s));
-  Ctrl c;
-  if ((rc = read_ctrl(e, &c))) return rc;
+  Ctrl c = c_scan;
+  if (!have_c && (rc = read_ctrl(e, &c))) return rc;  // (one host round trip fewer after a scan)
   const uint64_t n_hits = c.hits;
   const uint64_t scan_overflow = c.ev_overflow;
   const uint64_t n_outputs = c.outputs;
