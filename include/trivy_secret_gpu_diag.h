@@ -78,6 +78,13 @@ int tsg_ruleset_big_check(const tsg_ruleset* rs, const uint8_t* text, size_t len
  * 0 = unmodified.  *rc = TSG_OK (accepted) or TSG_ERR_INTERNAL (rejected). */
 int tsg_ruleset_big_forge_check(const tsg_ruleset* rs, int kind, int* rc);
 
+/* Visits per state of the keyword / anchor automaton walked over a host text
+ * (dense-row selection studies for k_scan_big): counts[n >= states], in the
+ * k_scan_big blob's numbering when blob != 0 (*n_dense = its dense rows: the
+ * ids at or past it are cold states), else in the automaton's own. */
+int tsg_ruleset_ac_visits(const tsg_ruleset* rs, const uint8_t* text, size_t len, int blob, uint64_t* counts,
+                          size_t n, uint32_t* n_dense);
+
 /* Candidate filter of rule i, run on host text from anchor position h:
  * *accept = 0 only when no match of the rule can contain an anchor hit at h
  * (k_expand drops such hits); *n_states = its DFA size (0 = no filter). */

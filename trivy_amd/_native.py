@@ -115,6 +115,9 @@ _SIGS = {
     "tsg_ruleset_dfa_accel_check": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
                                                    ctypes.c_size_t, ctypes.POINTER(ctypes.c_int),
                                                    ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_uint64)]),
+    "tsg_ruleset_ac_visits": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t,
+                                             ctypes.POINTER(ctypes.c_uint32)]),
     "tsg_engine_force_verify_split": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "tsg_ruleset_big_forge_check": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "tsg_ruleset_group_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int),

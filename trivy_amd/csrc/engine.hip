@@ -6137,6 +6137,33 @@ extern "C" int tsg_ruleset_dfa_accel_check(const tsg_ruleset* rs, size_t i, cons
   return TSG_OK;
 }
 
+// Visits per state of the keyword / anchor automaton over a host text
+// (diagnostics: dense-row selection studies); counts[blob order] with the
+// blob's numbering when blob != 0, else automaton ids.  n = states.
+extern "C" int tsg_ruleset_ac_visits(const tsg_ruleset* rs, const uint8_t* text, size_t len, int blob,
+                                     uint64_t* counts, size_t n, uint32_t* n_dense) {
+  if (!rs || (!text && len) || !counts || !n_dense) return TSG_ERR_INVALID_ARG;
+  const AcHost& ac = rs->ac;
+  if (n < ac.nstates) return TSG_ERR_INVALID_ARG;
+  BigBlobHost bb;
+  std::vector<uint32_t> at(ac.nstates);
+  for (uint32_t k = 0; k < ac.nstates; ++k) at[k] = k;
+  *n_dense = 0;
+  if (blob) {
+    if (!build_big_blob(ac, false, &bb)) return TSG_ERR_UNSUPPORTED;
+    for (uint32_t k = 0; k < ac.nstates; ++k) at[bb.ac_of[k]] = k;
+    *n_dense = bb.nd;
+  }
+  memset(counts, 0, n * sizeof(uint64_t));
+  const uint32_t K = ac.nclasses;
+  uint32_t a = 0;
+  for (size_t i = 0; i < len; ++i) {
+    a = ac.delta[(size_t)a * K + ac.cls[text[i]]] & 0x7FFFu;
+    ++counts[at[a]];
+  }
+  return TSG_OK;
+}
+
 // The blob validator against forged blobs (tests): the ruleset's blob with
 // one invariant broken -- kind 1: a cold state's failure link pointed at
 // itself (a cycle), 2: an overflow list's terminator removed, 3: a dense
