@@ -85,6 +85,12 @@ int tsg_ruleset_big_forge_check(const tsg_ruleset* rs, int kind, int* rc);
 int tsg_ruleset_ac_visits(const tsg_ruleset* rs, const uint8_t* text, size_t len, int blob, uint64_t* counts,
                           size_t n, uint32_t* n_dense);
 
+/* k_scan_big's blob keeps at least n cold-state records in LDS (default
+ * 4096); the rest are read from global memory.  Applies to blobs built after
+ * the call (rulesets compiled / first uploaded later); *previous = the old
+ * floor.  A GPU test sets 0 to send nearly every cold record to global. */
+int tsg_big_cold_lds_floor(uint32_t n, uint32_t* previous);
+
 /* Candidate filter of rule i, run on host text from anchor position h:
  * *accept = 0 only when no match of the rule can contain an anchor hit at h
  * (k_expand drops such hits); *n_states = its DFA size (0 = no filter). */

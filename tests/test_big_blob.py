@@ -69,3 +69,32 @@ def test_forged_blob_is_rejected(stress_rs, kind):
     rc = ctypes.c_int(-1)
     N.check(N.lib.tsg_ruleset_big_forge_check(sc._rs.handle, kind, ctypes.byref(rc)))
     assert rc.value == N.TSG_ERR_INTERNAL
+
+
+@pytest.mark.parametrize("floor", [0, 512])
+def test_global_cold_records_blob(tmp_path, floor):
+    """With a low LDS floor for the cold records the blob takes more dense
+    rows and leaves the deep states' records to global memory
+    (BigLds::gcold): the replay still equals the table, and the validator
+    accepts the blob and rejects its forgeries."""
+    prev = ctypes.c_uint32()
+    N.check(N.lib.tsg_big_cold_lds_floor(floor, ctypes.byref(prev)))
+    try:
+        rules = stress_rules.make_rules(20261019, 1000)
+        path = str(tmp_path / "trivy-secret.yaml")
+        stress_rules.write_config(path, rules)
+        sc = S.new_scanner(S.parse_config(path))
+        files = stress_rules.make_corpus(11, rules, 20, long_line_bytes=10_000)
+        rng = random.Random(6)
+        text = b"".join(d for _, d in files) + bytes(rng.randrange(256) for _ in range(100_000))
+        mm, hops, nd = _check(sc, text, 0)
+        assert mm == 0 and hops > 0
+        for kind in (0, 1, 2, 3, 4):
+            rc = ctypes.c_int(-1)
+            N.check(N.lib.tsg_ruleset_big_forge_check(sc._rs.handle, kind, ctypes.byref(rc)))
+            assert rc.value == (N.TSG_OK if kind == 0 else N.TSG_ERR_INTERNAL)
+    finally:
+        N.check(N.lib.tsg_big_cold_lds_floor(prev.value, None))
+    assert prev.value == 4096
+    _, _, nd_default = _check(S.new_scanner(S.parse_config(path)), text[:1000], 0)
+    assert nd > nd_default  # the low floor bought dense rows

@@ -32,3 +32,7 @@ cold = sum(vs[i] for i in range(S_) if i not in dense_set)
 print("train-frequency dense set: cold visits per byte", cold/n)
 # how many distinct states visited at all
 print("states visited in test:", (vs>0).sum(), " top-nd coverage of visits:", np.sort(vs)[::-1][:nd].sum()/vs.sum())
+
+# cold visits per byte if the blob's dense region (its own order) held more rows
+for nd2 in (1202, 1400, 1680, 2000, 2445):
+    print(f"dense rows {nd2}: cold visits per byte {vs[nd2:].sum() / n:.5f}")

@@ -119,6 +119,7 @@ _SIGS = {
                                              ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t,
                                              ctypes.POINTER(ctypes.c_uint32)]),
     "tsg_engine_force_verify_split": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "tsg_big_cold_lds_floor": (ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
     "tsg_ruleset_big_forge_check": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "tsg_ruleset_group_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int),
                                              ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_uint32),

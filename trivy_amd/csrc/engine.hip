@@ -154,7 +154,8 @@ inline const char* experiment_env(const char* name);
 struct BigDev {
   const uint8_t* blob;  // global copy
   uint32_t blob_bytes, n_dense, n_cold;
-  uint32_t o_cold, o_eval;  // byte offsets: uint2 [n_cold], u32 lists
+  uint32_t o_cold, o_eval;  // byte offsets: uint2 [n_cold] records, u32 lists (before the records)
+  uint32_t lds_bytes, n_cold_lds;  // the prefix staged in LDS: every list and the first n_cold_lds records
   const uint16_t* ac_of;    // blob state id -> the automaton's (AcDev) state id
 };
 
@@ -790,26 +791,45 @@ constexpr uint32_t kBigThreads = 1024;
 // per lane, each with a 2 x 16-byte ring, every chain's dense row read issued
 // before any cold walk -- 8.87 vs 9.63 ms (one chain, 8 x 16 B) on configs[4]
 constexpr int kBigMode = 8, kBigChains = 2, kBigRing = 2;
-constexpr uint32_t kBigLdsMax = 152 * 1024;
+constexpr uint32_t kBigLdsMax = 160 * 1024 - 256;  // the blob's LDS part (k_big_walk adds 80 B of its own)
+// Cold records kept in LDS at least (the rest of the blob's cold records
+// are read from global memory, L2-resident): more dense rows pay more than
+// LDS records of deep states -- on the bench text, cold-state visits per
+// byte are 0.0033 past 1202 dense rows and 0.0011 past 1400, 0.0003 past
+// 2445 (tools/big_visits.py, profiles/r04j/big_visits.txt).
+constexpr uint32_t kBigColdLdsMin = 4096;
+// (tsg_big_cold_lds_floor, diagnostics: a GPU test sets 0 to read nearly
+// every cold record from global memory)
+static std::atomic<uint32_t> g_big_cold_floor{kBigColdLdsMin};
 
 struct BigLds {
   const uint8_t* cls;
   const uint16_t* dense;
-  const uint2* cold;
+  const uint2* cold;   // LDS: records [0, CL)
+  __attribute__((address_space(1))) const uint32_t* gcold;  // global: every record, as dword pairs (read past CL)
   const uint32_t* eval;
-  uint32_t K, ND;
+  uint32_t K, ND, CL;
 };
 
 __device__ inline BigLds big_lds(const BigDev& B, const uint8_t* smem, uint32_t K) {
   return BigLds{smem, (const uint16_t*)(smem + 256), (const uint2*)(smem + B.o_cold),
-                (const uint32_t*)(smem + B.o_eval), K, B.n_dense};
+                (__attribute__((address_space(1))) const uint32_t*)(B.blob + B.o_cold),
+                (const uint32_t*)(smem + B.o_eval), K, B.n_dense, B.n_cold_lds};
 }
 
 // delta(st, c): own entry of a cold state, else its failure state's (the
-// chain ends in a dense row).  Entry bit 15 = output state.
+// chain ends in a dense row).  Entry bit 15 = output state.  The records of
+// the deepest (rarely visited) cold states are read from global memory.
 __device__ inline uint32_t big_next(const BigLds& L, uint32_t st, uint32_t c) {
   while (st >= L.ND) {
-    const uint2 r = L.cold[st - L.ND];  // x: c1 | c2 << 8 | entry1 << 16, y: entry2 | fail << 16
+    const uint32_t j = st - L.ND;
+    uint2 r;  // x: c1 | c2 << 8 | entry1 << 16, y: entry2 | fail << 16
+    if (j < L.CL) {
+      r = L.cold[j];
+    } else {  // (a global load of its own: a generic one would wait for the batch prefetches too)
+      r.x = L.gcold[2 * j];
+      r.y = L.gcold[2 * j + 1];
+    }
     if (c == (r.x & 0xFFu)) return r.x >> 16;
     if (c == ((r.x >> 8) & 0xFFu)) return r.y & 0xFFFFu;
     if ((r.x & 0xFFu) == kBigMore) {
@@ -821,7 +841,7 @@ __device__ inline uint32_t big_next(const BigLds& L, uint32_t st, uint32_t c) {
     }
     st = r.y >> 16;
   }
-  return L.dense[st * L.K + c];
+  return L.dense[__umul24(st, L.K) + c];
 }
 
 // 8 bytes (two dwords) of each of CH chains through the automaton from their
@@ -849,12 +869,23 @@ __device__ inline void big_group(const BigLds& L, uint32_t (&e)[CH], const uint3
     uint32_t nx[CH];
     if (kMode & 10) {
 #pragma unroll
-      for (int h = 0; h < CH; ++h) nx[h] = L.dense[min(e[h], L.ND - 1) * L.K + c[h][j]];
+      for (int h = 0; h < CH; ++h)  // (byte offset: one v_mad_u32_u24)
+        nx[h] = *(const uint16_t*)((const uint8_t*)L.dense + (__umul24(min(e[h], L.ND - 1), 2 * L.K) + 2 * c[h][j]));
     }
-    if (!(kMode & 2)) {
+    if ((kMode & 10) == 8) {
+      // one wave-uniform test for every chain (a divergent if per chain cost
+      // three scalar exec-mask instructions per byte each)
+      bool cold = false;
 #pragma unroll
-      for (int h = 0; h < CH; ++h)
-        if (!(kMode & 8) || e[h] >= L.ND) nx[h] = big_next(L, e[h], c[h][j]);
+      for (int h = 0; h < CH; ++h) cold |= e[h] >= L.ND;
+      if (__ballot(cold)) {
+#pragma unroll
+        for (int h = 0; h < CH; ++h)
+          if (e[h] >= L.ND) nx[h] = big_next(L, e[h], c[h][j]);
+      }
+    } else if (!(kMode & 2)) {
+#pragma unroll
+      for (int h = 0; h < CH; ++h) nx[h] = big_next(L, e[h], c[h][j]);
     }
 #pragma unroll
     for (int h = 0; h < CH; ++h) {
@@ -892,7 +923,7 @@ template <int kMode = 0, int CH = 1, int V = 8 / CH>
 __global__ __launch_bounds__(kBigThreads) void k_scan_big(ScanParams P) {
   extern __shared__ __align__(16) uint8_t smem[];
   const BigDev& B = P.big;
-  for (uint32_t i = threadIdx.x; i < B.blob_bytes / 4; i += kBigThreads)
+  for (uint32_t i = threadIdx.x; i < B.lds_bytes / 4; i += kBigThreads)
     ((uint32_t*)smem)[i] = ((const uint32_t*)B.blob)[i];
   __syncthreads();
   const BigLds L = big_lds(B, smem, P.rs.ac.nclasses);
@@ -1069,7 +1100,7 @@ __device__ inline uint32_t block_incl_sum32(uint32_t v, uint32_t* lds16, uint32_
 __global__ __launch_bounds__(1024) void k_big_walk(ScanParams P, uint32_t n_waves) {
   extern __shared__ __align__(16) uint8_t smem[];
   const BigDev& B = P.big;
-  for (uint32_t i = threadIdx.x; i < B.blob_bytes / 4; i += blockDim.x)
+  for (uint32_t i = threadIdx.x; i < B.lds_bytes / 4; i += blockDim.x)
     ((uint32_t*)smem)[i] = ((const uint32_t*)B.blob)[i];
   __shared__ uint32_t s32[16];
   __shared__ unsigned long long obase;
@@ -1777,7 +1808,7 @@ struct DfaRef {
 // From q: the first position whose byte is not in the 128-bit stay set bm
 // (every byte >= 0x80 is not), else n -- 16 bytes per load, one bitmap test
 // per byte, no table lookups.  The batch is padded past every file end.
-constexpr uint32_t kAccelRun = 8;
+[[maybe_unused]] constexpr uint32_t kAccelRun = 8;  // (used by the TSG_EXPERIMENTS build)
 template <class Pos>
 __device__ inline Pos dfa_accel_skip(const uint8_t* text, Pos n, Pos q, const uint4 bm) {
   const uintptr_t base = reinterpret_cast<uintptr_t>(text);
@@ -4603,6 +4634,7 @@ struct BigBlobHost {
   std::vector<uint8_t> blob;
   std::vector<uint16_t> ac_of;  // blob state id -> automaton state id
   uint32_t nd = 0, cold = 0, o_cold = 0, o_eval = 0;
+  uint32_t lds_bytes = 0, cold_lds = 0;  // the LDS prefix: classes, dense rows, lists, cold records [0, cold_lds)
 };
 static bool build_big_blob(const AcHost& ac, bool bfs, BigBlobHost* out) {
   if (ac.fail.size() != ac.nstates || ac.nclasses > kBigMore || ac.nstates > 0x8000u || !ac.nstates) return false;
@@ -4656,25 +4688,30 @@ static bool build_big_blob(const AcHost& ac, bool bfs, BigBlobHost* out) {
   std::vector<uint64_t> suffix(S + 1, 0);  // list words of cold states >= s
   for (uint32_t st = S; st-- > 0;) suffix[st] = suffix[st + 1] + (edges[st].size() > 2 ? edges[st].size() + 1 : 0);
   auto a8 = [](uint64_t x) { return (x + 7) & ~7ull; };
-  auto bytes_for = [&](uint32_t nd) {
-    return a8(256 + (uint64_t)nd * K * 2) + (uint64_t)(S - nd) * 8 + suffix[nd] * 4;
+  // layout: classes | dense rows | lists | cold records; LDS holds the prefix
+  // through the first kBigColdLdsMin records (or all of them)
+  uint32_t cold_min = g_big_cold_floor.load();
+  if (const char* e = experiment_env("TSG_BIG_COLD_LDS")) cold_min = (uint32_t)atoi(e);
+  auto lds_for = [&](uint32_t nd) {
+    return a8(a8(256 + (uint64_t)nd * K * 2) + suffix[nd] * 4) + (uint64_t)std::min<uint32_t>(S - nd, cold_min) * 8;
   };
-  if (bytes_for(1) > kBigLdsMax) return false;
-  uint32_t lo = 1, hi = S;  // a large nd with bytes_for(nd) <= kBigLdsMax (bytes mostly grow with nd)
+  if (lds_for(1) > kBigLdsMax) return false;
+  uint32_t lo = 1, hi = S;  // the largest nd that fits (bytes mostly grow with nd)
   {
     while (lo < hi) {
       const uint32_t mid = (lo + hi + 1) / 2;
-      if (bytes_for(mid) <= kBigLdsMax) lo = mid;
+      if (lds_for(mid) <= kBigLdsMax) lo = mid;
       else hi = mid - 1;
     }
     const uint32_t nd = lo, cold = S - nd;
-    std::vector<uint8_t> blob(bytes_for(nd), 0);
+    const uint32_t o_eval = (uint32_t)a8(256 + (uint64_t)nd * K * 2);
+    const uint32_t o_cold = (uint32_t)a8(o_eval + suffix[nd] * 4);
+    const uint32_t cold_lds = (uint32_t)std::min<uint64_t>(cold, (kBigLdsMax - o_cold) / 8);
+    std::vector<uint8_t> blob(o_cold + (size_t)cold * 8, 0);
     memcpy(blob.data(), ac.cls, 256);
     uint16_t* dense = (uint16_t*)(blob.data() + 256);
     for (uint32_t n = 0; n < nd; ++n)
       for (uint32_t c = 0; c < K; ++c) dense[(size_t)n * K + c] = (uint16_t)entry(order[n], c);
-    const uint32_t o_cold = (uint32_t)a8(256 + (uint64_t)nd * K * 2);
-    const uint32_t o_eval = o_cold + cold * 8;
     uint32_t* rec = (uint32_t*)(blob.data() + o_cold);
     uint32_t* ev = (uint32_t*)(blob.data() + o_eval);
     uint32_t k = 0;
@@ -4693,6 +4730,8 @@ static bool build_big_blob(const AcHost& ac, bool bfs, BigBlobHost* out) {
         ev[k++] = 0xFFFFFFFFu;
       }
     }
+    out->lds_bytes = o_cold + cold_lds * 8;
+    out->cold_lds = cold_lds;
     out->ac_of.assign(S, 0);
     for (uint32_t n = 0; n < S; ++n) out->ac_of[n] = (uint16_t)order[n];
     out->blob.swap(blob);
@@ -4716,8 +4755,9 @@ static std::string validate_big_blob(const BigBlobHost& bb, uint32_t K, uint32_t
   if (K == 0 || K >= kBigMore || S == 0 || S > 0x8000u) return "class or state count out of range";
   if (bb.nd == 0 || bb.nd + bb.cold != S || bb.ac_of.size() != S || bb.ac_of[0] != 0)
     return "state 0 is not the dense root";
-  if (bb.o_cold < 256 + (uint64_t)bb.nd * K * 2 || bb.o_eval != bb.o_cold + (uint64_t)bb.cold * 8 ||
-      bb.o_eval > bb.blob.size() || bb.blob.size() > kBigLdsMax)
+  if (bb.o_eval < 256 + (uint64_t)bb.nd * K * 2 || bb.o_cold < bb.o_eval || (bb.o_cold - bb.o_eval) % 4 ||
+      bb.blob.size() != bb.o_cold + (uint64_t)bb.cold * 8 || bb.cold_lds > bb.cold ||
+      bb.lds_bytes != bb.o_cold + (uint64_t)bb.cold_lds * 8 || bb.lds_bytes > kBigLdsMax)
     return "blob sections overlap or exceed the LDS budget";
   for (int b = 0; b < 256; ++b)
     if (bb.blob[b] >= K) return "byte class out of range";
@@ -4726,7 +4766,7 @@ static std::string validate_big_blob(const BigBlobHost& bb, uint32_t K, uint32_t
     if ((dense[i] & 0x7FFFu) >= S) return "dense entry out of range";
   const uint32_t* rec = (const uint32_t*)(bb.blob.data() + bb.o_cold);
   const uint32_t* ev = (const uint32_t*)(bb.blob.data() + bb.o_eval);
-  const uint64_t n_ev = (bb.blob.size() - bb.o_eval) / 4;
+  const uint64_t n_ev = (bb.o_cold - bb.o_eval) / 4;  // (every list sits in the LDS prefix)
   for (uint32_t j = 0; j < bb.cold; ++j) {
     const uint32_t st = bb.nd + j, x = rec[2 * j], y = rec[2 * j + 1];
     if ((y >> 16) >= st) return "a cold state's failure link does not point to a shallower state";
@@ -4775,7 +4815,7 @@ static uint32_t big_next_host(const BigBlobHost& bb, uint32_t K, uint32_t st, ui
   const uint16_t* dense = (const uint16_t*)(bb.blob.data() + 256);
   const uint32_t* rec = (const uint32_t*)(bb.blob.data() + bb.o_cold);
   const uint32_t* ev = (const uint32_t*)(bb.blob.data() + bb.o_eval);
-  const size_t n_ev = (bb.blob.size() - bb.o_eval) / 4;
+  const size_t n_ev = (bb.o_cold - bb.o_eval) / 4;
   while (st >= bb.nd) {
     if (++*hops > 64) return 0xFFFFFFFFu;  // (a cycle: the device would hang)
     const uint32_t x = rec[2 * (st - bb.nd)], y = rec[2 * (st - bb.nd) + 1];
@@ -5295,7 +5335,8 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
       HIP_TRY(hipMemcpy(im.big.p, bb.blob.data(), bb.blob.size(), hipMemcpyHostToDevice));
       HIP_TRY(im.big_ac_of.ensure(bb.ac_of.size()));
       HIP_TRY(hipMemcpy(im.big_ac_of.p, bb.ac_of.data(), bb.ac_of.size() * 2, hipMemcpyHostToDevice));
-      im.big_view = BigDev{im.big.p, (uint32_t)bb.blob.size(), bb.nd, bb.cold, bb.o_cold, bb.o_eval, im.big_ac_of.p};
+      im.big_view = BigDev{im.big.p, (uint32_t)bb.blob.size(), bb.nd, bb.cold, bb.o_cold, bb.o_eval, bb.lds_bytes,
+                           bb.cold_lds, im.big_ac_of.p};
     }
   }
   HIP_TRY(im.out_off.ensure(ac.out_off.size()));
@@ -5711,7 +5752,8 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
         {0, 1, 8, k_scan_big<0, 1>},     {1, 1, 8, k_scan_big<1, 1>},     {2, 1, 8, k_scan_big<2, 1>},
         {3, 1, 8, k_scan_big<3, 1>},     {4, 1, 8, k_scan_big<4, 1>},     {0, 2, 4, k_scan_big<0, 2>},
         {8, 2, 4, k_scan_big<8, 2>},     {0, 2, 2, k_scan_big<0, 2, 2>},  {8, 2, 2, k_scan_big<8, 2, 2>},
-        {12, 2, 2, k_scan_big<12, 2, 2>}, {2, 2, 2, k_scan_big<2, 2, 2>}, {4, 1, 4, k_scan_big<4, 1, 4>}};
+        {12, 2, 2, k_scan_big<12, 2, 2>}, {2, 2, 2, k_scan_big<2, 2, 2>}, {4, 1, 4, k_scan_big<4, 1, 4>},
+        {9, 2, 2, k_scan_big<9, 2, 2>},  {3, 2, 2, k_scan_big<3, 2, 2>}};
     BigFn pick = nullptr;
     for (const BigV& x : kBigVariants)
       if (x.mode == big_mode && x.ch == big_ch && x.v == big_v) pick = x.fn;
@@ -5733,11 +5775,11 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     P.ev_overflow = e->ev_overflow.p;
     P.ev_overflow_cap = e->ev_overflow.n;
     HIP_TRY(hipMemsetAsync(&P.ctrl->ev_overflow, 0, 8, s));
-    HIP_TRY(hipFuncSetAttribute(big_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.big.blob_bytes));
+    HIP_TRY(hipFuncSetAttribute(big_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.big.lds_bytes));
     if (e->events) HIP_TRY(hipEventRecord(e->ev[10], s));
     (void)big_mode;
     void* big_args[] = {&P};
-    HIP_TRY(hipLaunchKernel(big_fn, dim3(blocks), dim3(nt), big_args, P.big.blob_bytes, s));
+    HIP_TRY(hipLaunchKernel(big_fn, dim3(blocks), dim3(nt), big_args, P.big.lds_bytes, s));
     HIP_TRY(hipGetLastError());
     if (e->events) HIP_TRY(hipEventRecord(e->ev[11], s));
     e->fast_timed = e->events;
@@ -5745,9 +5787,9 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     P.big_outs = e->big_outs.p;
     P.big_out_cap = e->big_outs.n;
     HIP_TRY(hipFuncSetAttribute((const void*)k_big_walk, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)P.big.blob_bytes));
+                                (int)P.big.lds_bytes));
     hipLaunchKernelGGL(k_big_walk, dim3((uint32_t)std::min<uint64_t>(n_waves + 1, e->num_cus)), dim3(1024),
-                       P.big.blob_bytes, s, P, (uint32_t)n_waves);
+                       P.big.lds_bytes, s, P, (uint32_t)n_waves);
     hipLaunchKernelGGL(k_big_resolve, dim3(e->num_cus * 8), dim3(kResolveThreads), 0, s, P);
     HIP_TRY(hipGetLastError());
   } else {
@@ -6140,6 +6182,12 @@ extern "C" int tsg_ruleset_dfa_accel_check(const tsg_ruleset* rs, size_t i, cons
 // Visits per state of the keyword / anchor automaton over a host text
 // (diagnostics: dense-row selection studies); counts[blob order] with the
 // blob's numbering when blob != 0, else automaton ids.  n = states.
+extern "C" int tsg_big_cold_lds_floor(uint32_t n, uint32_t* previous) {
+  const uint32_t was = g_big_cold_floor.exchange(n);
+  if (previous) *previous = was;
+  return TSG_OK;
+}
+
 extern "C" int tsg_ruleset_ac_visits(const tsg_ruleset* rs, const uint8_t* text, size_t len, int blob,
                                      uint64_t* counts, size_t n, uint32_t* n_dense) {
   if (!rs || (!text && len) || !counts || !n_dense) return TSG_ERR_INVALID_ARG;
@@ -6177,7 +6225,7 @@ extern "C" int tsg_ruleset_big_forge_check(const tsg_ruleset* rs, int kind, int*
   if (!build_big_blob(ac, false, &bb)) return TSG_ERR_UNSUPPORTED;
   uint32_t* rec = (uint32_t*)(bb.blob.data() + bb.o_cold);
   uint32_t* ev = (uint32_t*)(bb.blob.data() + bb.o_eval);
-  const uint64_t n_ev = (bb.blob.size() - bb.o_eval) / 4;
+  const uint64_t n_ev = (bb.o_cold - bb.o_eval) / 4;
   if (kind == 1) {
     if (!bb.cold) return TSG_ERR_UNSUPPORTED;
     const uint32_t j = bb.cold / 2;
