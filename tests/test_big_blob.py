@@ -59,9 +59,9 @@ def test_big_blob_builtin_automaton():
 def test_forged_blob_is_rejected(stress_rs, kind):
     """A malformed blob is an error, never a device walk that cannot end: the
     validator the engine runs before every upload (and tsg_ruleset_compile
-    before handing out a ruleset) rejects a failure-link cycle, an
-    unterminated overflow list and out-of-range entries / classes, and
-    accepts the ruleset's real blob."""
+    before handing out a ruleset) rejects a cold record whose ancestor row is
+    not a dense row (kind 1), an unterminated overflow list and out-of-range
+    entries / classes, and accepts the ruleset's real blob."""
     sc, _ = stress_rs
     rc = ctypes.c_int(-1)
     N.check(N.lib.tsg_ruleset_big_forge_check(sc._rs.handle, 0, ctypes.byref(rc)))

@@ -817,27 +817,34 @@ __device__ inline BigLds big_lds(const BigDev& B, const uint8_t* smem, uint32_t 
                 (const uint32_t*)(smem + B.o_eval), K, B.n_dense, B.n_cold_lds};
 }
 
-// delta(st, c): own entry of a cold state, else its failure state's (the
-// chain ends in a dense row).  Entry bit 15 = output state.  The records of
-// the deepest (rarely visited) cold states are read from global memory.
+// delta(st, c): a cold state's own entry (where it differs from its first
+// dense ancestor), else the ancestor's dense entry.  Entry bit 15 = output
+// state.  The records of the deepest (rarely visited) cold states are read
+// from global memory.
+__device__ inline uint2 big_rec(const BigLds& L, uint32_t j) {
+  uint2 r;  // x: c1 | c2 << 8 | entry1 << 16, y: entry2 | dense ancestor << 16
+  if (j < L.CL) {
+    r = L.cold[j];
+  } else {  // (a global load of its own: a generic one would wait for the batch prefetches too)
+    r.x = L.gcold[2 * j];
+    r.y = L.gcold[2 * j + 1];
+  }
+  return r;
+}
+__device__ inline uint32_t big_list(const BigLds& L, uint2 r, uint32_t c) {  // 0xFFFFFFFF: not listed
+  for (uint32_t k = (r.x >> 16) | ((r.y & 0xFFFFu) << 16);; ++k) {
+    const uint32_t v = L.eval[k];
+    if (v == 0xFFFFFFFFu || (v >> 16) == c) return v == 0xFFFFFFFFu ? v : (v & 0xFFFFu);
+  }
+}
 __device__ inline uint32_t big_next(const BigLds& L, uint32_t st, uint32_t c) {
-  while (st >= L.ND) {
-    const uint32_t j = st - L.ND;
-    uint2 r;  // x: c1 | c2 << 8 | entry1 << 16, y: entry2 | fail << 16
-    if (j < L.CL) {
-      r = L.cold[j];
-    } else {  // (a global load of its own: a generic one would wait for the batch prefetches too)
-      r.x = L.gcold[2 * j];
-      r.y = L.gcold[2 * j + 1];
-    }
+  if (st >= L.ND) {
+    const uint2 r = big_rec(L, st - L.ND);
     if (c == (r.x & 0xFFu)) return r.x >> 16;
     if (c == ((r.x >> 8) & 0xFFu)) return r.y & 0xFFFFu;
     if ((r.x & 0xFFu) == kBigMore) {
-      for (uint32_t k = (r.x >> 16) | (r.y << 16);; ++k) {
-        const uint32_t v = L.eval[k];
-        if (v == 0xFFFFFFFFu) break;
-        if ((v >> 16) == c) return v & 0xFFFFu;
-      }
+      const uint32_t v = big_list(L, r, c);
+      if (v != 0xFFFFFFFFu) return v;
     }
     st = r.y >> 16;
   }
@@ -848,9 +855,10 @@ __device__ inline uint32_t big_next(const BigLds& L, uint32_t st, uint32_t c) {
 // entries e[c]; acc[c] = the OR of a chain's entries (bit 15 = some output
 // state was reached).  The chains are independent, so their row lookups
 // overlap in one lane.  kMode != 0 only in the -DTSG_EXPERIMENTS build
-// (TSG_BIG_VARIANT; bits 0/1 are timing bounds with wrong results): bit 0 =
+// (TSG_BIG_VARIANT; bits 0/1/4 are timing bounds with wrong results): bit 0 =
 // class from ALU instead of LDS, bit 1 = dense rows only, bit 3 = every
-// chain's dense row read issued before any cold walk.
+// chain's dense row read issued before any cold walk, bit 4 (with 3) = the
+// per-byte cold test and branch without the cold walk.
 template <int kMode, int CH>
 __device__ inline void big_group(const BigLds& L, uint32_t (&e)[CH], const uint32_t (&d)[2 * CH],
                                  uint32_t (&acc)[CH]) {
@@ -879,9 +887,36 @@ __device__ inline void big_group(const BigLds& L, uint32_t (&e)[CH], const uint3
 #pragma unroll
       for (int h = 0; h < CH; ++h) cold |= e[h] >= L.ND;
       if (__ballot(cold)) {
+        if (kMode & 16) {  // timing bound (wrong results): the test and branch without the cold walk
 #pragma unroll
-        for (int h = 0; h < CH; ++h)
-          if (e[h] >= L.ND) nx[h] = big_next(L, e[h], c[h][j]);
+          for (int h = 0; h < CH; ++h) nx[h] ^= e[h] >= L.ND ? 1u : 0u;
+        } else {
+          // every lane, both chains: record, then the row (own entry or the
+          // dense ancestor's), two LDS round trips per chain set; global
+          // records and overflow lists only for the lanes that have them
+          uint2 r[CH];
+          bool isc[CH];
+#pragma unroll
+          for (int h = 0; h < CH; ++h) {
+            isc[h] = e[h] >= L.ND;
+            const uint32_t jj = isc[h] ? e[h] - L.ND : 0u;
+            r[h] = L.cold[min(jj, L.CL - 1)];
+            if (jj >= L.CL) r[h] = big_rec(L, jj);
+          }
+          uint32_t dn[CH];
+#pragma unroll
+          for (int h = 0; h < CH; ++h) dn[h] = L.dense[__umul24(isc[h] ? r[h].y >> 16 : 0u, L.K) + c[h][j]];
+#pragma unroll
+          for (int h = 0; h < CH; ++h) {
+            const uint32_t cc = c[h][j], c1 = r[h].x & 0xFFu, c2 = (r[h].x >> 8) & 0xFFu;
+            uint32_t v = cc == c1 ? r[h].x >> 16 : cc == c2 ? r[h].y & 0xFFFFu : dn[h];
+            if (c1 == kBigMore && isc[h]) {
+              const uint32_t w = big_list(L, r[h], cc);
+              if (w != 0xFFFFFFFFu) v = w;
+            }
+            if (isc[h]) nx[h] = v;
+          }
+        }
       }
     } else if (!(kMode & 2)) {
 #pragma unroll
@@ -4679,33 +4714,52 @@ static bool build_big_blob(const AcHost& ac, bool bfs, BigBlobHost* out) {
     const uint16_t v = ac.delta[(size_t)st * K + c];
     return (uint32_t)((v & 0x8000u) | at[v & 0x7FFFu]);
   };
-  std::vector<std::vector<uint32_t>> edges(S);  // per blob state: class << 16 | entry where it differs from fail
-  for (uint32_t n = 1; n < S; ++n) {
-    const uint32_t st = order[n], f = ac.fail[st];
+  // A cold state's record is flat: its entries where they differ from its
+  // first dense ancestor d on the failure chain (delta(s,c) = delta(d,c) for
+  // every other class, since every state between s and d defers to its own
+  // failure state there), and d itself -- one record and one dense row per
+  // cold byte, no failure-chain walk.
+  auto dense_anc = [&](uint32_t n, uint32_t nd) {  // blob id of n's first dense ancestor
+    uint32_t a = at[ac.fail[order[n]]];
+    while (a >= nd) a = at[ac.fail[order[a]]];
+    return a;
+  };
+  auto flat_edges = [&](uint32_t n, uint32_t d, std::vector<uint32_t>* E) {  // class << 16 | entry
+    E->clear();
+    const uint32_t st = order[n], ds = order[d];
     for (uint32_t c = 0; c < K; ++c)
-      if (ac.delta[(size_t)st * K + c] != ac.delta[(size_t)f * K + c]) edges[n].push_back((c << 16) | entry(st, c));
-  }
-  std::vector<uint64_t> suffix(S + 1, 0);  // list words of cold states >= s
-  for (uint32_t st = S; st-- > 0;) suffix[st] = suffix[st + 1] + (edges[st].size() > 2 ? edges[st].size() + 1 : 0);
+      if (ac.delta[(size_t)st * K + c] != ac.delta[(size_t)ds * K + c]) E->push_back((c << 16) | entry(st, c));
+  };
+  std::vector<uint32_t> E;
+  auto list_words = [&](uint32_t nd) {
+    uint64_t w = 0;
+    for (uint32_t n = nd; n < S; ++n) {
+      flat_edges(n, dense_anc(n, nd), &E);
+      if (E.size() > 2) w += E.size() + 1;
+    }
+    return w;
+  };
   auto a8 = [](uint64_t x) { return (x + 7) & ~7ull; };
   // layout: classes | dense rows | lists | cold records; LDS holds the prefix
   // through the first kBigColdLdsMin records (or all of them)
   uint32_t cold_min = g_big_cold_floor.load();
   if (const char* e = experiment_env("TSG_BIG_COLD_LDS")) cold_min = (uint32_t)atoi(e);
+  cold_min = std::max(cold_min, 1u);  // (the device walk reads record min(j, CL - 1) in every lane)
   auto lds_for = [&](uint32_t nd) {
-    return a8(a8(256 + (uint64_t)nd * K * 2) + suffix[nd] * 4) + (uint64_t)std::min<uint32_t>(S - nd, cold_min) * 8;
+    return a8(a8(256 + (uint64_t)nd * K * 2) + list_words(nd) * 4) + (uint64_t)std::min<uint32_t>(S - nd, cold_min) * 8;
   };
-  if (lds_for(1) > kBigLdsMax) return false;
-  uint32_t lo = 1, hi = S;  // the largest nd that fits (bytes mostly grow with nd)
+  // the largest nd that fits: dense bytes grow with nd while the flat
+  // records' lists shrink (few dense ancestors = long lists), so step down
+  // from the most rows the dense part alone allows, coarse then fine
+  uint32_t nd = (uint32_t)std::min<uint64_t>(S, (kBigLdsMax - 256) / (2 * (uint64_t)K));
+  while (nd > 16 && lds_for(nd) > kBigLdsMax) nd -= 16;
+  while (nd > 1 && lds_for(nd) > kBigLdsMax) --nd;
+  if (!nd || lds_for(nd) > kBigLdsMax) return false;
+  while (nd < S && lds_for(nd + 1) <= kBigLdsMax) ++nd;
   {
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi + 1) / 2;
-      if (lds_for(mid) <= kBigLdsMax) lo = mid;
-      else hi = mid - 1;
-    }
-    const uint32_t nd = lo, cold = S - nd;
+    const uint32_t cold = S - nd;
     const uint32_t o_eval = (uint32_t)a8(256 + (uint64_t)nd * K * 2);
-    const uint32_t o_cold = (uint32_t)a8(o_eval + suffix[nd] * 4);
+    const uint32_t o_cold = (uint32_t)a8(o_eval + list_words(nd) * 4);
     const uint32_t cold_lds = (uint32_t)std::min<uint64_t>(cold, (kBigLdsMax - o_cold) / 8);
     std::vector<uint8_t> blob(o_cold + (size_t)cold * 8, 0);
     memcpy(blob.data(), ac.cls, 256);
@@ -4716,16 +4770,16 @@ static bool build_big_blob(const AcHost& ac, bool bfs, BigBlobHost* out) {
     uint32_t* ev = (uint32_t*)(blob.data() + o_eval);
     uint32_t k = 0;
     for (uint32_t j = 0; j < cold; ++j) {
-      const std::vector<uint32_t>& E = edges[nd + j];
-      const uint32_t fl = at[ac.fail[order[nd + j]]];
+      const uint32_t d = dense_anc(nd + j, nd);
+      flat_edges(nd + j, d, &E);
       if (E.size() <= 2) {
         const uint32_t c1 = E.size() > 0 ? E[0] >> 16 : kBigNone, c2 = E.size() > 1 ? E[1] >> 16 : kBigNone;
         const uint32_t n1 = E.size() > 0 ? E[0] & 0xFFFFu : 0, n2 = E.size() > 1 ? E[1] & 0xFFFFu : 0;
         rec[2 * j] = c1 | c2 << 8 | n1 << 16;
-        rec[2 * j + 1] = n2 | fl << 16;
+        rec[2 * j + 1] = n2 | d << 16;
       } else {
         rec[2 * j] = kBigMore | kBigMore << 8 | (k & 0xFFFFu) << 16;
-        rec[2 * j + 1] = (k >> 16) | fl << 16;
+        rec[2 * j + 1] = (k >> 16) | d << 16;
         for (uint32_t v : E) ev[k++] = v;
         ev[k++] = 0xFFFFFFFFu;
       }
@@ -4743,20 +4797,20 @@ static bool build_big_blob(const AcHost& ac, bool bfs, BigBlobHost* out) {
   return true;
 }
 
-// Invariants that make big_next (and k_big_walk's replay) terminate, checked
-// on every blob before it is uploaded, and at tsg_ruleset_compile: state 0 is
-// the root and has a dense row; every class byte is < K; every entry (dense,
-// inline, listed) names a state < S; every cold state's failure link names a
-// strictly smaller blob id (the numbering is by depth, and a failure state is
-// strictly shallower), so a walk's cold hops strictly decrease and end in a
-// dense row; every overflow list lies inside the blob and is terminated.
-// Returns an empty string, or what is violated.
+// Invariants that keep big_next (and k_big_walk's replay) inside the blob
+// and finite, checked on every blob before it is uploaded, and at
+// tsg_ruleset_compile: state 0 is the root and has a dense row; every class
+// byte is < K; every entry (dense, inline, listed) names a state < S; every
+// cold record's ancestor row is a dense row (so a cold byte reads one record
+// and one dense row); at least one cold record sits in LDS when there are any;
+// every overflow list lies inside the blob and is terminated.  Returns an
+// empty string, or what is violated.
 static std::string validate_big_blob(const BigBlobHost& bb, uint32_t K, uint32_t S) {
   if (K == 0 || K >= kBigMore || S == 0 || S > 0x8000u) return "class or state count out of range";
   if (bb.nd == 0 || bb.nd + bb.cold != S || bb.ac_of.size() != S || bb.ac_of[0] != 0)
     return "state 0 is not the dense root";
   if (bb.o_eval < 256 + (uint64_t)bb.nd * K * 2 || bb.o_cold < bb.o_eval || (bb.o_cold - bb.o_eval) % 4 ||
-      bb.blob.size() != bb.o_cold + (uint64_t)bb.cold * 8 || bb.cold_lds > bb.cold ||
+      bb.blob.size() != bb.o_cold + (uint64_t)bb.cold * 8 || bb.cold_lds > bb.cold || (bb.cold && !bb.cold_lds) ||
       bb.lds_bytes != bb.o_cold + (uint64_t)bb.cold_lds * 8 || bb.lds_bytes > kBigLdsMax)
     return "blob sections overlap or exceed the LDS budget";
   for (int b = 0; b < 256; ++b)
@@ -4769,7 +4823,8 @@ static std::string validate_big_blob(const BigBlobHost& bb, uint32_t K, uint32_t
   const uint64_t n_ev = (bb.o_cold - bb.o_eval) / 4;  // (every list sits in the LDS prefix)
   for (uint32_t j = 0; j < bb.cold; ++j) {
     const uint32_t st = bb.nd + j, x = rec[2 * j], y = rec[2 * j + 1];
-    if ((y >> 16) >= st) return "a cold state's failure link does not point to a shallower state";
+    if ((y >> 16) >= bb.nd) return "a cold record's ancestor row is not a dense row";
+    (void)st;
     const uint32_t c1 = x & 0xFFu, c2 = (x >> 8) & 0xFFu;
     if (c1 == kBigMore) {
       uint64_t k = (x >> 16) | ((uint64_t)(y & 0xFFFFu) << 16);
@@ -4816,13 +4871,13 @@ static uint32_t big_next_host(const BigBlobHost& bb, uint32_t K, uint32_t st, ui
   const uint32_t* rec = (const uint32_t*)(bb.blob.data() + bb.o_cold);
   const uint32_t* ev = (const uint32_t*)(bb.blob.data() + bb.o_eval);
   const size_t n_ev = (bb.o_cold - bb.o_eval) / 4;
-  while (st >= bb.nd) {
-    if (++*hops > 64) return 0xFFFFFFFFu;  // (a cycle: the device would hang)
+  if (st >= bb.nd) {
+    ++*hops;
     const uint32_t x = rec[2 * (st - bb.nd)], y = rec[2 * (st - bb.nd) + 1];
     if (c == (x & 0xFFu)) return x >> 16;
     if (c == ((x >> 8) & 0xFFu)) return y & 0xFFFFu;
     if ((x & 0xFFu) == kBigMore) {
-      for (size_t k = (x >> 16) | (y << 16);; ++k) {
+      for (size_t k = (x >> 16) | ((y & 0xFFFFu) << 16);; ++k) {
         if (k >= n_ev) return 0xFFFFFFFEu;  // (list runs off the blob)
         const uint32_t v = ev[k];
         if (v == 0xFFFFFFFFu) break;
@@ -4830,6 +4885,7 @@ static uint32_t big_next_host(const BigBlobHost& bb, uint32_t K, uint32_t st, ui
       }
     }
     st = y >> 16;
+    if (st >= bb.nd) return 0xFFFFFFFFu;  // (not a dense row: the device would read past the table)
   }
   return dense[st * K + c];
 }
@@ -5753,7 +5809,8 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
         {3, 1, 8, k_scan_big<3, 1>},     {4, 1, 8, k_scan_big<4, 1>},     {0, 2, 4, k_scan_big<0, 2>},
         {8, 2, 4, k_scan_big<8, 2>},     {0, 2, 2, k_scan_big<0, 2, 2>},  {8, 2, 2, k_scan_big<8, 2, 2>},
         {12, 2, 2, k_scan_big<12, 2, 2>}, {2, 2, 2, k_scan_big<2, 2, 2>}, {4, 1, 4, k_scan_big<4, 1, 4>},
-        {9, 2, 2, k_scan_big<9, 2, 2>},  {3, 2, 2, k_scan_big<3, 2, 2>}};
+        {9, 2, 2, k_scan_big<9, 2, 2>},  {3, 2, 2, k_scan_big<3, 2, 2>},  {24, 2, 2, k_scan_big<24, 2, 2>},
+        {25, 2, 2, k_scan_big<25, 2, 2>}};
     BigFn pick = nullptr;
     for (const BigV& x : kBigVariants)
       if (x.mode == big_mode && x.ch == big_ch && x.v == big_v) pick = x.fn;
