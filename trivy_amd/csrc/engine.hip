@@ -553,9 +553,10 @@ __device__ inline void fast_event(const ScanParams& P, uint32_t out_e, const Fas
 }
 
 // Walk one 8-byte group (d0, d1) of a chain and report it if it hit an output.
-// kMode (timing experiments only, TSG_SCAN_MODE; results are wrong unless 0):
-// 1 = no events, 2 = no newline count, 4 = loads from the batch's first MiB
-// (L2-resident: takes HBM out of the picture).
+// kMode: 2 = no newline counts (the product's default: k_nl_spans counts the
+// spans of files with locations afterwards); timing experiments only
+// (TSG_SCAN_MODE, wrong results): 1 = no events, 4 = loads from the batch's
+// first MiB (L2-resident: takes HBM out of the picture).
 template <int V, int kMode = 0>
 __device__ inline void fast_group(const ScanParams& P, const uint8_t* T, uint32_t out_e, FastChain<V>& C, uint32_t d0,
                                   uint32_t d1, uint64_t gpos, bool live, uint64_t lanes_lt, FastEvent* ev_seg,
@@ -791,6 +792,7 @@ constexpr uint32_t kBigThreads = 1024;
 // per lane, each with a 2 x 16-byte ring, every chain's dense row read issued
 // before any cold walk -- 8.87 vs 9.63 ms (one chain, 8 x 16 B) on configs[4]
 constexpr int kBigMode = 8, kBigChains = 2, kBigRing = 2;
+constexpr int kBigNoNl = 32;  // kMode bit: no per-span newline counts (the engine's nl_lazy)
 constexpr uint32_t kBigLdsMax = 160 * 1024 - 256;  // the blob's LDS part (k_big_walk adds 80 B of its own)
 // Cold records kept in LDS at least (the rest of the blob's cold records
 // are read from global memory, L2-resident): more dense rows pay more than
@@ -1028,7 +1030,7 @@ __global__ __launch_bounds__(kBigThreads) void k_scan_big(ScanParams P) {
           for (int h = 0; h < CH; ++h) {
             d[2 * h] = g ? cur[h][k].z : cur[h][k].x;
             d[2 * h + 1] = g ? cur[h][k].w : cur[h][k].y;
-            nl[h] += nl_count_dword(d[2 * h]) + nl_count_dword(d[2 * h + 1]);
+            if (!(kMode & kBigNoNl)) nl[h] += nl_count_dword(d[2 * h]) + nl_count_dword(d[2 * h + 1]);
             hi[h] |= d[2 * h] | d[2 * h + 1];
             gs[g][h] = e[h];
           }
@@ -3759,6 +3761,102 @@ __device__ inline void wave_nl_prefix3(const uint8_t* data, const uint32_t* nl_p
 
 // One wave per location: P(start), P(end) relative to the file start on the
 // uncensored content; censored_lines() turns them into findLocation's numbers.
+// Lazy newline counts.  Only the line searches after the locations are
+// known (k_lines: findLocation's bytes.Count, scanner.go:482-503; k_find_spans:
+// the Match line and the Code lines around it, :484-526) read the per-span
+// newline counts, and only inside files that have a location, so the scan
+// kernels skip them (a tenth of k_scan_fast's time: 11.95 -> 10.6 ms on
+// configs[2]) and these kernels count what those searches can reach:
+// k_nl_mark keeps each file's last location end; k_nl_spans (phase 0) counts
+// the file's spans from its first through the span after that end; k_nl_tail
+// sends a file to phase 1 (the rest of its spans) when that next span holds
+// fewer than kNlTailMin newlines (a forward search past the last location
+// could otherwise jump over uncounted spans).  A span is counted whole,
+// neighbouring files' bytes included, exactly as the scan would have, so
+// every prefix difference inside a file reads the same counts.  Each wave
+// takes 64 consecutive spans, ballots the ones it needs and counts each with
+// the whole wave (64 bytes per lane, SWAR).
+constexpr uint32_t kNlTailMin = 4;   // newlines of the span after the last location: Code's 2 lines + the end line's
+constexpr uint64_t kNlFull = 1ull << 63;  // nl_last flag: count the whole file
+
+// The counting starts before the locations exist: right after the sorted
+// candidates, on the side stream under k_verify (latency-bound, so the HBM
+// is free), each candidate's file is counted through kNlCandReach bytes past
+// its last candidate (a full-file rule's: to the file's end).  When the
+// locations are known, k_nl_check sends a file whose last location ends past
+// that bound to phase 1 (which then also covers what k_nl_tail asks for).
+constexpr uint64_t kNlCandReach = 16384;
+__global__ __launch_bounds__(256) void k_nl_cands(const uint64_t* keys, const uint32_t* vals, uint64_t n,
+                                                  const uint64_t* off, unsigned long long* nl_last) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t f = vals[i] & ~kFullFlag;
+  const uint64_t lim = (vals[i] & kFullFlag) ? off[f + 1] : (keys[i] & kPosMask) + kNlCandReach;
+  atomicMax(&nl_last[f], (unsigned long long)(lim + 1));
+}
+
+__global__ __launch_bounds__(256) void k_nl_check(const DevLoc* locs, uint64_t n, const uint64_t* off,
+                                                  unsigned long long* nl_last) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t f = locs[i].file;
+  const uint64_t l = nl_last[f] & ~kNlFull;
+  if (!l || (off[f] + locs[i].end) / kNlBlock > (l - 1) / kNlBlock) atomicOr(&nl_last[f], (unsigned long long)kNlFull);
+}
+
+__global__ __launch_bounds__(256) void k_nl_tail(const uint64_t* off, uint32_t n_files, const uint32_t* nl_blocks,
+                                                 uint64_t n_spans, unsigned long long* nl_last) {
+  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= n_files || !(nl_last[f] & ~kNlFull) || (nl_last[f] & kNlFull)) return;
+  const uint64_t next = ((nl_last[f] & ~kNlFull) - 1) / kNlBlock + 1;  // the span after the counted bound's
+  if (next * kNlBlock < off[f + 1] && next < n_spans && nl_blocks[next] < kNlTailMin) nl_last[f] |= kNlFull;
+}
+
+__global__ __launch_bounds__(256) void k_nl_spans(const uint8_t* data, uint64_t nbytes, const uint64_t* off,
+                                                  const uint32_t* region_file, uint64_t n_regions, uint32_t n_files,
+                                                  const unsigned long long* nl_last, uint32_t* nl_blocks,
+                                                  uint32_t phase) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t n_spans = (nbytes + kNlBlock - 1) / kNlBlock;
+  const uint64_t sp0 = ((uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * 64;
+  const uint64_t sp = sp0 + lane;
+  bool need = false;
+  if (sp < n_spans) {
+    // files overlapping span sp: the one holding its first byte through the
+    // one holding the next span's first byte
+    const uint32_t f0 = region_file[sp];
+    uint32_t f1 = sp + 1 < n_regions ? region_file[sp + 1] : n_files - 1;
+    if (f1 >= n_files) f1 = n_files - 1;
+    for (uint32_t f = f0; f <= f1 && !need; ++f) {
+      const uint64_t l = nl_last[f];
+      if (!l || off[f + 1] <= sp * kNlBlock) continue;  // (no location / an empty file before the span)
+      // spans counted in phase 0: [first, next]; phase 1 counts the rest of a
+      // kNlFull file (all of it when phase 0 counted none)
+      const uint64_t lim = l & ~kNlFull;
+      const uint64_t next = lim ? (lim - 1) / kNlBlock + 1 : 0;
+      need = phase == 0 ? sp <= next : ((l & kNlFull) && (!lim || sp > next));
+    }
+  }
+  uint64_t m = __ballot(need);
+  while (m) {
+    const uint32_t k = __builtin_ctzll(m);
+    m &= m - 1;
+    const uint64_t b = (sp0 + k) * kNlBlock + 64ull * lane;
+    uint32_t cnt = 0;
+    if (b + 64 <= nbytes) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 v = *(const uint4*)(data + b + 16 * q);
+        cnt += nl_count_dword(v.x) + nl_count_dword(v.y) + nl_count_dword(v.z) + nl_count_dword(v.w);
+      }
+    } else {
+      for (uint64_t x = b; x < b + 64 && x < nbytes; ++x) cnt += data[x] == '\n';
+    }
+    for (uint32_t d = 32; d; d >>= 1) cnt += __shfl_xor(cnt, d);
+    if (lane == 0) nl_blocks[sp0 + k] = cnt;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_lines(const uint8_t* data, const uint64_t* off, const uint32_t* nl_pre,
                                                DevLoc* locs, uint64_t n_locs) {
   const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -4984,6 +5082,13 @@ struct DevImage {
 struct tsg_engine {
   int device = 0;
   int verify_split = 0;  // 1: every job list through k_verify_fast (tests; tsg_engine_force_verify_split)
+  // launch_scan: the scan kernels skip the per-span newline counts (nl_lazy,
+  // set by the caller), and nl_deferred records that the last scan did, so
+  // k_nl_spans counts the spans of the files that have locations
+  bool nl_lazy = false, nl_deferred = false;
+  DBuf<unsigned long long> nl_last;  // per file: counted bound + 1 (0: none) | kNlFull (k_nl_cands / _check / _tail)
+  hipEvent_t ev_nl[2] = {nullptr, nullptr};  // candidates ready -> phase-0 count done (side stream)
+  bool nl_pending = false;                   // a phase-0 count was issued on the side stream
   hipStream_t stream = nullptr;
   std::mutex mu;
   DevImage img;
@@ -5655,6 +5760,18 @@ inline const char* experiment_env(const char* name) {
 #endif
 }
 
+// The side stream (D2H of the findings, the phase-0 newline count) and its events.
+hipError_t ensure_side(tsg_engine* e) {
+  if (e->side) return hipSuccess;
+  hipError_t r = hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking);
+  if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_code, hipEventDisableTiming);
+  if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_fill, hipEventDisableTiming);
+  if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_side, hipEventDisableTiming);
+  if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_nl[0], hipEventDisableTiming);
+  if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_nl[1], hipEventDisableTiming);
+  return r;
+}
+
 int read_ctrl(tsg_engine* e, Ctrl* h) {
   HIP_TRY(hipMemcpyAsync(h, e->ctrl.p, sizeof(Ctrl), hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -5665,6 +5782,7 @@ int read_ctrl(tsg_engine* e, Ctrl* h) {
 // else the generic kernel (transition table in LDS or, if too large, global).
 int launch_scan(tsg_engine* e, ScanParams& P) {
   hipStream_t s = e->stream;
+  bool nl_skipped = false;
   P.n_regions = P.nbytes / kNlBlock + 1;
   HIP_TRY(e->region_file.ensure(P.n_regions + 1));
   P.region_file = e->region_file.p;
@@ -5762,13 +5880,20 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     else if (chains == 1 && vecs == 8 && win == 8) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 8>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1 && vecs == 8 && win == 4 && pair && P.rs.ac.o_pair)
       hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 4, true>), dim3(blocks), dim3(nt), 0, s, P);
+    else if (chains == 1 && vecs == 8 && win == 4 && e->nl_lazy) {
+      hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 2, 4>), dim3(blocks), dim3(nt), 0, s, P);
+      nl_skipped = true;
+    }
     else if (chains == 1 && vecs == 8 && win == 4) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 4>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1 && vecs == 8) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1) hipLaunchKernelGGL((k_scan_fast<1, 4, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     else if (vecs == 4) hipLaunchKernelGGL((k_scan_fast<2, 4, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     else hipLaunchKernelGGL((k_scan_fast<2, 2, 1024>), dim3(blocks), dim3(nt), 0, s, P);
 #else
-    hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, kFastEventWin>), dim3(blocks), dim3(nt), 0, s, P);
+    // (kMode 2: no newline counts -- the engine counts them lazily, k_nl_spans)
+    if (e->nl_lazy) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 2, kFastEventWin>), dim3(blocks), dim3(nt), 0, s, P);
+    else hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, kFastEventWin>), dim3(blocks), dim3(nt), 0, s, P);
+    nl_skipped = e->nl_lazy;
 #endif
     HIP_TRY(hipGetLastError());
     if (e->events) HIP_TRY(hipEventRecord(e->ev[11], s));
@@ -5793,6 +5918,9 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     HIP_TRY(e->span_hi.ensure(units + 1));
     P.span_hi = e->span_hi.p;
     // one unit per lane: CH spans (kBigChains)
+    // (newline counts stay in this kernel: they cost it ~0.1 ms on configs[4],
+    // against ~0.9 ms for counting its many location files afterwards --
+    // TSG_BIG_VARIANT=40x2v2 skips them, exp build)
     const void* big_fn = (const void*)k_scan_big<kBigMode, kBigChains, kBigRing>;
     int big_mode = kBigMode, big_ch = kBigChains;
 #ifdef TSG_EXPERIMENTS
@@ -5810,7 +5938,7 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
         {8, 2, 4, k_scan_big<8, 2>},     {0, 2, 2, k_scan_big<0, 2, 2>},  {8, 2, 2, k_scan_big<8, 2, 2>},
         {12, 2, 2, k_scan_big<12, 2, 2>}, {2, 2, 2, k_scan_big<2, 2, 2>}, {4, 1, 4, k_scan_big<4, 1, 4>},
         {9, 2, 2, k_scan_big<9, 2, 2>},  {3, 2, 2, k_scan_big<3, 2, 2>},  {24, 2, 2, k_scan_big<24, 2, 2>},
-        {25, 2, 2, k_scan_big<25, 2, 2>}};
+        {25, 2, 2, k_scan_big<25, 2, 2>}, {40, 2, 2, k_scan_big<40, 2, 2>}};
     BigFn pick = nullptr;
     for (const BigV& x : kBigVariants)
       if (x.mode == big_mode && x.ch == big_ch && x.v == big_v) pick = x.fn;
@@ -5818,7 +5946,10 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
       set_last_error("TSG_BIG_VARIANT: no such k_scan_big instantiation");
       return TSG_ERR_INVALID_ARG;
     }
-    big_fn = (const void*)pick;
+    if (getenv("TSG_BIG_VARIANT")) {
+      big_fn = (const void*)pick;
+      nl_skipped = e->nl_lazy && (big_mode & kBigNoNl);
+    }
 #endif
     const uint64_t big_units = (units + big_ch - 1) / big_ch;
     const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((big_units + nt - 1) / nt, e->num_cus));
@@ -5873,6 +6004,7 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     }
   }
   HIP_TRY(hipGetLastError());
+  e->nl_deferred = nl_skipped;
   return TSG_OK;
 }
 
@@ -6017,12 +6149,7 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   R.file_flags = {base + o_flags, n_files};
   R.ties = {(uint32_t*)(base + o_ties), 0};
   R.ctrl_off = o_ctrl;
-  if (!e->side) {
-    HIP_TRY(hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&e->ev_code, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&e->ev_fill, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&e->ev_side, hipEventDisableTiming));
-  }
+  HIP_TRY(ensure_side(e));
   // the kept locations as tsg_loc records
   HIP_TRY(e->out_locs.ensure(n_locs));
   hipLaunchKernelGGL(k_out_locs, dim3(lane_blocks), dim3(256), 0, s, e->locs2.p, n_locs, e->out_locs.p, e->ctrl.p);
@@ -6657,6 +6784,14 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   HIP_TRY(e->nl_pre.ensure(n_nlb));
   P.nl_blocks = e->nl_blocks.p;
   const bool merge = sp && sp->mode == 2;
+  // newline counts: counted lazily after the locations (k_nl_spans), except
+  // for a part scan, whose blob exports its range's counts
+  e->nl_lazy = !(sp && sp->mode == 1);
+  e->nl_deferred = false;
+  if (e->nl_pending) {  // (an earlier call ended before its lines stage: its side count must not overlap this one)
+    HIP_TRY(hipStreamWaitEvent(s, e->ev_nl[1], 0));
+    e->nl_pending = false;
+  }
   bool scanned = nbytes == 0 || merge;
   if (merge) {  // the scan state comes from the parts (ev[8..9] bracket the import)
     HIP_TRY(hipEventRecord(e->ev[8], s));
@@ -6784,6 +6919,21 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
     HIP_TRY(hipcub::DeviceSelect::Flagged(e->cub_tmp.p, tmp2, cnt, e->flags8.p, e->job_start.p, e->nsel.p,
                                           (int)n_cands, s));
+    if (e->nl_deferred) {  // phase-0 newline counts of the candidate files, under the verify (k_nl_cands)
+      HIP_TRY(ensure_side(e));
+      HIP_TRY(e->nl_last.ensure(nf));
+      HIP_TRY(hipMemsetAsync(e->nl_last.p, 0, (size_t)nf * 8, s));
+      hipLaunchKernelGGL(k_nl_cands, dim3((uint32_t)((n_cands + 255) / 256)), dim3(256), 0, s, e->keys2.p,
+                         e->vals2.p, n_cands, d_off, e->nl_last.p);
+      HIP_TRY(hipEventRecord(e->ev_nl[0], s));
+      HIP_TRY(hipStreamWaitEvent(e->side, e->ev_nl[0], 0));
+      const uint64_t n_spans = (nbytes + kNlBlock - 1) / kNlBlock;
+      hipLaunchKernelGGL(k_nl_spans, dim3((uint32_t)((n_spans + 255) / 256)), dim3(256), 0, e->side, d_data, nbytes,
+                         d_off, e->region_file.p, nbytes / kNlBlock + 1, nf, e->nl_last.p, e->nl_blocks.p, 0u);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipEventRecord(e->ev_nl[1], e->side));
+      e->nl_pending = true;
+    }
   }
   // the job count stays on the device: k_verify reads it, and its grid and
   // the location lists are sized from n_cands (>= jobs); the host reads the
@@ -7152,6 +7302,24 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   // ---- 7. line numbers
   if (n_locs) {
     const int n_nlb = (int)(nbytes / kNlBlock + 2);
+    if (e->nl_deferred) {  // the scan skipped the newline counts: what the location files' searches reach
+      const uint64_t n_spans = (nbytes + kNlBlock - 1) / kNlBlock;
+      const uint32_t span_blocks = (uint32_t)((n_spans + 255) / 256);
+      if (!e->nl_pending) {  // (no candidate pass ran: count every location file whole)
+        HIP_TRY(e->nl_last.ensure(nf));
+        HIP_TRY(hipMemsetAsync(e->nl_last.p, 0, (size_t)nf * 8, s));
+      } else {
+        HIP_TRY(hipStreamWaitEvent(s, e->ev_nl[1], 0));
+        e->nl_pending = false;
+      }
+      hipLaunchKernelGGL(k_nl_check, dim3((uint32_t)((n_locs + 255) / 256)), dim3(256), 0, s, e->locs.p, n_locs,
+                         d_off, e->nl_last.p);
+      hipLaunchKernelGGL(k_nl_tail, dim3((nf + 255) / 256), dim3(256), 0, s, d_off, nf, e->nl_blocks.p, n_spans,
+                         e->nl_last.p);
+      hipLaunchKernelGGL(k_nl_spans, dim3(span_blocks), dim3(256), 0, s, d_data, nbytes, d_off, e->region_file.p,
+                         nbytes / kNlBlock + 1, nf, e->nl_last.p, e->nl_blocks.p, 1u);
+      HIP_TRY(hipGetLastError());
+    }
     size_t tmp = 0;
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->nl_blocks.p, e->nl_pre.p, n_nlb, s));
     HIP_TRY(e->cub_tmp.ensure(tmp + 1));
@@ -7339,6 +7507,8 @@ void tsg_engine_free(tsg_engine* e) {
     (void)hipEventDestroy(e->ev_code);
     (void)hipEventDestroy(e->ev_fill);
     (void)hipEventDestroy(e->ev_side);
+    (void)hipEventDestroy(e->ev_nl[0]);
+    (void)hipEventDestroy(e->ev_nl[1]);
     (void)hipStreamDestroy(e->side);
   }
   (void)hipStreamDestroy(e->stream);
@@ -7773,6 +7943,7 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
   P.file_flags = e->file_flags.p;
   P.hits = e->hits.p;
   P.hit_cap = 0;  // prefilter only: hits are counted, not stored
+  e->nl_lazy = true;  // (no line numbers here)
   P.ctrl = e->ctrl.p;
   HIP_TRY(e->fold_pos.ensure(std::max<uint64_t>(1 << 16, e->fold_need)));
   P.fold_pos = e->fold_pos.p;
