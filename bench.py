@@ -767,13 +767,17 @@ def main():
                                          ctypes.byref(w)))
         return w
 
+    trace_c3 = os.environ.get("TSG_C3_TRACE") is not None  # per-layer phase times on stderr
+
     def layer_step():
         # one tsg_result per layer; the step returns the last (timings) and
         # frees the others after reading their counts
+        t0 = time.perf_counter()
         futs = [pool.submit(walk_one, x) for _, x in layers]
         results = []
         for k, ((_, x), f) in enumerate(zip(layers, futs)):
             w = f.result()
+            t1 = time.perf_counter()
             r = ctypes.c_void_p()
             try:
                 N.check(N.lib.tsg_analyze_layer(eng, rs, ctypes.c_void_p(x.ctypes.data), len(x), w, b"",
@@ -781,6 +785,9 @@ def main():
             finally:
                 N.lib.tsg_tar_walk_free(w)
             results.append(r)
+            if trace_c3:
+                print(f"c3 layer {k}: walk ready {1e3 * (t1 - t0):.1f} ms, analyze {1e3 * (time.perf_counter() - t1):.1f} ms",
+                      file=sys.stderr)
         return results
 
     def one_step():

@@ -78,3 +78,42 @@ def test_builtin_global_allow_paths_dfa_equals_matchstring():
             assert bool(res.value) == rx.match_string(b), (src, p)
             checked += 1
     assert checked >= 300 * len(srcs), checked
+
+
+def test_host_allow_path_dfa_equals_vm():
+    """tsg_ruleset_allow_path (SecretAnalyzer.Required's global AllowPath,
+    scanner.go:200-207) now decides paths with the path DFAs and falls back
+    to the Pike VM only where a DFA cannot: on random paths built from the
+    builtin allow rules' vocabulary (ASCII, upper case, non-ASCII, invalid
+    UTF-8) it must equal MatchString of every rule on the VM alone."""
+    import ctypes
+    import json
+    import os
+    import random
+
+    import trivy_amd._native as N
+    import trivy_amd.secret as S
+
+    data = json.load(open(os.path.join(os.path.dirname(S.__file__), "data", "builtin_rules.json")))
+    pats = [a["path"] for a in data["allow_rules"] if a.get("path")]
+    sc = S.new_scanner(None)
+    rng = random.Random(41)
+    words = ["test", "tests", "_test", "-test", ".test", "vendor", "example", "Example", "node_modules", "docs",
+             "README.md", "a.md", "usr", "share", "doc", "src", "main.go", "lib", "x.min.js", "é", "ſ", "K",
+             "pkg", "testdata", "mock", "spec", ".git", "a" * 40]
+    paths = []
+    for _ in range(4000):
+        p = "/".join(rng.choice(words) for _ in range(rng.randint(1, 6)))
+        if rng.random() < 0.3:
+            p = "/" + p
+        paths.append(p.encode("utf-8"))
+    paths += [b"\xff/vendor/x", b"test\xc3", b"a/\xe2\x80/test"]
+    for p in paths:
+        want = False
+        for r in pats:
+            m = ctypes.c_int()
+            N.check(N.lib.tsg_regex_match(r.encode(), p, len(p), ctypes.byref(m)))
+            want = want or bool(m.value)
+        got = ctypes.c_int()
+        N.check(N.lib.tsg_ruleset_allow_path(sc._rs.handle, p, len(p), ctypes.byref(got)))
+        assert bool(got.value) == want, p

@@ -5763,6 +5763,8 @@ inline const char* experiment_env(const char* name) {
 // The side stream (D2H of the findings, the phase-0 newline count) and its events.
 hipError_t ensure_side(tsg_engine* e) {
   if (e->side) return hipSuccess;
+  // (a lowest-priority side stream left k_verify as slow under the phase-0
+  // newline count: 0.74 vs 0.76 ms, profiles/r04v)
   hipError_t r = hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking);
   if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_code, hipEventDisableTiming);
   if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_fill, hipEventDisableTiming);
@@ -7679,7 +7681,9 @@ static int stage_host_batch(tsg_engine* e, const tsg_file* files, size_t n_files
     e->h_stage = nullptr;
     e->h_stage_n = 0;
     const size_t cap = need + need / 4;
-    HIP_TRY(hipHostMalloc((void**)&e->h_stage, cap, hipHostMallocDefault));
+    unsigned flags = hipHostMallocDefault;
+    if (const char* v = experiment_env("TSG_STAGE_NC")) flags = atoi(v) ? hipHostMallocNonCoherent : flags;
+    HIP_TRY(hipHostMalloc((void**)&e->h_stage, cap, flags));
     e->h_stage_n = cap;
   }
   uint8_t* h = e->h_stage;
@@ -7703,17 +7707,24 @@ static int stage_host_batch(tsg_engine* e, const tsg_file* files, size_t n_files
     }
   };
   const unsigned nt = nbytes < (64u << 20) ? 1u : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  // chunk DMAs alternate over this many streams (A/B: TSG_DMA_STREAMS, exp build)
+  int n_dma = 1;
+  if (const char* v = experiment_env("TSG_DMA_STREAMS")) n_dma = atoi(v) == 2 ? 2 : 1;
+  if (n_dma == 2) HIP_TRY(ensure_side(e));
+  auto dma_stream = [&](uint64_t c) { return (n_dma == 2 && (c & 1)) ? e->side : s; };
   // chunks: the DMA of chunk k is issued as soon as every worker has packed
   // its slice of it, while the workers go on to the next chunks (one set of
   // threads per call: a spawn / join per 64 MiB chunk cost ~0.3 ms each)
-  constexpr uint64_t kStageChunk = 64ull << 20;
+  uint64_t kStageChunk = 64ull << 20;
+  if (const char* v = experiment_env("TSG_STAGE_CHUNK_MB")) kStageChunk = std::max(1, atoi(v)) * (1ull << 20);
   const uint64_t n_chunks = (nbytes + kStageChunk - 1) / kStageChunk;
   bool ok = true;
   if (nt == 1 || n_chunks == 0) {
     for (uint64_t lo = 0; lo < nbytes && ok; lo += kStageChunk) {
       const uint64_t hi = std::min(nbytes, lo + kStageChunk);
       pack_range(lo, hi);
-      ok = hipMemcpyAsync(e->data.p + lo, h + lo, hi - lo, hipMemcpyHostToDevice, s) == hipSuccess;
+      ok = hipMemcpyAsync(e->data.p + lo, h + lo, hi - lo, hipMemcpyHostToDevice, dma_stream(lo / kStageChunk)) ==
+           hipSuccess;
     }
   } else {
     std::unique_ptr<std::atomic<unsigned>[]> done(new std::atomic<unsigned>[n_chunks]);
@@ -7742,7 +7753,7 @@ static int stage_host_batch(tsg_engine* e, const tsg_file* files, size_t n_files
     for (uint64_t c = 0; c < n_chunks && ok; ++c) {
       while (done[c].load(std::memory_order_acquire) < nt) std::this_thread::yield();
       const uint64_t lo = c * kStageChunk, hi = std::min(nbytes, lo + kStageChunk);
-      ok = hipMemcpyAsync(e->data.p + lo, h + lo, hi - lo, hipMemcpyHostToDevice, s) == hipSuccess;
+      ok = hipMemcpyAsync(e->data.p + lo, h + lo, hi - lo, hipMemcpyHostToDevice, dma_stream(c)) == hipSuccess;
     }
     if (!ok) stop.store(true);
     for (auto& t : th) t.join();
@@ -7750,6 +7761,8 @@ static int stage_host_batch(tsg_engine* e, const tsg_file* files, size_t n_files
   for (size_t i = 0; i < n_files; ++i)
     if (files[i].path) memcpy(h + nbytes + poff[i], files[i].path, poff[i + 1] - poff[i]);
   const auto t1 = std::chrono::steady_clock::now();
+  if (ok && n_dma == 2)  // (the side stream's chunks before anything on the main stream reads the batch)
+    ok = hipEventRecord(e->ev_side, e->side) == hipSuccess && hipStreamWaitEvent(s, e->ev_side, 0) == hipSuccess;
   ok = ok && hipMemcpyAsync(e->paths.p, h + nbytes, pbytes, hipMemcpyHostToDevice, s) == hipSuccess &&
        hipMemcpyAsync(e->off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
        hipMemcpyAsync(e->path_off.p, poff.data(), poff.size() * 8, hipMemcpyHostToDevice, s) == hipSuccess &&

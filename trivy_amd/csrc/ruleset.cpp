@@ -817,6 +817,14 @@ extern "C++" namespace tsg {
 // every compiled global allow-path regex.  Per file, not per byte.
 bool host_allow_path(const tsg_ruleset* rs, const uint8_t* path, size_t len) {
   for (int r : rs->global_allow_path) {
+    // the regex's MatchString DFA (k_path_gate's) decides most paths in one
+    // table walk; the Pike VM only what it cannot (non-ASCII, DFA too big)
+    if ((size_t)r < rs->path_dfa.size() && rs->path_dfa[r].valid) {
+      size_t e = 0;
+      const int d = dfa_anchored(rs->path_dfa[r], path, len, 0, &e);
+      if (d == 1) return true;
+      if (d == 0) continue;
+    }
     const gre::Prog& p = rs->regexes[r].c.prog;
     // per-thread VM scratch, freed when the thread exits (tsg_analyze_layer's
     // Required workers are short-lived threads)
