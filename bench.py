@@ -769,26 +769,33 @@ def main():
 
     trace_c3 = os.environ.get("TSG_C3_TRACE") is not None  # per-layer phase times on stderr
 
+    if args.config == 3:  # layer k on engine k % 2 (trivy_amd.walker.analyze_layers' pipelining)
+        from trivy_amd.secret import get_engines
+        layer_engs = get_engines(device, 2)
+        apool = ThreadPoolExecutor(max_workers=len(layer_engs))
+
     def layer_step():
         # one tsg_result per layer; the step returns the last (timings) and
         # frees the others after reading their counts
         t0 = time.perf_counter()
         futs = [pool.submit(walk_one, x) for _, x in layers]
-        results = []
-        for k, ((_, x), f) in enumerate(zip(layers, futs)):
+
+        def one(k, x, f):
             w = f.result()
             t1 = time.perf_counter()
             r = ctypes.c_void_p()
             try:
-                N.check(N.lib.tsg_analyze_layer(eng, rs, ctypes.c_void_p(x.ctypes.data), len(x), w, b"",
-                                                c["kept"][k], ctypes.byref(c["n_kept"][k]), ctypes.byref(r)))
+                N.check(N.lib.tsg_analyze_layer(layer_engs[k % len(layer_engs)], rs, ctypes.c_void_p(x.ctypes.data),
+                                                len(x), w, b"", c["kept"][k], ctypes.byref(c["n_kept"][k]),
+                                                ctypes.byref(r)))
             finally:
                 N.lib.tsg_tar_walk_free(w)
-            results.append(r)
             if trace_c3:
                 print(f"c3 layer {k}: walk ready {1e3 * (t1 - t0):.1f} ms, analyze {1e3 * (time.perf_counter() - t1):.1f} ms",
                       file=sys.stderr)
-        return results
+            return r
+        afuts = [apool.submit(one, k, x, f) for k, ((_, x), f) in enumerate(zip(layers, futs))]
+        return [a.result() for a in afuts]
 
     def one_step():
         if args.config == 3:

@@ -299,6 +299,7 @@ struct tsg_ruleset {
   std::vector<tsg::RuleHost> rules;
   std::vector<int> global_allow_regex;  // AllowRules with Regex
   std::vector<int> global_allow_path;   // AllowRules with Path
+  tsg::DfaHost allow_path_union;        // MatchString of any of them, one DFA walk (host Required)
   std::vector<int> global_exclude;
   std::vector<std::string> keywords;     // unique lowercased keywords
   std::vector<uint8_t> kw_uni;           // per keyword: 1 = holds a non-ASCII rune (k_uni_keywords, not the automaton)

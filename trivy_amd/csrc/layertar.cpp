@@ -20,6 +20,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <string_view>
 #include <system_error>
 #include <thread>
 #include <vector>
@@ -525,21 +526,22 @@ static bool secret_required(const tsg_ruleset* rs, const std::string& fp, uint64
   static const char* kSkipExts[] = {".jpg", ".png", ".gif", ".doc", ".pdf", ".bin", ".svg", ".socket",
                                     ".deb", ".rpm", ".zip", ".gz", ".gzip", ".tar", ".pyc"};  // :38-41
   if (size < 10) return false;
-  size_t slash = fp.rfind('/');
-  std::string dir = slash == std::string::npos ? "" : fp.substr(0, slash + 1);
-  std::string name = slash == std::string::npos ? fp : fp.substr(slash + 1);
+  const std::string_view v(fp);  // (views: no allocation per file)
+  const size_t slash = v.rfind('/');
+  const std::string_view dir = slash == std::string_view::npos ? std::string_view() : v.substr(0, slash + 1);
+  const std::string_view name = slash == std::string_view::npos ? v : v.substr(slash + 1);
   for (size_t i = 0; i <= dir.size();) {  // strings.Split(dir, "/") contains .git / node_modules
     size_t j = dir.find('/', i);
-    if (j == std::string::npos) j = dir.size();
-    std::string c = dir.substr(i, j - i);
+    if (j == std::string_view::npos) j = dir.size();
+    const std::string_view c = dir.substr(i, j - i);
     if (c == ".git" || c == "node_modules") return false;
     i = j + 1;
   }
   for (const char* f : kSkipFiles)
     if (name == f) return false;
   if (config_base == fp) return false;
-  size_t dot = name.rfind('.');
-  std::string ext = dot == std::string::npos ? "" : name.substr(dot);  // filepath.Ext
+  const size_t dot = name.rfind('.');
+  const std::string_view ext = dot == std::string_view::npos ? std::string_view() : name.substr(dot);  // filepath.Ext
   for (const char* x : kSkipExts)
     if (ext == x) return false;
   return !tsg::host_allow_path(rs, (const uint8_t*)fp.data(), fp.size());

@@ -620,6 +620,17 @@ int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_r
       std::string err2;
       if (gre::compile("(?s:.)*?(?:" + rs->regexes[x].src + ")", &any, &err2)) build_dfa(any, &rs->path_dfa[x]);
     }
+    // the global allow paths as one alternation (each regex's flags stay
+    // inside its own group), for Required's per-file AllowPath on the host
+    if (rs->global_allow_path.size() > 1) {
+      std::string u = "(?s:.)*?(?:";
+      for (size_t k = 0; k < rs->global_allow_path.size(); ++k)
+        u += (k ? "|(?:" : "(?:") + rs->regexes[rs->global_allow_path[k]].src + ")";
+      u += ")";
+      gre::Compiled any;
+      std::string err2;
+      if (gre::compile(u, &any, &err2)) build_dfa(any, &rs->allow_path_union);
+    }
   }
   *out = rs;
   return TSG_OK;
@@ -816,6 +827,11 @@ extern "C++" namespace tsg {
 // Global AllowRules.AllowPath (scanner.go:200-207) on the host: MatchString of
 // every compiled global allow-path regex.  Per file, not per byte.
 bool host_allow_path(const tsg_ruleset* rs, const uint8_t* path, size_t len) {
+  if (rs->allow_path_union.valid) {
+    size_t e = 0;
+    const int d = dfa_anchored(rs->allow_path_union, path, len, 0, &e);
+    if (d != 2) return d == 1;
+  }
   for (int r : rs->global_allow_path) {
     // the regex's MatchString DFA (k_path_gate's) decides most paths in one
     // table walk; the Pike VM only what it cannot (non-ASCII, DFA too big)

@@ -178,6 +178,24 @@ def get_engine(device: Optional[int] = None):
         return _ENGINES[dev]
 
 
+_EXTRA_ENGINES = {}
+
+
+def get_engines(device: Optional[int] = None, n: int = 2):
+    """n engines on one GPU (the first is get_engine's): independent streams
+    and buffers, so one engine's host-to-device staging overlaps another's
+    pipeline (analyze_layers)."""
+    dev = default_device() if device is None else device
+    first = get_engine(dev)
+    with _ENGINE_LOCK:
+        extra = _EXTRA_ENGINES.setdefault(dev, [])
+        while len(extra) < n - 1:
+            h = ctypes.c_void_p()
+            N.check(N.lib.tsg_engine_create(dev, ctypes.byref(h)))
+            extra.append(h)
+        return [first] + extra[: n - 1]
+
+
 class _CompiledRuleSet:
     def __init__(self, rules: Sequence[Rule], allow_rules: Sequence[AllowRule], exclude: ExcludeBlock):
         keep = []

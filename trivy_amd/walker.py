@@ -170,14 +170,15 @@ class LayerTar:
             close()
 
 
-def _analyze_walked(analyzer, addr: int, n: int, w: _Walk) -> List[Secret]:
+def _analyze_walked(analyzer, addr: int, n: int, w: _Walk, engine=None) -> List[Secret]:
     from .secret import get_engine
 
     sc = analyzer.scanner
     kept = (ctypes.c_uint32 * max(1, w.count))()
     nk = ctypes.c_size_t()
     res = ctypes.c_void_p()
-    N.check(N.lib.tsg_analyze_layer(get_engine(sc.device), sc._rs.handle, addr or None, n, w.handle,
+    eng = engine if engine is not None else get_engine(sc.device)
+    N.check(N.lib.tsg_analyze_layer(eng, sc._rs.handle, addr or None, n, w.handle,
                                     (analyzer.config_path or "").encode(), kept, ctypes.byref(nk),
                                     ctypes.byref(res)))
     try:
@@ -207,29 +208,39 @@ def analyze_layer(analyzer, layer: Layer, skip_files: Sequence[str] = (),
 
 
 def analyze_layers(analyzer, layers: Sequence[Layer], skip_files: Sequence[str] = (),
-                   skip_dirs: Sequence[str] = (), walk_threads: int = 4
+                   skip_dirs: Sequence[str] = (), walk_threads: int = 4, engines: int = 2
                    ) -> List[Tuple[List[Secret], List[str], List[str]]]:
     """The layers of an image (image.go:242-331 inspects them concurrently),
     pipelined: up to `walk_threads` native walks run ahead on host threads
-    (ctypes drops the GIL) while the engine analyzes the layers in order, so
-    the serial header-chain walk of layer k+1 hides under the analyze of
-    layer k.  One (secrets, opqDirs, whFiles) per layer, in input order."""
+    (ctypes drops the GIL), and layer k is analyzed on engine k % `engines`
+    of the same GPU (secret.get_engines: own stream and buffers), so one
+    layer's host-to-device staging -- the PCIe-bound part -- overlaps the
+    Required pass, scan pipeline and findings of the layer before it.  One
+    (secrets, opqDirs, whFiles) per layer, in input order."""
     from concurrent.futures import ThreadPoolExecutor
 
+    from .secret import get_engines
+
+    engs = get_engines(analyzer.scanner.device, max(1, min(engines, len(layers))))
     opened = [_open_layer(x) for x in layers]
+
+    def one(k, f):
+        _, addr, n, _ = opened[k]
+        with f.result() as w:
+            return (_analyze_walked(analyzer, addr, n, w, engs[k % len(engs)]), w.opq_dirs, w.wh_files)
+
     try:
-        with ThreadPoolExecutor(max_workers=max(1, walk_threads)) as pool:
+        with ThreadPoolExecutor(max_workers=max(1, walk_threads)) as pool, \
+                ThreadPoolExecutor(max_workers=len(engs)) as apool:
             futs = [pool.submit(_Walk, addr, n, skip_files, skip_dirs) for _, addr, n, _ in opened]
-            out = []
             try:
-                for (_, addr, n, _), f in zip(opened, futs):
-                    with f.result() as w:
-                        out.append((_analyze_walked(analyzer, addr, n, w), w.opq_dirs, w.wh_files))
+                # (one worker per engine, layers taken in order: layer k runs on engine k % n)
+                afuts = [apool.submit(one, k, f) for k, f in enumerate(futs)]
+                return [a.result() for a in afuts]
             finally:
                 for f in futs:  # free walks left behind by an error
                     if f.done() and f.exception() is None:
                         f.result().close()
-            return out
     finally:
         for buf, _, _, close in opened:
             del buf
