@@ -1537,11 +1537,11 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
               const uint64_t key = ((uint64_t)fi << 32) | pd.kw;  // per-lane dedupe of repeated keywords
               if (last_kw != key) {
                 last_kw = key;
-                // most outputs repeat a keyword the file already has: an L2 read
-                // instead of a memory-side atomic for those
-                uint32_t* wp = &P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)];
-                const uint32_t bit = 1u << (pd.kw & 31);
-                if (!(__hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(wp, bit);
+                // fire-and-forget atomic: reading the word first to skip the
+                // atomics of repeated keywords put an L2 round trip on the lane's
+                // chain (k_report 650 -> 618 us on configs[2] without it,
+                // profiles/r04ac)
+                atomicOr(&P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)], 1u << (pd.kw & 31));
               }
             }
             if (want_hit) {
