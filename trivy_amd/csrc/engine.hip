@@ -3759,17 +3759,16 @@ __device__ inline void wave_nl_prefix3(const uint8_t* data, const uint32_t* nl_p
   for (int q = 0; q < 3; ++q) out[q] = nl_pre[xs[q] / kNlBlock] + (uint32_t)((packed >> (21 * q)) & 0x1FFFFFu);
 }
 
-// One wave per location: P(start), P(end) relative to the file start on the
-// uncensored content; censored_lines() turns them into findLocation's numbers.
 // Lazy newline counts.  Only the line searches after the locations are
 // known (k_lines: findLocation's bytes.Count, scanner.go:482-503; k_find_spans:
 // the Match line and the Code lines around it, :484-526) read the per-span
 // newline counts, and only inside files that have a location, so the scan
 // kernels skip them (a tenth of k_scan_fast's time: 11.95 -> 10.6 ms on
 // configs[2]) and these kernels count what those searches can reach:
-// k_nl_mark keeps each file's last location end; k_nl_spans (phase 0) counts
-// the file's spans from its first through the span after that end; k_nl_tail
-// sends a file to phase 1 (the rest of its spans) when that next span holds
+// k_nl_cands bounds each candidate file's counting (below); k_nl_spans
+// (phase 0) counts the file's spans from its first through the span after
+// that bound; k_nl_check / k_nl_tail send a file to phase 1 (the rest of its
+// spans) when a location ends past the bound or the span after it holds
 // fewer than kNlTailMin newlines (a forward search past the last location
 // could otherwise jump over uncounted spans).  A span is counted whole,
 // neighbouring files' bytes included, exactly as the scan would have, so
@@ -3857,6 +3856,8 @@ __global__ __launch_bounds__(256) void k_nl_spans(const uint8_t* data, uint64_t 
   }
 }
 
+// One wave per location: P(start), P(end) relative to the file start on the
+// uncensored content; censored_lines() turns them into findLocation's numbers.
 __global__ __launch_bounds__(256) void k_lines(const uint8_t* data, const uint64_t* off, const uint32_t* nl_pre,
                                                DevLoc* locs, uint64_t n_locs) {
   const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
