@@ -3856,10 +3856,26 @@ __global__ __launch_bounds__(256) void k_nl_spans(const uint8_t* data, uint64_t 
   }
 }
 
-// One wave per location: P(start), P(end) relative to the file start on the
-// uncensored content; censored_lines() turns them into findLocation's numbers.
+// The newline prefix at each location file's start, once per file: one wave
+// per location of the (file, start)-sorted list, the first of each file
+// counts (a file with thousands of locations -- minified lines full of rule
+// instances -- read its first block once per location before).
+__global__ __launch_bounds__(256) void k_file_base(const uint8_t* data, const uint64_t* off, const uint32_t* nl_pre,
+                                                   const DevLoc* locs, uint64_t n_locs, uint32_t* fbase) {
+  const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  if (w >= n_locs) return;
+  const uint32_t f = locs[w].file;
+  if (w > 0 && locs[w - 1].file == f) return;
+  const uint32_t g = wave_nl_prefix(data, nl_pre, off[f], lane);
+  if (lane == 0) fbase[f] = g;
+}
+
+// One wave per location (sorted by (file, start)): P(start), P(end)
+// relative to the file start (k_file_base) on the uncensored content;
+// censored_lines() turns them into findLocation's numbers.
 __global__ __launch_bounds__(256) void k_lines(const uint8_t* data, const uint64_t* off, const uint32_t* nl_pre,
-                                               DevLoc* locs, uint64_t n_locs) {
+                                               const uint32_t* fbase, DevLoc* locs, uint64_t n_locs) {
   const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63;
   if (w >= n_locs) return;
@@ -3867,13 +3883,13 @@ __global__ __launch_bounds__(256) void k_lines(const uint8_t* data, const uint64
   if (L.flags) return;
   const uint64_t fs = off[L.file];
   if (L.start > L.end || fs + L.end >= off[L.file + 1]) return;  // never read outside the file
-  // the three prefixes in one wave pass: a 4 KiB block shared by two of
-  // them is read once (the location and its file start usually share one)
+  // both prefixes in one wave pass (a 4 KiB block they share is read once)
   uint32_t g[3];
-  wave_nl_prefix3(data, nl_pre, fs, fs + L.start, fs + L.end, lane, g);
+  wave_nl_prefix3(data, nl_pre, fs + L.start, fs + L.start, fs + L.end, lane, g);
   if (lane == 0) {  // raw prefix counts P(start), P(end); see censored_lines()
-    locs[w].start_line = g[1] - g[0];
-    locs[w].end_line = g[2] - g[0];
+    const uint32_t b = fbase[L.file];
+    locs[w].start_line = g[1] - b;
+    locs[w].end_line = g[2] - b;
   }
 }
 
@@ -5087,6 +5103,7 @@ struct tsg_engine {
   // set by the caller), and nl_deferred records that the last scan did, so
   // k_nl_spans counts the spans of the files that have locations
   bool nl_lazy = false, nl_deferred = false;
+  DBuf<uint32_t> fbase;  // newline prefix at each location file's start (k_file_base)
   DBuf<unsigned long long> nl_last;  // per file: counted bound + 1 (0: none) | kNlFull (k_nl_cands / _check / _tail)
   hipEvent_t ev_nl[2] = {nullptr, nullptr};  // candidates ready -> phase-0 count done (side stream)
   bool nl_pending = false;                   // a phase-0 count was issued on the side stream
@@ -7327,9 +7344,6 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->nl_blocks.p, e->nl_pre.p, n_nlb, s));
     HIP_TRY(e->cub_tmp.ensure(tmp + 1));
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(e->cub_tmp.p, tmp, e->nl_blocks.p, e->nl_pre.p, n_nlb, s));
-    hipLaunchKernelGGL(k_lines, dim3((uint32_t)((n_locs * 64 + 255) / 256)), dim3(256), 0, s, d_data, d_off,
-                       e->nl_pre.p, e->locs.p, n_locs);
-    HIP_TRY(hipGetLastError());
     // order by (file, start) on the device (censored_lines walks files in order)
     HIP_TRY(e->keys.ensure(n_locs));
     HIP_TRY(e->keys2.ensure(n_locs));
@@ -7346,6 +7360,11 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
                                                (int)n_locs, 0, 64, s));
     hipLaunchKernelGGL(k_loc_gather, dim3((uint32_t)((n_locs + 255) / 256)), dim3(256), 0, s, e->locs.p,
                        e->vals2.p, n_locs, e->locs2.p);
+    HIP_TRY(e->fbase.ensure(nf + 1));
+    hipLaunchKernelGGL(k_file_base, dim3((uint32_t)((n_locs * 64 + 255) / 256)), dim3(256), 0, s, d_data, d_off,
+                       e->nl_pre.p, e->locs2.p, n_locs, e->fbase.p);
+    hipLaunchKernelGGL(k_lines, dim3((uint32_t)((n_locs * 64 + 255) / 256)), dim3(256), 0, s, d_data, d_off,
+                       e->nl_pre.p, e->fbase.p, e->locs2.p, n_locs);
     HIP_TRY(hipGetLastError());
     // ---- 8. findings (censored lines, Match, Code, order) on the device
     if ((rc = build_findings_dev(e, d_data, d_off, nbytes, nf, n_locs, res))) {
