@@ -313,6 +313,9 @@ __device__ inline void report_t(const ScanParams& P, uint32_t st, uint64_t p, ui
         *last_kw = key;
         uint32_t* wp = &P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)];
         const uint32_t bit = 1u << (pd.kw & 31);
+        // (read first: configs[4]'s C5 files repeat a keyword thousands of
+        // times, and plain atomics on those words slowed k_big_resolve's path
+        // by ~0.25 ms, profiles/r04ai; k_report's plain atomics are quicker)
         if (!(__hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(wp, bit);
       }
     }
