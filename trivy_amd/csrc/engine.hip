@@ -3820,7 +3820,9 @@ __global__ __launch_bounds__(256) void k_nl_spans(const uint8_t* data, uint64_t 
                                                   uint32_t phase) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t n_spans = (nbytes + kNlBlock - 1) / kNlBlock;
-  const uint64_t sp0 = ((uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * 64;
+  const uint64_t n_waves = (uint64_t)gridDim.x * (blockDim.x / 64);
+  for (uint64_t sp0 = ((uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * 64; sp0 < n_spans;
+       sp0 += n_waves * 64) {
   const uint64_t sp = sp0 + lane;
   bool need = false;
   if (sp < n_spans) {
@@ -3856,6 +3858,7 @@ __global__ __launch_bounds__(256) void k_nl_spans(const uint8_t* data, uint64_t 
     }
     for (uint32_t d = 32; d; d >>= 1) cnt += __shfl_xor(cnt, d);
     if (lane == 0) nl_blocks[sp0 + k] = cnt;
+  }
   }
 }
 
@@ -6951,7 +6954,10 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
       HIP_TRY(hipEventRecord(e->ev_nl[0], s));
       HIP_TRY(hipStreamWaitEvent(e->side, e->ev_nl[0], 0));
       const uint64_t n_spans = (nbytes + kNlBlock - 1) / kNlBlock;
-      hipLaunchKernelGGL(k_nl_spans, dim3((uint32_t)((n_spans + 255) / 256)), dim3(256), 0, e->side, d_data, nbytes,
+      uint32_t nl_blocks0 = (uint32_t)((n_spans + 255) / 256);
+      if (const char* v = experiment_env("TSG_NL_BLOCKS_PER_CU"))  // (A/B: a thinner phase-0 grid under k_verify)
+        nl_blocks0 = std::min<uint32_t>(nl_blocks0, std::max(1, atoi(v)) * std::max(1u, e->num_cus));
+      hipLaunchKernelGGL(k_nl_spans, dim3(nl_blocks0), dim3(256), 0, e->side, d_data, nbytes,
                          d_off, e->region_file.p, nbytes / kNlBlock + 1, nf, e->nl_last.p, e->nl_blocks.p, 0u);
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(e->ev_nl[1], e->side));
