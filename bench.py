@@ -440,41 +440,67 @@ def cpu_quota():
     return n
 
 
-def cpu_baseline(N, c, locs, rs, seconds, threads):
-    """Time bench_cpu/libtsg_cpu_scan.so — Scanner.Scan restated in C++ on
-    the repo's host Go-regexp VM, `threads` threads — on a bounded sample of the
-    same corpus: the first files in index order, copied from HBM (copy excluded
-    from the clock).  Per-file finding counts are checked against the GPU run."""
+def cpu_lib():
+    """bench_cpu/libtsg_cpu_scan.so: Scanner.Scan restated in C++ on the repo's
+    host Go-regexp VM (tsgb_cpu_scan), and per-file finding digests of an engine
+    result read through the drop-in ABI (tsgb_result_digest): tests/digest.py."""
     lib = ctypes.CDLL(os.path.join(ROOT, "bench_cpu", "libtsg_cpu_scan.so"))
     lib.tsgb_cpu_scan.restype = ctypes.c_int
     lib.tsgb_cpu_scan.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
-                                  ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
-                                  ctypes.POINTER(ctypes.c_double)]
+                                  ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double)]
+    lib.tsgb_result_digest.restype = ctypes.c_int
+    lib.tsgb_result_digest.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                       ctypes.c_void_p, ctypes.c_void_p]
+    return lib
+
+
+def gpu_digests(N, lib, res, n_files):
+    """(count, digest) per file of an engine result: every finding's rule,
+    location, StartLine, EndLine, Match and Code lines (tsg_result_findings)."""
+    cnt = np.zeros(n_files, dtype=np.uint32)
+    dig = np.zeros(n_files, dtype=np.uint64)
+    fn = ctypes.cast(N.lib.tsg_result_findings, ctypes.c_void_p)
+    N.check(lib.tsgb_result_digest(fn, res, 0, n_files, cnt.ctypes.data, dig.ctypes.data))
+    return cnt, dig
+
+
+def cpu_scan_range(N, lib, c, a, b, threads):
+    """tsgb_cpu_scan over files [a, b) of the corpus, copied from HBM (copy not
+    timed): (content bytes, wall seconds, per-file counts, per-file digests)."""
     off = c["off"]
-    poff = c["d_poff"].cpu().numpy()
-    gpu_counts = np.bincount(locs["file"].astype(np.int64), minlength=c["n_files"]) if len(locs) else \
-        np.zeros(c["n_files"], np.int64)
+    poff = c["poff_host"]
+    host = c["d_data"][int(off[a]): int(off[b])].cpu().numpy()
+    pb = c["d_paths"][int(poff[a]): int(poff[b])].cpu().numpy().tobytes()
+    p0 = int(poff[a])
+    paths = [pb[int(poff[i]) - p0:int(poff[i + 1]) - p0] for i in range(a, b)]
+    arr = (ctypes.c_char_p * (b - a))(*paths)
+    loff = (off[a:b + 1] - off[a]).astype(np.uint64)
+    per = np.zeros(b - a, dtype=np.uint32)
+    dig = np.zeros(b - a, dtype=np.uint64)
+    tot, sec = ctypes.c_uint64(), ctypes.c_double()
+    N.check(lib.tsgb_cpu_scan(c["rs_handle"], host.ctypes.data, loff.ctypes.data, b - a,
+                              ctypes.cast(arr, ctypes.c_void_p), threads, 0, per.ctypes.data, dig.ctypes.data,
+                              ctypes.byref(tot), ctypes.byref(sec)))
+    return int(off[b] - off[a]) - (b - a), sec.value, per, dig
 
-    def run(k):
-        host = c["d_data"][: int(off[k])].cpu().numpy()
-        pb = c["d_paths"][: int(poff[k])].cpu().numpy().tobytes()
-        paths = [pb[int(poff[i]):int(poff[i + 1])] for i in range(k)]
-        arr = (ctypes.c_char_p * k)(*paths)
-        per = np.zeros(k, dtype=np.uint32)
-        tot, sec = ctypes.c_uint64(), ctypes.c_double()
-        N.check(lib.tsgb_cpu_scan(rs, host.ctypes.data, off.ctypes.data, k, ctypes.cast(arr, ctypes.c_void_p),
-                                  threads, per.ctypes.data, ctypes.byref(tot), ctypes.byref(sec)))
-        nbytes = int(off[k]) - k  # content bytes (NUL separators excluded)
-        return nbytes, sec.value, per
 
+def cpu_baseline(N, c, res, seconds, threads):
+    """Time bench_cpu/libtsg_cpu_scan.so — Scanner.Scan restated in C++ on
+    the repo's host Go-regexp VM, `threads` threads — on a bounded sample of the
+    same corpus: the first files in index order, copied from HBM (copy excluded
+    from the clock).  Every sampled file's complete findings (digest of rule,
+    location, lines, Match, Code) are compared with the GPU run's."""
+    lib = cpu_lib()
+    off = c["off"]
+    g_cnt, g_dig = gpu_digests(N, lib, res, c["n_files"])
     # calibrate on ~64 MB, then size the sample for `seconds` of wall time
-    k0 = int(np.searchsorted(off, 64 << 20))
-    k0 = max(1, min(k0, c["n_files"]))
-    b0, t0, _ = run(k0)
+    k0 = max(1, min(int(np.searchsorted(off, 64 << 20)), c["n_files"]))
+    b0, t0, _, _ = cpu_scan_range(N, lib, c, 0, k0, threads)
     want = min(int(b0 / max(t0, 1e-6) * seconds), 16 << 30, int(off[-1]))
     k = max(k0, min(c["n_files"], int(np.searchsorted(off, want))))
-    nbytes, dt, per = run(k)
-    agree = int((per.astype(np.int64) == gpu_counts[:k]).sum())
+    nbytes, dt, per, dig = cpu_scan_range(N, lib, c, 0, k, threads)
+    same = (per == g_cnt[:k]) & (dig == g_dig[:k])
     phys = physical_cores()
     return dict(value=nbytes / dt / 1e9, unit="GB/s", cores=threads, kind="cpp-restatement",
                 physical_cores=phys,
@@ -483,9 +509,42 @@ def cpu_baseline(N, c, locs, rs, seconds, threads):
                        f"set of {len(os.sched_getaffinity(0))} capped by the cgroup CPU quota"
                        + (f"; the host has {phys} physical cores" if phys else "") + "); "
                        "bench_cpu/cpu_scan.cpp: Scanner.Scan restated in C++ on the repo's host Go-regexp VM "
-                       "(not Go: no Go toolchain in the image); per-file finding counts equal the GPU's on "
-                       f"{agree}/{k} files",
-                files_agree=agree, files=k)
+                       "(not Go: no Go toolchain in the image); complete findings (rule, offsets, lines, Match, "
+                       f"Code) identical to the GPU's on {int(same.sum())}/{k} files",
+                files_identical=int(same.sum()), files=k, findings=int(per.sum()))
+
+
+def full_parity(N, c, res, threads, ranges, label):
+    """Every file of `ranges` ([a, b) file index ranges) through the C++
+    restatement (pinned to the oracle by tests/test_cpu_baseline.py), its
+    complete findings compared with the GPU result's, file by file.  Chunks of
+    ~4 GB; a progress line per chunk on stderr."""
+    lib = cpu_lib()
+    g_cnt, g_dig = gpu_digests(N, lib, res, c["n_files"])
+    off = c["off"]
+    files = same = nbytes = f_cpu = f_gpu = 0
+    secs = 0.0
+    bad = []
+    t_all = time.perf_counter()
+    for a, b in ranges:
+        while a < b:
+            e = int(np.searchsorted(off, off[a] + (4 << 30), side="right")) - 1
+            e = min(b, max(a + 1, e))
+            nb, dt, per, dig = cpu_scan_range(N, lib, c, a, e, threads)
+            ok = (per == g_cnt[a:e]) & (dig == g_dig[a:e])
+            bad += [a + int(i) for i in np.nonzero(~ok)[0][:10]]
+            files += e - a
+            same += int(ok.sum())
+            nbytes += nb
+            secs += dt
+            f_cpu += int(per.sum())
+            f_gpu += int(g_cnt[a:e].sum())
+            print(f"full parity [{label}] files {a}..{e}: {same}/{files} identical, {nbytes / 1e9:.2f} GB, "
+                  f"cpu {secs:.0f}s", file=sys.stderr, flush=True)
+            a = e
+    return dict(files=files, files_identical=same, mismatched=bad[:10], bytes=nbytes, findings_cpu=f_cpu,
+                findings_gpu=f_gpu, cpu_seconds=round(secs, 1), wall_seconds=round(time.perf_counter() - t_all, 1),
+                threads=threads, scope=label)
 
 
 def shared_layers_main(args, N, S, torch, dist, barrier, rank, world, device, red_dev):
@@ -640,6 +699,10 @@ def main():
     ap.add_argument("--cpu-cores", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--full-parity", action="store_true",
+                    help="after the timed steps, compare EVERY file's complete findings with the C++ restatement "
+                         "(configs[2]; configs[4]: the unique C5 files + --full-parity-gb of text)")
+    ap.add_argument("--full-parity-gb", type=float, default=0.0, help="--full-parity: limit to the first GB")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for N > 1 (nccl = RCCL; gloo for several ranks on one GPU in tests)")
     ap.add_argument("--shared", action="store_true",
@@ -708,6 +771,8 @@ def main():
     sc = S.new_scanner(cfg, device=device)
     eng = S.get_engine(device)
     rs = sc._rs.handle
+    c["rs_handle"] = rs
+    c["poff_host"] = c["d_poff"].cpu().numpy().astype(np.int64)
     st = [ctypes.c_uint32() for _ in range(4)]
     fast = ctypes.c_int()
     N.check(N.lib.tsg_ruleset_stats(rs, *[ctypes.byref(x) for x in st], ctypes.byref(fast)))
@@ -896,7 +961,24 @@ def main():
         # every CPU this process may run on: the affinity set capped by the
         # cgroup quota (N = the cores used, stated)
         cores = args.cpu_cores or cpu_quota()
-        cpu = cpu_baseline(N, c, locs, rs, args.cpu_seconds, cores)
+        cpu = cpu_baseline(N, c, last, args.cpu_seconds, cores)
+    full = None
+    if rank == 0 and args.full_parity and args.config in (2, 4) and last is not None:
+        cores = args.cpu_cores or cpu_quota()
+        if args.config == 2:
+            lim = args.full_parity_gb
+            nf = c["n_files"] if not lim else int(np.searchsorted(c["off"], int(lim * 1e9)))
+            full = full_parity(N, c, last, cores, [(0, max(1, nf))],
+                               "configs[2]: every file" if not lim else f"configs[2]: first {lim:g} GB")
+        else:
+            # the C5 material's unique files (stress-rule instances, binary-ish
+            # files, the 1 MiB and 16 MiB minified lines) + the first
+            # --full-parity-gb of the generated text
+            f0 = c["first_stress"]
+            nf = int(np.searchsorted(c["off"], int((args.full_parity_gb or 0.25) * 1e9)))
+            full = full_parity(N, c, last, cores, [(f0, f0 + len(stress_unique)), (0, max(1, min(nf, f0)))],
+                               f"configs[4]: the {len(stress_unique)} unique C5 files + the first "
+                               f"{args.full_parity_gb or 0.25:g} GB of generated text")
     if last is not None and args.config != 3:
         N.lib.tsg_result_free(last)
     if rank == 0:
@@ -940,6 +1022,7 @@ def main():
                             "findings": round(stage[22], 3)} if len(stage) > 22 and args.config in (0, 3) else {})},
             "cpu_baseline": cpu,
             "parity": parity,
+            **({"full_parity": full} if full is not None else {}),
         }
         print(json.dumps(out), flush=True)
     if dist is not None:

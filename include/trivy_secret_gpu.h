@@ -32,6 +32,7 @@ extern "C" {
 #define TSG_ERR_UNSUPPORTED 5 /* rule feature outside this engine's coverage (e.g. a non-ASCII keyword) */
 #define TSG_ERR_INTERNAL 6
 #define TSG_ERR_PANIC 7       /* input on which the Go reference panics (secret group did not participate) */
+#define TSG_ERR_FULL 8        /* tsg_staging_add: the staging buffer has no room for the file */
 
 /* AllowRule — pkg/fanal/secret/scanner.go:191-196 (Description stays host-side). */
 typedef struct tsg_allow_rule {
@@ -156,6 +157,29 @@ void tsg_result_free(tsg_result* r);
  * Analyze hands it to Scan; findings are built from it. */
 int tsg_analyze(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, size_t n_files, tsg_result** out);
 
+/* Caller-filled staging: a page-locked batch buffer the caller reads files
+ * straight into (read(2) / io.ReadFull into *dst), so a batch costs one host
+ * write per byte and one H2D, with no intermediate copy or pack (tsg_scan /
+ * tsg_analyze pack the caller's buffers into the engine's own staging).
+ * tsg_staging_add reserves `len` bytes for one file (its NUL separator is
+ * written by the library) and returns where to put them; TSG_ERR_FULL when
+ * the buffer has no room -- run the batch, tsg_staging_reset, add again (a
+ * file larger than the whole buffer needs a larger staging or tsg_scan).
+ * A staging belongs to its caller and may be used with any engine; it must
+ * not be written while a staged call on it runs.  tsg_analyze_staged is
+ * tsg_analyze over the staged RAW files (IsBinary, '\r' strip, Scan),
+ * tsg_scan_staged is tsg_scan over CR-stripped ones; file i of the result is
+ * the i-th file added since the last reset. */
+typedef struct tsg_staging tsg_staging;
+int tsg_staging_create(size_t capacity_bytes, tsg_staging** out);
+int tsg_staging_add(tsg_staging* st, const char* path, uint64_t len, uint8_t** dst);
+size_t tsg_staging_count(const tsg_staging* st);
+size_t tsg_staging_bytes(const tsg_staging* st); /* contents + one separator per file */
+void tsg_staging_reset(tsg_staging* st);
+void tsg_staging_free(tsg_staging* st);
+int tsg_analyze_staged(tsg_engine* e, const tsg_ruleset* rs, const tsg_staging* st, tsg_result** out);
+int tsg_scan_staged(tsg_engine* e, const tsg_ruleset* rs, const tsg_staging* st, tsg_result** out);
+
 /* Byte-range split of ONE large file across GPUs (the reference
  * scans a file of any size whole, scanner.go:371-452, and the walker spools
  * tar entries >= 100 MiB to disk and still scans them, walker/cached_file.go:36-52).
@@ -184,8 +208,10 @@ void tsg_part_free(uint8_t* blob);
 /* The owner: d_file = the whole file in HBM followed by its NUL separator
  * (d_file[file_len] == 0); the parts must tile [0, file_len) (any order).
  * The result is a one-file result (file index 0), as tsg_scan_device's.
- * file_len must be below 2 GiB, as for every entry point that verifies (the
- * match search runs on 31-bit file positions): TSG_ERR_UNSUPPORTED otherwise. */
+ * Files of any size up to the batch limit (2^44 bytes) merge: the match search
+ * runs 64-bit positions for files past 2^31 - 1 bytes.  The one limit, as for
+ * every entry point that verifies: a single match of 4 GiB or more (its allow
+ * regexes run on 32-bit match strings) returns TSG_ERR_UNSUPPORTED. */
 int tsg_scan_merge_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_file, uint64_t file_len,
                           const char* path, const uint8_t* const* blobs, const size_t* blob_lens, size_t n_parts,
                           tsg_result** out);

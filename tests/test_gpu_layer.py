@@ -111,6 +111,26 @@ def test_analyze_layers_pipelined_matches_single():
         assert _plain(secs) == _oracle_plain(want)
 
 
+def test_analyze_layers_error_leaves_other_layers_intact():
+    """A layer whose walk fails (a corrupt header) among layers that are being
+    analyzed on both engines: the error surfaces as the walk error, every
+    other walk is closed by its own analysis or, if never picked up, by the
+    caller (no freed walk reaches tsg_analyze_layer), and the engines serve
+    the next call with results equal to the oracle's."""
+    a = SecretAnalyzer()
+    a.init("")
+    good = [_layer(60 + k, 150) for k in range(6)]
+    bad = bytearray(good[1])
+    bad[148:156] = b"99999999"  # header checksum no longer matches
+    layers = [good[0], bytes(bad)] + good[2:]
+    with pytest.raises(W.WalkError):
+        W.analyze_layers(a, layers, walk_threads=3)
+    got = W.analyze_layers(a, good[:3], walk_threads=3)
+    for data, (secs, _, _) in zip(good[:3], got):
+        want, _, _ = _oracle_layer(data)
+        assert _plain(secs) == _oracle_plain(want)
+
+
 def test_analyze_layer_finding_order():
     """Two findings of one rule whose Match order (Scan's sort) is the reverse
     of their line order: the layer result carries AnalysisResult.Sort's

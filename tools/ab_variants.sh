@@ -6,7 +6,7 @@ export TSG_LIB_VARIANT=exp
 # under a rocprofv3 kernel trace, printing per-kernel average times.
 set -o pipefail
 export TMPDIR=/tmp
-[ -n "$SKIP_CHECK" ] || bash tools/gpu_check.sh || exit 1
+[ -n "$SKIP_CHECK" ] || bash tools/gpu_run.sh ab_check pytest smoke || exit 1
 GB=${GB:-20}
 for v in ${VARIANTS:-1x8 1x4 2x4}; do
   TSG_FAST_VARIANT=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/ab_$v -o run -- python3 -u bench.py --gb $GB --steps 3 --warmup 1 --no-cpu > gpurun_out/ab_$v.log 2>&1 || { echo "bench $v failed"; tail -5 gpurun_out/ab_$v.log; exit 1; }

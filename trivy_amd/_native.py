@@ -33,6 +33,7 @@ TSG_ERR_NO_DEVICE = 4
 TSG_ERR_UNSUPPORTED = 5
 TSG_ERR_INTERNAL = 6
 TSG_ERR_PANIC = 7
+TSG_ERR_FULL = 8
 
 TSG_FILE_PATH_ALLOWED = 1
 TSG_FILE_SPECIAL = 2
@@ -164,6 +165,17 @@ _SIGS = {
     "tsg_result_free": (None, [ctypes.c_void_p]),
     "tsg_analyze": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(FileC), ctypes.c_size_t,
                                    ctypes.POINTER(ctypes.c_void_p)]),
+    "tsg_staging_create": (ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+    "tsg_staging_add": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint64,
+                                       ctypes.POINTER(ctypes.c_void_p)]),
+    "tsg_staging_count": (ctypes.c_size_t, [ctypes.c_void_p]),
+    "tsg_staging_bytes": (ctypes.c_size_t, [ctypes.c_void_p]),
+    "tsg_staging_reset": (None, [ctypes.c_void_p]),
+    "tsg_staging_free": (None, [ctypes.c_void_p]),
+    "tsg_analyze_staged": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.POINTER(ctypes.c_void_p)]),
+    "tsg_scan_staged": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.POINTER(ctypes.c_void_p)]),
     "tsg_engine_gate_timings": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_size_t,
                                                ctypes.POINTER(ctypes.c_size_t)]),
     "tsg_gate_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

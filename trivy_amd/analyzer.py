@@ -1,10 +1,14 @@
 """Mirror of the drop-in boundary, Trivy's SecretAnalyzer
 (pkg/fanal/analyzer/secret/secret.go:28-153) and utils.IsBinary
-(pkg/fanal/utils/utils.go:77-95), with a batched analyze for the GPU.
+(pkg/fanal/utils/utils.go:77-95), with a batched analyze for the GPU, and
+the post-analyzer hook of the tagged Go build
+(integration/go/pkg/fanal/analyzer/secret/secret_mi355x.go), mirrored line
+for line by SecretPostAnalyzer.
 """
 from __future__ import annotations
 
 import os
+import sys
 from typing import List, Optional, Sequence, Tuple
 
 from . import secret as S
@@ -92,3 +96,82 @@ class SecretAnalyzer:
                 if res is not None and res.Findings:
                     out[i] = [res]
         return out
+
+
+GPU_BATCH_BYTES = 512 << 20  # --secret-gpu-batch-bytes
+
+
+class SecretPostAnalyzer:
+    """The tagged build's secret analyzer (secret_mi355x.go): registered as a
+    PostAnalyzer (analyzer.go:78-82, RegisterPostAnalyzer :102-107), so the
+    artifact walk only calls Required per file and links the required files
+    into the post-analyzer FS (artifact/local/fs.go:100-106); PostAnalyze then
+    reads every file straight into GPU staging and runs Analyze's per-file
+    work (IsBinary, '\r' strip, Scan) batch by batch.  Paths are the FS's
+    relative paths: a filesystem artifact calls Analyze with Dir = the scan
+    root, so no '/' prefix (secret.go:95-98); image layers take
+    walker.analyze_layers instead."""
+
+    def __init__(self, analyzer: SecretAnalyzer, batch_bytes: int = GPU_BATCH_BYTES):
+        self.analyzer = analyzer
+        self.batch_bytes = batch_bytes
+
+    def type(self) -> str:
+        return TYPE
+
+    def version(self) -> int:
+        return VERSION
+
+    def required(self, file_path: str, size: int) -> bool:
+        return self.analyzer.required(file_path, size)
+
+    def post_analyze(self, root: str) -> Optional[List[Secret]]:
+        """PostAnalyze over the FS rooted at `root` (fs.WalkDir order:
+        lexical per directory).  Returns AnalysisResult.Secrets (None when no
+        file has findings)."""
+        secrets: List[Secret] = []
+        with self.analyzer.scanner.new_batch(self.batch_bytes) as batch:
+            def flush():
+                if len(batch) == 0:
+                    return
+                for s in batch.analyze():
+                    if s is not None and s.Findings:
+                        secrets.append(s)
+
+            for path, size in _walk_dir(root):
+                def fill(dst, p=path):
+                    try:
+                        with open(os.path.join(root, p), "rb") as f:
+                            n = f.readinto(dst)
+                        if n != len(dst):
+                            raise OSError("short read")
+                    except OSError as e:
+                        # Analyze's read error skips the file (analyzer.go:430-434 logs it):
+                        # NUL bytes make IsBinary skip it the same way
+                        dst[:] = bytes(len(dst))
+                        print(f"secret: read error {p}: {e}", file=sys.stderr)
+
+                if batch.add(path, size, fill):
+                    continue
+                flush()
+                if not batch.add(path, size, fill):  # larger than the whole staging: one file alone
+                    with open(os.path.join(root, path), "rb") as f:
+                        res = self.analyzer.analyze_batch([(path, f.read(), root)])[0]
+                    if res:
+                        secrets.extend(res)
+            flush()
+        return secrets or None
+
+
+def _walk_dir(root: str):
+    """fs.WalkDir(fsys, ".") regular files as (slash path, size), lexical order."""
+    def rec(rel):
+        full = os.path.join(root, rel) if rel else root
+        for name in sorted(os.listdir(full)):
+            p = f"{rel}/{name}" if rel else name
+            fp = os.path.join(root, p)
+            if os.path.isdir(fp) and not os.path.islink(fp):
+                yield from rec(p)
+            elif os.path.isfile(fp):
+                yield p, os.path.getsize(fp)
+    yield from rec("")

@@ -7328,6 +7328,10 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
       HIP_TRY(hipMemcpyAsync(e->locs.p, e->locs2.p, n_locs * sizeof(DevLoc), hipMemcpyDeviceToDevice, s));
   }
   HIP_TRY(hipEventRecord(e->ev[6], s));
+  if (!n_locs && e->nl_pending) {  // no lines stage: the side count reads the caller's batch, so the call's
+    HIP_TRY(hipStreamWaitEvent(s, e->ev_nl[1], 0));  // final synchronisation must cover it
+    e->nl_pending = false;
+  }
   // ---- 7. line numbers
   if (n_locs) {
     const int n_nlb = (int)(nbytes / kNlBlock + 2);
@@ -7850,16 +7854,10 @@ static int scan_device_impl(tsg_engine* e, const tsg_ruleset* rs, const uint8_t*
 
 // SecretAnalyzer.Analyze over raw files (secret.go:79-113): pack -> H2D ->
 // IsBinary (k_binary) -> '\r' deletion by compaction (k_strip_*) -> scan.
-static int analyze_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, size_t n_files,
-                        tsg_result** out) {
-  if (!e || !rs || !out || (n_files && !files)) return TSG_ERR_INVALID_ARG;
-  std::lock_guard<std::mutex> lk(e->mu);
-  *out = nullptr;
-  HIP_TRY(hipSetDevice(e->device));
-  const auto w0 = std::chrono::steady_clock::now();
-  uint64_t nbytes = 0;
-  int src = stage_host_batch(e, files, n_files, &nbytes);
-  if (src) return src;
+// The batch is in e->data / e->off / e->paths / e->path_off (staged by the
+// caller of this function, under e->mu, since w0).
+static int analyze_staged_batch(tsg_engine* e, const tsg_ruleset* rs, size_t n_files, uint64_t nbytes,
+                                std::chrono::steady_clock::time_point w0, tsg_result** out) {
   hipStream_t s = e->stream;
   const uint32_t nf = (uint32_t)n_files;
   const uint64_t n_blk = (nbytes + kStripBlock - 1) / kStripBlock;
@@ -7931,6 +7929,156 @@ static int analyze_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* fi
   return TSG_OK;
 }
 
+static int analyze_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, size_t n_files,
+                        tsg_result** out) {
+  if (!e || !rs || !out || (n_files && !files)) return TSG_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(e->mu);
+  *out = nullptr;
+  HIP_TRY(hipSetDevice(e->device));
+  const auto w0 = std::chrono::steady_clock::now();
+  uint64_t nbytes = 0;
+  int src = stage_host_batch(e, files, n_files, &nbytes);
+  if (src) return src;
+  return analyze_staged_batch(e, rs, n_files, nbytes, w0, out);
+}
+
+// ---- caller-filled staging (tsg_staging_*): files read straight into
+// page-locked memory in the batch layout, so a staged call needs no host pack
+struct tsg_staging {
+  uint8_t* buf = nullptr;  // hipHostMalloc'd, `cap` bytes: contents, each followed by its NUL separator
+  size_t cap = 0;
+  std::vector<uint64_t> off{0};   // n + 1 batch offsets
+  std::vector<uint64_t> poff{0};  // n + 1 path offsets
+  std::string paths;
+};
+
+int tsg_staging_create(size_t capacity_bytes, tsg_staging** out) {
+  if (!out || capacity_bytes == 0) return TSG_ERR_INVALID_ARG;
+  *out = nullptr;
+  try {
+    auto* st = new tsg_staging();
+    if (hipHostMalloc((void**)&st->buf, capacity_bytes, hipHostMallocDefault) != hipSuccess) {
+      delete st;
+      set_last_error("hipHostMalloc failed");
+      return TSG_ERR_DEVICE;
+    }
+    st->cap = capacity_bytes;
+    *out = st;
+    return TSG_OK;
+  } catch (const std::exception& ex) {
+    set_last_error(std::string("internal error: ") + ex.what());
+    return TSG_ERR_INTERNAL;
+  }
+}
+
+int tsg_staging_add(tsg_staging* st, const char* path, uint64_t len, uint8_t** dst) {
+  if (!st || !dst) return TSG_ERR_INVALID_ARG;
+  *dst = nullptr;
+  const uint64_t at = st->off.back();
+  if (len >= kMaxFileBytes || at + len + 1 > st->cap) {
+    set_last_error(st->off.size() == 1 ? "staging: the file is larger than the staging buffer"
+                                       : "staging: buffer full (run the batch, reset, add again)");
+    return TSG_ERR_FULL;
+  }
+  try {
+    const size_t plen = path ? strlen(path) : 0;
+    st->paths.append(path ? path : "", plen);
+    st->poff.push_back(st->paths.size());
+    st->off.push_back(at + len + 1);
+  } catch (const std::exception& ex) {
+    set_last_error(std::string("internal error: ") + ex.what());
+    return TSG_ERR_INTERNAL;
+  }
+  st->buf[at + len] = 0;  // the separator
+  *dst = st->buf + at;
+  return TSG_OK;
+}
+
+size_t tsg_staging_count(const tsg_staging* st) { return st ? st->off.size() - 1 : 0; }
+size_t tsg_staging_bytes(const tsg_staging* st) { return st ? st->off.back() : 0; }
+
+void tsg_staging_reset(tsg_staging* st) {
+  if (!st) return;
+  st->off.assign(1, 0);
+  st->poff.assign(1, 0);
+  st->paths.clear();
+}
+
+void tsg_staging_free(tsg_staging* st) {
+  if (!st) return;
+  if (st->buf) (void)hipHostFree(st->buf);
+  delete st;
+}
+
+// The staged batch -> e->data / e->off / e->paths / e->path_off: one H2D per
+// array straight from the page-locked buffer.
+static int upload_staging(tsg_engine* e, const tsg_staging* st, uint64_t* nbytes_out) {
+  const size_t n = st->off.size() - 1;
+  const uint64_t nbytes = st->off.back(), pbytes = st->paths.size();
+  if (e->data.ensure(nbytes + 16) != hipSuccess || e->off.ensure(n + 1) != hipSuccess ||
+      e->paths.ensure(pbytes + 16) != hipSuccess || e->path_off.ensure(n + 1) != hipSuccess) {
+    set_last_error("hipMalloc failed");
+    return TSG_ERR_DEVICE;
+  }
+  hipStream_t s = e->stream;
+  const auto t0 = std::chrono::steady_clock::now();
+  bool ok = (nbytes == 0 || hipMemcpyAsync(e->data.p, st->buf, nbytes, hipMemcpyHostToDevice, s) == hipSuccess) &&
+            (pbytes == 0 || hipMemcpyAsync(e->paths.p, st->paths.data(), pbytes, hipMemcpyHostToDevice, s) == hipSuccess) &&
+            hipMemcpyAsync(e->off.p, st->off.data(), (n + 1) * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
+            hipMemcpyAsync(e->path_off.p, st->poff.data(), (n + 1) * 8, hipMemcpyHostToDevice, s) == hipSuccess &&
+            hipStreamSynchronize(s) == hipSuccess;
+  if (!ok) {
+    set_last_error("host-to-device copy failed");
+    return TSG_ERR_DEVICE;
+  }
+  e->stage_ms[0] = 0.0;  // nothing packed: the caller read the files into place
+  e->stage_ms[1] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  *nbytes_out = nbytes;
+  return TSG_OK;
+}
+
+static int staged_impl(tsg_engine* e, const tsg_ruleset* rs, const tsg_staging* st, bool analyze, tsg_result** out) {
+  if (!e || !rs || !st || !out) return TSG_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(e->mu);
+  *out = nullptr;
+  HIP_TRY(hipSetDevice(e->device));
+  const auto w0 = std::chrono::steady_clock::now();
+  uint64_t nbytes = 0;
+  int rc = upload_staging(e, st, &nbytes);
+  if (rc) return rc;
+  const size_t n = st->off.size() - 1;
+  if (analyze) return analyze_staged_batch(e, rs, n, nbytes, w0, out);
+  auto* res = new tsg_result();
+  rc = run_pipeline(e, rs, e->data.p, e->off.p, e->paths.p, e->path_off.p, n, nbytes, res);
+  if (rc) {
+    delete res;
+    return rc;
+  }
+  res->impl.timings.resize(std::max<size_t>(res->impl.timings.size(), 20), 0.0);
+  res->impl.timings[18] = e->stage_ms[0];
+  res->impl.timings[19] = e->stage_ms[1];
+  *out = res;
+  return TSG_OK;
+}
+
+int tsg_analyze_staged(tsg_engine* e, const tsg_ruleset* rs, const tsg_staging* st, tsg_result** out) {
+  try {
+    return staged_impl(e, rs, st, true, out);
+  } catch (const std::exception& ex) {
+    set_last_error(std::string("internal error: ") + ex.what());
+    return TSG_ERR_INTERNAL;
+  }
+}
+
+int tsg_scan_staged(tsg_engine* e, const tsg_ruleset* rs, const tsg_staging* st, tsg_result** out) {
+  try {
+    return staged_impl(e, rs, st, false, out);
+  } catch (const std::exception& ex) {
+    set_last_error(std::string("internal error: ") + ex.what());
+    return TSG_ERR_INTERNAL;
+  }
+}
+
 int tsg_analyze(tsg_engine* e, const tsg_ruleset* rs, const tsg_file* files, size_t n_files, tsg_result** out) {
   try {
     return analyze_impl(e, rs, files, n_files, out);
@@ -7967,6 +8115,10 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
     e->events = true;
   }
   e->fast_timed = false;
+  if (e->nl_pending) {  // (an earlier scan's side newline count still writes nl_blocks)
+    HIP_TRY(hipStreamWaitEvent(s, e->ev_nl[1], 0));
+    e->nl_pending = false;
+  }
   HIP_TRY(e->ctrl.ensure(1));
   HIP_TRY(e->file_kw.ensure((size_t)nf * RS.kw_words + 1));
   HIP_TRY(e->file_flags.ensure(nf + 1));

@@ -610,10 +610,8 @@ int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_r
       if (r.path >= 0) pr.push_back(r.path);
       pr.insert(pr.end(), r.allow_path.begin(), r.allow_path.end());
     }
-    // ... and the allow regexes (AllowLocation on a match, scanner.go:145-148):
-    // k_verify_fast decides them with the same DFA, without the Pike VM
-    pr.insert(pr.end(), rs->global_allow_regex.begin(), rs->global_allow_regex.end());
-    for (auto& r : rs->rules) pr.insert(pr.end(), r.allow_regex.begin(), r.allow_regex.end());
+    // (only path regexes: AllowLocation's allow regexes run in k_allow /
+    // emit_match as literal prefilter + Pike VM, which need no DFA)
     for (int x : pr) {
       if (rs->path_dfa[x].valid) continue;
       gre::Compiled any;

@@ -358,6 +358,10 @@ class Scanner:
         for binary files (secret.go:80-86)."""
         return self._run(N.lib.tsg_analyze, batch)
 
+    def new_batch(self, capacity: int) -> "Batch":
+        """A caller-filled staging batch (tsg_staging_*) for this scanner."""
+        return Batch(self, capacity)
+
     def _run(self, fn, batch: Sequence[ScanArgs]):
         eng = get_engine(self.device)
         n = len(batch)
@@ -412,6 +416,70 @@ class Scanner:
                     Code=Code(Lines=lines), Match=_s(f.match, f.match_len)))
             out.append(Secret(FilePath=batch[i].file_path, Findings=findings))
         return out
+
+
+class Batch:
+    """Mirror of the Go backend's Batch (integration/go/pkg/fanal/secret/
+    gpu_mi355x.go): files are read straight into a page-locked staging buffer
+    (tsg_staging_add hands out where each file goes), then one call runs the
+    whole batch -- tsg_analyze_staged (RAW files: IsBinary, '\r' strip, Scan)
+    or tsg_scan_staged (CR-stripped content) -- and the staging is reset."""
+
+    def __init__(self, scanner: Scanner, capacity: int):
+        self.scanner = scanner
+        self.handle = ctypes.c_void_p()
+        get_engine(scanner.device)  # selects and initialises the device first
+        N.check(N.lib.tsg_staging_create(capacity, ctypes.byref(self.handle)))
+        self.paths: List[str] = []
+
+    def __len__(self) -> int:
+        return len(self.paths)
+
+    def add(self, file_path: str, size: int, fill) -> bool:
+        """Reserve `size` bytes for file_path and let fill(dst) write them in
+        place (dst: a writable memoryview of exactly `size` bytes).  False when
+        the staging has no room (run the batch and add again)."""
+        dst = ctypes.c_void_p()
+        rc = N.lib.tsg_staging_add(self.handle, file_path.encode("utf-8", "surrogateescape"), size,
+                                   ctypes.byref(dst))
+        if rc == N.TSG_ERR_FULL:
+            return False
+        N.check(rc)
+        if size:
+            fill(memoryview((ctypes.c_uint8 * size).from_address(dst.value)).cast("B"))
+        self.paths.append(file_path)
+        return True
+
+    def analyze(self) -> List[Optional[Secret]]:
+        """tsg_analyze_staged; None for binary files (secret.go:80-86)."""
+        return self._run(N.lib.tsg_analyze_staged)
+
+    def scan(self) -> List[Secret]:
+        return self._run(N.lib.tsg_scan_staged)
+
+    def _run(self, fn):
+        res = ctypes.c_void_p()
+        N.check(fn(get_engine(self.scanner.device), self.scanner._rs.handle, self.handle, ctypes.byref(res)))
+        try:
+            return self.scanner._convert(res, [ScanArgs(p, b"") for p in self.paths])
+        finally:
+            N.lib.tsg_result_free(res)
+            N.lib.tsg_staging_reset(self.handle)
+            self.paths = []
+
+    def close(self) -> None:
+        if self.handle:
+            N.lib.tsg_staging_free(self.handle)
+            self.handle = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        self.close()
 
 
 def new_scanner(config: Optional[Config] = None, device: Optional[int] = None) -> Scanner:

@@ -174,6 +174,8 @@ def _analyze_walked(analyzer, addr: int, n: int, w: _Walk, engine=None) -> List[
     from .secret import get_engine
 
     sc = analyzer.scanner
+    if not w.handle:
+        raise WalkError("layer walk already closed")
     kept = (ctypes.c_uint32 * max(1, w.count))()
     nk = ctypes.c_size_t()
     res = ctypes.c_void_p()
@@ -213,35 +215,55 @@ def analyze_layers(analyzer, layers: Sequence[Layer], skip_files: Sequence[str] 
     """The layers of an image (image.go:242-331 inspects them concurrently),
     pipelined: up to `walk_threads` native walks run ahead on host threads
     (ctypes drops the GIL), and layer k is analyzed on engine k % `engines`
-    of the same GPU (secret.get_engines: own stream and buffers), so one
-    layer's host-to-device staging -- the PCIe-bound part -- overlaps the
-    Required pass, scan pipeline and findings of the layer before it.  One
-    (secrets, opqDirs, whFiles) per layer, in input order."""
+    of the same GPU (secret.get_engines: own stream and buffers), each engine
+    fed by its own single-worker queue, so one layer's host-to-device staging
+    -- the PCIe-bound part -- overlaps the Required pass, scan pipeline and
+    findings of the layer before it.  An extra engine holds its own device
+    scratch and pinned staging: a layer whose analysis fails
+    on an extra engine with a device error (e.g. out of memory) is re-run on
+    the first engine, and that extra engine takes no more layers of this call.
+    One (secrets, opqDirs, whFiles) per layer, in input order."""
     from concurrent.futures import ThreadPoolExecutor
 
     from .secret import get_engines
 
     engs = get_engines(analyzer.scanner.device, max(1, min(engines, len(layers))))
     opened = [_open_layer(x) for x in layers]
+    dead = set()  # extra engines that failed with a device error
 
     def one(k, f):
         _, addr, n, _ = opened[k]
-        with f.result() as w:
-            return (_analyze_walked(analyzer, addr, n, w, engs[k % len(engs)]), w.opq_dirs, w.wh_files)
-
-    try:
-        with ThreadPoolExecutor(max_workers=max(1, walk_threads)) as pool, \
-                ThreadPoolExecutor(max_workers=len(engs)) as apool:
-            futs = [pool.submit(_Walk, addr, n, skip_files, skip_dirs) for _, addr, n, _ in opened]
+        e = k % len(engs)
+        with f.result() as w:  # this task owns the walk: closed here, whatever happens
+            if e in dead:
+                e = 0
             try:
-                # (one worker per engine, layers taken in order: layer k runs on engine k % n)
-                afuts = [apool.submit(one, k, f) for k, f in enumerate(futs)]
-                return [a.result() for a in afuts]
-            finally:
-                for f in futs:  # free walks left behind by an error
-                    if f.done() and f.exception() is None:
-                        f.result().close()
+                return (_analyze_walked(analyzer, addr, n, w, engs[e]), w.opq_dirs, w.wh_files)
+            except N.EngineError as err:
+                if e == 0 or err.code != N.TSG_ERR_DEVICE:
+                    raise
+                dead.add(e)
+                return (_analyze_walked(analyzer, addr, n, w, engs[0]), w.opq_dirs, w.wh_files)
+
+    pool = ThreadPoolExecutor(max_workers=max(1, walk_threads))
+    queues = [ThreadPoolExecutor(max_workers=1) for _ in engs]
+    futs, afuts = [], []
+    try:
+        futs = [pool.submit(_Walk, addr, n, skip_files, skip_dirs) for _, addr, n, _ in opened]
+        afuts = [queues[k % len(engs)].submit(one, k, f) for k, f in enumerate(futs)]
+        return [a.result() for a in afuts]
     finally:
+        # on an error: analyses not started are cancelled, running ones are
+        # waited for (each closes its own walk), and only walks that no
+        # analysis picked up are freed here
+        for a in afuts:
+            a.cancel()
+        for q in queues:
+            q.shutdown(wait=True)
+        pool.shutdown(wait=True)
+        for k, f in enumerate(futs):
+            if (k >= len(afuts) or afuts[k].cancelled()) and f.exception() is None:
+                f.result().close()
         for buf, _, _, close in opened:
             del buf
             close()
