@@ -34,6 +34,29 @@ def test_header_symbols_exported():
                                                  "tsg_regex_find_all") for n in abi)
 
 
+def test_staging_contract_without_gpu():
+    """The caller-filled staging API (tsg_staging_*): NULL handles are
+    rejected and, without a GPU, creating the page-locked buffer fails with
+    TSG_ERR_DEVICE -- no CPU fallback, no crash (the GPU behaviour, including
+    TSG_ERR_FULL and reset, is tests/test_gpu_staging.py)."""
+    import ctypes
+
+    import torch
+
+    d = ctypes.c_void_p()
+    assert N.lib.tsg_staging_add(None, b"x", 5, ctypes.byref(d)) == N.TSG_ERR_INVALID_ARG
+    assert N.lib.tsg_staging_count(None) == 0 and N.lib.tsg_staging_bytes(None) == 0
+    N.lib.tsg_staging_reset(None)
+    N.lib.tsg_staging_free(None)
+    r = ctypes.c_void_p()
+    assert N.lib.tsg_analyze_staged(None, None, None, ctypes.byref(r)) == N.TSG_ERR_INVALID_ARG
+    assert N.lib.tsg_scan_staged(None, None, None, ctypes.byref(r)) == N.TSG_ERR_INVALID_ARG
+    h = ctypes.c_void_p()
+    assert N.lib.tsg_staging_create(0, ctypes.byref(h)) == N.TSG_ERR_INVALID_ARG
+    if not torch.cuda.is_available():
+        assert N.lib.tsg_staging_create(1 << 20, ctypes.byref(h)) == N.TSG_ERR_DEVICE and not h.value
+
+
 def test_version():
     assert b"gfx950" in N.lib.tsg_version()
 
