@@ -172,6 +172,12 @@ struct ScanParams {
   uint32_t* file_flags;  // n_files
   uint64_t* hits;
   uint64_t hit_cap;
+  // k_report: each report wave's own hit region (hit_seg_cap records at
+  // hit_seg + wave * hit_seg_cap; counts in hit_seg_n), packed into `hits` by
+  // k_hits_pack -- null: flushes reserve on ctrl->hits
+  uint64_t* hit_seg;
+  uint32_t* hit_seg_n;
+  uint32_t hit_seg_cap;
   uint64_t* big_outs;  // k_big_walk -> k_big_resolve: output records (position << 16 | state)
   uint64_t big_out_cap;
   Ctrl* ctrl;
@@ -652,16 +658,181 @@ __device__ inline void fast_window(const ScanParams& P, const uint8_t* T, uint32
   C.prev = make_uint2(d[2 * G - 2], d[2 * G - 1]);
 }
 
-template <int CH, int V, int kFastThreads, int kMode = 0, int kWin = 1, bool kPair = false>
+// ---- event resolution (k_report, and the fused scan's own segments)
+constexpr uint32_t kReportThreads = 1024;
+constexpr uint32_t kReportHitCap = 1024;
+constexpr uint32_t kReportLds = kLdsMax - kReportHitCap * 8 - 64;
+constexpr uint32_t kReportWaveHits = kReportHitCap / (kReportThreads / 64);  // LDS hit slots per wave
+constexpr uint32_t kHitSegCap = 4096;  // hit records in each report wave's own region (32 KiB)
+
+__device__ inline uint32_t file_of_pos(const ScanParams& P, uint64_t pos) {
+  const uint64_t r = pos / kNlBlock;
+  const uint32_t hi = r + 1 < P.n_regions ? min(P.region_file[r + 1] + 1, P.n_files) : P.n_files;
+  return find_file(P.off, P.region_file[r], hi, pos);
+}
+
+// ASCII lowercase of 8 bytes at once (bytes 'A'-'Z' gain 0x20)
+__device__ inline uint64_t lower64(uint64_t x) {
+  const uint64_t t = x & 0x7F7F7F7F7F7F7F7Full;
+  const uint64_t up = ((t + 0x3F3F3F3F3F3F3F3Full) ^ (t + 0x2525252525252525ull)) & ~x & 0x8080808080808080ull;
+  return x | (up >> 2);
+}
+
+// The report blob's tables (LDS, or global memory when the blob is too big).
+struct RepView {
+  const uint8_t* B;  // blob base: the scan image first
+  const uint32_t* out_off;
+  const uint16_t* out_pat;
+  const PatDev* pats;
+  const uint8_t* pbytes;
+};
+
+__device__ inline RepView rep_view(const AcDev& ac, const uint8_t* B) {
+  return RepView{B, (const uint32_t*)(B + ac.o_out_off), (const uint16_t*)(B + ac.o_out_pat),
+                 (const PatDev*)(B + ac.o_pats), B + ac.o_pat_bytes};
+}
+
+// One event on one lane: replay its 8 bytes on the image, and per output
+// confirm the pattern on the real bytes, set the file's keyword gate bit and
+// stage the anchor hit in the wave's LDS slots (wbuf / *hcnt_w).
+__device__ inline void report_event(const ScanParams& P, const AcDev& ac, const RepView& R, const FastEvent& ev,
+                                    uint64_t* wbuf, uint32_t* hcnt_w, uint32_t& my_out, uint64_t& last_kw) {
+  const uint32_t out_e = ac.fast_out_entry;
+  uint64_t hist = ((uint64_t)ev.prev.y << 32) | ev.prev.x;  // the 8 raw bytes before (oldest low)
+  uint64_t hlow = lower64(hist);
+  uint32_t e = ev.entry;
+  const uint32_t fx = fold6(ev.cur.x), fy = fold6(ev.cur.y);
+  uint32_t fi = 0xFFFFFFFFu;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    e = fstep(R.B, e, j < 4 ? fx : fy, j & 3);
+    const uint32_t c = ((j < 4 ? ev.cur.x : ev.cur.y) >> (8 * (j & 3))) & 0xFFu;
+    hist = (hist >> 8) | ((uint64_t)c << 56);  // hist byte 7 = c
+    hlow = (hlow >> 8) | ((uint64_t)lower_ascii((uint8_t)c) << 56);
+    if (e < out_e || c >= 0x80) continue;  // an output ending on a byte >= 0x80 is an alias
+    const uint64_t pos = ev.pos + j;
+    const uint32_t st = e;
+    for (uint32_t o = R.out_off[st]; o < R.out_off[st + 1]; ++o) {
+      const uint32_t pid = R.out_pat[o];
+      const PatDev& pd = R.pats[pid];
+      // the automaton's prefix on the real bytes (it ran on folded ones)
+      if ((hlow & pd.m64) != pd.lo64) continue;
+      const bool want_kw = pd.kw_needed != 0;
+      bool want_hit = pd.rule_n != 0 && (hist & pd.rqm64) == pd.rq64;
+      if (!want_kw && !want_hit) continue;
+      const uint32_t tl = pd.len < ac.depth ? pd.len : ac.depth;
+      const uint64_t start = pos + 1 - tl - pd.ext;
+      if (pd.trunc) {  // the rest of a long pattern, on the batch (rare)
+        if (fi == 0xFFFFFFFFu) fi = (P.report_mode & 1) ? (uint32_t)((pos >> 12) % P.n_files) : file_of_pos(P, pos);
+        const uint64_t fend = P.off[fi + 1] - 1;
+        if (start + pd.len > fend) continue;
+        // chunks of 8 batch bytes issued before any compare (one memory
+        // latency per chunk; a byte-by-byte early-exit loop was a chain of
+        // dependent loads)
+        uint32_t bad = 0, req_bad = 0;
+        const uint8_t* pb = R.pbytes + pd.bytes_off;
+        for (uint32_t k0 = tl; k0 < pd.len && !bad; k0 += 8) {
+#pragma unroll
+          for (uint32_t k = k0; k < k0 + 8; ++k)
+            if (k < pd.len) {
+              const uint8_t b = P.data[start + k];
+              bad |= lower_ascii(b) ^ pb[k];
+              if (want_hit && pd.confirm) {
+                const uint8_t r = R.pbytes[pd.req_off + k];
+                req_bad |= (r != 0) & (b != r);
+              }
+            }
+        }
+        if (bad) continue;
+        if (req_bad) want_hit = false;
+      }
+      ++my_out;
+      if (want_kw) {
+        if (fi == 0xFFFFFFFFu) fi = (P.report_mode & 1) ? (uint32_t)((pos >> 12) % P.n_files) : file_of_pos(P, pos);
+        const uint64_t key = ((uint64_t)fi << 32) | pd.kw;  // per-lane dedupe of repeated keywords
+        if (last_kw != key) {
+          last_kw = key;
+          // fire-and-forget atomic: reading the word first to skip the
+          // atomics of repeated keywords put an L2 round trip on the lane's
+          // chain (k_report 650 -> 618 us on configs[2] without it,
+          // profiles/r04ac)
+          atomicOr(&P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)], 1u << (pd.kw & 31));
+        }
+      }
+      if (want_hit) {
+        const uint32_t slot = atomicAdd(hcnt_w, 1u);  // (this wave's slots only)
+        const uint64_t hrec = (start << 16) | pid;
+        if (slot < kReportWaveHits) {
+          wbuf[slot] = hrec;
+        } else {
+          unsigned long long idx = atomicAdd(&P.ctrl->hits, 1ull);
+          if (idx < P.hit_cap) P.hits[idx] = hrec;
+        }
+      }
+    }
+  }
+}
+
+// The wave's staged hits -> its own hit region (P.hit_seg, `seg`; *cursor
+// records used: no atomic at all) or, without one or once it is full, P.hits
+// with one global reservation -- when half full or `force`; the fences order
+// the wave's LDS stores before the reads.  (A returning atomic on one word
+// serialises chip-wide at ~90 per us: ~30 K flush reservations were half of
+// k_report's time on configs[2].)
+__device__ inline void report_flush(const ScanParams& P, uint64_t* wbuf, uint32_t* hcnt_w, uint32_t lane, bool force,
+                                    uint64_t* seg = nullptr, uint32_t* cursor = nullptr) {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const uint32_t hc = __shfl(atomicAdd(hcnt_w, 0u), 0);
+  if (hc >= kReportWaveHits / 2 || (force && hc)) {
+    const uint32_t nh = hc < kReportWaveHits ? hc : kReportWaveHits;
+    if (seg && *cursor + nh <= P.hit_seg_cap) {
+      for (uint32_t q = lane; q < nh; q += 64) seg[*cursor + q] = wbuf[q];
+      *cursor += nh;
+    } else {
+      unsigned long long base = 0;
+      if (lane == 0) base = atomicAdd(&P.ctrl->hits, (unsigned long long)nh);
+      base = __shfl(base, 0);
+      for (uint32_t q = lane; q < nh; q += 64)
+        if (base + q < P.hit_cap) P.hits[base + q] = wbuf[q];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (lane == 0) *hcnt_w = 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+}
+
+// The fused scan's resolution of its own segment's events [from, lim) (kept
+// out of line: the scan's streaming loop keeps its registers).
+__device__ __noinline__ void resolve_segment(const ScanParams& P, const AcDev& ac, const RepView& R,
+                                             const FastEvent* ev_seg, uint32_t from, uint32_t lim, uint64_t* wbuf,
+                                             uint32_t* hcnt_w, uint32_t lane, uint32_t& my_out, uint64_t& last_kw) {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // the wave's event stores before its loads
+  for (uint32_t d = from; d < lim; d += 64) {
+    const uint32_t i = d + lane;
+    if (i < lim) report_event(P, ac, R, ev_seg[i], wbuf, hcnt_w, my_out, last_kw);
+    report_flush(P, wbuf, hcnt_w, lane, false);
+  }
+}
+
+// kFuse: the scan resolves its own events (k_report's work, report_event) --
+// the whole report blob (the image followed by the output tables) sits in
+// LDS, and whenever a wave's segment holds 64 unresolved events the wave
+// replays them at a span boundary, one per lane (their global reads --
+// file lookups, keyword atomics -- are latency the wave's 15 siblings cover
+// by keeping the LDS busy); the rest after the wave's last span.  Only the
+// overflow bucket is left to k_report.
+template <int CH, int V, int kFastThreads, int kMode = 0, int kWin = 1, bool kPair = false, bool kFuse = false>
 __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
   constexpr uint32_t kUnit = CH * kNlBlock;          // bytes per lane per work unit
   constexpr int kStep = V * 16;                      // bytes per chain step
   constexpr int kSteps = kNlBlock / kStep;           // steps per span
   // static: LDS base folds to 0 in the step (kPair: the pair table follows the image)
-  __shared__ __align__(16) uint8_t smem[kFastImgMax + (kPair ? kFastCols * kFastCols * 2 : 0)];
+  __shared__ __align__(16) uint8_t smem[kFuse ? kReportLds : kFastImgMax + (kPair ? kFastCols * kFastCols * 2 : 0)];
+  __shared__ uint64_t hbuf[kFuse ? kReportHitCap : 1];
+  __shared__ uint32_t hcnt[kFuse ? kFastThreads / 64 : 1];
   const AcDev& ac = P.rs.ac;
   {
-    const uint32_t words = ac.fast_bytes / 4;
+    const uint32_t words = (kFuse ? ac.rep_bytes : ac.fast_bytes) / 4;
     const uint32_t* src = (const uint32_t*)ac.fast_lds;
     for (uint32_t i = threadIdx.x; i < words; i += kFastThreads) ((uint32_t*)smem)[i] = src[i];
     if (kPair) {
@@ -669,6 +840,7 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
       for (uint32_t i = threadIdx.x; i < kFastCols * kFastCols / 2; i += kFastThreads)
         ((uint32_t*)(smem + kFastImgMax))[i] = ps[i];
     }
+    if (kFuse && (threadIdx.x & 63) == 0) hcnt[threadIdx.x >> 6] = 0;
   }
   __syncthreads();
   const uint8_t* T = smem;
@@ -680,6 +852,16 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
   const uint64_t units = (P.nbytes + kUnit - 1) / kUnit;
   FastEvent* ev_seg = P.events + (uint64_t)wave * P.ev_cap_per_wave;
   uint32_t ev_count = 0;  // wave-uniform
+  // kFuse: events [0, ev_done) of the segment are resolved (wave-uniform)
+  uint32_t ev_done = 0, my_out = 0;
+  uint64_t last_kw = ~0ull;
+  const RepView R = rep_view(ac, smem);
+  uint64_t* wbuf = hbuf + (threadIdx.x >> 6) * (kFuse ? kReportWaveHits : 0);
+  uint32_t* hcnt_w = hcnt + (kFuse ? threadIdx.x >> 6 : 0);
+  auto resolve = [&](uint32_t lim) {  // events [ev_done, lim), one per lane, 64 at a time
+    resolve_segment(P, ac, R, ev_seg, ev_done, lim, wbuf, hcnt_w, lane, my_out, last_kw);
+    ev_done = lim;
+  };
   uint64_t u = (uint64_t)blockIdx.x * kFastThreads + threadIdx.x;
   FastChain<V> C[CH];
   uint4 nxt[CH][V];
@@ -776,8 +958,22 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
       }
     }
     u = un;
+    if (kFuse && !(P.report_mode & 4)) {  // whole rounds of 64 only: the wave goes back to streaming after them
+      const uint32_t lim = ev_count < P.ev_cap_per_wave ? ev_count : (uint32_t)P.ev_cap_per_wave;
+      if (lim - ev_done >= 64) resolve(ev_done + (lim - ev_done) / 64 * 64);
+    }
   }
   if (lane == 0) P.ev_counts[wave] = ev_count < P.ev_cap_per_wave ? ev_count : P.ev_cap_per_wave;
+  if (kFuse) {
+    const uint32_t lim = ev_count < P.ev_cap_per_wave ? ev_count : (uint32_t)P.ev_cap_per_wave;
+    resolve(lim);
+    report_flush(P, wbuf, hcnt_w, lane, true);
+    for (uint32_t d = 32; d; d >>= 1) my_out += __shfl_xor(my_out, d);
+    if (lane == 0) {
+      if (my_out) atomicAdd(&P.ctrl->outputs, (unsigned long long)my_out);
+      if (lim) atomicAdd(&P.ctrl->events, (unsigned long long)lim);
+    }
+  }
 }
 
 // Scan with an automaton too large for k_scan_fast's image (configs[4]: 1000+
@@ -1084,6 +1280,115 @@ __global__ __launch_bounds__(kBigThreads) void k_scan_big(ScanParams P) {
         P.span_hi[s0[h] / kNlBlock] = (hi[h] & 0x80808080u) ? 1 : 0;
       }
     u = un;
+  }
+  if (lane == 0) P.ev_counts[wave] = ev_count < P.ev_cap_per_wave ? ev_count : P.ev_cap_per_wave;
+}
+
+// k_scan_big with coalesced whole-line loads: the unit of a chain is ONE
+// 128-byte line, and lane l's chain h takes line base + 64 h + l, so a wave
+// reads 64 consecutive lines per chain with eight back-to-back dwordx4 loads
+// each (every line fetched once: the span-per-lane shape re-fetched each
+// line from L2 / MALL once per 32-byte ring step, 3.6x its bytes,
+// profiles/r04w_c4).  The price: every line restarts the automaton from the
+// root over the 7 bytes before it (kAcMaxLit - 1), 5.5 % more steps; those
+// bytes are the previous lane's (or chain's) last ones, passed by shuffle.
+// Per-span newline counts and >= 0x80 flags are summed over the 32 lanes of
+// a span.  Events as k_scan_big's (k_big_walk replays them).
+template <int kMode = 8, int CH = 2>
+__global__ __launch_bounds__(kBigThreads) void k_scan_lines(ScanParams P) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  const BigDev& B = P.big;
+  for (uint32_t i = threadIdx.x; i < B.lds_bytes / 4; i += kBigThreads)
+    ((uint32_t*)smem)[i] = ((const uint32_t*)B.blob)[i];
+  __syncthreads();
+  const BigLds L = big_lds(B, smem, P.rs.ac.nclasses);
+  constexpr uint32_t kLine = 128;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t lanes_lt = (1ull << lane) - 1;
+  const uint32_t wave = blockIdx.x * (kBigThreads / 64) + (threadIdx.x >> 6);
+  const uint64_t n_waves = (uint64_t)gridDim.x * (kBigThreads / 64);
+  const uint64_t n_lines = (P.nbytes + kLine - 1) / kLine;
+  FastEvent* ev_seg = P.events + (uint64_t)wave * P.ev_cap_per_wave;
+  uint32_t ev_count = 0;  // wave-uniform
+  for (uint64_t base = (uint64_t)wave * 64 * CH; base < n_lines; base += n_waves * 64 * CH) {
+    uint4 cur[CH][8];
+    uint64_t pos[CH];
+    bool live[CH];
+#pragma unroll
+    for (int h = 0; h < CH; ++h) {
+      pos[h] = (base + 64 * h + lane) * kLine;
+      live[h] = pos[h] < P.nbytes;
+      const uint8_t* src = fast_src(P, pos[h]) + pos[h];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) cur[h][k] = live[h] ? *(const uint4*)(src + 16 * k) : make_uint4(0, 0, 0, 0);
+    }
+    // the 8 bytes before each line: the previous lane's last 8, for lane 0 the
+    // previous chain's lane 63, for chain 0's lane 0 the batch
+    uint2 prev[CH];
+#pragma unroll
+    for (int h = 0; h < CH; ++h) {
+      uint32_t pz = __shfl_up(cur[h][7].z, 1), pw = __shfl_up(cur[h][7].w, 1);
+      if (h > 0) {
+        const uint32_t qz = __shfl(cur[h - 1][7].z, 63), qw = __shfl(cur[h - 1][7].w, 63);
+        if (lane == 0) pz = qz, pw = qw;
+      } else if (lane == 0) {
+        const uint2 w = live[0] && pos[0] >= 8 ? *(const uint2*)(fast_src(P, pos[0] - 8) + pos[0] - 8) : make_uint2(0, 0);
+        pz = w.x, pw = w.y;
+      }
+      prev[h] = make_uint2(pz, pw);
+    }
+    uint32_t e[CH];
+#pragma unroll
+    for (int h = 0; h < CH; ++h) {  // warm-up: the 7 bytes before the line (automaton depth <= kAcMaxLit)
+      e[h] = 0;
+#pragma unroll
+      for (int j = 1; j < 8; ++j)
+        e[h] = big_next(L, e[h], L.cls[((j < 4 ? prev[h].x : prev[h].y) >> (8 * (j & 3))) & 0xFFu]) & 0x7FFFu;
+    }
+    uint32_t nl[CH], hi[CH];
+#pragma unroll
+    for (int h = 0; h < CH; ++h) nl[h] = hi[h] = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        uint32_t d[2 * CH], gs[CH], acc[CH];
+#pragma unroll
+        for (int h = 0; h < CH; ++h) {
+          d[2 * h] = g ? cur[h][k].z : cur[h][k].x;
+          d[2 * h + 1] = g ? cur[h][k].w : cur[h][k].y;
+          if (!(kMode & kBigNoNl)) nl[h] += nl_count_dword(d[2 * h]) + nl_count_dword(d[2 * h + 1]);
+          hi[h] |= d[2 * h] | d[2 * h + 1];
+          gs[h] = e[h];
+        }
+        big_group<kMode, CH>(L, e, d, acc);
+#pragma unroll
+        for (int h = 0; h < CH; ++h) {
+          const uint64_t b = __ballot(live[h] && (acc[h] & 0x8000u));
+          if (b) {
+            big_event(P, b, lane, lanes_lt, pos[h] + 16 * k + 8 * g, gs[h], prev[h], d[2 * h], d[2 * h + 1], ev_seg,
+                      ev_count);
+            ev_count += (uint32_t)__popcll(b);
+          }
+          prev[h] = make_uint2(d[2 * h], d[2 * h + 1]);
+        }
+      }
+    }
+    // per 4 KiB span (32 lanes of a chain): newline count and the >= 0x80 flag
+#pragma unroll
+    for (int h = 0; h < CH; ++h) {
+      uint32_t n = nl[h], f = (hi[h] & 0x80808080u) ? 1u : 0u;
+#pragma unroll
+      for (int d = 1; d < 32; d <<= 1) {
+        n += __shfl_xor(n, d);
+        f |= __shfl_xor(f, d);
+      }
+      if ((lane & 31) == 0 && live[h]) {
+        const uint64_t sp = pos[h] / kNlBlock;
+        if (!(kMode & kBigNoNl)) P.nl_blocks[sp] = n;
+        P.span_hi[sp] = f;
+      }
+    }
   }
   if (lane == 0) P.ev_counts[wave] = ev_count < P.ev_cap_per_wave ? ev_count : P.ev_cap_per_wave;
 }
@@ -1417,36 +1722,24 @@ __global__ __launch_bounds__(1024) void k_scan_ring(ScanParams P) {
 // keyword gate bit (only keywords some non-implied gate needs; fire-and-forget
 // atomic, file looked up once per event) and anchor hit (LDS-staged, one
 // global reservation per block step).
-constexpr uint32_t kReportThreads = 1024;
-constexpr uint32_t kReportHitCap = 1024;
-constexpr uint32_t kReportLds = kLdsMax - kReportHitCap * 8 - 64;
-
-__device__ inline uint32_t file_of_pos(const ScanParams& P, uint64_t pos) {
-  const uint64_t r = pos / kNlBlock;
-  const uint32_t hi = r + 1 < P.n_regions ? min(P.region_file[r + 1] + 1, P.n_files) : P.n_files;
-  return find_file(P.off, P.region_file[r], hi, pos);
-}
-
-// ASCII lowercase of 8 bytes at once (bytes 'A'-'Z' gain 0x20)
-__device__ inline uint64_t lower64(uint64_t x) {
-  const uint64_t t = x & 0x7F7F7F7F7F7F7F7Full;
-  const uint64_t up = ((t + 0x3F3F3F3F3F3F3F3Full) ^ (t + 0x2525252525252525ull)) & ~x & 0x8080808080808080ull;
-  return x | (up >> 2);
-}
-
-// Each wave works on its own: it claims wave segments from a global counter
-// (their event counts differ by text), replays 64 events per round (one per
-// lane) and stages its anchor hits in its own LDS slots, flushed to P.hits
-// with one global reservation per wave when half full.  No block-wide
-// barrier after the image load: a lock-step block round lasted as long as
-// its slowest lane's chain of dependent global reads (file lookup, keyword
-// atomics) while the other 15 waves idled (0.69 ms on configs[2]).
-constexpr uint32_t kReportWaveHits = kReportHitCap / (kReportThreads / 64);
-
-__global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_t n_waves) {
+// The events of all wave segments (and the overflow bucket after them) form
+// one index space through ev_pre (the exclusive prefix of the segments'
+// counts, ev_pre[n_waves] = their total); report wave r takes the r-th equal
+// share of it, 64 events (one per lane) per round.  (Whole segments per wave
+// left the kernel as long as its densest segment: waves lived 22 % of the
+// kernel's 0.66 ms on average on configs[2], profiles/r04w_c2.)  Each wave
+// stages its anchor hits in its own LDS slots and flushes them to its own
+// hit region; with n_waves == 0 only the overflow bucket is left (the fused
+// scan resolved the segments) -- and nothing, not even the image load,
+// without one.
+__global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_t n_waves, const uint64_t* ev_pre) {
   __shared__ __align__(16) uint8_t L[kReportLds];
   __shared__ uint64_t hbuf[kReportHitCap];
   __shared__ uint32_t hcnt[kReportThreads / 64];
+  const uint64_t e_reg = n_waves ? ev_pre[n_waves] : 0;
+  const uint64_t n_ovf = P.ctrl->ev_overflow < P.ev_overflow_cap ? P.ctrl->ev_overflow : P.ev_overflow_cap;
+  const uint64_t E = e_reg + n_ovf;
+  if (E == 0) return;
   const AcDev& ac = P.rs.ac;
   const bool in_lds = ac.rep_bytes <= kReportLds;
   if (in_lds) {
@@ -1454,135 +1747,66 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
     const uint32_t* src = (const uint32_t*)ac.fast_lds;
     for (uint32_t i = threadIdx.x; i < words; i += kReportThreads) ((uint32_t*)L)[i] = src[i];
   }
-  const uint8_t* B = in_lds ? L : ac.fast_lds;  // blob base (LDS, or global when too big)
-  const uint32_t* out_off = (const uint32_t*)(B + ac.o_out_off);
-  const uint16_t* out_pat = (const uint16_t*)(B + ac.o_out_pat);
-  const PatDev* pats = (const PatDev*)(B + ac.o_pats);
-  const uint8_t* pbytes = B + ac.o_pat_bytes;
+  const RepView R = rep_view(ac, in_lds ? L : ac.fast_lds);  // (LDS, or global when too big)
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint64_t* wbuf = hbuf + wv * kReportWaveHits;
   if (lane == 0) hcnt[wv] = 0;
   __syncthreads();
-  const uint32_t out_e = ac.fast_out_entry;
   uint32_t my_out = 0;
   uint64_t last_kw = ~0ull;
-  unsigned long long my_events = 0;
-  for (;;) {
-    uint32_t w = 0;
-    if (lane == 0) w = (uint32_t)atomicAdd(&P.ctrl->rep_next, 1ull);
-    w = __shfl(w, 0);
-    if (w >= n_waves + 1) break;
-    const FastEvent* seg;
-    uint64_t n;
-    if (w < n_waves) {
-      seg = P.events + (uint64_t)w * P.ev_cap_per_wave;
-      n = P.ev_counts[w];
-      my_events += n;
-    } else {  // overflow bucket
-      seg = P.ev_overflow;
-      n = P.ctrl->ev_overflow < P.ev_overflow_cap ? P.ctrl->ev_overflow : P.ev_overflow_cap;
+  const uint32_t rw = blockIdx.x * (kReportThreads / 64) + wv;
+  const uint32_t n_rw = gridDim.x * (kReportThreads / 64);
+  uint64_t* hseg = P.hit_seg ? P.hit_seg + (uint64_t)rw * P.hit_seg_cap : nullptr;
+  uint32_t hcur = 0;
+  const uint64_t lo = E * rw / n_rw, hi = E * (rw + 1) / n_rw;
+  // the segment of event lo (s == n_waves: the overflow bucket)
+  uint32_t s = n_waves;
+  if (lo < e_reg) {
+    uint32_t a = 0, b = n_waves;  // largest a with ev_pre[a] <= lo
+    while (b - a > 1) {
+      const uint32_t m = (a + b) >> 1;
+      if (ev_pre[m] <= lo) a = m;
+      else b = m;
     }
-    for (uint64_t i0 = 0; i0 < n; i0 += 64) {
-      const uint64_t i = i0 + lane;
-      if (i < n) {
-        const FastEvent ev = seg[i];
-        uint64_t hist = ((uint64_t)ev.prev.y << 32) | ev.prev.x;  // the 8 raw bytes before (oldest low)
-        uint64_t hlow = lower64(hist);
-        uint32_t e = ev.entry;
-        const uint32_t fx = fold6(ev.cur.x), fy = fold6(ev.cur.y);
-        uint32_t fi = 0xFFFFFFFFu;
-  #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          e = fstep(B, e, j < 4 ? fx : fy, j & 3);
-          const uint32_t c = ((j < 4 ? ev.cur.x : ev.cur.y) >> (8 * (j & 3))) & 0xFFu;
-          hist = (hist >> 8) | ((uint64_t)c << 56);  // hist byte 7 = c
-          hlow = (hlow >> 8) | ((uint64_t)lower_ascii((uint8_t)c) << 56);
-          if (e < out_e || c >= 0x80) continue;  // an output ending on a byte >= 0x80 is an alias
-          const uint64_t pos = ev.pos + j;
-          const uint32_t st = e;
-          for (uint32_t o = out_off[st]; o < out_off[st + 1]; ++o) {
-            const uint32_t pid = out_pat[o];
-            const PatDev& pd = pats[pid];
-            // the automaton's prefix on the real bytes (it ran on folded ones)
-            if ((hlow & pd.m64) != pd.lo64) continue;
-            const bool want_kw = pd.kw_needed != 0;
-            bool want_hit = pd.rule_n != 0 && (hist & pd.rqm64) == pd.rq64;
-            if (!want_kw && !want_hit) continue;
-            const uint32_t tl = pd.len < ac.depth ? pd.len : ac.depth;
-            const uint64_t start = pos + 1 - tl - pd.ext;
-            if (pd.trunc) {  // the rest of a long pattern, on the batch (rare)
-              if (fi == 0xFFFFFFFFu) fi = (P.report_mode & 1) ? (uint32_t)((pos >> 12) % P.n_files) : file_of_pos(P, pos);
-              const uint64_t fend = P.off[fi + 1] - 1;
-              if (start + pd.len > fend) continue;
-              // chunks of 8 batch bytes issued before any compare (one memory
-              // latency per chunk; a byte-by-byte early-exit loop was a chain of
-              // dependent loads)
-              uint32_t bad = 0, req_bad = 0;
-              const uint8_t* pb = pbytes + pd.bytes_off;
-              for (uint32_t k0 = tl; k0 < pd.len && !bad; k0 += 8) {
-#pragma unroll
-                for (uint32_t k = k0; k < k0 + 8; ++k)
-                  if (k < pd.len) {
-                    const uint8_t b = P.data[start + k];
-                    bad |= lower_ascii(b) ^ pb[k];
-                    if (want_hit && pd.confirm) {
-                      const uint8_t r = pbytes[pd.req_off + k];
-                      req_bad |= (r != 0) & (b != r);
-                    }
-                  }
-              }
-              if (bad) continue;
-              if (req_bad) want_hit = false;
-            }
-            ++my_out;
-            if (want_kw) {
-              if (fi == 0xFFFFFFFFu) fi = (P.report_mode & 1) ? (uint32_t)((pos >> 12) % P.n_files) : file_of_pos(P, pos);
-              const uint64_t key = ((uint64_t)fi << 32) | pd.kw;  // per-lane dedupe of repeated keywords
-              if (last_kw != key) {
-                last_kw = key;
-                // fire-and-forget atomic: reading the word first to skip the
-                // atomics of repeated keywords put an L2 round trip on the lane's
-                // chain (k_report 650 -> 618 us on configs[2] without it,
-                // profiles/r04ac)
-                atomicOr(&P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)], 1u << (pd.kw & 31));
-              }
-            }
-            if (want_hit) {
-              const uint32_t slot = atomicAdd(&hcnt[wv], 1u);  // (this wave's slots only)
-              const uint64_t hrec = (start << 16) | pid;
-              if (slot < kReportWaveHits) {
-                wbuf[slot] = hrec;
-              } else {
-                unsigned long long idx = atomicAdd(&P.ctrl->hits, 1ull);
-                if (idx < P.hit_cap) P.hits[idx] = hrec;
-              }
-            }
-          }
-        }
-      }
-      // this wave's staged hits -> global, one reservation when half full (or at
-      // the segment's end); the fence orders the wave's LDS stores before the reads
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      const uint32_t hc = __shfl(atomicAdd(&hcnt[wv], 0u), 0);
-      if (hc >= kReportWaveHits / 2 || i0 + 64 >= n) {
-        const uint32_t nh = hc < kReportWaveHits ? hc : kReportWaveHits;
-        unsigned long long base = 0;
-        if (lane == 0 && nh) base = atomicAdd(&P.ctrl->hits, (unsigned long long)nh);
-        base = __shfl(base, 0);
-        for (uint32_t q = lane; q < nh; q += 64)
-          if (base + q < P.hit_cap) P.hits[base + q] = wbuf[q];
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (lane == 0) hcnt[wv] = 0;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      }
-    }
+    s = a;
   }
+  for (uint64_t g0 = lo; g0 < hi; g0 += 64) {
+    const uint64_t g = g0 + lane;
+    uint32_t sl = s;
+    if (g < hi) {
+      while (sl < n_waves && ev_pre[sl + 1] <= g) ++sl;  // (empty segments skipped; past e_reg: the bucket)
+      const FastEvent* ev =
+          sl < n_waves ? P.events + (uint64_t)sl * P.ev_cap_per_wave + (g - ev_pre[sl]) : P.ev_overflow + (g - e_reg);
+      report_event(P, ac, R, *ev, wbuf, &hcnt[wv], my_out, last_kw);
+    }
+    report_flush(P, wbuf, &hcnt[wv], lane, g0 + 64 >= hi, hseg, &hcur);
+    s = __shfl(sl, hi - g0 >= 64 ? 63 : (int)(hi - g0 - 1));  // the last lane's segment: the next round's start
+  }
+  if (hseg && lane == 0) P.hit_seg_n[rw] = hcur;
   // per-wave totals: one atomic each
   for (uint32_t d = 32; d; d >>= 1) my_out += __shfl_xor(my_out, d);
   if (lane == 0) {
     if (my_out) atomicAdd(&P.ctrl->outputs, (unsigned long long)my_out);
-    if (my_events) atomicAdd(&P.ctrl->events, my_events);
+    if (rw == 0 && e_reg) atomicAdd(&P.ctrl->events, (unsigned long long)e_reg);
   }
+}
+
+// The report waves' hit regions -> P.hits: one reservation on ctrl->hits for
+// all of them (k_hits_reserve, after an exclusive scan of the counts into
+// hit_pre), then one block per region copies it to its place.
+__global__ void k_hits_reserve(ScanParams P, uint32_t n_rw, const uint64_t* hit_pre, unsigned long long* base) {
+  const uint64_t total = hit_pre[n_rw - 1] + P.hit_seg_n[n_rw - 1];
+  *base = atomicAdd(&P.ctrl->hits, (unsigned long long)total);
+}
+
+__global__ __launch_bounds__(256) void k_hits_pack(ScanParams P, const uint64_t* hit_pre,
+                                                   const unsigned long long* base) {
+  const uint32_t r = blockIdx.x;
+  const uint32_t n = P.hit_seg_n[r];
+  const uint64_t at = *base + hit_pre[r];
+  const uint64_t* src = P.hit_seg + (uint64_t)r * P.hit_seg_cap;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+    if (at + i < P.hit_cap) P.hits[at + i] = src[i];
 }
 
 // Fold-special sequences (C4B0 U+0130, C5BF U+017F, E284AA U+212A) in the
@@ -1592,19 +1816,40 @@ __global__ __launch_bounds__(256) void k_fold_special(ScanParams P, uint64_t n_s
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-  constexpr uint32_t kPer = kNlBlock / 64;
+  constexpr uint32_t kPer = kNlBlock / 64;  // 64 bytes per lane: four 16-byte loads
+  static_assert(kPer == 64, "one lane = four dwordx4");
   for (uint64_t g = w0 * 64; g < n_spans; g += nw * 64) {  // 64 spans per wave step
     uint64_t m = __ballot(g + lane < n_spans && P.span_hi[g + lane]);
     while (m) {
       const uint64_t sp = g + (uint64_t)__ffsll((long long)m) - 1;
       m &= m - 1;
       const uint64_t a = sp * kNlBlock + (uint64_t)lane * kPer;
-      const uint64_t b = a + kPer < P.nbytes ? a + kPer : P.nbytes;
-      uint32_t b1 = a >= 1 && a - 1 < P.nbytes ? P.data[a - 1] : 0, b2 = a >= 2 && a - 2 < P.nbytes ? P.data[a - 2] : 0;
-      for (uint64_t q = a; q < b; ++q) {
-        const uint32_t c = P.data[q];
+      uint32_t w[16];
+      uint32_t hi = 0;
+      if (a < P.nbytes) {  // (the last span reads the zero-padded tail copy)
+        const uint8_t* src = fast_src(P, a) + a;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint4 v = *(const uint4*)(src + 16 * k);
+          w[4 * k] = v.x, w[4 * k + 1] = v.y, w[4 * k + 2] = v.z, w[4 * k + 3] = v.w;
+          hi |= v.x | v.y | v.z | v.w;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = 0;
+      }
+      // the two bytes before the lane's first: the previous lane's last dword
+      // (lane 0: the batch, or none at its start)
+      uint32_t before = __shfl_up(w[15], 1);
+      if (lane == 0) before = a >= 4 ? *(const uint32_t*)(fast_src(P, a - 4) + a - 4) : 0;
+      if (!((hi | (before & 0x80800000u)) & 0x80808080u)) continue;  // no byte >= 0x80 near this lane
+      uint32_t b1 = before >> 24, b2 = (before >> 16) & 0xFFu;
+#pragma unroll
+      for (uint32_t k = 0; k < kPer; ++k) {  // (unrolled: w stays in registers)
+        const uint32_t c = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        const uint64_t q = a + k;
         const bool fi = c == 0xB0 && b1 == 0xC4, fs = c == 0xBF && b1 == 0xC5, fk = c == 0xAA && b1 == 0x84 && b2 == 0xE2;
-        if (fi || fs || fk) {
+        if ((fi || fs || fk) && q < P.nbytes) {
           mark_special(P, file_of_pos(P, q));
           note_fold(P, fk ? q - 2 : q - 1, fi ? FOLD_I : fs ? FOLD_S : FOLD_K);
         }
@@ -2119,9 +2364,13 @@ struct PacLit {
   uint32_t req_off;  // case requirement bytes (0 = either case)
 };
 
+// kLds: the literal automaton staged in LDS; without (the launch after the
+// scan) it is read from global memory (L2), so the gate's blocks fit beside
+// k_report's, which take a CU's whole LDS.
+template <bool kLds>
 __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
-  __shared__ __align__(16) uint8_t pl[16384];
-  const bool lds = G.pac && G.pac_bytes <= sizeof(pl);
+  __shared__ __align__(16) uint8_t pl[kLds ? 16384 : 16];
+  const bool lds = kLds && G.pac && G.pac_bytes <= sizeof(pl);
   if (lds) {
     for (uint32_t i = threadIdx.x; i < G.pac_bytes / 4; i += blockDim.x) ((uint32_t*)pl)[i] = ((const uint32_t*)G.pac)[i];
     __syncthreads();
@@ -2221,6 +2470,9 @@ __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
   }
 }
 
+// Lazy newline counts reach this far past a file's last candidate (k_nl_spans phase 0).
+constexpr uint64_t kNlCandReach = 16384;
+
 struct ExpandParams {
   const uint8_t* data;
   const uint64_t* off;
@@ -2240,6 +2492,7 @@ struct ExpandParams {
   Ctrl* ctrl;
   const uint32_t* full_rules;  // rules in MODE_FULL
   uint32_t n_full_rules;
+  unsigned long long* nl_last;  // lazy newline counts: per file, 1 + the last byte a candidate's count needs (or null)
 };
 
 __device__ inline bool rule_gate(const RuleSetDev& rs, const RuleDev& r, const uint32_t* kw) {
@@ -2321,31 +2574,77 @@ __device__ inline void emit_cand(const ExpandParams& E, uint32_t rule, uint64_t 
   }
 }
 
+// One thread per anchor hit; the candidates of a block are reserved with ONE
+// atomic on the candidate counter (a returning atomic on one word serialises
+// chip-wide at ~90 per us: per wave it was ~14 K of them on configs[2]).
+// Rules 32+ of a pattern (large custom rule sets) take a per-candidate atomic.
 __global__ __launch_bounds__(256) void k_expand(ExpandParams E) {
+  __shared__ uint32_t wsum[4];
+  __shared__ unsigned long long bbase;
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= E.n_hits) return;
-  const uint64_t h = E.hits[i];
-  const bool fold = (h & kFoldHit) != 0;  // literal spelled with K / ſ (k_fold_windows)
-  const uint64_t gpos = (h & ~kFoldHit) >> 16;
-  const uint32_t pid = (uint32_t)(h & 0xFFFF);
-  const uint64_t rg = gpos / kNlBlock;
-  const uint32_t fhi = rg + 1 < E.n_regions ? min(E.region_file[rg + 1] + 1, E.n_files) : E.n_files;
-  const uint32_t fi = find_file(E.off, E.region_file[rg], fhi, gpos);
-  const uint32_t fl = E.file_flags[fi];
-  if (fl & kFileAllowed) return;
-  const PatDev pd = E.rs.ac.pats[pid];
-  const uint32_t* kw = E.file_kw + (size_t)fi * E.rs.kw_words;
-  const uint64_t fend = E.off[fi + 1] - 1;
-  for (uint32_t k = 0; k < pd.rule_n; ++k) {
-    const uint32_t r = E.rs.ac.pat_rules[pd.rule_off + k];
-    if (E.path_mask && ((E.path_mask[(size_t)fi * E.rule_words + (r >> 5)] >> (r & 31)) & 1)) continue;
-    const RuleDev& rd = E.rs.rules[r];
-    // an ASCII literal hit that holds a keyword proves the gate (gate_implied);
-    // a K/ſ spelling does not (ToLower(ſ) == ſ)
-    if ((fold || !rd.gate_implied) && !rule_gate(E.rs, rd, kw)) continue;
-    if (!follow_accepts_dev(E.rs, rd, E.data, gpos, fend)) continue;
-    if (!precede_accepts_dev(rd, E.data, gpos, E.off[fi])) continue;
-    emit_cand(E, r, gpos, fi);
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t acc = 0;  // accepted rules k < 32 of the hit's pattern
+  uint64_t gpos = 0;
+  uint32_t fi = 0, rule_off = 0;
+  if (i < E.n_hits) {
+    const uint64_t h = E.hits[i];
+    const bool fold = (h & kFoldHit) != 0;  // literal spelled with K / ſ (k_fold_windows)
+    gpos = (h & ~kFoldHit) >> 16;
+    const uint32_t pid = (uint32_t)(h & 0xFFFF);
+    const uint64_t rg = gpos / kNlBlock;
+    const uint32_t fhi = rg + 1 < E.n_regions ? min(E.region_file[rg + 1] + 1, E.n_files) : E.n_files;
+    fi = find_file(E.off, E.region_file[rg], fhi, gpos);
+    const uint32_t fl = E.file_flags[fi];
+    if (!(fl & kFileAllowed)) {
+      const PatDev pd = E.rs.ac.pats[pid];
+      rule_off = pd.rule_off;
+      const uint32_t* kw = E.file_kw + (size_t)fi * E.rs.kw_words;
+      const uint64_t fend = E.off[fi + 1] - 1;
+      for (uint32_t k = 0; k < pd.rule_n; ++k) {
+        const uint32_t r = E.rs.ac.pat_rules[pd.rule_off + k];
+        if (E.path_mask && ((E.path_mask[(size_t)fi * E.rule_words + (r >> 5)] >> (r & 31)) & 1)) continue;
+        const RuleDev& rd = E.rs.rules[r];
+        // an ASCII literal hit that holds a keyword proves the gate (gate_implied);
+        // a K/ſ spelling does not (ToLower(ſ) == ſ)
+        if ((fold || !rd.gate_implied) && !rule_gate(E.rs, rd, kw)) continue;
+        if (!follow_accepts_dev(E.rs, rd, E.data, gpos, fend)) continue;
+        if (!precede_accepts_dev(rd, E.data, gpos, E.off[fi])) continue;
+        if (k < 32) {
+          acc |= 1u << k;
+        } else {
+          emit_cand(E, r, gpos, fi);
+          if (E.nl_last) atomicMax(&E.nl_last[fi], (unsigned long long)(gpos + kNlCandReach + 1));
+        }
+      }
+    }
+  }
+  // block-wide exclusive prefix of the accepted counts, one reservation
+  const uint32_t cnt = (uint32_t)__popc(acc);
+  uint32_t incl = cnt;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(incl, d);
+    if (lane >= d) incl += v;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+  for (uint32_t w = 0; w < blockDim.x / 64; ++w) {
+    before += w < wv ? wsum[w] : 0;
+    total += wsum[w];
+  }
+  if (threadIdx.x == 0) bbase = total ? atomicAdd(&E.ctrl->cands, (unsigned long long)total) : 0ull;
+  __syncthreads();
+  uint64_t idx = bbase + before + incl - cnt;
+  if (acc && E.nl_last) atomicMax(&E.nl_last[fi], (unsigned long long)(gpos + kNlCandReach + 1));
+  while (acc) {
+    const uint32_t k = (uint32_t)__ffs(acc) - 1;
+    acc &= acc - 1;
+    if (idx < E.cand_cap) {
+      E.keys[idx] = ((uint64_t)E.rs.ac.pat_rules[rule_off + k] << kPosBits) | gpos;
+      E.vals[idx] = fi;
+    }
+    ++idx;
   }
 }
 
@@ -2361,6 +2660,7 @@ __global__ __launch_bounds__(256) void k_full_jobs(ExpandParams E) {
     if (E.path_mask && ((E.path_mask[(size_t)fi * E.rule_words + (r >> 5)] >> (r & 31)) & 1)) continue;
     if (!rule_gate(E.rs, E.rs.rules[r], kw)) continue;
     emit_cand(E, r, fstart, fi | kFullFlag);
+    if (E.nl_last) atomicMax(&E.nl_last[fi], (unsigned long long)(E.off[fi + 1] + 1));  // a full-file job: the file
   }
 }
 
@@ -2448,6 +2748,8 @@ struct VerifyParams {
   const uint32_t* n_jobs_dev;  // job count, written by the job-segmentation select (no host read)
   DevLoc* locs;
   uint64_t loc_cap;
+  unsigned long long* loc_shards;  // per-shard location counts (kLocShards; null: one counter, ctrl->locs)
+  uint64_t loc_shard_cap;          // locations per shard region of `locs` (loc_cap / kLocShards)
   Ctrl* ctrl;
   uint8_t* scratch;
   uint64_t scratch_stride;
@@ -2742,6 +3044,54 @@ __device__ bool bitstate_captures(const gre::ProgView& p, const uint8_t* text, P
   return false;
 }
 
+// A kept location.  The locations are reserved from kLocShards counters
+// (by block and wave), each owning a region of `locs` (loc_shard_cap
+// slots), past which a shard spills into a shared overflow region (counter
+// kLocShards); k_loc_compact packs everything densely afterwards.  One
+// returning atomic on one word serialises chip-wide at ~90 per us, which was
+// most of k_verify's time on configs[2] (29 K locations, one atomic each from
+// divergent lanes).
+constexpr uint32_t kLocShards = 64;
+__device__ inline void loc_emit(const VerifyParams& V, const DevLoc& L) {
+  if (V.loc_shards) {
+    const uint32_t sh = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kLocShards - 1);
+    const unsigned long long k = atomicAdd(&V.loc_shards[sh], 1ull);
+    if (k < V.loc_shard_cap) {
+      V.locs[(uint64_t)sh * V.loc_shard_cap + k] = L;
+      return;
+    }
+    const unsigned long long o = atomicAdd(&V.loc_shards[kLocShards], 1ull);
+    const uint64_t at = (uint64_t)kLocShards * V.loc_shard_cap + o;
+    if (at < V.loc_cap) V.locs[at] = L;
+    return;
+  }
+  const unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
+  if (idx < V.loc_cap) V.locs[idx] = L;
+}
+
+// Block b < kLocShards copies shard b's region, block kLocShards the
+// overflow region, to their dense place in `out`; block 0 sets ctrl->locs
+// to the total (when the overflow region overflowed: capacity + emitted,
+// above every capacity, so the host grows the lists and re-runs).
+__global__ __launch_bounds__(256) void k_loc_compact(VerifyParams V, DevLoc* out) {
+  __shared__ unsigned long long cnt[kLocShards + 1];
+  if (threadIdx.x <= kLocShards) cnt[threadIdx.x] = V.loc_shards[threadIdx.x];
+  __syncthreads();
+  const uint64_t sc = V.loc_shard_cap, ocap = V.loc_cap - (uint64_t)kLocShards * sc;
+  uint64_t start = 0, total = 0, emitted = cnt[kLocShards];
+  for (uint32_t k = 0; k <= kLocShards; ++k) {
+    const uint64_t c = k < kLocShards ? (cnt[k] < sc ? cnt[k] : sc) : (cnt[k] < ocap ? cnt[k] : ocap);
+    if (k < blockIdx.x) start += c;
+    total += c;
+    if (k < kLocShards) emitted += cnt[k] < sc ? cnt[k] : sc;
+  }
+  const uint64_t b = blockIdx.x;
+  const uint64_t n = b < kLocShards ? (cnt[b] < sc ? cnt[b] : sc) : (cnt[b] < ocap ? cnt[b] : ocap);
+  const DevLoc* src = V.locs + b * sc;  // (b == kLocShards: the overflow region)
+  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) out[start + i] = src[i];
+  if (b == 0 && threadIdx.x == 0) V.ctrl->locs = emitted > total ? V.loc_cap + emitted : total;
+}
+
 // Secret-group spans of one kept match (getMatchSubgroupsLocations,
 // scanner.go:150-163) with the bit-state backtracker in the lane's LDS arena
 // of `words` words; a match too long for it goes on to the next stage's list
@@ -2765,11 +3115,8 @@ __device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t r
   if (bs_ok) {
     for (uint32_t g = 0; g < rd.group_n; ++g) {
       const Slot s = gcap[2 * g], e = gcap[2 * g + 1];
-      unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
-      if (idx < V.loc_cap) {
-        if (s < 0 || e < 0) V.locs[idx] = DevLoc{fi, rule, 0, 0, 0, 0, 1, job};
-        else V.locs[idx] = DevLoc{fi, rule, (uint64_t)s, (uint64_t)e, 0, 0, 0, job};
-      }
+      if (s < 0 || e < 0) loc_emit(V, DevLoc{fi, rule, 0, 0, 0, 0, 1, job});
+      else loc_emit(V, DevLoc{fi, rule, (uint64_t)s, (uint64_t)e, 0, 0, 0, job});
     }
     return;
   }
@@ -2779,11 +3126,8 @@ __device__ void emit_groups(const VerifyParams& V, const RuleDev& rd, uint32_t r
   for (uint32_t g = 0; g < rd.group_n; ++g) {
     const uint32_t slot = gnum[g];
     const Slot s = out[2 * slot], e = out[2 * slot + 1];
-    unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
-    if (idx < V.loc_cap) {
-      if (s < 0 || e < 0) V.locs[idx] = DevLoc{fi, rule, 0, 0, 0, 0, 1, job};
-      else V.locs[idx] = DevLoc{fi, rule, (uint64_t)s, (uint64_t)e, 0, 0, 0, job};
-    }
+    if (s < 0 || e < 0) loc_emit(V, DevLoc{fi, rule, 0, 0, 0, 0, 1, job});
+    else loc_emit(V, DevLoc{fi, rule, (uint64_t)s, (uint64_t)e, 0, 0, 0, job});
   }
 }
 
@@ -2813,8 +3157,7 @@ template <class Pos>
 __device__ inline void emit_kept(const VerifyParams& V, const RuleDev& rd, uint32_t rule, uint32_t fi, uint32_t job,
                                  const uint8_t* text, Pos ms, Pos me) {
   if (!rd.use_groups) {
-    unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
-    if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, ms, me, 0, 0, 0, job};
+    loc_emit(V, DevLoc{fi, rule, ms, me, 0, 0, 0, job});
     return;
   }
   if (rd.grp_fast || rd.grp_run) {  // the group's span follows from [ms, me) on ASCII text (gre::group_span / group_run)
@@ -2832,8 +3175,7 @@ __device__ inline void emit_kept(const VerifyParams& V, const RuleDev& rd, uint3
       const int64_t gs = rd.grp_pre >= 0 ? (int64_t)ms + rd.grp_pre : (int64_t)me - rd.grp_suf - rd.grp_len;
       const int64_t ge = rd.grp_suf >= 0 ? (int64_t)me - rd.grp_suf : gs + rd.grp_len;
       if (gs >= (int64_t)ms && gs <= ge && ge <= (int64_t)me) {
-        unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
-        if (idx < V.loc_cap) V.locs[idx] = DevLoc{fi, rule, (uint64_t)gs, (uint64_t)ge, 0, 0, 0, job};
+        loc_emit(V, DevLoc{fi, rule, (uint64_t)gs, (uint64_t)ge, 0, 0, 0, job});
         return;
       }
       // (unreachable for a real match of the rule; the capture search decides)
@@ -2977,8 +3319,7 @@ __global__ __launch_bounds__(256) void k_group_runs(VerifyParams V) {
       const uint32_t bm[4] = {rd.grp_b[0], rd.grp_b[1], rd.grp_b[2], rd.grp_b[3]};
       gs = run_back<Pos>(text, ms, ge, bm);
     }
-    const unsigned long long idx = atomicAdd(&V.ctrl->locs, 1ull);
-    if (idx < V.loc_cap) V.locs[idx] = DevLoc{c.file, c.rule, (uint64_t)gs, (uint64_t)ge, 0, 0, 0, c.job};
+    loc_emit(V, DevLoc{c.file, c.rule, (uint64_t)gs, (uint64_t)ge, 0, 0, 0, c.job});
   }
 }
 
@@ -3781,22 +4122,13 @@ __device__ inline void wave_nl_prefix3(const uint8_t* data, const uint32_t* nl_p
 constexpr uint32_t kNlTailMin = 4;   // newlines of the span after the last location: Code's 2 lines + the end line's
 constexpr uint64_t kNlFull = 1ull << 63;  // nl_last flag: count the whole file
 
-// The counting starts before the locations exist: right after the sorted
-// candidates, on the side stream under k_verify (latency-bound, so the HBM
+// The counting starts before the locations exist: right after the
+// candidates (k_expand / k_full_jobs mark each file's reach), on the side
+// stream under the candidate sort and k_verify (latency-bound, so the HBM
 // is free), each candidate's file is counted through kNlCandReach bytes past
 // its last candidate (a full-file rule's: to the file's end).  When the
 // locations are known, k_nl_check sends a file whose last location ends past
 // that bound to phase 1 (which then also covers what k_nl_tail asks for).
-constexpr uint64_t kNlCandReach = 16384;
-__global__ __launch_bounds__(256) void k_nl_cands(const uint64_t* keys, const uint32_t* vals, uint64_t n,
-                                                  const uint64_t* off, unsigned long long* nl_last) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t f = vals[i] & ~kFullFlag;
-  const uint64_t lim = (vals[i] & kFullFlag) ? off[f + 1] : (keys[i] & kPosMask) + kNlCandReach;
-  atomicMax(&nl_last[f], (unsigned long long)(lim + 1));
-}
-
 __global__ __launch_bounds__(256) void k_nl_check(const DevLoc* locs, uint64_t n, const uint64_t* off,
                                                   unsigned long long* nl_last) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -5112,6 +5444,7 @@ struct tsg_engine {
   DBuf<uint32_t> fbase;  // newline prefix at each location file's start (k_file_base)
   DBuf<unsigned long long> nl_last;  // per file: counted bound + 1 (0: none) | kNlFull (k_nl_cands / _check / _tail)
   hipEvent_t ev_nl[2] = {nullptr, nullptr};  // candidates ready -> phase-0 count done (side stream)
+  hipEvent_t ev_pg[2] = {nullptr, nullptr};  // the side-stream path gate: start, end
   bool nl_pending = false;                   // a phase-0 count was issued on the side stream
   hipStream_t stream = nullptr;
   std::mutex mu;
@@ -5128,7 +5461,10 @@ struct tsg_engine {
   DBuf<uint32_t> job_start;
   DBuf<uint32_t> nsel;
   DBuf<uint8_t> cub_tmp;
+  DBuf<uint64_t> hit_seg, hit_pre, ev_pre;  // k_report's per-wave hit regions, their exclusive offsets (+ the base)
+  DBuf<uint32_t> hit_seg_n;
   DBuf<DevLoc> locs, locs2;
+  DBuf<unsigned long long> loc_cnt;  // sharded location counters (kLocShards + the overflow region's)
   DBuf<uint8_t> scratch;
   DBuf<Ctrl> ctrl;
   DBuf<uint32_t> nl_blocks, nl_pre;
@@ -5795,6 +6131,8 @@ hipError_t ensure_side(tsg_engine* e) {
   if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_side, hipEventDisableTiming);
   if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_nl[0], hipEventDisableTiming);
   if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_nl[1], hipEventDisableTiming);
+  if (r == hipSuccess) r = hipEventCreate(&e->ev_pg[0]);  // (timed: the path gate's stage time)
+  if (r == hipSuccess) r = hipEventCreate(&e->ev_pg[1]);
   return r;
 }
 
@@ -5860,6 +6198,16 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
       vecs = kFastVecs;
     }
 #endif
+    // the scan resolving its own events (kFuse) measured slower: 14.4 ms for
+    // the fused scan against 10.7 + 0.64 (k_report) on configs[2], 13.9 ms with
+    // the resolution after each wave's last span only (profiles/r05c) -- the
+    // out-of-line resolution's call frame and spills sit on the streaming
+    // loop, and inlined (128 VGPRs) it cost 11.5 ms (profiles/r05b).  Exp
+    // build only (TSG_FUSE=1).
+    bool fuse = false;
+#ifdef TSG_EXPERIMENTS
+    if (const char* f = getenv("TSG_FUSE")) fuse = ac.rep_bytes <= kReportLds && atoi(f) != 0;
+#endif
     const uint64_t unit = ring ? (uint64_t)kNlBlock : (uint64_t)chains * kNlBlock;
     P.tail_base = (P.nbytes / unit) * unit;
     const uint64_t lead = P.tail_base >= 8 ? 8 : P.tail_base;
@@ -5882,7 +6230,7 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     const uint64_t n_waves = (uint64_t)blocks * (nt / 64);
     P.ev_cap_per_wave = std::max<uint64_t>(1024, (P.nbytes / 256) / n_waves + 256);
     HIP_TRY(e->ev_buf.ensure(n_waves * P.ev_cap_per_wave));
-    HIP_TRY(e->ev_counts.ensure(n_waves));
+    HIP_TRY(e->ev_counts.ensure(n_waves + 1));
     HIP_TRY(e->ev_overflow.ensure(std::max<uint64_t>(1 << 20, e->ev_ovf_need)));
     P.events = e->ev_buf.p;
     P.ev_counts = e->ev_counts.p;
@@ -5892,6 +6240,7 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     // (the image lives in the kernel's static kFastImgMax array: no dynamic LDS)
     if (e->events) HIP_TRY(hipEventRecord(e->ev[10], s));
 #ifdef TSG_EXPERIMENTS
+    bool fused = false;  // (only the product shape has a fused instantiation)
     if (ring) hipLaunchKernelGGL(k_scan_ring, dim3(blocks), dim3(nt), 0, s, P);
 #define TSG_DEEP(VV, DD, M)                                                                 \
   else if (deep_v == VV && deep_d == DD && mode == M)                                      \
@@ -5906,6 +6255,11 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     else if (chains == 1 && vecs == 8 && win == 8) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 8>), dim3(blocks), dim3(nt), 0, s, P);
     else if (chains == 1 && vecs == 8 && win == 4 && pair && P.rs.ac.o_pair)
       hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, 4, true>), dim3(blocks), dim3(nt), 0, s, P);
+    else if (chains == 1 && vecs == 8 && win == 4 && e->nl_lazy && fuse) {
+      hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 2, 4, false, true>), dim3(blocks), dim3(nt), 0, s, P);
+      nl_skipped = true;
+      fused = true;
+    }
     else if (chains == 1 && vecs == 8 && win == 4 && e->nl_lazy) {
       hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 2, 4>), dim3(blocks), dim3(nt), 0, s, P);
       nl_skipped = true;
@@ -5915,6 +6269,7 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     else if (chains == 1) hipLaunchKernelGGL((k_scan_fast<1, 4, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     else if (vecs == 4) hipLaunchKernelGGL((k_scan_fast<2, 4, 1024>), dim3(blocks), dim3(nt), 0, s, P);
     else hipLaunchKernelGGL((k_scan_fast<2, 2, 1024>), dim3(blocks), dim3(nt), 0, s, P);
+    fuse = fused;
 #else
     // (kMode 2: no newline counts -- the engine counts them lazily, k_nl_spans)
     if (e->nl_lazy) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 2, kFastEventWin>), dim3(blocks), dim3(nt), 0, s, P);
@@ -5924,9 +6279,41 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     HIP_TRY(hipGetLastError());
     if (e->events) HIP_TRY(hipEventRecord(e->ev[11], s));
     e->fast_timed = e->events;
-    hipLaunchKernelGGL(k_report, dim3((uint32_t)std::min<uint64_t>(n_waves + 1, e->num_cus)), dim3(kReportThreads), 0, s, P,
-                       (uint32_t)n_waves);
+    // the wave segments (unless the scan resolved them) and the overflow bucket
+    // (with n_waves 0, k_report returns at once when the bucket is empty);
+    // each report wave stages its hits in a region of its own, packed into
+    // P.hits afterwards with one reservation
+    const uint32_t rep_blocks = (uint32_t)std::min<uint64_t>(fuse ? 1 : n_waves + 1, e->num_cus);
+    const uint32_t n_rw = rep_blocks * (kReportThreads / 64);
+    P.hit_seg_cap = kHitSegCap;
+    HIP_TRY(e->hit_seg.ensure((uint64_t)n_rw * kHitSegCap));
+    HIP_TRY(e->hit_seg_n.ensure(n_rw));
+    HIP_TRY(e->hit_pre.ensure(n_rw + 1));
+    P.hit_seg = e->hit_seg.p;
+    P.hit_seg_n = e->hit_seg_n.p;
+    HIP_TRY(hipMemsetAsync(e->hit_seg_n.p, 0, (size_t)n_rw * 4, s));
+    if (!fuse) {  // the events' index space: exclusive prefix of the segments' counts
+      HIP_TRY(e->ev_pre.ensure(n_waves + 1));
+      HIP_TRY(hipMemsetAsync(e->ev_counts.p + n_waves, 0, 4, s));
+      size_t tmp = 0;
+      HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->ev_counts.p, e->ev_pre.p, (int)(n_waves + 1), s));
+      HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+      HIP_TRY(hipcub::DeviceScan::ExclusiveSum(e->cub_tmp.p, tmp, e->ev_counts.p, e->ev_pre.p, (int)(n_waves + 1), s));
+    }
+    hipLaunchKernelGGL(k_report, dim3(rep_blocks), dim3(kReportThreads), 0, s, P, fuse ? 0u : (uint32_t)n_waves,
+                       (const uint64_t*)e->ev_pre.p);
     HIP_TRY(hipGetLastError());
+    {
+      size_t tmp = 0;
+      HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->hit_seg_n.p, e->hit_pre.p, (int)n_rw, s));
+      HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+      HIP_TRY(hipcub::DeviceScan::ExclusiveSum(e->cub_tmp.p, tmp, e->hit_seg_n.p, e->hit_pre.p, (int)n_rw, s));
+      unsigned long long* base = (unsigned long long*)(e->hit_pre.p + n_rw);
+      hipLaunchKernelGGL(k_hits_reserve, dim3(1), dim3(1), 0, s, P, n_rw, e->hit_pre.p, base);
+      hipLaunchKernelGGL(k_hits_pack, dim3(n_rw), dim3(256), 0, s, P, e->hit_pre.p, base);
+      HIP_TRY(hipGetLastError());
+    }
+    P.hit_seg = nullptr;  // (the later passes reserve on ctrl->hits)
     hipLaunchKernelGGL(k_fold_special, dim3((uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_spans + 255) / 256, 2048))),
                        dim3(256), 0, s, P, n_spans);
   } else if (P.big.blob && !experiment_env("TSG_NO_BIG")) {
@@ -5949,6 +6336,7 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     // TSG_BIG_VARIANT=40x2v2 skips them, exp build)
     const void* big_fn = (const void*)k_scan_big<kBigMode, kBigChains, kBigRing>;
     int big_mode = kBigMode, big_ch = kBigChains;
+    int lines = 0;  // (exp: TSG_BIG_LINES)
 #ifdef TSG_EXPERIMENTS
     int big_v = kBigRing;
     if (const char* v = getenv("TSG_BIG_VARIANT")) {  // "<mode>[x<chains>][v<ring uint4s>]"
@@ -5962,6 +6350,7 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
         {0, 1, 8, k_scan_big<0, 1>},     {1, 1, 8, k_scan_big<1, 1>},     {2, 1, 8, k_scan_big<2, 1>},
         {3, 1, 8, k_scan_big<3, 1>},     {4, 1, 8, k_scan_big<4, 1>},     {0, 2, 4, k_scan_big<0, 2>},
         {8, 2, 4, k_scan_big<8, 2>},     {0, 2, 2, k_scan_big<0, 2, 2>},  {8, 2, 2, k_scan_big<8, 2, 2>},
+        {8, 1, 8, k_scan_big<8, 1>},
         {12, 2, 2, k_scan_big<12, 2, 2>}, {2, 2, 2, k_scan_big<2, 2, 2>}, {4, 1, 4, k_scan_big<4, 1, 4>},
         {9, 2, 2, k_scan_big<9, 2, 2>},  {3, 2, 2, k_scan_big<3, 2, 2>},  {24, 2, 2, k_scan_big<24, 2, 2>},
         {25, 2, 2, k_scan_big<25, 2, 2>}, {40, 2, 2, k_scan_big<40, 2, 2>}};
@@ -5976,13 +6365,19 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
       big_fn = (const void*)pick;
       nl_skipped = e->nl_lazy && (big_mode & kBigNoNl);
     }
+    if (const char* v = getenv("TSG_BIG_LINES")) {  // the coalesced whole-line shape: "1" = 2 chains, "2" = 1 chain
+      lines = atoi(v);
+      if (lines == 1) big_fn = (const void*)k_scan_lines<8, 2>;
+      if (lines == 2) big_fn = (const void*)k_scan_lines<8, 1>;
+      nl_skipped = false;
+    }
 #endif
-    const uint64_t big_units = (units + big_ch - 1) / big_ch;
+    const uint64_t big_units = lines ? (P.nbytes + 127) / 128 / 64 * 64 : (units + big_ch - 1) / big_ch;
     const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((big_units + nt - 1) / nt, e->num_cus));
     const uint64_t n_waves = (uint64_t)blocks * (nt / 64);
     P.ev_cap_per_wave = std::max<uint64_t>(1024, (P.nbytes / 256) / n_waves + 256);
     HIP_TRY(e->ev_buf.ensure(n_waves * P.ev_cap_per_wave));
-    HIP_TRY(e->ev_counts.ensure(n_waves));
+    HIP_TRY(e->ev_counts.ensure(n_waves + 1));
     HIP_TRY(e->ev_overflow.ensure(std::max<uint64_t>(1 << 20, e->ev_ovf_need)));
     P.events = e->ev_buf.p;
     P.ev_counts = e->ev_counts.p;
@@ -6743,11 +7138,17 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     e->events = true;
   }
   HIP_TRY(hipEventRecord(e->ev[0], s));
-  // ---- 1. path gates (per file).  Not overlapped with the scan: the scan
-  // fills every CU's VGPRs, so a side-stream launch only delays k_report.
+  // ---- 1. path gates (per file).  Not overlapped with the scan (it fills
+  // every CU's VGPRs and LDS): after a scan the gate runs on the side stream
+  // beside the fold passes and the host's read of the scan counters, and
+  // the candidates wait for it; without a scan (merge, empty batch) it runs
+  // here.
   const bool path_gates = nf && (im.n_gpath || rs->any_path_rules);
+  const bool merge_mode = sp && sp->mode == 2;
+  const bool gate_on_side = path_gates && !merge_mode && nbytes > 0;
+  GateParams G{};
+  uint32_t gate_blocks = 0;
   if (path_gates) {
-    GateParams G{};
     G.off = d_off;
     G.paths = d_paths;
     G.path_off = d_path_off;
@@ -6779,10 +7180,15 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     G.pac_always = im.pac_always;
     G.n_progs = (uint32_t)rs->regexes.size();
     G.pdfa = im.u32.p + im.o_pdfa;
-    uint32_t blocks = std::min<uint32_t>((nf + 255) / 256, e->vm_threads / 256);
-    hipLaunchKernelGGL(k_path_gate, dim3(std::max(1u, blocks)), dim3(256), 0, s, G);
-    HIP_TRY(hipGetLastError());
+    gate_blocks = std::max(1u, std::min<uint32_t>((nf + 255) / 256, e->vm_threads / 256));
+    if (!gate_on_side) {
+      hipLaunchKernelGGL(k_path_gate<true>, dim3(gate_blocks), dim3(256), 0, s, G);
+      HIP_TRY(hipGetLastError());
+    } else {
+      HIP_TRY(ensure_side(e));
+    }
   }
+  bool gate_pending = false;  // the side-stream gate has been launched and not yet waited for
   HIP_TRY(hipEventRecord(e->ev[1], s));
   // ---- 2. keyword/anchor scan
   uint64_t hit_cap = std::max<uint64_t>(1 << 20, nbytes / 256);
@@ -6835,6 +7241,17 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(hipEventRecord(e->ev[8], s));
     if ((rc = launch_scan(e, P))) return rc;
     HIP_TRY(hipEventRecord(e->ev[9], s));
+    if (gate_on_side && !gate_pending) {  // (once: a rescan leaves the gates as they are)
+      // right after the scan kernel (ev[11]), beside k_report (whose blocks
+      // leave VGPRs and wave slots but no LDS: the gate's automaton stays in
+      // global memory)
+      HIP_TRY(hipStreamWaitEvent(e->side, e->fast_timed ? e->ev[11] : e->ev[9], 0));
+      HIP_TRY(hipEventRecord(e->ev_pg[0], e->side));
+      hipLaunchKernelGGL(k_path_gate<false>, dim3(gate_blocks), dim3(256), 0, e->side, G);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipEventRecord(e->ev_pg[1], e->side));
+      gate_pending = true;
+    }
     // the fold-window pass reads the scan's rune count on the device; one
     // read of the counters afterwards checks every buffer of both passes
     if ((rc = launch_fold_windows(e, P, true))) return rc;
@@ -6869,6 +7286,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     return TSG_ERR_INTERNAL;
   }
   if ((rc = launch_uni_keywords(e, P))) return rc;
+  if (gate_pending) HIP_TRY(hipStreamWaitEvent(s, e->ev_pg[1], 0));  // file flags and path masks complete
   HIP_TRY(hipEventRecord(e->ev[2], s));
   Ctrl c = c_scan;
   if (!have_c && (rc = read_ctrl(e, &c))) return rc;  // (one host round trip fewer after a scan)
@@ -6899,6 +7317,11 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   E.full_rules = im.u32.p + im.o_full;
   E.n_full_rules = im.n_full;
   uint64_t n_cands = 0;
+  if (e->nl_deferred) {  // the lazy newline counts' reach per file, marked by the candidates' kernels
+    HIP_TRY(ensure_side(e));
+    HIP_TRY(e->nl_last.ensure(nf));
+    E.nl_last = e->nl_last.p;
+  }
   for (int attempt = 0; attempt < 3; ++attempt) {
     HIP_TRY(e->keys.ensure(cand_cap));
     HIP_TRY(e->vals.ensure(cand_cap));
@@ -6906,6 +7329,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     E.vals = e->vals.p;
     E.cand_cap = e->keys.n;
     HIP_TRY(hipMemsetAsync(&e->ctrl.p->cands, 0, 8, s));
+    if (E.nl_last) HIP_TRY(hipMemsetAsync(e->nl_last.p, 0, (size_t)nf * 8, s));
     if (n_hits)
       hipLaunchKernelGGL(k_expand, dim3((uint32_t)((n_hits + 255) / 256)), dim3(256), 0, s, E);
     if (nf) hipLaunchKernelGGL(k_full_jobs, dim3((nf + 255) / 256), dim3(256), 0, s, E);
@@ -6945,24 +7369,23 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
     HIP_TRY(hipcub::DeviceSelect::Flagged(e->cub_tmp.p, tmp2, cnt, e->flags8.p, e->job_start.p, e->nsel.p,
                                           (int)n_cands, s));
-    if (e->nl_deferred) {  // phase-0 newline counts of the candidate files, under the verify (k_nl_cands)
-      HIP_TRY(ensure_side(e));
-      HIP_TRY(e->nl_last.ensure(nf));
-      HIP_TRY(hipMemsetAsync(e->nl_last.p, 0, (size_t)nf * 8, s));
-      hipLaunchKernelGGL(k_nl_cands, dim3((uint32_t)((n_cands + 255) / 256)), dim3(256), 0, s, e->keys2.p,
-                         e->vals2.p, n_cands, d_off, e->nl_last.p);
-      HIP_TRY(hipEventRecord(e->ev_nl[0], s));
-      HIP_TRY(hipStreamWaitEvent(e->side, e->ev_nl[0], 0));
-      const uint64_t n_spans = (nbytes + kNlBlock - 1) / kNlBlock;
-      uint32_t nl_blocks0 = (uint32_t)((n_spans + 255) / 256);
-      if (const char* v = experiment_env("TSG_NL_BLOCKS_PER_CU"))  // (A/B: a thinner phase-0 grid under k_verify)
-        nl_blocks0 = std::min<uint32_t>(nl_blocks0, std::max(1, atoi(v)) * std::max(1u, e->num_cus));
-      hipLaunchKernelGGL(k_nl_spans, dim3(nl_blocks0), dim3(256), 0, e->side, d_data, nbytes,
-                         d_off, e->region_file.p, nbytes / kNlBlock + 1, nf, e->nl_last.p, e->nl_blocks.p, 0u);
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipEventRecord(e->ev_nl[1], e->side));
-      e->nl_pending = true;
-    }
+  }
+  if (e->nl_deferred && n_cands) {
+    // phase-0 newline counts of the candidate files on the side stream, under
+    // the verify (the reach comes from k_expand / k_full_jobs).  Not under the
+    // candidate sort: the count's blocks starved its short kernels (0.09 ->
+    // 0.6 ms, profiles/r05d)
+    HIP_TRY(hipEventRecord(e->ev_nl[0], s));
+    HIP_TRY(hipStreamWaitEvent(e->side, e->ev_nl[0], 0));
+    const uint64_t n_spans = (nbytes + kNlBlock - 1) / kNlBlock;
+    uint32_t nl_blocks0 = (uint32_t)((n_spans + 255) / 256);
+    if (const char* v = experiment_env("TSG_NL_BLOCKS_PER_CU"))  // (A/B: a thinner phase-0 grid under k_verify)
+      nl_blocks0 = std::min<uint32_t>(nl_blocks0, std::max(1, atoi(v)) * std::max(1u, e->num_cus));
+    hipLaunchKernelGGL(k_nl_spans, dim3(nl_blocks0), dim3(256), 0, e->side, d_data, nbytes, d_off,
+                       e->region_file.p, nbytes / kNlBlock + 1, nf, e->nl_last.p, e->nl_blocks.p, 0u);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(e->ev_nl[1], e->side));
+    e->nl_pending = true;
   }
   // the job count stays on the device: k_verify reads it, and its grid and
   // the location lists are sized from n_cands (>= jobs); the host reads the
@@ -6975,8 +7398,23 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   uint64_t redo_cap = std::max<uint64_t>(1 << 12, n_cands / 64);
   uint64_t n_locs = 0, n_dropped = 0, n_deferred = 0;
   bool verified = n_cands == 0;
+  bool shard_locs = true;  // (A/B: TSG_LOC_SHARDS=0, exp build: one location counter)
+#ifdef TSG_EXPERIMENTS
+  if (const char* v = getenv("TSG_LOC_SHARDS")) shard_locs = atoi(v) != 0;
+#endif
   for (int attempt = 0; attempt < 4 && !verified; ++attempt) {
-    HIP_TRY(e->locs.ensure(loc_cap));
+    // sharded: kLocShards regions of loc_cap / kLocShards (at least 256) and
+    // an overflow region of loc_cap; the dense copy goes to locs2
+    // (both lists sized from loc_total, never from each other's capacity: they
+    // swap roles after every call)
+    const uint64_t shard_cap = std::max<uint64_t>(256, loc_cap / kLocShards);
+    const uint64_t loc_total = shard_locs ? kLocShards * shard_cap + loc_cap : loc_cap;
+    HIP_TRY(e->locs.ensure(loc_total));
+    if (shard_locs) {
+      HIP_TRY(e->locs2.ensure(loc_total));
+      HIP_TRY(e->loc_cnt.ensure(kLocShards + 1));
+      HIP_TRY(hipMemsetAsync(e->loc_cnt.p, 0, (kLocShards + 1) * 8, s));
+    }
     HIP_TRY(e->caps.ensure(caps_cap));
     HIP_TRY(e->caps_big.ensure(caps_big_cap));
     HIP_TRY(e->caps_run.ensure(caps_run_cap));
@@ -7001,7 +7439,9 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     V.job_start = e->job_start.p;
     V.n_jobs_dev = e->nsel.p;
     V.locs = e->locs.p;
-    V.loc_cap = e->locs.n;
+    V.loc_cap = shard_locs ? loc_total : e->locs.n;
+    V.loc_shards = shard_locs ? e->loc_cnt.p : nullptr;
+    V.loc_shard_cap = shard_cap;
     V.ctrl = e->ctrl.p;
     V.scratch = e->scratch.p;
     V.scratch_stride = e->scratch_stride;
@@ -7108,7 +7548,16 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     hipLaunchKernelGGL((k_captures<64, 1, kBigBsWords, true, uint32_t>), dim3(e->num_cus * 4), dim3(64), 0, s, V);
     if (any_long)
       hipLaunchKernelGGL((k_captures<64, 1, kBigBsWords, true, uint64_t>), dim3(e->num_cus * 4), dim3(64), 0, s, V);
-    hipLaunchKernelGGL(k_drop_spec, dim3(e->num_cus * 4), dim3(256), 0, s, V);
+    if (shard_locs) {  // the shard regions packed densely into locs2; k_drop_spec works on that
+      hipLaunchKernelGGL(k_loc_compact, dim3(kLocShards + 1), dim3(256), 0, s, V, e->locs2.p);
+      VerifyParams D = V;
+      D.locs = e->locs2.p;
+      D.loc_cap = loc_total;
+      D.loc_shards = nullptr;
+      hipLaunchKernelGGL(k_drop_spec, dim3(e->num_cus * 4), dim3(256), 0, s, D);
+    } else {
+      hipLaunchKernelGGL(k_drop_spec, dim3(e->num_cus * 4), dim3(256), 0, s, V);
+    }
     HIP_TRY(hipGetLastError());
     if (prof) {  // the jobs that end last (their waves set k_verify's length), per-rule totals
       std::vector<uint64_t> hp(4ull * n_jobs);
@@ -7196,9 +7645,10 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     n_locs = c.locs;
     n_dropped = c.n_dropped;
     n_deferred = c.n_defer;
-    if (n_locs <= e->locs.n && c.n_caps <= e->caps.n && c.n_caps_big <= e->caps_big.n && c.n_redo <= e->redo.n &&
-        c.n_caps_run <= e->caps_run.n && c.n_match <= e->matches.n) {
+    if (n_locs <= V.loc_cap && c.n_caps <= e->caps.n && c.n_caps_big <= e->caps_big.n &&
+        c.n_redo <= e->redo.n && c.n_caps_run <= e->caps_run.n && c.n_match <= e->matches.n) {
       verified = true;
+      if (shard_locs) std::swap(e->locs, e->locs2);  // the dense list is the location list from here on
       break;
     }
     // a list overflowed: grow it and re-run the search and the capture stages
@@ -7412,6 +7862,11 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(hipEventElapsedTime(&ms, e->ev[k], e->ev[k + 1]));
     tm[k] = ms;
   }
+  if (gate_pending) {  // the path gate ran on the side stream: its own time
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, e->ev_pg[0], e->ev_pg[1]));
+    tm[0] = ms;
+  }
 
   tm[8] = (double)n_hits;
   tm[9] = (double)n_cands;
@@ -7522,6 +7977,7 @@ void tsg_engine_free(tsg_engine* e) {
   e->file_kw.release(); e->file_flags.release(); e->path_mask.release(); e->hits.release();
   e->keys.release(); e->keys2.release(); e->vals.release(); e->vals2.release(); e->flags8.release();
   e->job_start.release(); e->nsel.release(); e->cub_tmp.release(); e->locs.release(); e->locs2.release();
+  e->hit_seg.release(); e->hit_pre.release(); e->hit_seg_n.release(); e->loc_cnt.release(); e->ev_pre.release();
   e->scratch.release(); e->ctrl.release(); e->excl_out.release(); e->part_buf.release(); e->caps_run.release();
   e->nl_blocks.release(); e->nl_pre.release(); e->tail.release(); e->region_file.release(); e->region_tmp.release();
   e->ev_buf.release(); e->ev_overflow.release(); e->ev_counts.release(); e->span_hi.release(); e->fold_pos.release(); e->caps.release(); e->caps_big.release();
@@ -7544,6 +8000,8 @@ void tsg_engine_free(tsg_engine* e) {
     (void)hipEventDestroy(e->ev_side);
     (void)hipEventDestroy(e->ev_nl[0]);
     (void)hipEventDestroy(e->ev_nl[1]);
+    (void)hipEventDestroy(e->ev_pg[0]);
+    (void)hipEventDestroy(e->ev_pg[1]);
     (void)hipStreamDestroy(e->side);
   }
   (void)hipStreamDestroy(e->stream);
