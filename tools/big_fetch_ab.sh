@@ -26,9 +26,9 @@ for v in $VARS; do
 import csv, glob, sys
 o, v = sys.argv[1], sys.argv[2]
 fs = [float(r["Counter_Value"]) for f in glob.glob(f"{o}/fetch_{v}/**/*counter_collection.csv", recursive=True)
-      for r in csv.DictReader(open(f)) if "k_scan_big" in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE"]
+      for r in csv.DictReader(open(f)) if ("k_scan_big" in r["Kernel_Name"] or "k_scan_lines" in r["Kernel_Name"]) and r["Counter_Name"] == "FETCH_SIZE"]
 ts = [r for f in glob.glob(f"{o}/trace_{v}/**/*kernel_stats.csv", recursive=True) for r in csv.DictReader(open(f))
-      if "k_scan_big" in r["Name"]]
+      if "k_scan_big" in r["Name"] or "k_scan_lines" in r["Name"]]
 fetch = sum(fs) / len(fs) * 1024 * 2 / 1e9 if fs else None
 ms = float(ts[0]["AverageNs"]) / 1e6 if ts else None
 print(f"{v}: k_scan_big fetch {fetch:.2f} GB/launch (x2 corrected), avg {ms:.3f} ms, launches {len(fs)}")

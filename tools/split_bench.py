@@ -67,6 +67,8 @@ def main():
         p = N.lib.tsg_result_locs(res)
         return sorted((p[i].rule, p[i].start, p[i].end, p[i].start_line) for i in range(n))
 
+    whole_stages = {}
+
     def whole():
         res = ctypes.c_void_p()
         t = time.perf_counter()
@@ -75,6 +77,13 @@ def main():
                                       ctypes.byref(res)))
         dt = (time.perf_counter() - t) * 1e3
         out = locs_of(res)
+        tm = (ctypes.c_double * 32)()
+        nt = ctypes.c_size_t()
+        N.lib.tsg_result_timings(res, tm, 32, ctypes.byref(nt))
+        # (bench.py's stages_ms names; [15] the call's host wall, [16] its post-device part)
+        names = ["path_gate", "scan_total", "expand", "sort_jobs", "verify", "exclude", "lines", "scan_kernels"]
+        whole_stages.update({k: round(tm[i], 3) for i, k in enumerate(names)},
+                            call_wall=round(tm[15], 3), post=round(tm[16], 3))
         N.lib.tsg_result_free(res)
         return dt, out
 
@@ -117,7 +126,8 @@ def main():
         best["speedup_vs_whole"] = round(w_ms / best["projected_ms"], 2)
         rows.append(best)
     print(json.dumps(dict(tool="split_bench", file_gb=size / 1e9, whole_ms=round(w_ms, 3),
-                          whole_gbps=round(size / w_ms / 1e6, 1), findings=len(want), splits=rows)))
+                          whole_gbps=round(size / w_ms / 1e6, 1), whole_stages_ms=whole_stages, findings=len(want),
+                          splits=rows)))
 
 
 if __name__ == "__main__":

@@ -37,6 +37,7 @@
 #include <set>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "engine.h"
@@ -172,6 +173,7 @@ struct ScanParams {
   uint32_t* file_flags;  // n_files
   uint64_t* hits;
   uint64_t hit_cap;
+  uint64_t nl_big;  // lazy newline counts: the scan counts the spans of files this big (0: none)
   // k_report: each report wave's own hit region (hit_seg_cap records at
   // hit_seg + wave * hit_seg_cap; counts in hit_seg_n), packed into `hits` by
   // k_hits_pack -- null: flushes reserve on ctrl->hits
@@ -530,6 +532,7 @@ struct FastChain {
   uint32_t nl;   // newlines of the current span
   uint32_t hi;   // OR of the span's dwords: bit 7 of a byte = a byte >= 0x80
   uint2 prev;    // the 8 raw bytes before the next group
+  bool cnt = false;  // kMode 2: wave-uniform -- count this round's newlines anyway
 };
 
 // Append an event for a group whose automaton max reached an output state
@@ -570,7 +573,7 @@ template <int V, int kMode = 0>
 __device__ inline void fast_group(const ScanParams& P, const uint8_t* T, uint32_t out_e, FastChain<V>& C, uint32_t d0,
                                   uint32_t d1, uint64_t gpos, bool live, uint64_t lanes_lt, FastEvent* ev_seg,
                                   uint32_t* ev_count) {
-  if (!(kMode & 2)) C.nl += nl_count_dword(d0) + nl_count_dword(d1);
+  if (!(kMode & 2) || C.cnt) C.nl += nl_count_dword(d0) + nl_count_dword(d1);
   C.hi |= d0 | d1;
   const uint32_t f0 = fold6(d0), f1 = fold6(d1);
   const uint32_t gs = C.e;
@@ -623,7 +626,7 @@ __device__ inline void fast_window(const ScanParams& P, const uint8_t* T, uint32
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const uint32_t d0 = d[2 * g], d1 = d[2 * g + 1];
-    if (!(kMode & 2)) C.nl += nl_count_dword(d0) + nl_count_dword(d1);
+    if (!(kMode & 2) || C.cnt) C.nl += nl_count_dword(d0) + nl_count_dword(d1);
     C.hi |= d0 | d1;
     const uint32_t f0 = fold6(d0), f1 = fold6(d1);
     gs[g] = C.e;
@@ -692,6 +695,8 @@ __device__ inline RepView rep_view(const AcDev& ac, const uint8_t* B) {
                  (const PatDev*)(B + ac.o_pats), B + ac.o_pat_bytes};
 }
 
+constexpr uint64_t kKwReadFirst = 1ull << 20;  // (report_event's keyword bits)
+
 // One event on one lane: replay its 8 bytes on the image, and per output
 // confirm the pattern on the real bytes, set the file's keyword gate bit and
 // stage the anchor hit in the wave's LDS slots (wbuf / *hcnt_w).
@@ -755,8 +760,15 @@ __device__ inline void report_event(const ScanParams& P, const AcDev& ac, const 
           // fire-and-forget atomic: reading the word first to skip the
           // atomics of repeated keywords put an L2 round trip on the lane's
           // chain (k_report 650 -> 618 us on configs[2] without it,
-          // profiles/r04ac)
-          atomicOr(&P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)], 1u << (pd.kw & 31));
+          // profiles/r04ac) -- except in files of kKwReadFirst bytes or more,
+          // whose keyword words every wave hits: atomics on one address
+          // serialise in its L2 channel (one 20 GB file: k_report 11.3 ms
+          // for a 5.5 ms scan, profiles/r05f)
+          uint32_t* wp = &P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)];
+          const uint32_t bit = 1u << (pd.kw & 31);
+          if (P.off[fi + 1] - P.off[fi] < kKwReadFirst ||
+              !(__hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit))
+            atomicOr(wp, bit);
         }
       }
       if (want_hit) {
@@ -812,6 +824,26 @@ __device__ __noinline__ void resolve_segment(const ScanParams& P, const AcDev& a
     if (i < lim) report_event(P, ac, R, ev_seg[i], wbuf, hcnt_w, my_out, last_kw);
     report_flush(P, wbuf, hcnt_w, lane, false);
   }
+}
+
+// 64 MiB: on configs[2] a 256 KiB threshold moved 0.43 ms into the scan for
+// 0.33 ms less verify / lazy count (step +0.1 ms, profiles/r05g); for one
+// 20 GB file the lazy count would read the whole file after the scan.
+constexpr uint64_t kNlBig = 64ull << 20;  // (tools/ab_env.sh, TSG_NL_BIG)
+// Span sp's newline count comes from the scan (not the lazy k_nl_spans) when
+// a file of nl_big bytes or more overlaps it: only the files holding its first
+// and its last byte can (the others lie inside the span).  The batch's big
+// files are most of the bytes the lazy count would read (every plant file of
+// several MB, counted up to its last candidate), and in the scan their count
+// costs VALU beside the LDS-bound walk instead of HBM time under k_verify.
+__device__ inline bool span_scan_counted(const uint64_t* off, const uint32_t* region_file, uint64_t n_regions,
+                                         uint32_t n_files, uint64_t sp, uint64_t nl_big) {
+  if (!nl_big || !n_files) return false;
+  const uint32_t f0 = region_file[sp];
+  uint32_t f1 = sp + 1 < n_regions ? region_file[sp + 1] : n_files - 1;
+  if (f1 >= n_files) f1 = n_files - 1;
+  auto big = [&](uint32_t f) { return off[f + 1] - off[f] - 1 >= nl_big; };
+  return big(f0) || (f1 != f0 && off[f1] < (sp + 1) * kNlBlock && big(f1));
 }
 
 // kFuse: the scan resolves its own events (k_report's work, report_event) --
@@ -891,6 +923,21 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
       C[c].nl = 0;
       C[c].hi = 0;
     }
+    // lazy newline counts (kMode 2) except in the spans of files of nl_big
+    // bytes or more (span_scan_counted): those this scan counts -- the wave
+    // takes the counting loop when any of its lanes' spans needs it
+    bool count_nl = false;
+    if ((kMode & 2) && P.nl_big && live) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c)
+        count_nl |= C[c].pos < P.nbytes &&
+                    span_scan_counted(P.off, P.region_file, P.n_regions, P.n_files, C[c].pos / kNlBlock, P.nl_big);
+    }
+    {
+      const bool cnt = (kMode & 2) && __builtin_amdgcn_readfirstlane((uint32_t)(__ballot(count_nl) != 0));
+#pragma unroll
+      for (int c = 0; c < CH; ++c) C[c].cnt = cnt;
+    }
     for (int step = 0; step < kSteps; ++step) {
       // take the prefetched bytes, then prefetch the chain's next step (same
       // span, or the first step of the lane's next unit)
@@ -952,7 +999,7 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
       for (int c = 0; c < CH; ++c) {
         const uint64_t s0 = u * kUnit + (uint64_t)c * kNlBlock;
         if (s0 < P.nbytes) {
-          P.nl_blocks[s0 / kNlBlock] = C[c].nl;
+          if (!(kMode & 2) || count_nl) P.nl_blocks[s0 / kNlBlock] = C[c].nl;
           P.span_hi[s0 / kNlBlock] = (C[c].hi & 0x80808080u) ? 1 : 0;
         }
       }
@@ -976,6 +1023,71 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
   }
 }
 
+#ifdef TSG_EXPERIMENTS
+// Timing bound of a stride-2 trigram front filter (exp
+// build, WRONG results): k_scan_fast's load shape (one 4 KiB span per lane,
+// 128-byte register ring), but instead of one DFA step per byte, per even
+// position one ds_read_b64 of a 64-bit mask indexed by the fold columns of
+// bytes p, p + 1 (32 KiB: 4096 pairs) and a test of bit column(p + 2) -- 0.5
+// LDS gathers per byte, no dependent chain, no replay of flagged groups and
+// no events (a ballot per window keeps the work).  Whatever this costs is a
+// floor for a filter-then-replay design on this load shape.
+__global__ __launch_bounds__(1024) void k_scan_tri(ScanParams P) {
+  __shared__ __align__(16) uint64_t tri[4096];
+  for (uint32_t i = threadIdx.x; i < 4096; i += 1024) tri[i] = (i * 0x9E3779B97F4A7C15ull) & 0x0000010000000101ull;
+  __syncthreads();
+  const uint64_t nlanes = (uint64_t)gridDim.x * 1024;
+  const uint64_t units = (P.nbytes + kNlBlock - 1) / kNlBlock;
+  uint64_t u = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+  uint4 nxt[8];
+  uint64_t pos = u * kNlBlock;
+  if (u < units) {
+    const uint8_t* src = fast_src(P, pos);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) nxt[k] = *(const uint4*)(src + pos + 16 * k);
+  }
+  uint32_t found = 0;
+  while (__ballot(u < units)) {
+    const bool live = u < units;
+    const uint64_t un = u + nlanes;
+    for (int step = 0; step < (int)(kNlBlock / 128); ++step) {
+      uint4 cur[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) cur[k] = nxt[k];
+      const uint64_t np = step + 1 < (int)(kNlBlock / 128) ? pos + 128 : un * kNlBlock;
+      if (live && (step + 1 < (int)(kNlBlock / 128) || un < units)) {
+        const uint8_t* src = fast_src(P, np);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) nxt[k] = *(const uint4*)(src + np + 16 * k);
+      }
+      uint32_t flag = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t w[5] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w, k + 1 < 8 ? cur[k + 1].x : cur[k].x};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t f = fold6(w[q]), fn = fold6(w[q + 1]);  // bytes = 2 x column
+#pragma unroll
+          for (int j = 0; j < 4; j += 2) {  // positions 4q + j, j even
+            const uint32_t b0 = (f >> (8 * j)) & 0xFFu, b1 = j + 1 < 4 ? (f >> (8 * (j + 1))) & 0xFFu : fn & 0xFFu;
+            const uint32_t b2 = j + 2 < 4 ? (f >> (8 * (j + 2))) & 0xFFu : (fn >> (8 * (j - 2))) & 0xFFu;
+            const uint64_t m = tri[(b0 << 5) | (b1 >> 1)];
+            flag |= (uint32_t)(m >> (b2 >> 1)) & 1u;
+          }
+        }
+        if ((k & 3) == 3) {  // one wave-level check per 64 bytes (as k_scan_fast's event window)
+          if (__ballot(flag & (live ? 1u : 0u))) found += flag;
+          flag = 0;
+        }
+      }
+      pos = np;
+    }
+    u = un;
+  }
+  if (found == 0xFFFFFFFFu) P.ctrl->err = found;  // (keeps the work observable)
+}
+#endif
+
 // Scan with an automaton too large for k_scan_fast's image (configs[4]: 1000+
 // custom rules), in k_scan_fast's shape: 4 KiB spans (7 bytes of warm-up)
 // streamed through register rings, 1024 threads and ONE LDS copy of the
@@ -990,7 +1102,8 @@ constexpr uint32_t kBigThreads = 1024;
 // k_scan_big's product shape (tools/big_ab.sh, profiles/r03l): two chains
 // per lane, each with a 2 x 16-byte ring, every chain's dense row read issued
 // before any cold walk -- 8.87 vs 9.63 ms (one chain, 8 x 16 B) on configs[4]
-constexpr int kBigMode = 8, kBigChains = 2, kBigRing = 2;
+constexpr int kBigMode = 8, kBigChains = 2;
+[[maybe_unused]] constexpr int kBigRing = 2;  // (k_scan_big, exp build only)
 constexpr int kBigNoNl = 32;  // kMode bit: no per-span newline counts (the engine's nl_lazy)
 constexpr uint32_t kBigLdsMax = 160 * 1024 - 256;  // the blob's LDS part (k_big_walk adds 80 B of its own)
 // Cold records kept in LDS at least (the rest of the blob's cold records
@@ -1758,7 +1871,11 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
   const uint32_t n_rw = gridDim.x * (kReportThreads / 64);
   uint64_t* hseg = P.hit_seg ? P.hit_seg + (uint64_t)rw * P.hit_seg_cap : nullptr;
   uint32_t hcur = 0;
-  const uint64_t lo = E * rw / n_rw, hi = E * (rw + 1) / n_rw;
+  uint64_t lo = E * rw / n_rw, hi = E * (rw + 1) / n_rw;
+  if ((P.report_mode & 8) && n_waves <= n_rw) {  // (A/B, exp: whole segment rw per wave; the last wave also
+    lo = rw < n_waves ? ev_pre[rw] : E;           //  takes the overflow bucket)
+    hi = rw + 1 == n_rw ? E : rw < n_waves ? ev_pre[rw + 1] : E;
+  }
   // the segment of event lo (s == n_waves: the overflow bucket)
   uint32_t s = n_waves;
   if (lo < e_reg) {
@@ -4149,7 +4266,7 @@ __global__ __launch_bounds__(256) void k_nl_tail(const uint64_t* off, uint32_t n
 __global__ __launch_bounds__(256) void k_nl_spans(const uint8_t* data, uint64_t nbytes, const uint64_t* off,
                                                   const uint32_t* region_file, uint64_t n_regions, uint32_t n_files,
                                                   const unsigned long long* nl_last, uint32_t* nl_blocks,
-                                                  uint32_t phase) {
+                                                  uint32_t phase, uint64_t nl_big) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t n_spans = (nbytes + kNlBlock - 1) / kNlBlock;
   const uint64_t n_waves = (uint64_t)gridDim.x * (blockDim.x / 64);
@@ -4157,7 +4274,7 @@ __global__ __launch_bounds__(256) void k_nl_spans(const uint8_t* data, uint64_t 
        sp0 += n_waves * 64) {
   const uint64_t sp = sp0 + lane;
   bool need = false;
-  if (sp < n_spans) {
+  if (sp < n_spans && !span_scan_counted(off, region_file, n_regions, n_files, sp, nl_big)) {
     // files overlapping span sp: the one holding its first byte through the
     // one holding the next span's first byte
     const uint32_t f0 = region_file[sp];
@@ -5441,6 +5558,7 @@ struct tsg_engine {
   // set by the caller), and nl_deferred records that the last scan did, so
   // k_nl_spans counts the spans of the files that have locations
   bool nl_lazy = false, nl_deferred = false;
+  uint64_t nl_big = 0;  // the last scan's span_scan_counted threshold (k_nl_spans skips those spans)
   DBuf<uint32_t> fbase;  // newline prefix at each location file's start (k_file_base)
   DBuf<unsigned long long> nl_last;  // per file: counted bound + 1 (0: none) | kNlFull (k_nl_cands / _check / _tail)
   hipEvent_t ev_nl[2] = {nullptr, nullptr};  // candidates ready -> phase-0 count done (side stream)
@@ -6247,6 +6365,7 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
       hipLaunchKernelGGL((k_scan_deep<VV, DD, 1024, M>), dim3(blocks), dim3(nt), 0, s, P);
     TSG_DEEP(8, 1, 0) TSG_DEEP(4, 3, 0) TSG_DEEP(4, 1, 0) TSG_DEEP(2, 3, 0)
 #undef TSG_DEEP
+    else if (mode == 8) hipLaunchKernelGGL(k_scan_tri, dim3(blocks), dim3(nt), 0, s, P);  // trigram filter timing bound
 #define TSG_MODE(M) \
   else if (chains == 1 && vecs == 8 && mode == M) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, M>), dim3(blocks), dim3(nt), 0, s, P);
     TSG_MODE(1) TSG_MODE(2) TSG_MODE(3) TSG_MODE(4) TSG_MODE(5) TSG_MODE(6) TSG_MODE(7)
@@ -6334,9 +6453,12 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     // (newline counts stay in this kernel: they cost it ~0.1 ms on configs[4],
     // against ~0.9 ms for counting its many location files afterwards --
     // TSG_BIG_VARIANT=40x2v2 skips them, exp build)
-    const void* big_fn = (const void*)k_scan_big<kBigMode, kBigChains, kBigRing>;
+    // product: the coalesced whole-line shape, one chain per lane (k_scan_lines;
+    // configs[4]: 5.05 ms and 1.006x FETCH against 7.33 ms and 3.63x for the
+    // span-per-lane k_scan_big, profiles/r05e_big)
+    const void* big_fn = (const void*)k_scan_lines<kBigMode, 1>;
     int big_mode = kBigMode, big_ch = kBigChains;
-    int lines = 0;  // (exp: TSG_BIG_LINES)
+    int lines = 2;  // 0: k_scan_big (exp: TSG_BIG_VARIANT), 1 / 2: k_scan_lines with 2 / 1 chains
 #ifdef TSG_EXPERIMENTS
     int big_v = kBigRing;
     if (const char* v = getenv("TSG_BIG_VARIANT")) {  // "<mode>[x<chains>][v<ring uint4s>]"
@@ -6364,6 +6486,7 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     if (getenv("TSG_BIG_VARIANT")) {
       big_fn = (const void*)pick;
       nl_skipped = e->nl_lazy && (big_mode & kBigNoNl);
+      lines = 0;
     }
     if (const char* v = getenv("TSG_BIG_LINES")) {  // the coalesced whole-line shape: "1" = 2 chains, "2" = 1 chain
       lines = atoi(v);
@@ -6963,6 +7086,60 @@ uint64_t part_right_halo(const tsg_ruleset* rs) {
   return ((m + 64 + kNlBlock - 1) / kNlBlock) * kNlBlock;
 }
 
+// Part blobs come from a process-wide pool of page-locked blocks:
+// hipHostMalloc of a blob (~5 MB of newline counts per 10 GB part) took
+// 1.2 ms of a 10 GB part's 10.4 ms (profiles/r05f).  tsg_part_free returns a
+// block to the pool; at most kBlobPoolBytes stay parked there.
+constexpr size_t kBlobPoolBytes = 256ull << 20;
+struct BlobPool {
+  std::mutex mu;
+  std::multimap<size_t, uint8_t*> parked;        // capacity -> block
+  std::unordered_map<uint8_t*, size_t> cap_of;   // every block handed out or parked
+  size_t parked_bytes = 0;
+};
+BlobPool& blob_pool() {
+  static BlobPool* p = new BlobPool;  // (never destroyed: frees may come at exit)
+  return *p;
+}
+uint8_t* blob_alloc(size_t n) {
+  BlobPool& bp = blob_pool();
+  {
+    std::lock_guard<std::mutex> lk(bp.mu);
+    auto it = bp.parked.lower_bound(n);
+    if (it != bp.parked.end() && it->first <= 4 * n + (1 << 20)) {  // (no huge block for a small blob)
+      uint8_t* b = it->second;
+      bp.parked_bytes -= it->first;
+      bp.parked.erase(it);
+      return b;
+    }
+  }
+  const size_t cap = std::max<size_t>((n + (n >> 2) + 4095) & ~(size_t)4095, 64 << 10);
+  uint8_t* b = nullptr;
+  if (hipHostMalloc((void**)&b, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(bp.mu);
+  bp.cap_of[b] = cap;
+  return b;
+}
+void blob_release(uint8_t* b) {
+  BlobPool& bp = blob_pool();
+  std::unique_lock<std::mutex> lk(bp.mu);
+  auto it = bp.cap_of.find(b);
+  if (it == bp.cap_of.end()) return;  // (not a blob of this library)
+  const size_t cap = it->second;
+  bp.parked.emplace(cap, b);
+  bp.parked_bytes += cap;
+  std::vector<uint8_t*> drop;
+  while (bp.parked_bytes > kBlobPoolBytes && !bp.parked.empty()) {  // the largest go first
+    auto last = std::prev(bp.parked.end());
+    bp.parked_bytes -= last->first;
+    drop.push_back(last->second);
+    bp.cap_of.erase(last->second);
+    bp.parked.erase(last);
+  }
+  lk.unlock();
+  for (uint8_t* d : drop) (void)hipHostFree(d);
+}
+
 int export_part(tsg_engine* e, const tsg_ruleset* rs, const ScanParams& P, uint64_t n_hits, const SplitIo& sp) {
   hipStream_t s = e->stream;
   const uint64_t base = sp.text_base;
@@ -6980,8 +7157,8 @@ int export_part(tsg_engine* e, const tsg_ruleset* rs, const ScanParams& P, uint6
                      0, s, K);
   HIP_TRY(hipGetLastError());
   // one D2H of the packed buffer into page-locked memory (the blob itself)
-  uint8_t* blob = nullptr;
-  if (hipHostMalloc((void**)&blob, sizeof(PartHeader) + cap, hipHostMallocDefault) != hipSuccess) {
+  uint8_t* blob = blob_alloc(sizeof(PartHeader) + cap);
+  if (!blob) {
     set_last_error("hipHostMalloc failed for a part blob");
     return TSG_ERR_DEVICE;
   }
@@ -6990,7 +7167,7 @@ int export_part(tsg_engine* e, const tsg_ruleset* rs, const ScanParams& P, uint6
   if (he == hipSuccess) he = hipMemcpyAsync(&flags, e->file_flags.p, 4, hipMemcpyDeviceToHost, s);
   if (he == hipSuccess) he = hipStreamSynchronize(s);
   if (he != hipSuccess) {  // the blob is not handed out: free it here
-    (void)hipHostFree(blob);
+    blob_release(blob);
     set_last_error(std::string("HIP error in export_part: ") + hipGetErrorString(he));
     return TSG_ERR_DEVICE;
   }
@@ -7145,7 +7322,8 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   // here.
   const bool path_gates = nf && (im.n_gpath || rs->any_path_rules);
   const bool merge_mode = sp && sp->mode == 2;
-  const bool gate_on_side = path_gates && !merge_mode && nbytes > 0;
+  bool gate_on_side = path_gates && !merge_mode && nbytes > 0;
+  if (experiment_env("TSG_GATE_MAIN")) gate_on_side = false;  // (A/B: the gate before the scan, on the main stream)
   GateParams G{};
   uint32_t gate_blocks = 0;
   if (path_gates) {
@@ -7215,10 +7393,15 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   HIP_TRY(e->nl_blocks.ensure(n_nlb));
   HIP_TRY(e->nl_pre.ensure(n_nlb));
   P.nl_blocks = e->nl_blocks.p;
+  // the scan counts the newlines of big files' spans itself (span_scan_counted)
+  e->nl_big = kNlBig;
+  if (const char* v = experiment_env("TSG_NL_BIG")) e->nl_big = strtoull(v, nullptr, 10);  // (A/B; 0 = all lazy)
+  P.nl_big = e->nl_big;
   const bool merge = sp && sp->mode == 2;
   // newline counts: counted lazily after the locations (k_nl_spans), except
-  // for a part scan, whose blob exports its range's counts
-  e->nl_lazy = !(sp && sp->mode == 1);
+  // for a part scan, whose blob exports its range's counts, and a batch of
+  // one file the scan would count anyway (span_scan_counted: every span)
+  e->nl_lazy = !(sp && sp->mode == 1) && !(nf == 1 && e->nl_big && nbytes > e->nl_big);
   e->nl_deferred = false;
   if (e->nl_pending) {  // (an earlier call ended before its lines stage: its side count must not overlap this one)
     HIP_TRY(hipStreamWaitEvent(s, e->ev_nl[1], 0));
@@ -7344,6 +7527,17 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     cand_cap = n_cands;
   }
   HIP_TRY(hipEventRecord(e->ev[3], s));
+  const bool nl_early = experiment_env("TSG_NL_EARLY") != nullptr;  // (A/B: the count under the candidate sort too)
+  if (e->nl_deferred && n_cands && nl_early) {
+    HIP_TRY(hipEventRecord(e->ev_nl[0], s));
+    HIP_TRY(hipStreamWaitEvent(e->side, e->ev_nl[0], 0));
+    const uint64_t n_spans = (nbytes + kNlBlock - 1) / kNlBlock;
+    hipLaunchKernelGGL(k_nl_spans, dim3((uint32_t)((n_spans + 255) / 256)), dim3(256), 0, e->side, d_data, nbytes, d_off,
+                       e->region_file.p, nbytes / kNlBlock + 1, nf, e->nl_last.p, e->nl_blocks.p, 0u, e->nl_big);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(e->ev_nl[1], e->side));
+    e->nl_pending = true;
+  }
   // ---- 4. sort by (rule, position) and segment into jobs
   uint32_t n_jobs = 0;
   if (n_cands) {
@@ -7370,7 +7564,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(hipcub::DeviceSelect::Flagged(e->cub_tmp.p, tmp2, cnt, e->flags8.p, e->job_start.p, e->nsel.p,
                                           (int)n_cands, s));
   }
-  if (e->nl_deferred && n_cands) {
+  if (e->nl_deferred && n_cands && !nl_early) {
     // phase-0 newline counts of the candidate files on the side stream, under
     // the verify (the reach comes from k_expand / k_full_jobs).  Not under the
     // candidate sort: the count's blocks starved its short kernels (0.09 ->
@@ -7382,7 +7576,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     if (const char* v = experiment_env("TSG_NL_BLOCKS_PER_CU"))  // (A/B: a thinner phase-0 grid under k_verify)
       nl_blocks0 = std::min<uint32_t>(nl_blocks0, std::max(1, atoi(v)) * std::max(1u, e->num_cus));
     hipLaunchKernelGGL(k_nl_spans, dim3(nl_blocks0), dim3(256), 0, e->side, d_data, nbytes, d_off,
-                       e->region_file.p, nbytes / kNlBlock + 1, nf, e->nl_last.p, e->nl_blocks.p, 0u);
+                       e->region_file.p, nbytes / kNlBlock + 1, nf, e->nl_last.p, e->nl_blocks.p, 0u, e->nl_big);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(e->ev_nl[1], e->side));
     e->nl_pending = true;
@@ -7800,7 +7994,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
       hipLaunchKernelGGL(k_nl_tail, dim3((nf + 255) / 256), dim3(256), 0, s, d_off, nf, e->nl_blocks.p, n_spans,
                          e->nl_last.p);
       hipLaunchKernelGGL(k_nl_spans, dim3(span_blocks), dim3(256), 0, s, d_data, nbytes, d_off, e->region_file.p,
-                         nbytes / kNlBlock + 1, nf, e->nl_last.p, e->nl_blocks.p, 1u);
+                         nbytes / kNlBlock + 1, nf, e->nl_last.p, e->nl_blocks.p, 1u, e->nl_big);
       HIP_TRY(hipGetLastError());
     }
     size_t tmp = 0;
@@ -8107,7 +8301,7 @@ int tsg_scan_part_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_
 }
 
 void tsg_part_free(uint8_t* blob) {
-  if (blob) (void)hipHostFree(blob);
+  if (blob) blob_release(blob);
 }
 
 static int scan_merge_impl(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_file, uint64_t file_len,
