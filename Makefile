@@ -36,7 +36,7 @@ $(BUILD)/%.o: $(SRC_DIR)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJS) -lamdhip64
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJS) -lamdhip64 -lhsa-runtime64
 
 # ablation build for tools/*.sh A/B runs (TSG_LIB_VARIANT=exp selects it in
 # trivy_amd/_native.py): dead kernel shapes + getenv switches, some of which
@@ -55,7 +55,7 @@ build_exp/%.o: $(SRC_DIR)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -DTSG_EXPERIMENTS -c $< -o $@
 
 $(EXP_LIB): $(EXP_OBJS)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(EXP_OBJS) -lamdhip64
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(EXP_OBJS) -lamdhip64 -lhsa-runtime64
 
 clean:
 	rm -rf $(BUILD) build_exp $(LIB) $(BENCH_LIB) $(GEN_LIB) $(EXP_LIB)

@@ -776,10 +776,10 @@ def main():
     st = [ctypes.c_uint32() for _ in range(4)]
     fast = ctypes.c_int()
     N.check(N.lib.tsg_ruleset_stats(rs, *[ctypes.byref(x) for x in st], ctypes.byref(fast)))
-    # k_scan_fast when the automaton fits its LDS image, else k_scan_big (the
+    # k_scan_fast when the automaton fits its LDS image, else k_scan_lines (the
     # configs[4] automaton: dense + sparse rows in LDS); both are bracketed by
     # the engine's HIP events (timings[17])
-    scan_kernel = "k_scan_fast" if fast.value else "k_scan_big"
+    scan_kernel = "k_scan_fast" if fast.value else "k_scan_lines"
     gate_words = (len(sc.rules) + 31) // 32
     gates = (ctypes.c_uint32 * (c["n_files"] * gate_words))() if args.config == 1 else None
 
@@ -1014,7 +1014,8 @@ def main():
                                "scan_kernels"], stage)}),
             "counts": None if args.config == 1 else dict(zip(
                 ["hits", "candidates", "jobs", "locs", "event_overflow", "events", "outputs", "verify_deferred"],
-                [int(v) for v in stage[8:15] + stage[23:24]])),
+                [int(v) for v in stage[8:15] + stage[23:24]]),
+                **({"arena_bytes": int(stage[24]), "match_bytes": int(stage[25])} if len(stage) > 25 else {})),
             "host_ms": {"call_wall": round(stage[15], 3), "post": round(stage[16], 3),
                         **({"pack": round(stage[18], 3), "h2d": round(stage[19], 3)}
                            if len(stage) > 19 and args.config in (0, 3) else {}),

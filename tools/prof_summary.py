@@ -88,11 +88,11 @@ def main(src, dst):
     # per-launch HBM read traffic of the scan kernel, for bench.py's roofline
     alg = os.environ.get("PROF_ALG_BYTES")
     for k, e in out.items():
-        if k.startswith(("k_scan_fast", "k_scan_big")) and "hbm_read_bytes_corrected" in e and alg:
+        if k.startswith(("k_scan_fast", "k_scan_big", "k_scan_lines")) and "hbm_read_bytes_corrected" in e and alg:
             t = {"kernel": k, "hbm_read_bytes_per_launch": e["hbm_read_bytes_corrected"],
                  "algorithmic_bytes_per_launch": int(alg), "source": os.path.join(dst, "pmc_summary.json"),
                  "note": "FETCH_SIZE KiB x 1024 x 2 (gfx950: FETCH_SIZE reports half of a 16 B/lane stream)"}
-            name = "k_scan_big" if k.startswith("k_scan_big") else "k_scan_fast"
+            name = k.split("<")[0]
             json.dump(t, open(os.path.join(os.path.dirname(dst.rstrip("/")), f"traffic_{name}.json"), "w"), indent=1)
     for k, e in sorted(out.items()):
         print(k, {c: round(v, 3) for c, v in e.items()})

@@ -333,18 +333,25 @@ constexpr uint32_t kMaxCap = 64;  // capture slots of a SecretGroupName rule's r
 // records shared by the device and the host copy of a result.
 constexpr uint32_t kCodeLines = 4;  // Code window: lines [StartLine - 2, EndLine + 2), EndLine == StartLine
 
+// FindRec::m_off / c_off: bit 62 set = an offset into the dense files'
+// region (ResultImpl::dense), else into the string arena (strs).
+constexpr uint64_t kArenaDense = 1ull << 62;
+
+// One finding: the location, its Match window and its Code lines.  The Code
+// lines [StartLine - 2, EndLine + 2) (EndLine == StartLine: a censored secret
+// holds no newline) are consecutive in the arena: in the dense region the
+// file's own bytes ('\n' between lines), else distinct-line segments in
+// (file, line start) order, adjacent with no separator.  So line k starts at
+// c_off + sum of the earlier lines' lengths (+ 1 each in the dense region),
+// its Number is first + k + 1 with first = max(StartLine - 3, 0), and it is
+// the cause line (IsCause, FirstCause, LastCause) iff that is StartLine.
 struct FindRec {
   uint32_t file, rule, line, n_lines;  // line = StartLine = EndLine (1-based, censored buffer)
   uint64_t start, end;                 // the kept location
-  uint64_t m_src, m_off;               // match window: file-relative source start / arena offset
-  uint32_t m_len, loc;                 // its length / index of the location (its line records)
+  uint64_t m_off, c_off;               // arena offsets: Match window, first Code line
+  uint32_t m_len, loc;                 // Match length / index of the location
   uint32_t rank, pad;                  // RuleDev::id_rank of the rule
-};
-
-struct CodeRec {
-  uint64_t off;          // arena offset of the line's text
-  uint32_t len;
-  uint32_t number_flags;  // Number | flags << 29: 1 IsCause, 2 FirstCause, 4 LastCause
+  uint32_t c_len[kCodeLines];          // Code line lengths
 };
 
 // Page-locked host blocks for the findings' string arena, recycled across
@@ -384,14 +391,24 @@ struct ResultImpl {
   View<uint32_t> ties;        // findings equal to their predecessor in (file, RuleID, Match prefix)
   size_t ties_cap = 0, ctrl_off = 0;  // (the block also holds a copy of the device counters)
   View<FindRec> frec;
-  View<CodeRec> code;  // kCodeLines per location, indexed by FindRec::loc
   const char* strs = nullptr;
   std::shared_ptr<PinnedBlock> arena;
+  // the censored contents of the dense files (build_findings_dev), copied
+  // back early in a block of their own: arena offsets with kArenaDense set
+  // point here (arena_at)
+  const char* dense = nullptr;
+  std::shared_ptr<PinnedBlock> dense_block;
   mutable std::mutex fmu;     // tsg_result_findings materialises a file's views once
   mutable std::unordered_map<uint32_t, std::pair<std::vector<tsg_finding>, std::vector<tsg_line>>> fcache;
   std::vector<double> timings;
   bool have_findings = false;
 };
+}  // namespace tsg
+
+namespace tsg {
+inline const char* arena_at(const ResultImpl& R, uint64_t off) {
+  return (off & kArenaDense) ? R.dense + (off & ~kArenaDense) : R.strs + off;
+}
 }  // namespace tsg
 
 struct tsg_result {

@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 
 #include <hipcub/hipcub.hpp>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -111,6 +113,10 @@ struct Ctrl {
   unsigned long long n_caps_run; // matches whose secret group k_group_runs cuts by byte runs
   unsigned long long n_defer;    // jobs k_verify_fast handed to k_verify_slow
   unsigned long long n_match;    // matches k_verify_fast found (k_allow's list)
+  unsigned long long match_bytes;  // the Match windows' share of find_bytes (diagnostics)
+  unsigned long long dense_bytes;  // the dense files' region (k_dense_at) ...
+  unsigned long long dense_groups; // ... and the location file groups (dense or not) ...
+  unsigned long long sparse_locs;  // ... and the locations outside dense files (their Code slots are sorted)
 };
 
 struct DevLoc {
@@ -4377,7 +4383,6 @@ struct FindParams {
   uint64_t* iv;        // merged censor intervals, 2 u64 per slot, at the group's slots
   uint2* grp;          // per location: (first slot of its file group, intervals in it)
   FindRec* rec;
-  CodeRec* code;       // kCodeLines per location (slot = location * kCodeLines + k)
   uint64_t* line_key;  // per code slot: file << kKeyPosBits | line start (~0: unused slot); sorted with slot ids
   uint32_t* line_slot;
   uint32_t* line_head; // per sorted slot: 1 at the first slot of each distinct line, then its inclusive prefix
@@ -4401,6 +4406,8 @@ struct FindParams {
   uint32_t* sort_idx;
   uint32_t rank_bits;  // bits of RuleDev::id_rank: sort key = file << rank_bits | rank
   Ctrl* ctrl;
+  const uint64_t* dense_at;  // per location: its file's offset in the dense region, ~0 (sparse); may be null
+  const uint32_t* slot_base; // with dense_at: per sparse location its index among them (its line keys' place)
 };
 
 // Wave-wide scans (inclusive) over the 64 lanes.
@@ -4678,7 +4685,9 @@ __device__ inline int64_t censor_holder_near(const uint64_t* iv, uint32_t g0, ui
 __device__ inline uint4 ld16_guard(const uint8_t* data, uint64_t p, uint64_t end) {
   if (p + 16 <= end) return *(const uint4*)(data + p);
   uint32_t w[4] = {0, 0, 0, 0};
-  for (uint32_t k = 0; k < 16 && p + k < end; ++k) w[k >> 2] |= (uint32_t)data[p + k] << (8 * (k & 3));
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k)  // (unrolled: constant indices, no scratch)
+    if (p + k < end) w[k >> 2] |= (uint32_t)data[p + k] << (8 * (k & 3));
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
@@ -4796,6 +4805,154 @@ __device__ uint64_t cens_line_begin(const FindParams& F, uint64_t fs, uint32_t g
   return 0;
 }
 
+// Dense files: a file with at most kDenseBytesPerLoc bytes per kept location
+// (configs[4]'s stress files: a rule instance every ~4 lines, so the 4-line
+// Code windows cover every line) goes into the arena WHOLE, censored, in a
+// region of its own: its Code lines and Match windows are offsets into it
+// (kArenaDense), no per-line segments.  The region is known once k_censor has
+// merged the intervals, so it is filled and copied back on the side stream
+// under k_find_spans and the rest of the findings stage, instead of after the
+// arena fill (the results' ~200 MB of D2H were configs[4]'s critical path).
+constexpr uint64_t kDenseBytesPerLoc = 384;
+constexpr uint32_t kDenseLaneBytes = 256;  // k_dense_fill: bytes per lane step (one group search each)
+
+__global__ void k_dense_heads(FindParams F, uint32_t* head) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < F.n_locs) head[w] = (w == 0 || F.locs[w].file != F.locs[w - 1].file) ? 1u : 0u;
+}
+// gid: inclusive prefix of the heads (1-based group of each location)
+__global__ void k_dense_groups(FindParams F, const uint32_t* gid, uint32_t* gstart) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < F.n_locs && (w == 0 || gid[w] != gid[w - 1])) gstart[gid[w] - 1] = (uint32_t)w;
+}
+__global__ void k_dense_size(FindParams F, const uint32_t* gid, const uint32_t* gstart, uint64_t* dsize) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t G = gid[F.n_locs - 1];
+  if (g >= G) return;  // (the rest stay 0: memset)
+  const uint64_t s0 = gstart[g], s1 = g + 1 < G ? gstart[g + 1] : F.n_locs;
+  const uint32_t file = F.locs[s0].file;
+  const uint64_t bytes = F.off[file + 1] - 1 - F.off[file];
+  dsize[g] = bytes && bytes <= kDenseBytesPerLoc * (s1 - s0) ? (bytes + 15) & ~15ull : 0;  // (16-byte aligned files)
+}
+__global__ void k_dense_at(FindParams F, const uint32_t* gid, const uint64_t* dsize, const uint64_t* doff,
+                           uint64_t* dense_at) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= F.n_locs) return;
+  const uint32_t g = gid[w] - 1;
+  dense_at[w] = dsize[g] ? doff[g] : ~0ull;
+  if (w == 0) {
+    F.ctrl->dense_bytes = doff[F.n_locs - 1] + dsize[F.n_locs - 1];
+    F.ctrl->dense_groups = gid[F.n_locs - 1];
+  }
+}
+
+// Locations outside dense files: flags for their exclusive prefix (their
+// Code slots' keys are packed at 4 x that index, so the distinct-line sort
+// takes only theirs), and the total.
+__global__ void k_dense_sparse_flags(FindParams F, const uint64_t* dense_at, uint32_t* flag) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < F.n_locs) flag[w] = dense_at[w] == ~0ull ? 1u : 0u;
+}
+__global__ void k_dense_sparse_total(FindParams F, const uint32_t* flag, const uint32_t* idx) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) F.ctrl->sparse_locs = (uint64_t)idx[F.n_locs - 1] + flag[F.n_locs - 1];
+}
+
+// Per location: file << 40 | its end (0 for a location k_censor skips); an
+// inclusive max-scan makes it the running maximum end within the file (files
+// ascend in the high bits), i.e. the censored bytes' union up to it.
+constexpr uint32_t kPmaxShift = 40;
+__global__ void k_dense_pmax_keys(FindParams F, uint64_t* keys) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= F.n_locs) return;
+  const DevLoc& L = F.locs[w];
+  keys[w] = ((uint64_t)L.file << kPmaxShift) | (L.flags ? 0ull : L.end);
+}
+
+// The dense region: kDenseLaneBytes per lane step, the file group by binary
+// search over the G group offsets, 16 bytes at a time.  A byte is censored
+// ('*') iff some valid location [start, end) of its file holds it -- the
+// union k_censor merges (censorLocation, scanner.go:454-462): the running
+// maximum end of the locations starting at or before the chunk (pmax) and
+// the locations starting inside it.  Needs only the sorted locations, so it
+// runs before k_lines / k_censor.
+__global__ __launch_bounds__(256) void k_dense_fill(FindParams F, const uint32_t* gstart, const uint64_t* dsize,
+                                                    const uint64_t* doff, const uint64_t* pmax, uint32_t G,
+                                                    uint64_t total, uint8_t* out) {
+  constexpr uint64_t kEndMask = (1ull << kPmaxShift) - 1;
+  for (uint64_t a0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kDenseLaneBytes; a0 < total;
+       a0 += (uint64_t)gridDim.x * blockDim.x * kDenseLaneBytes) {
+    uint32_t lo = 0, hi = G;  // the last group with doff <= a0 (non-empty: it holds byte a0)
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (doff[mid] <= a0) lo = mid;
+      else hi = mid;
+    }
+    uint32_t g = lo;
+    uint64_t gend = 0, fbase = 0, x0 = 0, s0 = 0, s1 = 0, k = 0;
+    bool fresh = true;
+    for (uint64_t a = a0; a < a0 + kDenseLaneBytes && a < total; a += 16) {
+      if (!fresh && a >= gend) {
+        do ++g;
+        while (g < G && doff[g] + dsize[g] <= a);
+        fresh = true;
+      }
+      const uint64_t x = a - (fresh ? doff[g] : x0);  // file-relative
+      if (fresh) {
+        fresh = false;
+        gend = doff[g] + dsize[g];
+        x0 = doff[g];
+        s0 = gstart[g];
+        s1 = g + 1 < G ? gstart[g + 1] : F.n_locs;
+        fbase = F.off[F.locs[s0].file];
+        uint64_t l2 = s0, h2 = s1;  // k = the first location starting after x
+        while (l2 < h2) {
+          const uint64_t mid = (l2 + h2) >> 1;
+          if (F.locs[mid].start <= x) l2 = mid + 1;
+          else h2 = mid;
+        }
+        k = l2;
+      }
+      while (k < s1 && F.locs[k].start <= x) ++k;
+      // bytes before the running maximum end of the locations starting <= x
+      const uint64_t cover = k > s0 ? (pmax[k - 1] & kEndMask) : 0;
+      uint32_t cmask = cover > x ? (cover >= x + 16 ? 0xFFFFu : (1u << (uint32_t)(cover - x)) - 1u) : 0u;
+      for (uint64_t j = k; j < s1; ++j) {  // the locations starting inside the chunk
+        const DevLoc& L = F.locs[j];
+        if (L.start >= x + 16) break;
+        if (L.flags || L.end <= L.start) continue;
+        const uint32_t b = (uint32_t)(L.start - x), e2 = L.end < x + 16 ? (uint32_t)(L.end - x) : 16u;
+        cmask |= ((1u << (e2 - b)) - 1u) << b;
+      }
+      const uint64_t src = fbase + x;
+      const uint64_t b0 = src & ~15ull;
+      const uint32_t sh = (uint32_t)(src - b0);
+      const uint4 u = ld16_guard(F.data, b0, F.data_end);
+      uint32_t r[4] = {u.x, u.y, u.z, u.w};
+      if (sh) {
+        const uint4 v = ld16_guard(F.data, b0 + 16, F.data_end);
+        const uint32_t d[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+        const uint32_t q = sh >> 2, bs = 8 * (sh & 3);
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+          const uint32_t lo32 = q == 0 ? d[z] : q == 1 ? d[z + 1] : q == 2 ? d[z + 2] : d[z + 3];
+          const uint32_t hi32 = q == 0 ? d[z + 1] : q == 1 ? d[z + 2] : q == 2 ? d[z + 3] : d[z + 4];
+          r[z] = bs ? (lo32 >> bs) | (hi32 << (32 - bs)) : lo32;
+        }
+      }
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        const uint32_t m4 = (cmask >> (4 * z)) & 0xFu;
+        const uint32_t bm = ((m4 & 1u) ? 0xFFu : 0u) | ((m4 & 2u) ? 0xFF00u : 0u) | ((m4 & 4u) ? 0xFF0000u : 0u) |
+                            ((m4 & 8u) ? 0xFF000000u : 0u);
+        r[z] = (r[z] & ~bm) | (0x2A2A2A2Au & bm);  // '*'
+      }
+      *(uint4*)(out + a) = make_uint4(r[0], r[1], r[2], r[3]);
+    }
+  }
+}
+
+constexpr uint64_t kMatchInLine = 1ull << 63, kMatchInLineOff = (1ull << 48) - 1;  // FindRec::m_off before k_find_finalize
+
 // One wave per location: the Match window and Code line spans.
 __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
   const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -4810,6 +4967,10 @@ __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
   r.loc = (uint32_t)w;
   const uint64_t fs = F.off[L.file];
   const uint64_t n = F.off[L.file + 1] - 1 - fs;
+  const uint64_t dz = F.dense_at ? F.dense_at[w] : ~0ull;  // the file's place in the dense region
+  // where this location's line keys go: its slots, or packed among the sparse locations'
+  const uint64_t kb = F.dense_at ? (uint64_t)F.slot_base[w] * kCodeLines : w * kCodeLines;
+  uint64_t m_src = 0;  // the Match window's file-relative start
   if (!L.flags && L.start <= L.end && L.end <= n) {
     const uint2 g = F.grp[w];
     // match window (scanner.go:484-502)
@@ -4824,40 +4985,44 @@ __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
       ls = L.start >= 30 ? L.start - 30 : 0;
       le = L.end + 20 > n ? n : L.end + 20;
     }
-    r.m_src = ls;
+    m_src = ls;
     r.m_len = (uint32_t)(le - ls);
     // code lines (scanner.go:505-534), 0-based numbers [sl - 2, el + 2)
     const uint32_t sl = L.start_line - 1, el = L.end_line - 1;
     const uint32_t cs = sl >= 2 ? sl - 2 : 0, ce = el + 2;
     uint64_t p = ls0;
     for (uint32_t cur = sl; cur > cs && p > 0; --cur) p = cens_line_begin(F, fs, g.x, g.y, h, p - 1, lane);
-    uint32_t k = 0;
-    bool found_first = false;
-    for (uint32_t ln = cs; ln < ce && p <= n && k < kCodeLines; ++ln, ++k) {
+    uint32_t nk = 0, kc = kCodeLines;  // kc: the Code slot of the line [ls0, le0)
+#pragma unroll
+    for (uint32_t k = 0; k < kCodeLines; ++k) {  // (unrolled: c_len stays in registers)
+      if (cs + k >= ce || p > n) break;
+      if (p == ls0) kc = k;
       const uint64_t q = p == ls0 ? le0 : cens_next_nl(F, fs, n, g.x, g.y, h, p, lane);
-      const bool cause = ln >= sl && ln <= el;
-      if (lane == 0) {
-        CodeRec c{};
-        c.len = (uint32_t)(q - p);
-        const uint32_t flags = (cause ? 1u : 0u) | (cause && !found_first ? 2u : 0u) | (cause && ln == el ? 4u : 0u);
-        c.number_flags = (ln + 1) | (flags << 29);
-        F.code[w * kCodeLines + k] = c;
-        F.line_key[w * kCodeLines + k] = ((uint64_t)L.file << kKeyPosBits) | p;
-      }
-      found_first = found_first || cause;
+      r.c_len[k] = (uint32_t)(q - p);
+      if (k == 0 && dz != ~0ull) r.c_off = kArenaDense | (dz + p);  // (final: no line segments)
+      if (lane == 0 && dz == ~0ull) F.line_key[kb + k] = ((uint64_t)L.file << kKeyPosBits) | p;
       p = q + 1;
+      nk = k + 1;
     }
-    r.n_lines = k;
+    r.n_lines = nk;
     r.line = L.start_line;
+    // a Match window inside the line holding the start (always when that
+    // line is <= 100 bytes: then it IS the line) is that Code line's text:
+    // no segment of its own, k_find_finalize points it into the line's
+    // (configs[4]: most Match bytes, all of them PCIe D2H)
+    if (dz != ~0ull) r.m_off = kArenaDense | (dz + ls);
+    else if (kc < kCodeLines && ls >= ls0 && le <= le0) r.m_off = kMatchInLine | ((uint64_t)kc << 48) | (ls - ls0);
   }
   if (lane == 0) {
     F.rec[w] = r;
-    for (uint32_t k = r.n_lines; k < kCodeLines; ++k) F.line_key[w * kCodeLines + k] = ~0ull;
-    for (uint32_t k = 0; k < kCodeLines; ++k) F.line_slot[w * kCodeLines + k] = (uint32_t)(w * kCodeLines + k);
+    if (dz == ~0ull) {  // (a dense file's lines are offsets into its region: no keys)
+      for (uint32_t k = r.n_lines; k < kCodeLines; ++k) F.line_key[kb + k] = ~0ull;
+      for (uint32_t k = 0; k < kCodeLines; ++k) F.line_slot[kb + k] = (uint32_t)(w * kCodeLines + k);
+    }
     F.seg_file[w] = r.file;
     F.seg_grp[w] = F.grp[w];
-    F.seg_src[w] = r.m_src;
-    F.seg_len[w] = r.m_len;
+    F.seg_src[w] = m_src;
+    F.seg_len[w] = (r.m_off & (kMatchInLine | kArenaDense)) ? 0 : r.m_len;
   }
 }
 
@@ -4878,14 +5043,16 @@ __global__ void k_line_map(FindParams F, const uint64_t* keys, const uint32_t* s
     const uint64_t sg = F.n_locs + uid;
     F.seg_file[sg] = (uint32_t)(keys[i] >> kKeyPosBits);
     F.seg_src[sg] = keys[i] & kKeyPosMask;
-    F.seg_len[sg] = F.code[slot].len;
+    F.seg_len[sg] = F.rec[slot / kCodeLines].c_len[slot % kCodeLines];
     F.seg_grp[sg] = F.grp[slot / kCodeLines];
   }
 }
 
 __global__ void k_seg_total(FindParams F) {
-  if (threadIdx.x == 0 && blockIdx.x == 0)
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
     F.ctrl->find_bytes = F.seg_off[F.n_seg_cap - 1] + F.seg_len[F.n_seg_cap - 1];
+    F.ctrl->match_bytes = F.n_locs < F.n_seg_cap ? F.seg_off[F.n_locs] : F.ctrl->find_bytes;
+  }
 }
 
 // Arena granule index: a non-empty segment k records itself at the first
@@ -4996,7 +5163,23 @@ __global__ __launch_bounds__(256) void k_arena_fill(FindParams F) {
     uint64_t kk = ~0ull, fbase = 0;
     uint32_t g0 = 0, gm = 0, t = 0;  // the segment's file intervals, t = first one ending after x
     for (uint32_t j = 0; j < 16 && a + j < total; ++j) {
-      while (a + j >= F.seg_off[k] + F.seg_len[k]) ++k;  // (never past the last non-empty segment)
+      if (a + j >= F.seg_off[k] + F.seg_len[k]) {
+        // the next segment holding byte a + j: galloping then binary search --
+        // runs of empty segments (Match windows kept inside their lines, blank
+        // lines) can be 10^5 long, one dependent load each when walked
+        uint64_t lo = k, d = 1;
+        while (lo + d < F.n_seg_cap && F.seg_off[lo + d] <= a + j) {
+          lo += d;
+          d <<= 1;
+        }
+        uint64_t hi = lo + d < F.n_seg_cap ? lo + d : F.n_seg_cap;  // seg_off[hi] > a + j (or the end)
+        while (hi - lo > 1) {
+          const uint64_t mid = (lo + hi) >> 1;
+          if (F.seg_off[mid] <= a + j) lo = mid;
+          else hi = mid;
+        }
+        k = lo;  // the last segment starting at or before a + j: non-empty (it covers a + j)
+      }
       const uint64_t x = F.seg_src[k] + (a + j - F.seg_off[k]);  // file-relative
       if (k != kk) {  // a new segment: its intervals and the first one ending after x (binary search)
         kk = k;
@@ -5029,9 +5212,12 @@ __global__ void k_find_finalize(FindParams F) {
   const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= F.n_locs) return;
   FindRec& r = F.rec[w];
-  r.m_off = F.seg_off[w];
-  for (uint32_t k = 0; k < r.n_lines; ++k)
-    F.code[w * kCodeLines + k].off = F.seg_off[F.n_locs + F.line_uid[w * kCodeLines + k]];
+  if (r.m_off & kMatchInLine)  // (k_find_spans: the Match window inside Code slot kc's line, at offset d)
+    r.m_off = F.seg_off[F.n_locs + F.line_uid[w * kCodeLines + ((r.m_off >> 48) & 0xFF)]] + (r.m_off & kMatchInLineOff);
+  else if (!(r.m_off & kArenaDense))
+    r.m_off = F.seg_off[w];
+  if (r.n_lines && !(r.c_off & kArenaDense))  // (the window's lines are adjacent segments: consecutive line ids)
+    r.c_off = F.seg_off[F.n_locs + F.line_uid[w * kCodeLines]];
   const uint32_t rank = F.rules[r.rule].id_rank;
   r.rank = rank;
   F.sort_key[w] = ((uint64_t)r.file << F.rank_bits) | rank;
@@ -5049,14 +5235,15 @@ __global__ void k_find_gather(const FindRec* in, const uint32_t* idx, uint64_t n
 // the host only breaks ties of equal prefixes.  (8 bytes left 19 k ties on
 // configs[4] -- lines opening with the same assignment -- and 2.7 ms of host
 // sorting.)
-__global__ void k_match_prefix(const FindRec* rec, const uint8_t* arena, uint64_t n, uint64_t* key, uint64_t* key_b,
-                               uint32_t* idx) {
+__global__ void k_match_prefix(const FindRec* rec, const uint8_t* arena, const uint8_t* dense, uint64_t n,
+                               uint64_t* key, uint64_t* key_b, uint32_t* idx) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const FindRec& r = rec[i];
+  const uint8_t* m = (r.m_off & kArenaDense) ? dense + (r.m_off & ~kArenaDense) : arena + r.m_off;
   uint64_t k = 0, kb = 0;
-  for (uint32_t j = 0; j < 8; ++j) k = (k << 8) | (j < r.m_len ? arena[r.m_off + j] : 0u);
-  for (uint32_t j = 8; j < 16; ++j) kb = (kb << 8) | (j < r.m_len ? arena[r.m_off + j] : 0u);
+  for (uint32_t j = 0; j < 8; ++j) k = (k << 8) | (j < r.m_len ? m[j] : 0u);
+  for (uint32_t j = 8; j < 16; ++j) kb = (kb << 8) | (j < r.m_len ? m[j] : 0u);
   key[i] = k;
   key_b[i] = kb;
   idx[i] = (uint32_t)i;
@@ -5631,10 +5818,22 @@ struct tsg_engine {
   DBuf<FindRec> f_rec, f_rec2;
   DBuf<uint32_t> f_ties;   // k_tie_list
   DBuf<tsg_loc> out_locs;  // k_out_locs
-  DBuf<CodeRec> f_code;
   DBuf<uint8_t> f_arena;
   DBuf<uint32_t> f_gran, f_gcarry;  // arena granule index (k_arena_gran_*)
   DBuf<uint64_t> f_lkeyb;            // Match bytes 8..15 (k_match_prefix)
+  // dense files' region of the arena (k_dense_*): per file group its size and
+  // offset, per location its file's offset; the censored contents
+  DBuf<uint64_t> f_dsize, f_doff, f_dense_at;
+  DBuf<uint32_t> f_gstart;
+  DBuf<uint8_t> f_dense;
+  uint64_t* h_dense = nullptr;  // page-locked: the region's bytes and file groups, read mid-pipeline
+  hipEvent_t ev_dense = nullptr, ev_dfill = nullptr, ev_frec = nullptr;
+  bool dense_active = false;   // this call's locations have dense_at (dense_begin)
+  DBuf<uint64_t> f_pmax;       // per location: (file << 40 | max end so far in its file), k_dense_fill's censoring
+  DBuf<uint32_t> f_spidx;      // per location: exclusive prefix of the sparse ones (FindParams::slot_base)
+  uint64_t n_line_slots = 0;   // Code slots the distinct-line sort takes (4 per sparse location)
+  hsa_signal_t dma_sig{0};  // dma_d2h's completion signal
+  bool dma_pending = false;
   std::shared_ptr<PinnedPool> pinned = std::make_shared<PinnedPool>();
 };
 
@@ -6247,12 +6446,67 @@ hipError_t ensure_side(tsg_engine* e) {
   if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_code, hipEventDisableTiming);
   if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_fill, hipEventDisableTiming);
   if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_side, hipEventDisableTiming);
+  if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_dense, hipEventDisableTiming);
+  if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_dfill, hipEventDisableTiming);
+  if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_frec, hipEventDisableTiming);
   if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_nl[0], hipEventDisableTiming);
   if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_nl[1], hipEventDisableTiming);
   if (r == hipSuccess) r = hipEventCreate(&e->ev_pg[0]);  // (timed: the path gate's stage time)
   if (r == hipSuccess) r = hipEventCreate(&e->ev_pg[1]);
   return r;
 }
+
+// D2H on a DMA engine (hsa_amd_memory_async_copy), ordered by the caller
+// (the source is complete when it is issued).  hipMemcpyAsync runs a D2H into
+// page-locked memory as blit kernels on the CUs: the ~200 MB dense region's
+// copy beside k_find_spans made that kernel 1.9 -> 5.8 ms (profiles/r05i).
+// false: not issued (the caller copies with hipMemcpyAsync).
+hsa_status_t find_cpu_agent(hsa_agent_t a, void* out) {
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+    *(hsa_agent_t*)out = a;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+bool dma_d2h(tsg_engine* e, void* dst, const void* src, size_t n) {
+  if (experiment_env("TSG_DMA_OFF")) return false;  // (A/B: blit copies)
+  static hsa_agent_t cpu{0};
+  static std::once_flag once;
+  std::call_once(once, [] { (void)hsa_iterate_agents(find_cpu_agent, &cpu); });
+  if (!cpu.handle) return false;
+  if (!e->dma_sig.handle && hsa_signal_create(1, 0, nullptr, &e->dma_sig) != HSA_STATUS_SUCCESS) return false;
+  hsa_amd_pointer_info_t pd{};
+  pd.size = sizeof(pd);
+  if (hsa_amd_pointer_info(src, &pd, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+      pd.type == HSA_EXT_POINTER_TYPE_UNKNOWN)
+    return false;
+  // one signal counts the call's copies down (each completion subtracts 1)
+  if (e->dma_pending) hsa_signal_add_screlease(e->dma_sig, 1);
+  else hsa_signal_store_screlease(e->dma_sig, 1);
+  if (hsa_amd_memory_async_copy(dst, cpu, src, pd.agentOwner, n, 0, nullptr, e->dma_sig) != HSA_STATUS_SUCCESS) {
+    if (e->dma_pending) hsa_signal_subtract_screlease(e->dma_sig, 1);
+    return false;
+  }
+  e->dma_pending = true;
+  return true;
+}
+// Waits for the call's dma_d2h copies (every exit of a call that issued one).
+int dma_wait(tsg_engine* e) {
+  if (!e->dma_pending) return TSG_OK;
+  const hsa_signal_value_t v =
+      hsa_signal_wait_scacquire(e->dma_sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+  e->dma_pending = false;
+  if (v < 0) {
+    set_last_error("a DMA copy of the findings failed");
+    return TSG_ERR_DEVICE;
+  }
+  return TSG_OK;
+}
+struct DmaGuard {  // (the copy's destination belongs to the result: never outlive the call)
+  tsg_engine* e;
+  ~DmaGuard() { (void)dma_wait(e); }
+};
 
 int read_ctrl(tsg_engine* e, Ctrl* h) {
   HIP_TRY(hipMemcpyAsync(h, e->ctrl.p, sizeof(Ctrl), hipMemcpyDeviceToHost, e->stream));
@@ -6574,6 +6828,107 @@ int launch_uni_keywords(tsg_engine* e, const ScanParams& P) {
   return TSG_OK;
 }
 
+// ---- the dense files' region (k_dense_*), started right after the
+// location sort: dense_begin sizes it on the device (no host wait);
+// dense_issue -- after k_lines is enqueued -- reads the size, fills the region
+// on the side stream and hands its D2H to a DMA engine, so ~200 MB of
+// configs[4] results cross PCIe under k_lines, k_censor and k_find_spans.
+int dense_begin(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_off, uint64_t nbytes, uint64_t n_locs) {
+  e->dense_active = false;
+  if (!n_locs || experiment_env("TSG_DENSE_OFF")) return TSG_OK;  // (A/B)
+  hipStream_t s = e->stream;
+  HIP_TRY(ensure_side(e));
+  const uint64_t n_slots = (uint64_t)kCodeLines * n_locs;
+  HIP_TRY(e->f_dsize.ensure(n_locs));
+  HIP_TRY(e->f_doff.ensure(n_locs));
+  HIP_TRY(e->f_dense_at.ensure(n_locs));
+  HIP_TRY(e->f_gstart.ensure(n_locs));
+  HIP_TRY(e->f_pmax.ensure(n_locs));
+  HIP_TRY(e->f_lhead.ensure(n_slots));  // (build_findings_dev's sizes: no reallocation under the side fill)
+  HIP_TRY(e->f_lscan.ensure(n_slots));
+  HIP_TRY(e->f_lkey.ensure(n_slots));
+  if (!e->h_dense) HIP_TRY(hipHostMalloc((void**)&e->h_dense, 64, hipHostMallocDefault));
+  FindParams F{};
+  F.data = d_data;
+  F.data_end = nbytes;
+  F.off = d_off;
+  F.locs = e->locs2.p;
+  F.n_locs = n_locs;
+  F.ctrl = e->ctrl.p;
+  const uint32_t lane_blocks = (uint32_t)((n_locs + 255) / 256);
+  // heads -> 1-based group ids
+  hipLaunchKernelGGL(k_dense_heads, dim3(lane_blocks), dim3(256), 0, s, F, e->f_lhead.p);
+  size_t tmp = 0;
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, e->f_lhead.p, e->f_lscan.p, (int)n_locs, s));
+  HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(e->cub_tmp.p, tmp, e->f_lhead.p, e->f_lscan.p, (int)n_locs, s));
+  HIP_TRY(hipMemsetAsync(e->f_dsize.p, 0, n_locs * 8, s));
+  hipLaunchKernelGGL(k_dense_groups, dim3(lane_blocks), dim3(256), 0, s, F, e->f_lscan.p, e->f_gstart.p);
+  hipLaunchKernelGGL(k_dense_size, dim3(lane_blocks), dim3(256), 0, s, F, e->f_lscan.p, e->f_gstart.p, e->f_dsize.p);
+  tmp = 0;
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->f_dsize.p, e->f_doff.p, (int)n_locs, s));
+  HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(e->cub_tmp.p, tmp, e->f_dsize.p, e->f_doff.p, (int)n_locs, s));
+  hipLaunchKernelGGL(k_dense_at, dim3(lane_blocks), dim3(256), 0, s, F, e->f_lscan.p, e->f_dsize.p, e->f_doff.p,
+                     e->f_dense_at.p);
+  // the sparse locations' packed index (f_lhead is free again: the group ids are in f_lscan)
+  HIP_TRY(e->f_spidx.ensure(n_locs));
+  hipLaunchKernelGGL(k_dense_sparse_flags, dim3(lane_blocks), dim3(256), 0, s, F, e->f_dense_at.p, e->f_lhead.p);
+  tmp = 0;
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->f_lhead.p, e->f_spidx.p, (int)n_locs, s));
+  HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+  HIP_TRY(hipcub::DeviceScan::ExclusiveSum(e->cub_tmp.p, tmp, e->f_lhead.p, e->f_spidx.p, (int)n_locs, s));
+  hipLaunchKernelGGL(k_dense_sparse_total, dim3(1), dim3(64), 0, s, F, e->f_lhead.p, e->f_spidx.p);
+  // the censor cover: running maximum end per file
+  hipLaunchKernelGGL(k_dense_pmax_keys, dim3(lane_blocks), dim3(256), 0, s, F, e->f_lkey.p);
+  tmp = 0;
+  HIP_TRY(hipcub::DeviceScan::InclusiveScan(nullptr, tmp, e->f_lkey.p, e->f_pmax.p, hipcub::Max(), (int)n_locs, s));
+  HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+  HIP_TRY(hipcub::DeviceScan::InclusiveScan(e->cub_tmp.p, tmp, e->f_lkey.p, e->f_pmax.p, hipcub::Max(), (int)n_locs, s));
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(e->h_dense, &e->ctrl.p->dense_bytes, 24, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipEventRecord(e->ev_dense, s));
+  e->dense_active = true;
+  return TSG_OK;
+}
+
+int dense_issue(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_off, uint64_t nbytes, uint64_t n_locs,
+                tsg_result* res) {
+  if (!e->dense_active) return TSG_OK;
+  auto& R = res->impl;
+  HIP_TRY(hipEventSynchronize(e->ev_dense));  // (k_file_base / k_lines are queued behind it)
+  const uint64_t dense_bytes = e->h_dense[0];
+  const uint32_t groups = (uint32_t)e->h_dense[1];
+  e->n_line_slots = (uint64_t)kCodeLines * e->h_dense[2];
+  if (!dense_bytes) return TSG_OK;
+  R.dense_block = pinned_get(e->pinned, dense_bytes);
+  if (!R.dense_block) {
+    set_last_error("hipHostMalloc failed for the findings' dense region");
+    return TSG_ERR_DEVICE;
+  }
+  R.dense = (const char*)R.dense_block->p;
+  HIP_TRY(e->f_dense.ensure(dense_bytes));
+  FindParams F{};
+  F.data = d_data;
+  F.data_end = nbytes;
+  F.off = d_off;
+  F.locs = e->locs2.p;
+  F.n_locs = n_locs;
+  HIP_TRY(hipStreamWaitEvent(e->side, e->ev_dense, 0));
+  const uint64_t lanes = (dense_bytes + kDenseLaneBytes - 1) / kDenseLaneBytes;
+  hipLaunchKernelGGL(k_dense_fill, dim3((uint32_t)std::min<uint64_t>((lanes + 255) / 256, 4096)), dim3(256), 0,
+                     e->side, F, e->f_gstart.p, e->f_dsize.p, e->f_doff.p, e->f_pmax.p, groups, dense_bytes,
+                     e->f_dense.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(e->ev_dfill, e->side));  // (k_match_prefix reads the region)
+  // the copy on a DMA engine once the fill is done (k_lines and the findings
+  // kernels keep the CUs meanwhile), else on the side stream
+  HIP_TRY(hipEventSynchronize(e->ev_dfill));
+  if (!dma_d2h(e, (void*)R.dense, e->f_dense.p, dense_bytes))
+    HIP_TRY(hipMemcpyAsync((void*)R.dense, e->f_dense.p, dense_bytes, hipMemcpyDeviceToHost, e->side));
+  return TSG_OK;
+}
+
 // Findings of the sorted kept locations (e->locs2): k_censor, k_find_spans,
 // the arena prefix, k_find_copy, the (file, RuleID rank) order; the records
 // and the string arena come back with the caller's final synchronisation.
@@ -6585,7 +6940,6 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   HIP_TRY(e->f_grp.ensure(n_locs));
   HIP_TRY(e->f_rec.ensure(n_locs));
   HIP_TRY(e->f_rec2.ensure(n_locs));
-  HIP_TRY(e->f_code.ensure(n_slots));
   HIP_TRY(e->f_lkey.ensure(n_slots));
   HIP_TRY(e->f_lkey2.ensure(n_slots));
   HIP_TRY(e->f_lslot.ensure(n_slots));
@@ -6611,7 +6965,6 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   F.iv = e->f_iv.p;
   F.grp = e->f_grp.p;
   F.rec = e->f_rec.p;
-  F.code = e->f_code.p;
   F.line_key = e->f_lkey.p;
   F.line_slot = e->f_lslot.p;
   F.line_head = e->f_lhead.p;
@@ -6630,27 +6983,36 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   int key_bits = (int)F.rank_bits + 1;
   while (key_bits < 64 && (1ull << (key_bits - F.rank_bits)) <= n_files) ++key_bits;
   const uint32_t lane_blocks = (uint32_t)((n_locs + 255) / 256), wave_blocks = (uint32_t)((n_locs * 64 + 255) / 256);
-  const uint32_t slot_blocks = (uint32_t)((n_slots + 255) / 256);
   HIP_TRY(hipMemsetAsync(e->f_slen.p, 0, n_seg * 8, s));  // unused line segments stay empty
   hipLaunchKernelGGL(k_censor, dim3(wave_blocks), dim3(256), 0, s, F);
   if (n_locs >= kCensorBig)
     hipLaunchKernelGGL(k_censor_big, dim3((uint32_t)((n_locs + kCensorBig - 1) / kCensorBig)), dim3(1024), 0, s, F);
+  // the dense files' region: sizes and offsets now (k_dense_*), filled and
+  // copied back on the side stream while k_find_spans runs
+  auto& R = res->impl;
+  HIP_TRY(ensure_side(e));
+  F.dense_at = e->dense_active ? e->f_dense_at.p : nullptr;  // (dense_begin / dense_issue)
+  F.slot_base = e->dense_active ? e->f_spidx.p : nullptr;
+  const uint64_t n_lslots = e->dense_active ? e->n_line_slots : n_slots;  // the sparse locations' slots
+  const uint32_t lslot_blocks = (uint32_t)std::max<uint64_t>((n_lslots + 255) / 256, 1);
   hipLaunchKernelGGL(k_find_spans, dim3(wave_blocks), dim3(256), 0, s, F);
   HIP_TRY(hipGetLastError());
   // distinct Code lines: sort the slots by (file, line start), number the runs
   size_t tmp = 0;
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p, e->f_lslot2.p,
-                                             (int)n_slots, 0, 64, s));
-  HIP_TRY(e->cub_tmp.ensure(tmp + 1));
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p,
-                                             e->f_lslot2.p, (int)n_slots, 0, 64, s));
-  hipLaunchKernelGGL(k_line_heads, dim3(slot_blocks), dim3(256), 0, s, e->f_lkey2.p, n_slots, e->f_lhead.p);
-  tmp = 0;
-  HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, e->f_lhead.p, e->f_lscan.p, (int)n_slots, s));
-  HIP_TRY(e->cub_tmp.ensure(tmp + 1));
-  HIP_TRY(hipcub::DeviceScan::InclusiveSum(e->cub_tmp.p, tmp, e->f_lhead.p, e->f_lscan.p, (int)n_slots, s));
-  hipLaunchKernelGGL(k_line_map, dim3(slot_blocks), dim3(256), 0, s, F, e->f_lkey2.p, e->f_lslot2.p, e->f_lscan.p,
-                     e->f_lhead.p, n_slots);
+  if (n_lslots) {
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p, e->f_lslot2.p,
+                                               (int)n_lslots, 0, 64, s));
+    HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p,
+                                               e->f_lslot2.p, (int)n_lslots, 0, 64, s));
+    hipLaunchKernelGGL(k_line_heads, dim3(lslot_blocks), dim3(256), 0, s, e->f_lkey2.p, n_lslots, e->f_lhead.p);
+    tmp = 0;
+    HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, e->f_lhead.p, e->f_lscan.p, (int)n_lslots, s));
+    HIP_TRY(e->cub_tmp.ensure(tmp + 1));
+    HIP_TRY(hipcub::DeviceScan::InclusiveSum(e->cub_tmp.p, tmp, e->f_lhead.p, e->f_lscan.p, (int)n_lslots, s));
+    hipLaunchKernelGGL(k_line_map, dim3(lslot_blocks), dim3(256), 0, s, F, e->f_lkey2.p, e->f_lslot2.p, e->f_lscan.p,
+                       e->f_lhead.p, n_lslots);
+  }
   // arena offsets of the segments (Match windows, then distinct lines)
   tmp = 0;
   HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, e->f_slen.p, e->f_soff.p, (int)n_seg, s));
@@ -6661,6 +7023,10 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   HIP_TRY(hipGetLastError());
   Ctrl c;
   if (int rc = read_ctrl(e, &c)) return rc;  // the arena size
+  if (res->impl.timings.size() > 25) {
+    res->impl.timings[24] = (double)c.find_bytes;
+    res->impl.timings[25] = (double)c.match_bytes;
+  }
   HIP_TRY(e->f_arena.ensure(c.find_bytes + 16));
   F.arena = e->f_arena.p;
   F.n_gran = c.find_bytes / kArenaGran + 2;
@@ -6673,10 +7039,9 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   // kept locations are final already: their D2H starts on a side stream under
   // the arena fill; the string arena's (most of the bytes) follows it there,
   // under the Match sorts
-  auto& R = res->impl;
   const uint64_t tie_cap = std::max<uint64_t>(1024, n_locs / 8);
-  const size_t rec_bytes = n_locs * sizeof(FindRec), code_bytes = n_slots * sizeof(CodeRec);
-  const size_t o_locs = (rec_bytes + code_bytes + c.find_bytes + 15) & ~(size_t)15;
+  const size_t rec_bytes = n_locs * sizeof(FindRec);
+  const size_t o_locs = (rec_bytes + c.find_bytes + 15) & ~(size_t)15;
   const size_t o_flags = o_locs + n_locs * sizeof(tsg_loc);
   const size_t o_ties = (o_flags + n_files + 15) & ~(size_t)15;
   const size_t o_ctrl = (o_ties + tie_cap * 4 + 15) & ~(size_t)15;
@@ -6687,21 +7052,27 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   }
   uint8_t* base = (uint8_t*)R.arena->p;
   R.frec = {(FindRec*)base, n_locs};
-  R.code = {(CodeRec*)(base + rec_bytes), n_slots};
-  R.strs = (const char*)(base + rec_bytes + code_bytes);
+  R.strs = (const char*)(base + rec_bytes);
   R.locs = {(tsg_loc*)(base + o_locs), n_locs};
   R.file_flags = {base + o_flags, n_files};
   R.ties = {(uint32_t*)(base + o_ties), 0};
   R.ctrl_off = o_ctrl;
-  HIP_TRY(ensure_side(e));
   // the kept locations as tsg_loc records
   HIP_TRY(e->out_locs.ensure(n_locs));
   hipLaunchKernelGGL(k_out_locs, dim3(lane_blocks), dim3(256), 0, s, e->locs2.p, n_locs, e->out_locs.p, e->ctrl.p);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(e->ev_code, s));
-  HIP_TRY(hipStreamWaitEvent(e->side, e->ev_code, 0));
-  HIP_TRY(hipMemcpyAsync(R.code.p, e->f_code.p, code_bytes, hipMemcpyDeviceToHost, e->side));
-  HIP_TRY(hipMemcpyAsync(R.locs.p, e->out_locs.p, n_locs * sizeof(tsg_loc), hipMemcpyDeviceToHost, e->side));
+  // The kept locations and the string arena go back on a DMA engine
+  // (dma_d2h) once their producers are done -- issued after the rest of the
+  // stage is enqueued, so the sorts below keep the CUs; without it as
+  // blit-kernel copies (hipMemcpyAsync) on the side stream.  (hipMemcpyAsync
+  // with hipMemcpyDeviceToDeviceNoCU into the page-locked block still ran as
+  // blit kernels, profiles/r05h_c4.)
+  const bool use_dma = experiment_env("TSG_DMA_OFF") == nullptr;
+  if (!use_dma) {
+    HIP_TRY(hipStreamWaitEvent(e->side, e->ev_code, 0));
+    HIP_TRY(hipMemcpyAsync(R.locs.p, e->out_locs.p, n_locs * sizeof(tsg_loc), hipMemcpyDeviceToHost, e->side));
+  }
   if (c.find_bytes) {
     HIP_TRY(hipMemsetAsync(F.gran_seg, 0, F.n_gran * 4, s));
     hipLaunchKernelGGL(k_arena_gran_mark, dim3((uint32_t)((n_seg + 255) / 256)), dim3(256), 0, s, F);
@@ -6712,15 +7083,18 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(e->ev_fill, s));
-  HIP_TRY(hipStreamWaitEvent(e->side, e->ev_fill, 0));
-  if (c.find_bytes)
-    HIP_TRY(hipMemcpyAsync(base + rec_bytes + code_bytes, e->f_arena.p, c.find_bytes, hipMemcpyDeviceToHost, e->side));
+  if (!use_dma) {
+    HIP_TRY(hipStreamWaitEvent(e->side, e->ev_fill, 0));
+    if (c.find_bytes)
+      HIP_TRY(hipMemcpyAsync(base + rec_bytes, e->f_arena.p, c.find_bytes, hipMemcpyDeviceToHost, e->side));
+  }
   HIP_TRY(hipEventRecord(e->ev_side, e->side));
   // order: (file, RuleID rank) major, Match prefix minor -- two stable radix
   // sorts, least significant key first (f_lkey / f_lkey2 / f_lslot* are free now)
   HIP_TRY(e->f_lkeyb.ensure(n_locs));
-  hipLaunchKernelGGL(k_match_prefix, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->f_arena.p, n_locs, e->f_lkey.p,
-                     e->f_lkeyb.p, e->f_lslot.p);
+  if (R.dense) HIP_TRY(hipStreamWaitEvent(s, e->ev_dfill, 0));  // (the Match windows of dense files)
+  hipLaunchKernelGGL(k_match_prefix, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->f_arena.p, e->f_dense.p,
+                     n_locs, e->f_lkey.p, e->f_lkeyb.p, e->f_lslot.p);
   size_t tmp2 = 0;
   HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p, e->f_lslot2.p,
                                              (int)n_locs, 0, 64, s));
@@ -6743,9 +7117,27 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   hipLaunchKernelGGL(k_tie_list, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lkey.p, e->f_lkeyb.p, e->vals2.p,
                      n_locs, e->f_ties.p, tie_cap, e->ctrl.p);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(R.frec.p, e->f_rec2.p, rec_bytes, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(R.ties.p, e->f_ties.p, tie_cap * 4, hipMemcpyDeviceToHost, s));
+  if (!use_dma) {
+    HIP_TRY(hipMemcpyAsync(R.frec.p, e->f_rec2.p, rec_bytes, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(R.ties.p, e->f_ties.p, tie_cap * 4, hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(hipEventRecord(e->ev_frec, s));
   HIP_TRY(hipStreamWaitEvent(s, e->ev_side, 0));  // the caller's final synchronisation covers the side copies
+  if (use_dma) {  // (run_pipeline waits for the DMA copies with its final synchronisation)
+    HIP_TRY(hipEventSynchronize(e->ev_code));
+    if (!dma_d2h(e, R.locs.p, e->out_locs.p, n_locs * sizeof(tsg_loc)))
+      HIP_TRY(hipMemcpyAsync(R.locs.p, e->out_locs.p, n_locs * sizeof(tsg_loc), hipMemcpyDeviceToHost, s));
+    if (c.find_bytes) {
+      HIP_TRY(hipEventSynchronize(e->ev_fill));
+      if (!dma_d2h(e, base + rec_bytes, e->f_arena.p, c.find_bytes))
+        HIP_TRY(hipMemcpyAsync(base + rec_bytes, e->f_arena.p, c.find_bytes, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(hipEventSynchronize(e->ev_frec));  // the ordered records and the tie list
+    if (!dma_d2h(e, R.frec.p, e->f_rec2.p, rec_bytes))
+      HIP_TRY(hipMemcpyAsync(R.frec.p, e->f_rec2.p, rec_bytes, hipMemcpyDeviceToHost, s));
+    if (!dma_d2h(e, R.ties.p, e->f_ties.p, tie_cap * 4))
+      HIP_TRY(hipMemcpyAsync(R.ties.p, e->f_ties.p, tie_cap * 4, hipMemcpyDeviceToHost, s));
+  }
   R.ties_cap = tie_cap;
   return TSG_OK;
 }
@@ -6755,9 +7147,8 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
 // only runs with an equal (file, RuleID) are ordered here, by Match and then
 // (rule, start, end) -- the order the reference's matches arrive in.
 void order_finding_ties(ResultImpl& R, bool all_runs) {
-  const uint8_t* A = (const uint8_t*)R.strs;
   auto less = [&](const FindRec& x, const FindRec& y) {
-    const int c = memcmp(A + x.m_off, A + y.m_off, std::min(x.m_len, y.m_len));
+    const int c = memcmp(arena_at(R, x.m_off), arena_at(R, y.m_off), std::min(x.m_len, y.m_len));
     if (c != 0) return c < 0;
     if (x.m_len != y.m_len) return x.m_len < y.m_len;
     if (x.rule != y.rule) return x.rule < y.rule;
@@ -7281,7 +7672,9 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
                  const uint8_t* d_paths, const uint64_t* d_path_off, size_t n_files, uint64_t nbytes,
                  tsg_result* res, const SplitIo* sp = nullptr) {
   const auto wall0 = std::chrono::steady_clock::now();
+  DmaGuard dma_guard{e};
   e->fast_timed = false;
+  e->dense_active = false;
   int rc = upload_ruleset(e, rs);
   if (rc) return rc;
   const DevImage& im = e->img;
@@ -7309,7 +7702,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   }
   HIP_TRY(e->scratch.ensure((size_t)e->vm_threads * e->scratch_stride));
   std::vector<double>& tm = res->impl.timings;
-  tm.assign(24, 0.0);  // [18..22]: tsg_analyze's host stages, [23]: jobs k_verify_fast deferred
+  tm.assign(26, 0.0);  // [18..22]: tsg_analyze's host stages, [23]: jobs k_verify_fast deferred, [24..25] arena bytes
   if (!e->events) {
     for (auto& ev : e->ev) HIP_TRY(hipEventCreate(&ev));
     e->events = true;
@@ -8017,12 +8410,17 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
                                                (int)n_locs, 0, 64, s));
     hipLaunchKernelGGL(k_loc_gather, dim3((uint32_t)((n_locs + 255) / 256)), dim3(256), 0, s, e->locs.p,
                        e->vals2.p, n_locs, e->locs2.p);
+    if ((rc = dense_begin(e, d_data, d_off, nbytes, n_locs))) return rc;
     HIP_TRY(e->fbase.ensure(nf + 1));
     hipLaunchKernelGGL(k_file_base, dim3((uint32_t)((n_locs * 64 + 255) / 256)), dim3(256), 0, s, d_data, d_off,
                        e->nl_pre.p, e->locs2.p, n_locs, e->fbase.p);
     hipLaunchKernelGGL(k_lines, dim3((uint32_t)((n_locs * 64 + 255) / 256)), dim3(256), 0, s, d_data, d_off,
                        e->nl_pre.p, e->fbase.p, e->locs2.p, n_locs);
     HIP_TRY(hipGetLastError());
+    if ((rc = dense_issue(e, d_data, d_off, nbytes, n_locs, res))) {
+      if (e->side) (void)hipStreamSynchronize(e->side);
+      return rc;
+    }
     // ---- 8. findings (censored lines, Match, Code, order) on the device
     if ((rc = build_findings_dev(e, d_data, d_off, nbytes, nf, n_locs, res))) {
       if (e->side) (void)hipStreamSynchronize(e->side);  // no side copy may outlive the result block
@@ -8050,6 +8448,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   Ctrl* hc = (Ctrl*)((uint8_t*)R.arena->p + R.ctrl_off);
   HIP_TRY(hipMemcpyAsync(hc, e->ctrl.p, sizeof(Ctrl), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  if ((rc = dma_wait(e))) return rc;
   const auto wall1 = std::chrono::steady_clock::now();
   for (int k = 0; k < 7; ++k) {
     float ms = 0;
@@ -8182,9 +8581,16 @@ void tsg_engine_free(tsg_engine* e) {
   e->f_iv.release(); e->f_lkey.release(); e->f_lkey2.release(); e->f_ssrc.release(); e->f_slen.release();
   e->f_soff.release(); e->f_lslot.release(); e->f_lslot2.release(); e->f_lhead.release(); e->f_lscan.release();
   e->f_luid.release(); e->f_sfile.release(); e->f_sgrp.release(); e->f_grp.release();
-  e->f_rec.release(); e->f_rec2.release(); e->f_code.release(); e->f_arena.release();
+  e->f_rec.release(); e->f_rec2.release(); e->f_arena.release();
   e->f_gran.release(); e->f_gcarry.release(); e->big_outs.release(); e->f_lkeyb.release();
   e->f_ties.release(); e->out_locs.release();
+  e->f_dsize.release(); e->f_doff.release(); e->f_dense_at.release(); e->f_gstart.release(); e->f_dense.release();
+  e->f_pmax.release(); e->f_spidx.release();
+  if (e->h_dense) (void)hipHostFree(e->h_dense);
+  if (e->dma_sig.handle) {
+    (void)dma_wait(e);
+    (void)hsa_signal_destroy(e->dma_sig);
+  }
   if (e->events)
     for (auto& ev : e->ev) (void)hipEventDestroy(ev);
   if (e->side) {
@@ -8192,6 +8598,9 @@ void tsg_engine_free(tsg_engine* e) {
     (void)hipEventDestroy(e->ev_code);
     (void)hipEventDestroy(e->ev_fill);
     (void)hipEventDestroy(e->ev_side);
+    (void)hipEventDestroy(e->ev_dense);
+    (void)hipEventDestroy(e->ev_dfill);
+    (void)hipEventDestroy(e->ev_frec);
     (void)hipEventDestroy(e->ev_nl[0]);
     (void)hipEventDestroy(e->ev_nl[1]);
     (void)hipEventDestroy(e->ev_pg[0]);
@@ -8899,7 +9308,6 @@ size_t tsg_result_findings(const tsg_result* r, size_t file, const tsg_finding**
   auto it = R.fcache.find((uint32_t)file);
   if (it == R.fcache.end()) {  // views into the result's string arena, built once per file
     auto& slot = R.fcache[(uint32_t)file];
-    const char* A = R.strs;
     size_t nl = 0;
     for (auto q = lo; q != hi; ++q) nl += q->n_lines;
     slot.second.reserve(nl);
@@ -8909,21 +9317,26 @@ size_t tsg_result_findings(const tsg_result* r, size_t file, const tsg_finding**
       fd.rule = q->rule;
       fd.start_line = q->line;
       fd.end_line = q->line;
-      fd.match = A + q->m_off;
+      fd.match = arena_at(R, q->m_off);
       fd.match_len = q->m_len;
       fd.start = q->start;
       fd.end = q->end;
       fd.n_lines = q->n_lines;
+      // (FindRec: lines [first, first + n_lines), consecutive in the arena)
+      const uint32_t first = q->line >= 3 ? q->line - 3 : 0;
+      const uint64_t sep = (q->c_off & kArenaDense) ? 1 : 0;
+      uint64_t off = q->c_off;
       for (uint32_t k = 0; k < q->n_lines; ++k) {
-        const CodeRec& c = R.code[(size_t)q->loc * kCodeLines + k];
         tsg_line tl{};
-        tl.number = c.number_flags & 0x1FFFFFFFu;
-        tl.content = A + c.off;
-        tl.content_len = c.len;
-        tl.is_cause = (c.number_flags >> 29) & 1;
-        tl.first_cause = (c.number_flags >> 30) & 1;
-        tl.last_cause = (c.number_flags >> 31) & 1;
+        tl.number = first + k + 1;
+        tl.content = arena_at(R, off);
+        tl.content_len = q->c_len[k];
+        const bool cause = tl.number == q->line;
+        tl.is_cause = cause;
+        tl.first_cause = cause;
+        tl.last_cause = cause;
         slot.second.push_back(tl);
+        off += q->c_len[k] + sep;
       }
       slot.first.push_back(fd);
     }
