@@ -345,13 +345,12 @@ constexpr uint64_t kArenaDense = 1ull << 62;
 // c_off + sum of the earlier lines' lengths (+ 1 each in the dense region),
 // its Number is first + k + 1 with first = max(StartLine - 3, 0), and it is
 // the cause line (IsCause, FirstCause, LastCause) iff that is StartLine.
+// (The rule, start and end are the location's: ResultImpl::locs[loc].)
 struct FindRec {
-  uint32_t file, rule, line, n_lines;  // line = StartLine = EndLine (1-based, censored buffer)
-  uint64_t start, end;                 // the kept location
-  uint64_t m_off, c_off;               // arena offsets: Match window, first Code line
-  uint32_t m_len, loc;                 // Match length / index of the location
-  uint32_t rank, pad;                  // RuleDev::id_rank of the rule
-  uint32_t c_len[kCodeLines];          // Code line lengths
+  uint32_t file, line, n_lines, loc;  // line = StartLine = EndLine (1-based, censored buffer); loc: its location
+  uint64_t m_off, c_off;              // arena offsets: Match window, first Code line
+  uint32_t m_len, rank;               // Match length / RuleDev::id_rank of the rule
+  uint32_t c_len[kCodeLines];         // Code line lengths
 };
 
 // Page-locked host blocks for the findings' string arena, recycled across

@@ -4961,9 +4961,6 @@ __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
   const DevLoc L = F.locs[w];
   FindRec r{};
   r.file = L.file;
-  r.rule = L.rule;
-  r.start = L.start;
-  r.end = L.end;
   r.loc = (uint32_t)w;
   const uint64_t fs = F.off[L.file];
   const uint64_t n = F.off[L.file + 1] - 1 - fs;
@@ -5218,7 +5215,7 @@ __global__ void k_find_finalize(FindParams F) {
     r.m_off = F.seg_off[w];
   if (r.n_lines && !(r.c_off & kArenaDense))  // (the window's lines are adjacent segments: consecutive line ids)
     r.c_off = F.seg_off[F.n_locs + F.line_uid[w * kCodeLines]];
-  const uint32_t rank = F.rules[r.rule].id_rank;
+  const uint32_t rank = F.rules[F.locs[w].rule].id_rank;
   r.rank = rank;
   F.sort_key[w] = ((uint64_t)r.file << F.rank_bits) | rank;
   F.sort_idx[w] = (uint32_t)w;
@@ -7151,9 +7148,10 @@ void order_finding_ties(ResultImpl& R, bool all_runs) {
     const int c = memcmp(arena_at(R, x.m_off), arena_at(R, y.m_off), std::min(x.m_len, y.m_len));
     if (c != 0) return c < 0;
     if (x.m_len != y.m_len) return x.m_len < y.m_len;
-    if (x.rule != y.rule) return x.rule < y.rule;
-    if (x.start != y.start) return x.start < y.start;
-    return x.end < y.end;
+    const tsg_loc &a = R.locs[x.loc], &b = R.locs[y.loc];
+    if (a.rule != b.rule) return a.rule < b.rule;
+    if (a.start != b.start) return a.start < b.start;
+    return a.end < b.end;
   };
   // the device ordered (file, RuleID, Match prefix); runs of equal
   // (file, RuleID, prefix) -- the positions k_tie_list flagged, each equal to
@@ -7181,6 +7179,22 @@ void order_finding_ties(ResultImpl& R, bool all_runs) {
       k = q;
     }
   }
+  // the records and Match strings of the runs were just written by DMA and
+  // are cold: each batch of runs is prefetched first (records, then their
+  // strings: independent misses overlap; compared one by one they cost
+  // ~170 ns per tie, 1.4 ms for configs[4]'s 8 K ties, 0.77 ms prefetched on
+  // one thread, profiles/r05n)
+  auto prefetch = [&](size_t k0, size_t k1) {
+    for (size_t k = k0; k < k1; ++k)
+      for (size_t i = runs[k].first; i < runs[k].second; ++i) __builtin_prefetch(&R.frec[i]);
+    for (size_t k = k0; k < k1; ++k)
+      for (size_t i = runs[k].first; i < runs[k].second; ++i) {
+        const char* m = arena_at(R, R.frec[i].m_off);
+        __builtin_prefetch(m);
+        if (R.frec[i].m_len > 64) __builtin_prefetch(m + 64);
+        __builtin_prefetch(&R.locs[R.frec[i].loc]);
+      }
+  };
   auto sort_run = [&](const std::pair<size_t, size_t>& r) {
     if (r.second - r.first <= 16) {  // short runs (most): stable insertion sort, no temporary buffer
       for (size_t a = r.first + 1; a < r.second; ++a) {
@@ -7193,18 +7207,25 @@ void order_finding_ties(ResultImpl& R, bool all_runs) {
     }
     std::stable_sort(R.frec.begin() + r.first, R.frec.begin() + r.second, less);
   };
-  // (16 threads cost ~0.5 ms to start and join: below ~64 k records one
-  // thread finishes sooner -- configs[4]'s 8 k ties took 1.1 ms threaded)
-  const unsigned nt = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-  if (work < (1u << 16) || nt == 1 || runs.size() < 2) {
-    for (auto& r : runs) sort_run(r);
+  constexpr size_t kBatch = 256;  // runs per prefetch batch
+  auto batch = [&](size_t k0) {
+    const size_t k1 = std::min(runs.size(), k0 + kBatch);
+    prefetch(k0, k1);
+    for (size_t k = k0; k < k1; ++k) sort_run(runs[k]);
+  };
+  // threads: ~30 us each to start and join, so one per ~2 K records of work
+  // (at most 16; configs[4]'s 8 K ties take 4)
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const unsigned nt = (unsigned)std::min<size_t>(std::min(16u, hw), work / 2048);
+  if (nt <= 1 || runs.size() < 2 * kBatch) {
+    for (size_t k0 = 0; k0 < runs.size(); k0 += kBatch) batch(k0);
     return;
   }
   std::atomic<size_t> next{0};
   std::vector<std::thread> th;
   for (unsigned t = 0; t < nt; ++t)
     th.emplace_back([&] {
-      for (size_t k; (k = next.fetch_add(1)) < runs.size();) sort_run(runs[k]);
+      for (size_t k0; (k0 = next.fetch_add(kBatch)) < runs.size();) batch(k0);
     });
   for (auto& t : th) t.join();
 }
@@ -9314,13 +9335,14 @@ size_t tsg_result_findings(const tsg_result* r, size_t file, const tsg_finding**
     for (auto q = lo; q != hi; ++q) {
       tsg_finding fd{};
       fd.file = q->file;
-      fd.rule = q->rule;
+      const tsg_loc& lq = R.locs[q->loc];
+      fd.rule = lq.rule;
       fd.start_line = q->line;
       fd.end_line = q->line;
       fd.match = arena_at(R, q->m_off);
       fd.match_len = q->m_len;
-      fd.start = q->start;
-      fd.end = q->end;
+      fd.start = lq.start;
+      fd.end = lq.end;
       fd.n_lines = q->n_lines;
       // (FindRec: lines [first, first + n_lines), consecutive in the arena)
       const uint32_t first = q->line >= 3 ? q->line - 3 : 0;
