@@ -7729,15 +7729,14 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     e->events = true;
   }
   HIP_TRY(hipEventRecord(e->ev[0], s));
-  // ---- 1. path gates (per file).  Not overlapped with the scan (it fills
-  // every CU's VGPRs and LDS): after a scan the gate runs on the side stream
-  // beside the fold passes and the host's read of the scan counters, and
-  // the candidates wait for it; without a scan (merge, empty batch) it runs
-  // here.
+  // ---- 1. path gates (per file), before the scan on the main stream.  Not
+  // overlapped with the scan (it fills every CU's VGPRs and LDS); beside
+  // k_report on the side stream (TSG_GATE_SIDE, exp) it slowed k_report more
+  // than it saved: step 14.86 vs 14.72 ms over three alternating runs each
+  // (`profiles/r05q_gate`).
   const bool path_gates = nf && (im.n_gpath || rs->any_path_rules);
   const bool merge_mode = sp && sp->mode == 2;
-  bool gate_on_side = path_gates && !merge_mode && nbytes > 0;
-  if (experiment_env("TSG_GATE_MAIN")) gate_on_side = false;  // (A/B: the gate before the scan, on the main stream)
+  const bool gate_on_side = path_gates && !merge_mode && nbytes > 0 && experiment_env("TSG_GATE_SIDE") != nullptr;
   GateParams G{};
   uint32_t gate_blocks = 0;
   if (path_gates) {
