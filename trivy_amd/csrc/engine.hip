@@ -180,6 +180,7 @@ struct ScanParams {
   uint64_t* hits;
   uint64_t hit_cap;
   uint64_t nl_big;  // lazy newline counts: the scan counts the spans of files this big (0: none)
+  uint64_t kw_plain;  // report_event: files below this many bytes set keyword bits with plain atomics (else read first)
   // k_report: each report wave's own hit region (hit_seg_cap records at
   // hit_seg + wave * hit_seg_cap; counts in hit_seg_n), packed into `hits` by
   // k_hits_pack -- null: flushes reserve on ctrl->hits
@@ -772,7 +773,7 @@ __device__ inline void report_event(const ScanParams& P, const AcDev& ac, const 
           // for a 5.5 ms scan, profiles/r05f)
           uint32_t* wp = &P.file_kw[(size_t)fi * P.rs.kw_words + (pd.kw >> 5)];
           const uint32_t bit = 1u << (pd.kw & 31);
-          if (P.off[fi + 1] - P.off[fi] < kKwReadFirst ||
+          if (P.off[fi + 1] - P.off[fi] < P.kw_plain ||
               !(__hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit))
             atomicOr(wp, bit);
         }
@@ -7810,6 +7811,8 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   e->nl_big = kNlBig;
   if (const char* v = experiment_env("TSG_NL_BIG")) e->nl_big = strtoull(v, nullptr, 10);  // (A/B; 0 = all lazy)
   P.nl_big = e->nl_big;
+  P.kw_plain = kKwReadFirst;
+  if (const char* v = experiment_env("TSG_KW_PLAIN")) P.kw_plain = strtoull(v, nullptr, 10);  // (A/B)
   const bool merge = sp && sp->mode == 2;
   // newline counts: counted lazily after the locations (k_nl_spans), except
   // for a part scan, whose blob exports its range's counts, and a batch of
@@ -9227,6 +9230,8 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
   HIP_TRY(e->nl_blocks.ensure(n_nlb));
   HIP_TRY(hipMemsetAsync(e->nl_blocks.p, 0, n_nlb * 4, s));
   P.nl_blocks = e->nl_blocks.p;
+  P.kw_plain = kKwReadFirst;
+  if (const char* v = experiment_env("TSG_KW_PLAIN")) P.kw_plain = strtoull(v, nullptr, 10);  // (A/B)
   HIP_TRY(hipEventRecord(e->ev[8], s));
   bool scanned = nbytes == 0;
   for (int attempt = 0; attempt < 3 && !scanned; ++attempt) {
