@@ -117,6 +117,7 @@ struct Ctrl {
   unsigned long long dense_bytes;  // the dense files' region (k_dense_at) ...
   unsigned long long dense_groups; // ... and the location file groups (dense or not) ...
   unsigned long long sparse_locs;  // ... and the locations outside dense files (their Code slots are sorted)
+  unsigned long long n_long_spans; // locations k_find_spans_lane left to the wave search (long lines)
 };
 
 struct DevLoc {
@@ -4409,6 +4410,7 @@ struct FindParams {
   Ctrl* ctrl;
   const uint64_t* dense_at;  // per location: its file's offset in the dense region, ~0 (sparse); may be null
   const uint32_t* slot_base; // with dense_at: per sparse location its index among them (its line keys' place)
+  uint32_t* long_list;       // k_find_spans_lane -> k_find_spans: the locations left to the wave search (may be null)
 };
 
 // Wave-wide scans (inclusive) over the 64 lanes.
@@ -4954,11 +4956,11 @@ __global__ __launch_bounds__(256) void k_dense_fill(FindParams F, const uint32_t
 
 constexpr uint64_t kMatchInLine = 1ull << 63, kMatchInLineOff = (1ull << 48) - 1;  // FindRec::m_off before k_find_finalize
 
-// One wave per location: the Match window and Code line spans.
-__global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
-  const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t lane = threadIdx.x & 63;
-  if (w >= F.n_locs) return;
+// The Match window and Code line spans of location w (one wave, or one
+// lane, per location: `Srch` supplies the censored-buffer line searches).
+// Returns false when the searcher gave up (a lane's window): nothing written.
+template <class Srch>
+__device__ __forceinline__ bool find_spans_one(const FindParams& F, uint64_t w, bool writer, Srch& srch) {
   const DevLoc L = F.locs[w];
   FindRec r{};
   r.file = L.file;
@@ -4969,15 +4971,16 @@ __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
   // where this location's line keys go: its slots, or packed among the sparse locations'
   const uint64_t kb = F.dense_at ? (uint64_t)F.slot_base[w] * kCodeLines : w * kCodeLines;
   uint64_t m_src = 0;  // the Match window's file-relative start
+  uint64_t keys[kCodeLines] = {~0ull, ~0ull, ~0ull, ~0ull};
   if (!L.flags && L.start <= L.end && L.end <= n) {
     const uint2 g = F.grp[w];
+    srch.begin(fs, n, g.x, g.y, F.line_uid[w], L.start, L.end);  // (line_uid: the location's own interval, k_censor)
     // match window (scanner.go:484-502)
     // the (censored) line holding the start: the Match window's and the first
     // cause Code line's bounds, searched once (a search on a multi-MiB line
     // costs a binary search over the newline prefix)
-    const uint32_t h = F.line_uid[w];  // the location's own interval (k_censor)
-    const uint64_t ls0 = cens_line_begin(F, fs, g.x, g.y, h, L.start, lane);
-    const uint64_t le0 = cens_next_nl(F, fs, n, g.x, g.y, h, L.start, lane);
+    const uint64_t ls0 = srch.line_begin(L.start);
+    const uint64_t le0 = srch.next_nl(L.start);
     uint64_t ls = ls0, le = le0;
     if (le - ls > 100) {
       ls = L.start >= 30 ? L.start - 30 : 0;
@@ -4989,19 +4992,20 @@ __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
     const uint32_t sl = L.start_line - 1, el = L.end_line - 1;
     const uint32_t cs = sl >= 2 ? sl - 2 : 0, ce = el + 2;
     uint64_t p = ls0;
-    for (uint32_t cur = sl; cur > cs && p > 0; --cur) p = cens_line_begin(F, fs, g.x, g.y, h, p - 1, lane);
+    for (uint32_t cur = sl; cur > cs && p > 0; --cur) p = srch.line_begin(p - 1);
     uint32_t nk = 0, kc = kCodeLines;  // kc: the Code slot of the line [ls0, le0)
 #pragma unroll
     for (uint32_t k = 0; k < kCodeLines; ++k) {  // (unrolled: c_len stays in registers)
       if (cs + k >= ce || p > n) break;
       if (p == ls0) kc = k;
-      const uint64_t q = p == ls0 ? le0 : cens_next_nl(F, fs, n, g.x, g.y, h, p, lane);
+      const uint64_t q = p == ls0 ? le0 : srch.next_nl(p);
       r.c_len[k] = (uint32_t)(q - p);
       if (k == 0 && dz != ~0ull) r.c_off = kArenaDense | (dz + p);  // (final: no line segments)
-      if (lane == 0 && dz == ~0ull) F.line_key[kb + k] = ((uint64_t)L.file << kKeyPosBits) | p;
+      keys[k] = ((uint64_t)L.file << kKeyPosBits) | p;
       p = q + 1;
       nk = k + 1;
     }
+    if (srch.failed()) return false;
     r.n_lines = nk;
     r.line = L.start_line;
     // a Match window inside the line holding the start (always when that
@@ -5011,16 +5015,144 @@ __global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
     if (dz != ~0ull) r.m_off = kArenaDense | (dz + ls);
     else if (kc < kCodeLines && ls >= ls0 && le <= le0) r.m_off = kMatchInLine | ((uint64_t)kc << 48) | (ls - ls0);
   }
-  if (lane == 0) {
+  if (writer) {
     F.rec[w] = r;
     if (dz == ~0ull) {  // (a dense file's lines are offsets into its region: no keys)
-      for (uint32_t k = r.n_lines; k < kCodeLines; ++k) F.line_key[kb + k] = ~0ull;
-      for (uint32_t k = 0; k < kCodeLines; ++k) F.line_slot[kb + k] = (uint32_t)(w * kCodeLines + k);
+#pragma unroll
+      for (uint32_t k = 0; k < kCodeLines; ++k) {
+        F.line_key[kb + k] = k < r.n_lines ? keys[k] : ~0ull;
+        F.line_slot[kb + k] = (uint32_t)(w * kCodeLines + k);
+      }
     }
     F.seg_file[w] = r.file;
     F.seg_grp[w] = F.grp[w];
     F.seg_src[w] = m_src;
     F.seg_len[w] = (r.m_off & (kMatchInLine | kArenaDense)) ? 0 : r.m_len;
+  }
+  return true;
+}
+
+// The wave's searches: 1 KiB per wave step, 4 KiB blocks without '\n'
+// skipped by the newline prefix (any line length).
+struct WaveSrch {
+  const FindParams& F;
+  uint32_t lane;
+  uint64_t fs = 0, n = 0;
+  uint32_t g0 = 0, gm = 0, h = 0;
+  __device__ WaveSrch(const FindParams& f, uint32_t l) : F(f), lane(l) {}
+  __device__ void begin(uint64_t fs_, uint64_t n_, uint32_t g0_, uint32_t gm_, uint32_t h_, uint64_t, uint64_t) {
+    fs = fs_, n = n_, g0 = g0_, gm = gm_, h = h_;
+  }
+  __device__ __forceinline__ uint64_t line_begin(uint64_t pos) { return cens_line_begin(F, fs, g0, gm, h, pos, lane); }
+  __device__ __forceinline__ uint64_t next_nl(uint64_t from) { return cens_next_nl(F, fs, n, g0, gm, h, from, lane); }
+  __device__ bool failed() const { return false; }
+};
+
+// One lane's searches, 16 bytes per load, inside a window of kLaneSpanWin
+// bytes either side of the location (the file's ends count as found); a
+// search that would leave the window fails the location, which then goes to
+// the wave search (k_find_spans over long_list).
+constexpr uint64_t kLaneSpanWin = 512;
+struct LaneSrch {
+  const FindParams& F;
+  uint64_t fs = 0, n = 0, lo = 0, hi = 0;
+  uint32_t g0 = 0, gm = 0, h = 0;
+  bool bad = false;
+  __device__ explicit LaneSrch(const FindParams& f) : F(f) {}
+  __device__ void begin(uint64_t fs_, uint64_t n_, uint32_t g0_, uint32_t gm_, uint32_t h_, uint64_t start,
+                        uint64_t end) {
+    fs = fs_, n = n_, g0 = g0_, gm = gm_, h = h_;
+    lo = start > kLaneSpanWin ? start - kLaneSpanWin : 0;
+    hi = end + kLaneSpanWin < n ? end + kLaneSpanWin : n;
+  }
+  // last raw '\n' in [lo, b) (file-relative), or -1
+  __device__ int64_t raw_bwd(uint64_t b) {
+    while (b > lo) {
+      const uint64_t a0 = (fs + b - 1) & ~15ull;  // the 16-byte chunk holding byte b - 1
+      uint32_t m = nl_mask16(ld16_guard(F.data, a0, F.data_end));
+      const uint64_t first = a0 - fs;  // (may lie before lo or the file: masked below)
+      const uint32_t top = (uint32_t)(fs + b - a0);  // bytes of the chunk before b
+      m &= top >= 16 ? 0xFFFFu : ((1u << top) - 1u);
+      if (a0 < fs + lo) m &= ~0u << (uint32_t)(fs + lo - a0);
+      if (m) return (int64_t)(first + (31 - __builtin_clz(m)));
+      b = a0 > fs + lo ? a0 - fs : lo;
+    }
+    return -1;
+  }
+  // first raw '\n' in [a, hi), or hi
+  __device__ uint64_t raw_fwd(uint64_t a) {
+    while (a < hi) {
+      const uint64_t a0 = (fs + a) & ~15ull;
+      uint32_t m = nl_mask16(ld16_guard(F.data, a0, F.data_end));
+      m &= ~0u << (uint32_t)(fs + a - a0);
+      const uint64_t end = fs + hi;
+      if (a0 + 16 > end) m &= end > a0 ? ((1u << (uint32_t)(end - a0)) - 1u) : 0u;
+      if (m) return a0 - fs + __builtin_ctz(m);
+      a = a0 + 16 - fs;
+    }
+    return hi;
+  }
+  __device__ uint64_t line_begin(uint64_t pos) {  // cens_line_begin within [lo, ...)
+    while (pos) {
+      const int64_t i = raw_bwd(pos);
+      if (i < 0) {
+        if (lo > 0) bad = true;  // (the window ends before the file does)
+        return 0;
+      }
+      const int64_t hold = censor_holder_near(F.iv, g0, gm, (uint64_t)i, h);
+      if (hold < 0) return (uint64_t)i + 1;
+      pos = F.iv[2 * hold];
+    }
+    return 0;
+  }
+  __device__ uint64_t next_nl(uint64_t from) {  // cens_next_nl within [..., hi)
+    while (from < n) {
+      const uint64_t i = raw_fwd(from);
+      if (i >= hi) {
+        if (hi < n) bad = true;
+        return n;
+      }
+      const int64_t hold = censor_holder_near(F.iv, g0, gm, i, h);
+      if (hold < 0) return i;
+      from = F.iv[2 * hold + 1];
+    }
+    return n;
+  }
+  __device__ bool failed() const { return bad; }
+};
+
+// One lane per location; a location whose lines run past the lane's window
+// is listed for the wave search.
+__global__ __launch_bounds__(256) void k_find_spans_lane(FindParams F) {
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= F.n_locs) return;
+  // a location inside a 4 KiB block without newlines (a minified line) goes
+  // straight to the wave search (a stale count only sends it there early)
+  const DevLoc& L = F.locs[w];
+  const uint64_t blk = (F.off[L.file] + L.start) / kNlBlock;
+  LaneSrch srch(F);
+  if ((blk < F.n_nlb && F.nl_blocks[blk] == 0) || !find_spans_one(F, w, true, srch)) {
+    const unsigned long long k = atomicAdd(&F.ctrl->n_long_spans, 1ull);
+    F.long_list[k] = (uint32_t)w;
+  }
+}
+
+// One wave per location: every location (long_list null), or those
+// k_find_spans_lane listed (the count read on the device; a fixed grid).
+__global__ __launch_bounds__(256) void k_find_spans(FindParams F) {
+  const uint64_t wv = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  if (!F.long_list) {
+    if (wv >= F.n_locs) return;
+    WaveSrch srch(F, lane);
+    (void)find_spans_one(F, wv, lane == 0, srch);
+    return;
+  }
+  const uint64_t n_long = F.ctrl->n_long_spans;
+  const uint64_t n_waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  for (uint64_t i = wv; i < n_long; i += n_waves) {
+    WaveSrch srch(F, lane);
+    (void)find_spans_one(F, F.long_list[i], lane == 0, srch);
   }
 }
 
@@ -5829,6 +5961,7 @@ struct tsg_engine {
   bool dense_active = false;   // this call's locations have dense_at (dense_begin)
   DBuf<uint64_t> f_pmax;       // per location: (file << 40 | max end so far in its file), k_dense_fill's censoring
   DBuf<uint32_t> f_spidx;      // per location: exclusive prefix of the sparse ones (FindParams::slot_base)
+  DBuf<uint32_t> f_long;       // k_find_spans_lane's list of long-line locations
   uint64_t n_line_slots = 0;   // Code slots the distinct-line sort takes (4 per sparse location)
   hsa_signal_t dma_sig{0};  // dma_d2h's completion signal
   bool dma_pending = false;
@@ -6993,7 +7126,16 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   F.slot_base = e->dense_active ? e->f_spidx.p : nullptr;
   const uint64_t n_lslots = e->dense_active ? e->n_line_slots : n_slots;  // the sparse locations' slots
   const uint32_t lslot_blocks = (uint32_t)std::max<uint64_t>((n_lslots + 255) / 256, 1);
-  hipLaunchKernelGGL(k_find_spans, dim3(wave_blocks), dim3(256), 0, s, F);
+  // spans: one lane per location, the long lines' locations then one wave each
+  if (experiment_env("TSG_SPANS_WAVE")) {  // (A/B: every location one wave)
+    hipLaunchKernelGGL(k_find_spans, dim3(wave_blocks), dim3(256), 0, s, F);
+  } else {
+    HIP_TRY(e->f_long.ensure(n_locs));
+    F.long_list = e->f_long.p;
+    hipLaunchKernelGGL(k_find_spans_lane, dim3(lane_blocks), dim3(256), 0, s, F);
+    hipLaunchKernelGGL(k_find_spans, dim3(std::min<uint32_t>(wave_blocks, std::max(1u, e->num_cus) * 32)), dim3(256),
+                       0, s, F);
+  }
   HIP_TRY(hipGetLastError());
   // distinct Code lines: sort the slots by (file, line start), number the runs
   size_t tmp = 0;
@@ -8608,7 +8750,7 @@ void tsg_engine_free(tsg_engine* e) {
   e->f_gran.release(); e->f_gcarry.release(); e->big_outs.release(); e->f_lkeyb.release();
   e->f_ties.release(); e->out_locs.release();
   e->f_dsize.release(); e->f_doff.release(); e->f_dense_at.release(); e->f_gstart.release(); e->f_dense.release();
-  e->f_pmax.release(); e->f_spidx.release();
+  e->f_pmax.release(); e->f_spidx.release(); e->f_long.release();
   if (e->h_dense) (void)hipHostFree(e->h_dense);
   if (e->dma_sig.handle) {
     (void)dma_wait(e);
