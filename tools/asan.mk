@@ -17,7 +17,7 @@ LIB      = trivy_amd/libtrivy_secret_gpu_asan.so
 HDRS     = $(wildcard $(SRC_DIR)/*.h) $(wildcard include/*.h)
 
 $(LIB): $(OBJS)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -shared-libsan $(SAN) -o $@ $(OBJS) -lamdhip64
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -shared-libsan $(SAN) -o $@ $(OBJS) -lamdhip64 -lhsa-runtime64
 
 build_asan/%.o: $(SRC_DIR)/% $(HDRS)
 	@mkdir -p build_asan
