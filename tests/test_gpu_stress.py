@@ -62,8 +62,8 @@ def _pack(files):
     return _DevBuf(bytes(buf)), _DevBuf(off.tobytes())
 
 
-def _gates(sc, files):
-    eng = S.get_engine(0)
+def _gates(sc, files, eng=None):
+    eng = eng or S.get_engine(0)
     d_data, d_off = _pack(files)
     nr = len(sc.rules)
     words = (nr + 31) // 32
@@ -73,11 +73,11 @@ def _gates(sc, files):
     return [[bool((g[f, r // 32] >> (r % 32)) & 1) for r in range(nr)] for f in range(len(files))]
 
 
-def _check_gates(cfg_path, files):
+def _check_gates(cfg_path, files, eng=None):
     sc = S.new_scanner(S.parse_config(cfg_path) if cfg_path else None, device=0)
     oc = o.Scanner(o.parse_config(cfg_path) if cfg_path else None)
     assert [r.id for r in sc.rules] == [r.id for r in oc.rules]
-    got = _gates(sc, files)
+    got = _gates(sc, files, eng)
     n_pass = 0
     for (p, d), g in zip(files, got):
         low = o.go_bytes_to_lower(d)
@@ -93,6 +93,27 @@ def test_gate_device_builtin_vs_oracle():
     files += [("kelvin.txt", "K key".encode()), ("longs.txt", "ſk_live_ token".encode()),
               ("idot.txt", "İ private KEY".encode()), ("empty.txt", b""), ("nul.txt", b"\x00ghp_\x00aws")]
     assert _check_gates(None, files) > 0
+
+
+def test_gate_device_fold_overflow_retry():
+    """More K/ſ fold sequences than a fresh engine's fold-position buffer holds
+    (65536): the prefilter pass queues scan, fold windows, keyword and rule
+    gates before its one host wait, finds the lost positions there and redoes
+    the pass with grown buffers -- the gate bits must be the oracle's."""
+    eng = ctypes.c_void_p()
+    N.check(N.lib.tsg_engine_create(0, ctypes.byref(eng)))
+    try:
+        kel = "\u212a".encode()  # KELVIN SIGN: ToLower -> 'k'
+        files = [("kelvins.txt", (kel + b"ey x ") * 70_000),
+                 ("plain.txt", b"nothing here " * 100),
+                 ("longs.txt", ("\u017fk_live_ " * 20).encode()),
+                 ("mixed.txt", (kel + b"EY " + "\u017f".encode() + b"g.\n") * 2000 + b"AKIA token")]
+        files += corpus_gen.make_corpus(78, 50)
+        assert _check_gates(None, files, eng) > 0
+        # a second call on the grown engine takes the first attempt
+        assert _check_gates(None, files, eng) > 0
+    finally:
+        N.lib.tsg_engine_free(eng)
 
 
 def test_gate_device_stress_rules_vs_oracle(stress_cfg):

@@ -9374,18 +9374,58 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
   P.nl_blocks = e->nl_blocks.p;
   P.kw_plain = kKwReadFirst;
   if (const char* v = experiment_env("TSG_KW_PLAIN")) P.kw_plain = strtoull(v, nullptr, 10);  // (A/B)
+  const bool want_gates = h_gates_out && nf && gate_words_per_file;
+  const uint32_t R = (uint32_t)rs->rules.size();
+  std::vector<uint32_t> csr;
+  if (want_gates) {
+    // rule -> keyword-id CSR (host, per ruleset: not per byte), gates on the GPU
+    csr.resize(R + 1);
+    std::vector<uint32_t> ids;
+    for (uint32_t r = 0; r < R; ++r) {
+      csr[r] = (uint32_t)ids.size();
+      for (auto& k : rs->rules[r].keywords) {
+        if (k.empty()) { ids.push_back(0xFFFFFFFFu); continue; }
+        ids.push_back((uint32_t)(std::find(rs->keywords.begin(), rs->keywords.end(), k) - rs->keywords.begin()));
+      }
+    }
+    csr[R] = (uint32_t)ids.size();
+    csr.insert(csr.end(), ids.begin(), ids.end());
+    HIP_TRY(e->gate_rules.ensure(csr.size()));
+    HIP_TRY(hipMemcpyAsync(e->gate_rules.p, csr.data(), csr.size() * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(e->gate_out.ensure((size_t)nf * gate_words_per_file));
+  }
+  // The whole pass -- scan, fold windows, non-ASCII keywords, rule gates and
+  // their D2H -- is queued before the one host wait, which then checks the
+  // scan's buffers: every kernel after the scan clamps to them (k_fold_windows
+  // to fold_cap), keyword bits are idempotent and the gate words are
+  // rewritten, so an overflowed attempt is simply redone with grown buffers.
+  // (One host round trip fewer than checking between the scan and the rest.)
   HIP_TRY(hipEventRecord(e->ev[8], s));
-  bool scanned = nbytes == 0;
+  bool scanned = false;
   for (int attempt = 0; attempt < 3 && !scanned; ++attempt) {
-    if ((rc = launch_scan(e, P))) return rc;
+    if (nbytes) {
+      if ((rc = launch_scan(e, P))) return rc;
+      if ((rc = launch_fold_windows(e, P, false))) return rc;
+      if ((rc = launch_uni_keywords(e, P))) return rc;
+    }
+    if (e->events) HIP_TRY(hipEventRecord(e->ev[9], s));
+    if (want_gates) {
+      const size_t words = gate_words_per_file;
+      hipLaunchKernelGGL(k_rule_gates, dim3((nf + 255) / 256), dim3(256), 0, s, e->file_kw.p, RS.kw_words, nf,
+                         e->gate_rules.p, R, e->gate_out.p, (uint32_t)words);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemcpyAsync(h_gates_out, e->gate_out.p, (size_t)nf * words * 4, hipMemcpyDeviceToHost, s));
+    }
     Ctrl c;
-    if ((rc = read_ctrl(e, &c))) return rc;
+    if ((rc = read_ctrl(e, &c))) return rc;  // (the stream's one synchronisation)
+    if (!nbytes) {
+      scanned = true;
+      break;
+    }
     const bool ev_lost = (rs->ac.fast.size() || P.big.blob) && c.ev_overflow > e->ev_overflow.n;
     const bool outs_lost = P.big.blob && c.outputs > P.big_out_cap;  // (k_big_walk's records)
     if (outs_lost) e->big_out_need = c.outputs + (c.outputs >> 2);
     if (!ev_lost && !outs_lost && c.n_fold <= P.fold_cap) {
-      if ((rc = launch_fold_windows(e, P, false))) return rc;
-      if ((rc = launch_uni_keywords(e, P))) return rc;
       scanned = true;
       break;
     }
@@ -9402,31 +9442,6 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
     set_last_error("internal: scan buffers still overflowed after regrowing them twice");
     return TSG_ERR_INTERNAL;
   }
-  if (e->events) HIP_TRY(hipEventRecord(e->ev[9], s));
-  if (h_gates_out && nf && gate_words_per_file) {
-    // rule -> keyword-id CSR (host, per ruleset: not per byte), gates on the GPU
-    const uint32_t R = (uint32_t)rs->rules.size();
-    std::vector<uint32_t> csr(R + 1);
-    std::vector<uint32_t> ids;
-    for (uint32_t r = 0; r < R; ++r) {
-      csr[r] = (uint32_t)ids.size();
-      for (auto& k : rs->rules[r].keywords) {
-        if (k.empty()) { ids.push_back(0xFFFFFFFFu); continue; }
-        ids.push_back((uint32_t)(std::find(rs->keywords.begin(), rs->keywords.end(), k) - rs->keywords.begin()));
-      }
-    }
-    csr[R] = (uint32_t)ids.size();
-    csr.insert(csr.end(), ids.begin(), ids.end());
-    HIP_TRY(e->gate_rules.ensure(csr.size()));
-    HIP_TRY(hipMemcpyAsync(e->gate_rules.p, csr.data(), csr.size() * 4, hipMemcpyHostToDevice, s));
-    const size_t words = gate_words_per_file;
-    HIP_TRY(e->gate_out.ensure((size_t)nf * words));
-    hipLaunchKernelGGL(k_rule_gates, dim3((nf + 255) / 256), dim3(256), 0, s, e->file_kw.p, RS.kw_words, nf,
-                       e->gate_rules.p, R, e->gate_out.p, (uint32_t)words);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(h_gates_out, e->gate_out.p, (size_t)nf * words * 4, hipMemcpyDeviceToHost, s));
-  }
-  HIP_TRY(hipStreamSynchronize(s));
   e->gate_tm.assign(18, 0.0);
   if (e->events && nbytes) {
     float ms = 0;
