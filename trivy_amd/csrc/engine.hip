@@ -1895,17 +1895,23 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
     }
     s = a;
   }
+  // Each lane takes events lo + lane, lo + lane + 64, ...; its segment index
+  // only moves forward (empty segments skipped; past e_reg: the bucket).  The
+  // next round's event is loaded before this round's is resolved, so its HBM
+  // latency runs under the replay instead of in front of it.
+  uint32_t sl = s;
+  const auto ev_at = [&](uint64_t g) -> const FastEvent* {
+    while (sl < n_waves && ev_pre[sl + 1] <= g) ++sl;
+    return sl < n_waves ? P.events + (uint64_t)sl * P.ev_cap_per_wave + (g - ev_pre[sl]) : P.ev_overflow + (g - e_reg);
+  };
+  FastEvent nxt{};
+  if (lo + lane < hi) nxt = *ev_at(lo + lane);
   for (uint64_t g0 = lo; g0 < hi; g0 += 64) {
     const uint64_t g = g0 + lane;
-    uint32_t sl = s;
-    if (g < hi) {
-      while (sl < n_waves && ev_pre[sl + 1] <= g) ++sl;  // (empty segments skipped; past e_reg: the bucket)
-      const FastEvent* ev =
-          sl < n_waves ? P.events + (uint64_t)sl * P.ev_cap_per_wave + (g - ev_pre[sl]) : P.ev_overflow + (g - e_reg);
-      report_event(P, ac, R, *ev, wbuf, &hcnt[wv], my_out, last_kw);
-    }
+    const FastEvent cur = nxt;
+    if (g + 64 < hi) nxt = *ev_at(g + 64);
+    if (g < hi) report_event(P, ac, R, cur, wbuf, &hcnt[wv], my_out, last_kw);
     report_flush(P, wbuf, &hcnt[wv], lane, g0 + 64 >= hi, hseg, &hcur);
-    s = __shfl(sl, hi - g0 >= 64 ? 63 : (int)(hi - g0 - 1));  // the last lane's segment: the next round's start
   }
   if (hseg && lane == 0) P.hit_seg_n[rw] = hcur;
   // per-wave totals: one atomic each
