@@ -1904,12 +1904,14 @@ __global__ __launch_bounds__(kReportThreads) void k_report(ScanParams P, uint32_
     while (sl < n_waves && ev_pre[sl + 1] <= g) ++sl;
     return sl < n_waves ? P.events + (uint64_t)sl * P.ev_cap_per_wave + (g - ev_pre[sl]) : P.ev_overflow + (g - e_reg);
   };
-  FastEvent nxt{};
+  FastEvent nxt{}, nxt2{};  // (two rounds ahead)
   if (lo + lane < hi) nxt = *ev_at(lo + lane);
+  if (lo + lane + 64 < hi) nxt2 = *ev_at(lo + lane + 64);
   for (uint64_t g0 = lo; g0 < hi; g0 += 64) {
     const uint64_t g = g0 + lane;
     const FastEvent cur = nxt;
-    if (g + 64 < hi) nxt = *ev_at(g + 64);
+    nxt = nxt2;
+    if (g + 128 < hi) nxt2 = *ev_at(g + 128);
     if (g < hi) report_event(P, ac, R, cur, wbuf, &hcnt[wv], my_out, last_kw);
     report_flush(P, wbuf, &hcnt[wv], lane, g0 + 64 >= hi, hseg, &hcur);
   }
