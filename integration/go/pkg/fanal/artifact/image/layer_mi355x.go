@@ -4,24 +4,31 @@
 // per GPU call instead of one file per Analyze.
 //
 // Artifact.inspectLayer (image.go:242-331) walks each uncompressed layer once
-// and calls every analyzer per file; required post-analyzer files are copied
-// to temp files (image.go:274-286).  For secrets that is one temp copy and one
-// cgo call per file.  In the mi355x build the artifact's AnalyzerGroup is
-// built with analyzer.TypeSecret disabled (the per-file analyzer and the
-// post-analyzer of analyzer/secret/secret_mi355x.go then never see a layer
-// file), and inspectLayer makes two changes, marked below:
+// and calls every analyzer per file.  For secrets that is one cgo call per
+// file (analyzer/secret/secret_mi355x.go analyzes tar-header files per file).
+// In the mi355x build NewArtifact tries newGPUSecrets; when the backend exists
+// (a usable GPU and a ruleset the engine covers) the artifact's AnalyzerGroup
+// is built with analyzer.TypeSecret disabled -- the per-file analyzer then
+// never sees a layer file -- and inspectLayer makes two changes, marked below;
+// without it nothing changes and Trivy's per-file analyzer runs as today:
 //
-//	layer, n, free, err := readLayer(rc)              // (1) the layer, once, in C memory
+//	layer, n, free, err := readLayer(rc)                          // (1) the layer, once, in C memory
 //	defer free()
-//	secrets, err := a.gpuSecrets.layerSecrets(layer, n) // (2) tsg_analyze_layer
+//	secrets, err := a.gpuSecrets.layerSecrets(layer, n, disabled) // (2) tsg_analyze_layer
 //	... a.walker.Walk(bytes.NewReader(unsafe.Slice((*byte)(layer), n)), ...) // other analyzers as today
-//	result.Secrets = append(result.Secrets, secrets...) // before result.Sort()
+//	result.Secrets = append(result.Secrets, secrets...)           // before result.Sort()
+//
+// `disabled` is inspectLayer's own argument: the image's base layers carry
+// analyzer.TypeSecret there (image.go:209-213) and yield no secrets, as the
+// reference's AnalyzeFile skips the secret analyzer for them
+// (analyzer.go:405-409).
 //
 // The walk inside the library applies the same skip rules and whiteout
 // handling as walker.LayerTar (tar.go:35-117), and Required + Analyze of every
 // regular file run in one tsg_analyze_layer call with the "/" path prefix of
 // Dir "" (secret.go:95-98).  Executable mirror: trivy_amd/walker.py
-// analyze_layer / analyze_layers (two engines per GPU take layers in turn).
+// analyze_layer / analyze_layers (two engines per GPU take layers in turn;
+// `disabled` marks base layers).
 package image
 
 /*
@@ -31,10 +38,14 @@ import "C"
 
 import (
 	"io"
+	"os"
+	"strconv"
 	"unsafe"
 
+	"golang.org/x/exp/slices"
 	"golang.org/x/xerrors"
 
+	"github.com/aquasecurity/trivy/pkg/fanal/analyzer"
 	"github.com/aquasecurity/trivy/pkg/fanal/secret"
 	"github.com/aquasecurity/trivy/pkg/fanal/types"
 	"github.com/aquasecurity/trivy/pkg/fanal/walker"
@@ -48,9 +59,28 @@ type gpuSecrets struct {
 	skipDirs   []string
 }
 
-func newGPUSecrets(be *secret.GPUBackend, configPath string, opt walker.Option) *gpuSecrets {
+// newGPUSecrets: nil when secret scanning is disabled for the artifact
+// (nothing is created then) or the host has no usable backend (Trivy's
+// per-file analyzer stays).
+func newGPUSecrets(opt analyzer.AnalyzerOptions, wopt walker.Option) *gpuSecrets {
+	if slices.Contains(opt.DisabledAnalyzers, analyzer.TypeSecret) {
+		return nil
+	}
+	configPath := opt.SecretScannerOption.ConfigPath
+	c, err := secret.ParseConfig(configPath)
+	if err != nil {
+		return nil // the per-file analyzer's Init reports the config error as today
+	}
+	device := 0
+	if v, err := strconv.Atoi(os.Getenv("TRIVY_SECRET_GPU_DEVICE")); err == nil {
+		device = v
+	}
+	be, err := secret.NewGPUBackend(secret.NewScanner(c), device)
+	if err != nil {
+		return nil
+	}
 	return &gpuSecrets{backend: be, configPath: configPath,
-		skipFiles: walker.CleanSkipPaths(opt.SkipFiles), skipDirs: walker.CleanSkipPaths(opt.SkipDirs)}
+		skipFiles: walker.CleanSkipPaths(wopt.SkipFiles), skipDirs: walker.CleanSkipPaths(wopt.SkipDirs)}
 }
 
 // readLayer reads an uncompressed layer into C memory (outside the Go heap,
@@ -85,8 +115,12 @@ func readLayer(rc io.Reader) (unsafe.Pointer, int, func(), error) {
 }
 
 // layerSecrets: the layer's secrets (files with findings), as the per-file
-// secret analyzer would have merged them into the layer's AnalysisResult.
-func (g *gpuSecrets) layerSecrets(layer unsafe.Pointer, n int) ([]types.Secret, error) {
+// secret analyzer would have merged them into the layer's AnalysisResult;
+// none for a layer whose `disabled` list holds TypeSecret (a base layer).
+func (g *gpuSecrets) layerSecrets(layer unsafe.Pointer, n int, disabled []analyzer.Type) ([]types.Secret, error) {
+	if slices.Contains(disabled, analyzer.TypeSecret) {
+		return nil, nil
+	}
 	secrets, _, _, err := g.backend.AnalyzeLayer(layer, n, g.skipFiles, g.skipDirs, g.configPath)
 	if err != nil {
 		return nil, xerrors.Errorf("secret gpu layer analysis: %w", err)

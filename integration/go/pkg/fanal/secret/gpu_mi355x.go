@@ -68,8 +68,12 @@ func (c *cstrs) free() {
 }
 
 // NewGPUBackend compiles s's rules (builtin ∪ custom, already filtered by
-// NewScanner) for GPU `device`.  A rule outside the engine's coverage
-// returns TSG_ERR_UNSUPPORTED: the caller keeps the pure-Go Scanner then.
+// NewScanner) for GPU `device` and creates the device's engine.  It fails
+// with TSG_ERR_NO_DEVICE on a host without a usable GPU and with
+// TSG_ERR_UNSUPPORTED for a rule outside the engine's coverage; every caller
+// in the mi355x build (analyzer/secret/secret_mi355x.go, the image-config and
+// layer hooks) then keeps Trivy's pure-Go Scanner.  Close frees the engine
+// (a finalizer does it too, for a backend nobody closed).
 func NewGPUBackend(s Scanner, device int) (*GPUBackend, error) {
 	g := s.Global
 	var keep cstrs
@@ -118,11 +122,23 @@ func NewGPUBackend(s Scanner, device int) (*GPUBackend, error) {
 		C.tsg_engine_free(b.engine)
 		return nil, xerrors.Errorf("regexp compile error: %s", C.GoString(&errbuf[0]))
 	}
-	runtime.SetFinalizer(b, func(b *GPUBackend) {
-		C.tsg_ruleset_free(b.ruleset)
-		C.tsg_engine_free(b.engine)
-	})
+	runtime.SetFinalizer(b, (*GPUBackend).Close)
 	return b, nil
+}
+
+// Close frees the ruleset and the engine (its device memory); safe to call
+// twice.
+func (b *GPUBackend) Close() {
+	b.mu.Lock()
+	defer b.mu.Unlock()
+	if b.ruleset != nil {
+		C.tsg_ruleset_free(b.ruleset)
+		b.ruleset = nil
+	}
+	if b.engine != nil {
+		C.tsg_engine_free(b.engine)
+		b.engine = nil
+	}
 }
 
 // Batch is a caller-filled, page-locked staging buffer (tsg_staging_*):
@@ -132,6 +148,7 @@ type Batch struct {
 	b     *GPUBackend
 	st    *C.tsg_staging
 	paths []string
+	slots [][]byte // each file's region of the staging buffer (C memory)
 }
 
 // NewBatch allocates a staging buffer of `capacity` bytes (contents + one
@@ -147,32 +164,56 @@ func (b *GPUBackend) NewBatch(capacity int) (*Batch, error) {
 // Len is the number of files added since the last run.
 func (t *Batch) Len() int { return len(t.paths) }
 
-// Add reserves `size` bytes for filePath and calls fill with that region of
-// the staging buffer (C memory: fill may read a file into it, e.g.
-// io.ReadFull).  ok is false when the buffer has no room: run the batch and
-// add again; a file larger than the whole buffer never fits (use ScanBatch).
-func (t *Batch) Add(filePath string, size int, fill func(dst []byte) error) (ok bool, err error) {
+// Reserve reserves `size` bytes for filePath and returns that region of the
+// staging buffer (C memory: the caller reads the file into it, e.g.
+// io.ReadFull, before the batch runs).  ok is false when the buffer has no
+// room: run the batch and reserve again; a file larger than the whole buffer
+// never fits (use AnalyzeBatch / ScanBatch).  A slot holds whatever an
+// earlier batch left there until it is written: a caller that cannot fill it
+// must clear it (NUL bytes: utils.IsBinary skips the file).
+func (t *Batch) Reserve(filePath string, size int) (dst []byte, ok bool, err error) {
 	cpath := C.CString(filePath)
 	defer C.free(unsafe.Pointer(cpath))
-	var dst *C.uint8_t
-	switch rc := C.tsg_staging_add(t.st, cpath, C.uint64_t(size), &dst); rc {
+	var p *C.uint8_t
+	switch rc := C.tsg_staging_add(t.st, cpath, C.uint64_t(size), &p); rc {
 	case C.TSG_OK:
 	case C.TSG_ERR_FULL:
-		return false, nil
+		return nil, false, nil
 	default:
-		return false, lastError("mi355x staging")
+		return nil, false, lastError("mi355x staging")
+	}
+	if size > 0 {
+		dst = unsafe.Slice((*byte)(unsafe.Pointer(p)), size)
 	}
 	t.paths = append(t.paths, filePath)
-	if size > 0 {
-		buf := unsafe.Slice((*byte)(unsafe.Pointer(dst)), size)
-		if err := fill(buf); err != nil {
-			// the slot stays in the batch: NUL bytes make utils.IsBinary skip
-			// the file, as Analyze's read error does (analyzer.go:430-434)
-			clear(buf)
+	t.slots = append(t.slots, dst)
+	return dst, true, nil
+}
+
+// Add is Reserve followed by fill(dst); a fill error clears the slot (it
+// stays in the batch and scans as binary) and is returned.
+func (t *Batch) Add(filePath string, size int, fill func(dst []byte) error) (ok bool, err error) {
+	dst, ok, err := t.Reserve(filePath, size)
+	if err != nil || !ok {
+		return ok, err
+	}
+	if len(dst) > 0 {
+		if err := fill(dst); err != nil {
+			clear(dst)
 			return true, err
 		}
 	}
 	return true, nil
+}
+
+// Content is file i's staged bytes (valid until the batch runs or resets).
+func (t *Batch) Content(i int) []byte { return t.slots[i] }
+
+// Reset empties the batch without running it.
+func (t *Batch) Reset() {
+	C.tsg_staging_reset(t.st)
+	t.paths = t.paths[:0]
+	t.slots = t.slots[:0]
 }
 
 // Analyze runs SecretAnalyzer.Analyze's per-file work (secret.go:79-113:
@@ -184,14 +225,15 @@ func (t *Batch) Analyze() ([]types.Secret, error) { return t.run(true) }
 // Scan is Scanner.Scan over the staged (already CR-stripped) contents.
 func (t *Batch) Scan() ([]types.Secret, error) { return t.run(false) }
 
+// run: one staged call.  On success the batch is reset; on an error the
+// staged files stay (Content) until the caller resets it.
 func (t *Batch) run(analyze bool) ([]types.Secret, error) {
 	b := t.b
 	b.mu.Lock()
 	defer b.mu.Unlock()
-	defer func() {
-		C.tsg_staging_reset(t.st)
-		t.paths = t.paths[:0]
-	}()
+	if b.engine == nil {
+		return nil, xerrors.New("mi355x scan: backend closed")
+	}
 	var res *C.tsg_result
 	var rc C.int
 	if analyze { // (cgo: C functions are not Go values, so no func variable here)
@@ -203,7 +245,9 @@ func (t *Batch) run(analyze bool) ([]types.Secret, error) {
 		return nil, lastError("mi355x scan")
 	}
 	defer C.tsg_result_free(res)
-	return b.convert(res, t.paths), nil
+	out := b.convert(res, t.paths)
+	t.Reset()
+	return out, nil
 }
 
 // Close frees the staging buffer.
@@ -217,7 +261,13 @@ func (t *Batch) Close() {
 // ScanBatch is Scan over many in-memory files in one GPU pass (each content
 // copied once, into the staging buffer).  Each result equals what
 // (*Scanner).Scan returns for that file.
-func (b *GPUBackend) ScanBatch(args []ScanArgs) ([]types.Secret, error) {
+func (b *GPUBackend) ScanBatch(args []ScanArgs) ([]types.Secret, error) { return b.batchOf(args, false) }
+
+// AnalyzeBatch is SecretAnalyzer.Analyze's per-file work (IsBinary, "\r"
+// strip, Scan) over RAW in-memory files in one GPU pass.
+func (b *GPUBackend) AnalyzeBatch(args []ScanArgs) ([]types.Secret, error) { return b.batchOf(args, true) }
+
+func (b *GPUBackend) batchOf(args []ScanArgs, analyze bool) ([]types.Secret, error) {
 	total := 1
 	for _, a := range args {
 		total += len(a.Content) + 1
@@ -228,12 +278,13 @@ func (b *GPUBackend) ScanBatch(args []ScanArgs) ([]types.Secret, error) {
 	}
 	defer t.Close()
 	for _, a := range args {
-		a := a
-		if _, err := t.Add(a.FilePath, len(a.Content), func(dst []byte) error { copy(dst, a.Content); return nil }); err != nil {
+		dst, _, err := t.Reserve(a.FilePath, len(a.Content))
+		if err != nil {
 			return nil, err
 		}
+		copy(dst, a.Content)
 	}
-	return t.Scan()
+	return t.run(analyze)
 }
 
 // convert turns a result into types.Secret values (scanner.go:436-451):
@@ -318,6 +369,10 @@ func (b *GPUBackend) AnalyzeLayer(layer unsafe.Pointer, n int, skipFiles, skipDi
 	var nk C.size_t
 	var res *C.tsg_result
 	b.mu.Lock()
+	if b.engine == nil {
+		b.mu.Unlock()
+		return nil, nil, nil, xerrors.New("secret scan error: backend closed")
+	}
 	rc := C.tsg_analyze_layer(b.engine, b.ruleset, (*C.uint8_t)(layer), C.size_t(n), w, keep.str(configPath),
 		&kept[0], &nk, &res)
 	b.mu.Unlock()

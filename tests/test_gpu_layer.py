@@ -131,6 +131,57 @@ def test_analyze_layers_error_leaves_other_layers_intact():
         assert _plain(secs) == _oracle_plain(want)
 
 
+def test_analyze_layers_base_layer_yields_no_secrets():
+    """image.go:209-213: a base layer (its DiffID in the base image's) carries
+    TypeSecret in its disabled list, so the reference's AnalyzeFile never calls
+    the secret analyzer on its files.  The layer hook honours the same list:
+    the base layer is walked (whiteouts and opaque dirs still count) and
+    yields no secrets; the other layers are untouched."""
+    a = SecretAnalyzer()
+    a.init("")
+    layers = [_layer(70 + k, 150) for k in range(3)]
+    got = W.analyze_layers(a, layers, walk_threads=2, disabled=[True, False, True])
+    for k, (data, (secs, opq, wh)) in enumerate(zip(layers, got)):
+        want, wopq, wwh = _oracle_layer(data)
+        assert (opq, wh) == (wopq, wwh)
+        if k in (0, 2):
+            assert secs == [] and len(want) > 5  # the layer had secrets; a base layer reports none
+        else:
+            assert _plain(secs) == _oracle_plain(want)
+
+
+def test_analyze_layers_dead_extra_engine_falls_back_in_order(monkeypatch):
+    """an extra engine failing with a device error hands its layer
+    -- and every later layer queued on it -- to the first engine's queue; the
+    results stay in input order and equal the oracle's, and every walk is
+    closed (the next call works on both engines)."""
+    import trivy_amd._native as N
+    import trivy_amd.secret as S
+
+    a = SecretAnalyzer()
+    a.init("")
+    engs = S.get_engines(a.scanner.device, 2)
+    real = W._analyze_walked
+    calls = {"dead": 0}
+
+    def flaky(analyzer, addr, n, w, engine=None):
+        if engine is not None and engine.value == engs[1].value:
+            calls["dead"] += 1
+            raise N.EngineError(N.TSG_ERR_DEVICE, "injected device error")
+        return real(analyzer, addr, n, w, engine)
+
+    monkeypatch.setattr(W, "_analyze_walked", flaky)
+    layers = [_layer(80 + k, 100) for k in range(6)]
+    got = W.analyze_layers(a, layers, walk_threads=3, engines=2)
+    assert calls["dead"] == 1  # the engine is tried once, then skipped
+    for data, (secs, _, _) in zip(layers, got):
+        want, _, _ = _oracle_layer(data)
+        assert _plain(secs) == _oracle_plain(want)
+    monkeypatch.setattr(W, "_analyze_walked", real)
+    again = W.analyze_layers(a, layers[:2], walk_threads=2, engines=2)
+    assert [_plain(s) for s, _, _ in again] == [_plain(s) for s, _, _ in got[:2]]
+
+
 def test_analyze_layer_finding_order():
     """Two findings of one rule whose Match order (Scan's sort) is the reverse
     of their line order: the layer result carries AnalysisResult.Sort's

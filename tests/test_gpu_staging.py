@@ -1,23 +1,16 @@
-"""Caller-filled staging (tsg_staging_*, tsg_analyze_staged / tsg_scan_staged)
-and the tagged Go build's post-analyzer that drives it
-(integration/go/pkg/fanal/analyzer/secret/secret_mi355x.go, mirrored by
-trivy_amd.analyzer.SecretPostAnalyzer): files read straight into page-locked
-memory give the same findings as the packing entry points and as the oracle's
-per-file Analyze (pkg/fanal/analyzer/secret/secret.go:79-113)."""
-import os
-
+"""Caller-filled staging (tsg_staging_*, tsg_analyze_staged / tsg_scan_staged):
+files read straight into page-locked memory give the same findings as the
+packing entry points.  The tagged Go build's analyzer that drives it inside
+Trivy's AnalyzerGroup is tested in tests/test_gpu_analyzer_group.py."""
 import pytest
 
-from oracle import secret_oracle as o
-
 from . import corpus_gen
-from .test_gpu_parity import _canon, _oracle_plain, _plain
+from .test_gpu_parity import _plain
 
 pytestmark = pytest.mark.gpu
 
 S = pytest.importorskip("trivy_amd.secret")
 N = pytest.importorskip("trivy_amd._native")
-from trivy_amd.analyzer import SecretAnalyzer, SecretPostAnalyzer  # noqa: E402
 
 
 def _files(seed, n):
@@ -80,33 +73,19 @@ def test_staging_full_and_refill():
         assert (None if g is None else _plain(g)) == (None if want[p] is None else _plain(want[p])), p
 
 
-def test_post_analyzer_equals_per_file_analyze(tmp_path):
-    """PostAnalyze over the post-analyzer FS -- the files Required accepted,
-    linked by the artifact walk (artifact/local/fs.go:100-106) -- with a small
-    staging (several batches, one file larger than the staging alone) == the
-    oracle's per-file Analyze with Dir set (no '/' prefix), in walk order."""
-    from trivy_amd.analyzer import _walk_dir
+def test_reserve_failure_zeroes_slot():
+    """Batch.add: a fill that raises leaves its slot zeroed -- the slot of a
+    reset batch holds the previous batch's bytes until written -- so the
+    file scans as binary instead of as an earlier file's content."""
+    sc = S.new_scanner(None)
+    body = b"x = 1\ntoken: ghp_" + b"K" * 36 + b"\n"
+    with sc.new_batch(1 << 16) as b:
+        assert b.add("a.env", len(body), _fill(body))
+        first = b.analyze()
+        assert first[0] is not None and len(first[0].Findings) == 1
 
-    files = _files(33, 200)
-    files.append(("big/huge.env", b"x = 1\n" * 30000 + b"token: ghp_" + b"Q" * 36 + b"\n"))
-    a = SecretAnalyzer()
-    a.init("")
-    post = SecretPostAnalyzer(a, batch_bytes=128 << 10)
-    n_req = 0
-    for p, d in files:
-        if not post.required(p, len(d)):
-            continue
-        n_req += 1
-        f = tmp_path / p
-        f.parent.mkdir(parents=True, exist_ok=True)
-        f.write_bytes(d)
-    got = post.post_analyze(str(tmp_path))
-    oa = o.SecretAnalyzer("")
-    want = []
-    for p, _ in _walk_dir(str(tmp_path)):
-        r = oa.analyze(p, open(os.path.join(tmp_path, p), "rb").read(), str(tmp_path))
-        if r:
-            want.extend(r)
-    assert [_canon(_plain(g)) for g in got] == [_canon(_oracle_plain(w)) for w in want]
-    assert any(g.FilePath == "big/huge.env" for g in got)
-    assert n_req > 150 and len(want) > 50
+        def broken(dst):  # writes nothing: the slot still holds a.env's bytes
+            raise OSError("input/output error")
+        with pytest.raises(OSError):
+            b.add("b.env", len(body), broken)
+        assert b.analyze() == [None]  # binary: NUL bytes

@@ -435,20 +435,44 @@ class Batch:
     def __len__(self) -> int:
         return len(self.paths)
 
-    def add(self, file_path: str, size: int, fill) -> bool:
-        """Reserve `size` bytes for file_path and let fill(dst) write them in
-        place (dst: a writable memoryview of exactly `size` bytes).  False when
-        the staging has no room (run the batch and add again)."""
+    def reserve(self, file_path: str, size: int) -> Optional[memoryview]:
+        """Reserve `size` bytes for file_path (Batch.Reserve in Go): the
+        writable slot (empty for size 0), or None when the staging has no room
+        (run the batch and reserve again).  The caller fills the slot before
+        the batch runs -- and zeroes it if it cannot (a slot keeps whatever an
+        earlier batch left there)."""
         dst = ctypes.c_void_p()
         rc = N.lib.tsg_staging_add(self.handle, file_path.encode("utf-8", "surrogateescape"), size,
                                    ctypes.byref(dst))
         if rc == N.TSG_ERR_FULL:
-            return False
+            return None
         N.check(rc)
-        if size:
-            fill(memoryview((ctypes.c_uint8 * size).from_address(dst.value)).cast("B"))
         self.paths.append(file_path)
+        if not size:
+            return memoryview(bytearray(0))
+        return memoryview((ctypes.c_uint8 * size).from_address(dst.value)).cast("B")
+
+    def add(self, file_path: str, size: int, fill) -> bool:
+        """Reserve `size` bytes for file_path and let fill(dst) write them in
+        place (dst: a writable memoryview of exactly `size` bytes).  False when
+        the staging has no room (run the batch and add again).  A fill that
+        raises leaves the slot zeroed (IsBinary then skips the file) and the
+        error propagates."""
+        dst = self.reserve(file_path, size)
+        if dst is None:
+            return False
+        if size:
+            try:
+                fill(dst)
+            except BaseException:
+                dst[:] = bytes(size)
+                raise
         return True
+
+    def reset(self) -> None:
+        """Empty the batch without running it (tsg_staging_reset)."""
+        N.lib.tsg_staging_reset(self.handle)
+        self.paths = []
 
     def analyze(self) -> List[Optional[Secret]]:
         """tsg_analyze_staged; None for binary files (secret.go:80-86)."""
@@ -458,14 +482,16 @@ class Batch:
         return self._run(N.lib.tsg_scan_staged)
 
     def _run(self, fn):
+        """One staged call; on success the batch is reset.  On an error the
+        staged files stay (the caller may re-scan them from their slots, then
+        reset)."""
         res = ctypes.c_void_p()
         N.check(fn(get_engine(self.scanner.device), self.scanner._rs.handle, self.handle, ctypes.byref(res)))
         try:
             return self.scanner._convert(res, [ScanArgs(p, b"") for p in self.paths])
         finally:
             N.lib.tsg_result_free(res)
-            N.lib.tsg_staging_reset(self.handle)
-            self.paths = []
+            self.reset()
 
     def close(self) -> None:
         if self.handle:

@@ -210,8 +210,8 @@ def analyze_layer(analyzer, layer: Layer, skip_files: Sequence[str] = (),
 
 
 def analyze_layers(analyzer, layers: Sequence[Layer], skip_files: Sequence[str] = (),
-                   skip_dirs: Sequence[str] = (), walk_threads: int = 4, engines: int = 2
-                   ) -> List[Tuple[List[Secret], List[str], List[str]]]:
+                   skip_dirs: Sequence[str] = (), walk_threads: int = 4, engines: int = 2,
+                   disabled: Sequence[bool] = ()) -> List[Tuple[List[Secret], List[str], List[str]]]:
     """The layers of an image (image.go:242-331 inspects them concurrently),
     pipelined: up to `walk_threads` native walks run ahead on host threads
     (ctypes drops the GIL), and layer k is analyzed on engine k % `engines`
@@ -221,7 +221,13 @@ def analyze_layers(analyzer, layers: Sequence[Layer], skip_files: Sequence[str] 
     findings of the layer before it.  An extra engine holds its own device
     scratch and pinned staging: a layer whose analysis fails
     on an extra engine with a device error (e.g. out of memory) is re-run on
-    the first engine, and that extra engine takes no more layers of this call.
+    the first engine -- on the first engine's own queue, so it never runs
+    beside that queue's layers -- and that extra engine takes no more layers
+    of this call (its queued layers go to the first queue too).
+    `disabled[k]` true: secret scanning is disabled for layer k -- a base
+    layer of the image (image.go:209-213 passes TypeSecret in the per-layer
+    disabled list): the layer is walked (its opaque dirs and whiteouts are
+    still needed) but not analyzed, and it yields no secrets.
     One (secrets, opqDirs, whFiles) per layer, in input order."""
     from concurrent.futures import ThreadPoolExecutor
 
@@ -231,19 +237,27 @@ def analyze_layers(analyzer, layers: Sequence[Layer], skip_files: Sequence[str] 
     opened = [_open_layer(x) for x in layers]
     dead = set()  # extra engines that failed with a device error
 
-    def one(k, f):
+    def on(e, k, w):
         _, addr, n, _ = opened[k]
+        return (_analyze_walked(analyzer, addr, n, w, engs[e]), w.opq_dirs, w.wh_files)
+
+    def one(k, f):
         e = k % len(engs)
         with f.result() as w:  # this task owns the walk: closed here, whatever happens
-            if e in dead:
-                e = 0
-            try:
-                return (_analyze_walked(analyzer, addr, n, w, engs[e]), w.opq_dirs, w.wh_files)
-            except N.EngineError as err:
-                if e == 0 or err.code != N.TSG_ERR_DEVICE:
-                    raise
-                dead.add(e)
-                return (_analyze_walked(analyzer, addr, n, w, engs[0]), w.opq_dirs, w.wh_files)
+            if k < len(disabled) and disabled[k]:
+                return ([], w.opq_dirs, w.wh_files)
+            if e != 0 and e not in dead:
+                try:
+                    return on(e, k, w)
+                except N.EngineError as err:
+                    if err.code != N.TSG_ERR_DEVICE:
+                        raise
+                    dead.add(e)
+            if e == 0:
+                return on(0, k, w)
+            # a dead extra engine's layer: run on the first engine's queue (this
+            # worker waits; the first queue never waits on another)
+            return queues[0].submit(on, 0, k, w).result()
 
     pool = ThreadPoolExecutor(max_workers=max(1, walk_threads))
     queues = [ThreadPoolExecutor(max_workers=1) for _ in engs]
