@@ -547,6 +547,90 @@ def full_parity(N, c, res, threads, ranges, label):
                 threads=threads, scope=label)
 
 
+_ORACLE_W = {}
+
+
+def _oracle_worker_init(gen_path, seed, density):
+    """A worker of oracle_parity: the bench corpus generator (host side of
+    bench_gen/corpus.hip, regenerating each file from its seed) and the
+    Python oracle's Scanner (the independent checker: its own regex engine)."""
+    from oracle import secret_oracle as O
+
+    gen = ctypes.CDLL(gen_path)
+    gen.tsg_gen_file.restype = ctypes.c_int
+    gen.tsg_gen_file.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double, ctypes.c_void_p]
+    _ORACLE_W.update(gen=gen, seed=seed, density=density, scanner=O.Scanner(None))
+
+
+def _oracle_worker(item):
+    f, n, path = item
+    w = _ORACLE_W
+    buf = (ctypes.c_uint8 * max(1, n))()
+    rc = w["gen"].tsg_gen_file(w["seed"], f, n, w["density"], buf)
+    if rc:
+        raise RuntimeError(f"tsg_gen_file({f}) failed: {rc}")
+    want = w["scanner"].scan(path, bytes(buf)[:n])
+    return f, sorted(oracle_findings(want))
+
+
+def oracle_parity(N, c, res, rules, seed, density, random_gb, workers):
+    """Independent full-size parity: the Python oracle --
+    not the C++ restatement, which shares the engine's Go-RE2 parser and VM --
+    over every configs[2] file that holds a plant or a decoy, every file the
+    GPU reported a finding in, every non-ASCII file (é / K / ſ / İ), and
+    random files up to `random_gb`, each regenerated on the host from the
+    corpus seed in `workers` processes; complete findings (RuleID, lines,
+    Match, every Code line with its flags) compared with the GPU result's."""
+    import multiprocessing as mp
+
+    t0 = time.perf_counter()
+    sizes = c["sizes"]
+    n_gen = c.get("first_stress", c["n_files"])
+    locs, _ = read_result(N, res)
+    plants = c["plants"]
+    pick = set(int(f) for f in np.unique(plants["file"]))
+    n_plant = len(pick)
+    gpu_files = set(int(f) for f in np.unique(locs["file"]))
+    pick |= gpu_files
+    nonascii = [f for f in range(n_gen) if N.gen.tsg_gen_file_nonascii(seed, f)]
+    pick |= set(nonascii)
+    rng = np.random.default_rng(seed + 11)
+    rand_bytes = 0
+    for f in rng.permutation(n_gen):
+        if rand_bytes >= random_gb * 1e9:
+            break
+        if int(f) not in pick:
+            pick.add(int(f))
+            rand_bytes += int(sizes[f])
+    pick = sorted(f for f in pick if f < n_gen)
+    paths = c["d_paths"].cpu().numpy()
+    items = [(f, int(sizes[f]), bytes(paths[f * 31:(f + 1) * 31]).decode()) for f in pick]
+    items.sort(key=lambda x: -x[1])  # largest first: the pool ends together
+    total = sum(x[1] for x in items)
+    print(f"oracle parity: {len(items)} files, {total / 1e9:.2f} GB on {workers} processes", file=sys.stderr,
+          flush=True)
+    bad = []
+    n_find = 0
+    done = 0
+    # spawned, not forked: the workers never hold this process's GPU handles
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(workers, initializer=_oracle_worker_init, initargs=(N.GEN_PATH, seed, density)) as pool:
+        for k, (f, want) in enumerate(pool.imap_unordered(_oracle_worker, items, chunksize=1)):
+            got = sorted(result_findings(N, res, f, rules))
+            n_find += len(want)
+            if got != want:
+                bad.append(f)
+            done += 1
+            if done % 20000 == 0:
+                print(f"oracle parity: {done}/{len(items)} files, {len(bad)} mismatched, "
+                      f"{time.perf_counter() - t0:.0f}s", file=sys.stderr, flush=True)
+    return dict(checker="oracle/secret_oracle.py (Python regex engine, independent of the engine's parser and VM)",
+                files=len(items), bytes=total, plant_or_decoy_files=n_plant, gpu_finding_files=len(gpu_files),
+                nonascii_files=len(nonascii), random_bytes=rand_bytes, findings=n_find,
+                files_identical=len(items) - len(bad), mismatched=bad[:10], workers=workers,
+                wall_seconds=round(time.perf_counter() - t0, 1))
+
+
 def shared_layers_main(args, N, S, torch, dist, barrier, rank, world, device, red_dev):
     """configs[3] as one shared image: every rank derives the same layer list
     (shared_layer_set), trivy_amd.shard.partition assigns layers to ranks by
@@ -703,6 +787,10 @@ def main():
                     help="after the timed steps, compare EVERY file's complete findings with the C++ restatement "
                          "(configs[2]; configs[4]: the unique C5 files + --full-parity-gb of text)")
     ap.add_argument("--full-parity-gb", type=float, default=0.0, help="--full-parity: limit to the first GB")
+    ap.add_argument("--oracle-parity", action="store_true",
+                    help="configs[2]: the Python oracle over every plant / decoy / finding / non-ASCII file "
+                         "and --oracle-random-gb of random files (independent checker)")
+    ap.add_argument("--oracle-random-gb", type=float, default=1.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for N > 1 (nccl = RCCL; gloo for several ranks on one GPU in tests)")
     ap.add_argument("--shared", action="store_true",
@@ -979,6 +1067,10 @@ def main():
             full = full_parity(N, c, last, cores, [(f0, f0 + len(stress_unique)), (0, max(1, min(nf, f0)))],
                                f"configs[4]: the {len(stress_unique)} unique C5 files + the first "
                                f"{args.full_parity_gb or 0.25:g} GB of generated text")
+    oracle_full = None
+    if rank == 0 and args.oracle_parity and args.config == 2 and last is not None:
+        oracle_full = oracle_parity(N, c, last, sc.rules, seed, args.density, args.oracle_random_gb,
+                                    max(1, (args.cpu_cores or cpu_quota()) - 1))
     if last is not None and args.config != 3:
         N.lib.tsg_result_free(last)
     if rank == 0:
@@ -1024,6 +1116,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             **({"full_parity": full} if full is not None else {}),
+            **({"oracle_parity": oracle_full} if oracle_full is not None else {}),
         }
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -36,6 +36,11 @@ int tsg_ruleset_scan_pattern(const tsg_ruleset* rs, size_t k, char* lower, size_
  * the ruleset has no fast image), *out_entry = the first output state's entry. */
 int tsg_ruleset_scan_image(const tsg_ruleset* rs, uint8_t* buf, size_t cap, size_t* len, uint32_t* out_entry);
 
+/* k_scan_fast's keyword states: output states whose every output is a
+ * keyword-only pattern the scan resolves itself (no k_report event), and the
+ * keywords they set (lowercased, each NUL-terminated, into buf up to cap). */
+int tsg_ruleset_kw_states(const tsg_ruleset* rs, uint32_t* n_states, uint32_t* n_keywords, char* buf, size_t cap);
+
 /* Instruction count and capture slots of rule i's compiled regex. */
 int tsg_ruleset_rule_prog(const tsg_ruleset* rs, size_t i, uint32_t* n_inst, uint32_t* n_cap);
 

@@ -103,6 +103,8 @@ _SIGS = {
     "tsg_ruleset_scan_pattern": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
                                                 ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_uint32),
                                                 ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
+    "tsg_ruleset_kw_states": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
+                                             ctypes.POINTER(ctypes.c_uint32), ctypes.c_char_p, ctypes.c_size_t]),
     "tsg_ruleset_scan_image": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                               ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_uint32)]),
     "tsg_ruleset_rule_prog": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32),

@@ -108,6 +108,9 @@ struct AcDev {
   const uint8_t* fast_lds;   // LDS image for k_scan_fast (AcHost::fast); null => generic kernel
   uint32_t fast_bytes;       // image size
   uint32_t fast_out_entry;   // entries >= this are output states
+  uint32_t fast_ev_entry;    // ... and from this one on k_report events (below: keyword states, AcHost)
+  uint32_t fast_kw_n;        // keyword states (fast_ev_entry - fast_out_entry)
+  const uint8_t* fast_kw;    // their FastKwRec records (kFastKwPer each), then the local bits' keyword ids (u16)
   uint32_t depth;            // trie depth
   // k_report's LDS blob = fast image | out_off | out_pat | pats | pat_bytes
   // (fast_lds is its start; offsets in bytes)
@@ -275,12 +278,33 @@ struct AcHost {
   // k_scan_fast pair table: the state two bytes after the root, per column
   // pair (64 x 64 u16); empty when a state one byte from the root has outputs
   std::vector<uint16_t> fast_pair;
+  // keyword states (build_fast): the output states whose every output is a
+  // keyword-only pattern the scan resolves itself (FastKwRec, kFastKwPer per
+  // state), numbered [fast_out_entry, fast_ev_entry); states from
+  // fast_ev_entry on become k_report events.  fast_kw_map: local keyword bit
+  // -> keyword id.
+  uint32_t fast_ev_entry = 0;
+  std::vector<uint8_t> fast_kw;
+  std::vector<uint16_t> fast_kw_map;
+};
+
+// One keyword pattern of a k_scan_fast keyword state: the lowered bytes and
+// their mask, top-aligned in the 8 bytes ending at the output byte (as
+// PatDev::lo64 / m64), and the keyword's local bit (< kFastKwBits).
+constexpr uint32_t kFastKwPer = 2;     // patterns per keyword state (an unused record: m64 = 0, lo64 = 1, never matches)
+constexpr uint32_t kFastKwBits = 32;   // local keyword bits a scan lane accumulates
+constexpr uint32_t kFastKwStates = 64; // keyword states at most (the LDS table's size)
+struct FastKwRec {
+  uint64_t lo64, m64;
+  uint32_t bit;
+  uint32_t pad;
 };
 
 struct PatternHost {
   std::string lower;   // full lowercased pattern
   std::string req;     // confirm spec (same length), '\0' = any case
   int kw = -1;
+  bool kw_needed = false;  // its keyword is one some non-implied gate needs (engine.hip's kw_needed)
   bool special = false;
   bool confirm = false;
   bool any_anchor = false;

@@ -105,7 +105,7 @@ struct Ctrl {
   unsigned long long rep_next;   // k_report: next wave segment to claim
   unsigned long long n_caps;     // matches whose secret-group spans k_captures resolves
   unsigned long long n_caps_big; // ... and those too long for its arenas (k_captures_big)
-  unsigned long long long_files; // files longer than kMaxVerifyFile (k_region_mark)
+  unsigned long long long_files; // files longer than kMaxVerifyFile (k_region_fill)
   unsigned long long n_panic;    // kept locations whose secret group did not participate (k_out_locs)
   unsigned long long n_ties;     // findings whose (file, RuleID, Match prefix) equals the previous one's
   unsigned long long n_redo;     // speculative job chains re-run from a conflict (k_chain_fix)
@@ -225,15 +225,36 @@ __device__ inline void note_fold(const ScanParams& P, uint64_t pos, uint32_t kin
 
 
 // region_file[r] = index of the file holding byte r * kNlBlock = the largest f
-// with off[f] <= r * kNlBlock: each file marks the first region boundary at or
-// after its start (atomicMax), an inclusive max-scan fills the rest.
-__global__ __launch_bounds__(256) void k_region_mark(const uint64_t* off, uint32_t n_files, uint64_t n_regions,
+// with off[f] <= r * kNlBlock.
+// Written directly: file f holds the region starts
+// [ceil(off[f] / B), ceil(off[f + 1] / B)) (the last file: through n_regions).
+// A lane writes its file's first kRegionDirect regions; the wave then writes
+// the rest of each longer file of its lanes together (coalesced, one file at a
+// time).  No memset, no mark pass, no max-scan -- and no list of long files:
+// an append to one counter serialised at L2 (0.75 ms for ~160 K long files of
+// configs[2], profiles/r06c_ab).
+constexpr uint64_t kRegionDirect = 16;
+__global__ __launch_bounds__(256) void k_region_fill(const uint64_t* off, uint32_t n_files, uint64_t n_regions,
                                                      uint32_t* region_file, Ctrl* ctrl) {
   const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= n_files) return;
-  if (off[f + 1] - off[f] - 1 > kMaxVerifyFile) atomicAdd(&ctrl->long_files, 1ull);
-  const uint64_t r = (off[f] + kNlBlock - 1) / kNlBlock;
-  if (r < n_regions) atomicMax(&region_file[r], (uint32_t)f);
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t rd = 0, r1 = 0;
+  if (f < n_files) {
+    const uint64_t o0 = off[f], o1 = off[f + 1];
+    if (o1 - o0 - 1 > kMaxVerifyFile) atomicAdd(&ctrl->long_files, 1ull);
+    const uint64_t r0 = (o0 + kNlBlock - 1) / kNlBlock;
+    r1 = f + 1 == n_files ? n_regions : std::min<uint64_t>((o1 + kNlBlock - 1) / kNlBlock, n_regions);
+    rd = std::min(r1, r0 + kRegionDirect);
+    for (uint64_t r = r0; r < rd; ++r) region_file[r] = (uint32_t)f;
+  }
+  uint64_t m = __ballot(r1 > rd);
+  while (m) {
+    const uint32_t k = (uint32_t)__builtin_ctzll(m);
+    m &= m - 1;
+    const uint64_t lo = __shfl(rd, k), hi = __shfl(r1, k);
+    const uint32_t fk = (uint32_t)__shfl((uint32_t)f, k);
+    for (uint64_t r = lo + lane; r < hi; r += 64) region_file[r] = fk;
+  }
 }
 
 __device__ inline uint32_t find_file(const uint64_t* off, uint32_t lo, uint32_t hi, uint64_t pos) {
@@ -543,6 +564,85 @@ struct FastChain {
   bool cnt = false;  // kMode 2: wave-uniform -- count this round's newlines anyway
 };
 
+// ASCII lowercase of 8 bytes at once (bytes 'A'-'Z' gain 0x20)
+__device__ inline uint64_t lower64(uint64_t x) {
+  const uint64_t t = x & 0x7F7F7F7F7F7F7F7Full;
+  const uint64_t up = ((t + 0x3F3F3F3F3F3F3F3Full) ^ (t + 0x2525252525252525ull)) & ~x & 0x8080808080808080ull;
+  return x | (up >> 2);
+}
+
+// Keyword states (AcHost::fast_kw): a group whose automaton max is a keyword
+// state -- in [fast_out_entry, fast_ev_entry) -- holds only keyword-only
+// outputs, which the scan resolves itself instead of handing k_report an event
+// (the 2-3 letter keywords jwt / lob / key of the builtin rules were most of
+// configs[2]'s 6.3 M events).  The lane appends the group (a FastEvent) to
+// its wave's queue in LDS; at the end of each span the wave drains the queue,
+// one record per lane: replay of the 8 bytes from the entry state (8 LDS
+// steps, as k_report), each keyword state's patterns confirmed on the real
+// bytes (lowered window: FastKwRec lo64 / m64), the file looked up by
+// position and the keyword's bit set (one atomic, read-first in files of
+// kw_plain bytes or more, whose words every lane hits).  A full queue turns
+// the group into an event.  The drain sits outside the scan's unrolled step
+// (inlined per group it doubled the loop's code, which the compiler then no
+// longer unrolled: the register ring went to scratch).
+constexpr uint32_t kFastKwQ = 48;  // queue records per wave (16 waves x 48 x 32 B of LDS)
+
+struct KwScan {
+  const FastKwRec* rec;
+  const uint16_t* map;
+  FastEvent* q;   // this wave's queue (LDS)
+  uint32_t ev_e;  // first event state
+};
+
+__device__ inline uint32_t file_of_pos_off(const uint64_t* off, const uint32_t* region_file, uint64_t n_regions,
+                                           uint32_t n_files, uint64_t pos) {
+  const uint64_t r = pos / kNlBlock;
+  const uint32_t hi = r + 1 < n_regions ? min(region_file[r + 1] + 1, n_files) : n_files;
+  return find_file(off, region_file[r], hi, pos);
+}
+
+__device__ inline void kw_resolve(const ScanParams& P, const uint8_t* T, const KwScan& kw, uint32_t out_e,
+                                  const FastEvent& ev) {
+  uint64_t hlow = lower64(((uint64_t)ev.prev.y << 32) | ev.prev.x);
+  uint32_t e = ev.entry;
+  const uint32_t f0 = fold6(ev.cur.x), f1 = fold6(ev.cur.y);
+  uint32_t fi = 0xFFFFFFFFu;
+  for (int j = 0; j < 8; ++j) {
+    e = fstep(T, e, j < 4 ? f0 : f1, j & 3);
+    const uint32_t c = ((j < 4 ? ev.cur.x : ev.cur.y) >> (8 * (j & 3))) & 0xFFu;
+    hlow = (hlow >> 8) | ((uint64_t)lower_ascii((uint8_t)c) << 56);
+    if (e < out_e) continue;
+    const FastKwRec* r = kw.rec + (size_t)(e - out_e) * kFastKwPer;
+    uint32_t bits = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kFastKwPer; ++q)
+      if ((hlow & r[q].m64) == r[q].lo64) bits |= 1u << r[q].bit;
+    if (!bits) continue;
+    // (a file separator resets the automaton: every pattern lies in one file)
+    if (fi == 0xFFFFFFFFu || ev.pos + j >= P.off[fi + 1])
+      fi = file_of_pos_off(P.off, P.region_file, P.n_regions, P.n_files, ev.pos + j);
+    const bool read_first = P.off[fi + 1] - P.off[fi] >= P.kw_plain;
+    while (bits) {
+      const uint32_t b = (uint32_t)__builtin_ctz(bits);
+      bits &= bits - 1;
+      const uint32_t g = kw.map[b];
+      uint32_t* wp = &P.file_kw[(size_t)fi * P.rs.kw_words + (g >> 5)];
+      const uint32_t bit = 1u << (g & 31);
+      if (!read_first || !(__hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(wp, bit);
+    }
+  }
+}
+
+// The wave's queued keyword groups, one per lane (wave-uniform count).
+__device__ inline void kw_drain(const ScanParams& P, const uint8_t* T, const KwScan& kw, uint32_t out_e,
+                                uint32_t& kwn, uint32_t lane) {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the queue's stores before its loads
+  for (uint32_t q0 = 0; q0 < kwn; q0 += 64)
+    if (q0 + lane < kwn) kw_resolve(P, T, kw, out_e, kw.q[q0 + lane]);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the loads before the queue is refilled
+  kwn = 0;
+}
+
 // Append an event for a group whose automaton max reached an output state
 // (ballot + popcount into the wave's segment, no atomics; every lane calls
 // this, so ev_count stays wave-uniform).
@@ -626,10 +726,13 @@ __device__ inline void fast_group2(const ScanParams& P, const uint8_t* T, uint32
 // output state anywhere in the window (rare: ~one group in 10^3) are the
 // groups' events appended in order.  Cuts the compare / ballot / branch per
 // group that otherwise sits on every chain step.
+// kw: keyword groups go to the wave's queue (kwn: its wave-uniform count);
+// without, every output state is an event.
 template <int V, int kMode, int G, bool kPair = false>
 __device__ inline void fast_window(const ScanParams& P, const uint8_t* T, uint32_t out_e, FastChain<V>& C,
                                    const uint32_t (&d)[2 * G], uint64_t gpos, bool live, uint64_t lanes_lt,
-                                   FastEvent* ev_seg, uint32_t* ev_count) {
+                                   FastEvent* ev_seg, uint32_t* ev_count, const KwScan* kw = nullptr,
+                                   uint32_t* kwn = nullptr) {
   uint32_t gs[G], m[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -659,9 +762,32 @@ __device__ inline void fast_window(const ScanParams& P, const uint8_t* T, uint32
 #pragma unroll
     for (int g = 1; g < G; ++g) mx = mx > m[g] ? mx : m[g];
     if (__builtin_amdgcn_uicmp(mx, out_e, 35) & __ballot(live)) {
+      const uint32_t ev_e = kw ? kw->ev_e : out_e;
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        fast_event(P, out_e, C, m[g], gs[g], d[2 * g], d[2 * g + 1], gpos + 8 * g, live, lanes_lt, ev_seg, ev_count);
+        uint32_t mg = m[g];
+        if (kw) {  // keyword groups into the queue; a full queue makes them events
+          const bool kl = live && mg >= out_e && mg < ev_e;
+          const uint64_t kb = __ballot(kl);
+          if (kb) {
+            const uint32_t nq = (uint32_t)__popcll(kb);
+            if (*kwn + nq <= kFastKwQ) {
+              if (kl) {
+                FastEvent r;
+                r.pos = gpos + 8 * g;
+                r.entry = gs[g];
+                r.pad = 0;
+                r.prev = C.prev;
+                r.cur = make_uint2(d[2 * g], d[2 * g + 1]);
+                kw->q[*kwn + (uint32_t)__popcll(kb & lanes_lt)] = r;
+              }
+              *kwn += nq;
+            } else if (kl) {
+              mg = ev_e;
+            }
+          }
+        }
+        fast_event(P, ev_e, C, mg, gs[g], d[2 * g], d[2 * g + 1], gpos + 8 * g, live, lanes_lt, ev_seg, ev_count);
         C.prev = make_uint2(d[2 * g], d[2 * g + 1]);
       }
     }
@@ -682,12 +808,6 @@ __device__ inline uint32_t file_of_pos(const ScanParams& P, uint64_t pos) {
   return find_file(P.off, P.region_file[r], hi, pos);
 }
 
-// ASCII lowercase of 8 bytes at once (bytes 'A'-'Z' gain 0x20)
-__device__ inline uint64_t lower64(uint64_t x) {
-  const uint64_t t = x & 0x7F7F7F7F7F7F7F7Full;
-  const uint64_t up = ((t + 0x3F3F3F3F3F3F3F3Full) ^ (t + 0x2525252525252525ull)) & ~x & 0x8080808080808080ull;
-  return x | (up >> 2);
-}
 
 // The report blob's tables (LDS, or global memory when the blob is too big).
 struct RepView {
@@ -870,11 +990,22 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
   __shared__ __align__(16) uint8_t smem[kFuse ? kReportLds : kFastImgMax + (kPair ? kFastCols * kFastCols * 2 : 0)];
   __shared__ uint64_t hbuf[kFuse ? kReportHitCap : 1];
   __shared__ uint32_t hcnt[kFuse ? kFastThreads / 64 : 1];
+  // keyword states' records and local bits (kw_resolve; not in the exp shapes)
+  constexpr bool kKw = !kFuse && !kPair && CH == 1 && kWin != 1;
+  __shared__ __align__(16) FastKwRec kwrec[kKw ? kFastKwStates * kFastKwPer : 1];
+  __shared__ uint16_t kwmap[kKw ? kFastKwBits : 1];
+  __shared__ __align__(16) FastEvent kwq[kKw ? kFastThreads / 64 * kFastKwQ : 1];
   const AcDev& ac = P.rs.ac;
   {
     const uint32_t words = (kFuse ? ac.rep_bytes : ac.fast_bytes) / 4;
     const uint32_t* src = (const uint32_t*)ac.fast_lds;
     for (uint32_t i = threadIdx.x; i < words; i += kFastThreads) ((uint32_t*)smem)[i] = src[i];
+    if (kKw && ac.fast_kw_n) {
+      const uint32_t rw = ac.fast_kw_n * kFastKwPer * (uint32_t)sizeof(FastKwRec) / 4;
+      for (uint32_t i = threadIdx.x; i < rw; i += kFastThreads) ((uint32_t*)kwrec)[i] = ((const uint32_t*)ac.fast_kw)[i];
+      const uint16_t* mp = (const uint16_t*)(ac.fast_kw + (size_t)ac.fast_kw_n * kFastKwPer * sizeof(FastKwRec));
+      for (uint32_t i = threadIdx.x; i < kFastKwBits; i += kFastThreads) kwmap[i] = mp[i];
+    }
     if (kPair) {
       const uint32_t* ps = (const uint32_t*)(ac.fast_lds + ac.o_pair);
       for (uint32_t i = threadIdx.x; i < kFastCols * kFastCols / 2; i += kFastThreads)
@@ -905,6 +1036,8 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
   uint64_t u = (uint64_t)blockIdx.x * kFastThreads + threadIdx.x;
   FastChain<V> C[CH];
   uint4 nxt[CH][V];
+  const KwScan kws{kwrec, kwmap, kwq + (kKw ? (threadIdx.x >> 6) * kFastKwQ : 0), kKw ? ac.fast_ev_entry : out_e};
+  uint32_t kwn = 0;  // wave-uniform: records in this wave's keyword queue
   if (u < units) {
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
@@ -978,20 +1111,22 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
         } else if (kWin == 2) {
           const uint4 v = C[0].cur[k];
           const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-          fast_window<V, kMode, 2>(P, T, out_e, C[0], d, C[0].pos + 16 * k, live, lanes_lt, ev_seg, &ev_count);
+          fast_window<V, kMode, 2>(P, T, out_e, C[0], d, C[0].pos + 16 * k, live, lanes_lt, ev_seg, &ev_count,
+                                   kKw ? &kws : nullptr, &kwn);
         } else if (kWin == 8) {
           if (k % 4 == 0) {
             const uint4 a = C[0].cur[k], b = C[0].cur[k + 1 < V ? k + 1 : k];
             const uint4 c2 = C[0].cur[k + 2 < V ? k + 2 : k], d2 = C[0].cur[k + 3 < V ? k + 3 : k];
             const uint32_t d[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c2.x, c2.y, c2.z, c2.w, d2.x, d2.y, d2.z, d2.w};
-            fast_window<V, kMode, 8>(P, T, out_e, C[0], d, C[0].pos + 16 * k, live, lanes_lt, ev_seg, &ev_count);
+            fast_window<V, kMode, 8>(P, T, out_e, C[0], d, C[0].pos + 16 * k, live, lanes_lt, ev_seg, &ev_count,
+                                     kKw ? &kws : nullptr, &kwn);
           }
         } else if (kWin == 4) {
           if (k % 2 == 0) {
             const uint4 v = C[0].cur[k], w = C[0].cur[k + 1 < V ? k + 1 : k];
             const uint32_t d[8] = {v.x, v.y, v.z, v.w, w.x, w.y, w.z, w.w};
             fast_window<V, kMode, 4, kPair>(P, T, out_e, C[0], d, C[0].pos + 16 * k, live, lanes_lt, ev_seg,
-                                            &ev_count);
+                                            &ev_count, kKw ? &kws : nullptr, &kwn);
           }
         } else {
           const uint4 v = C[0].cur[k];
@@ -1012,6 +1147,7 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
         }
       }
     }
+    if (kKw && kwn) kw_drain(P, T, kws, out_e, kwn, lane);  // (wave-uniform)
     u = un;
     if (kFuse && !(P.report_mode & 4)) {  // whole rounds of 64 only: the wave goes back to streaming after them
       const uint32_t lim = ev_count < P.ev_cap_per_wave ? ev_count : (uint32_t)P.ev_cap_per_wave;
@@ -2360,6 +2496,13 @@ struct GateParams {
   uint64_t pac_always;  // path progs without a literal filter
   uint32_t n_progs;
   const uint32_t* pdfa;  // per program: its MatchString DFA record (kPathDfaRec u32; valid flag last)
+  uint32_t* defer;       // k_path_gate kPass 1: files a path program may match ([0] = count), for kPass 2
+  uint32_t pac_lds;      // dynamic LDS bytes of the launch (0: the automaton stays in global memory)
+  // kPass 1's test, without a per-program loop: the literal-mask bits of the
+  // global allow paths / of the rules' paths and allow paths, and whether one
+  // of them has no bit (it may always match)
+  uint64_t gpath_bits, rpath_bits;
+  uint32_t gpath_nobit, rpath_nobit;
 };
 
 __device__ inline gre::VmScratch make_scratch(uint8_t* base, const RuleSetDev& rs) {
@@ -2500,10 +2643,21 @@ struct PacLit {
 // kLds: the literal automaton staged in LDS; without (the launch after the
 // scan) it is read from global memory (L2), so the gate's blocks fit beside
 // k_report's, which take a CU's whole LDS.
-template <bool kLds>
+// kPass 0: every file, the MatchString DFA / Pike VM where a literal occurs
+// (one VM scratch slot per lane: the grid is capped at vm_threads).
+// kPass 1: every file, at full occupancy (no VM scratch): a file for which
+// some path program may match (a literal occurs, a byte >= 0x80, a program
+// without literals) is appended to G.defer and left alone; every other file
+// is decided here -- no program can match its path.  kPass 2: the deferred
+// files, as kPass 0.  (kPass 0's grid -- two blocks per CU -- left the AC walk
+// latency-bound: 0.23 ms for 2.25 M paths that no literal occurs in.)
+// (kLds: the automaton in dynamic LDS of G.pac_lds bytes, 0 = global memory;
+// the builtin rules' blob is ~20 KiB, which a static 16 KiB array missed:
+// every AC step was an L2 round trip)
+template <bool kLds, int kPass = 0>
 __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
-  __shared__ __align__(16) uint8_t pl[kLds ? 16384 : 16];
-  const bool lds = kLds && G.pac && G.pac_bytes <= sizeof(pl);
+  extern __shared__ __align__(16) uint8_t pl[];
+  const bool lds = kLds && G.pac && G.pac_bytes <= G.pac_lds;
   if (lds) {
     for (uint32_t i = threadIdx.x; i < G.pac_bytes / 4; i += blockDim.x) ((uint32_t*)pl)[i] = ((const uint32_t*)G.pac)[i];
     __syncthreads();
@@ -2519,16 +2673,50 @@ __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
   const uint32_t nthreads = gridDim.x * blockDim.x;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   gre::VmScratch sc = make_scratch(G.scratch + (uint64_t)t * G.scratch_stride, G.rs);
-  for (uint32_t f = t; f < G.n_files; f += nthreads) {
-    const uint8_t* path = G.paths + G.path_off[f];
-    const uint32_t plen = (uint32_t)(G.path_off[f + 1] - G.path_off[f]);
+  // the next file's path offsets are loaded a file ahead, and a path is read
+  // with aligned 16-byte loads (the next block before the current one is
+  // walked): a byte load per step was a chain of dependent global reads
+  // (0.21 ms for 2.25 M paths)
+  const uint32_t n_items = kPass == 2 ? G.defer[0] : G.n_files;
+  auto file_at = [&](uint32_t q) { return kPass == 2 ? G.defer[1 + q] : q; };
+  uint64_t po0 = 0, po1 = 0;
+  if (t < n_items) {
+    const uint32_t f0 = file_at(t);
+    po0 = G.path_off[f0];
+    po1 = G.path_off[f0 + 1];
+  }
+  for (uint32_t q = t; q < n_items; q += nthreads) {
+    const uint32_t f = file_at(q);
+    const uint8_t* path = G.paths + po0;
+    const uint32_t plen = (uint32_t)(po1 - po0);
+    if (q + nthreads < n_items) {
+      const uint32_t fn = file_at(q + nthreads);
+      po0 = G.path_off[fn];
+      po1 = G.path_off[fn + 1];
+    }
     uint64_t mask = ~0ull;
     if (G.pac) {
       mask = G.pac_always;
       uint32_t st = 0;
       bool hi = false;
-      for (uint32_t i = 0; i < plen; ++i) {
-        const uint8_t b = path[i];
+      const uintptr_t pbase = reinterpret_cast<uintptr_t>(path), pend = pbase + plen;
+      uintptr_t blk = pbase & ~(uintptr_t)15;
+      auto load16 = [](uintptr_t a) {
+        return *as_global<__attribute__((address_space(1))) const u32x4>(reinterpret_cast<const void*>(a));
+      };
+      u32x4 v{0, 0, 0, 0}, nv{0, 0, 0, 0};
+      if (plen) v = load16(blk);
+      if (blk + 16 < pend) nv = load16(blk + 16);
+      uint32_t k = (uint32_t)(pbase - blk);  // byte of v (0..15)
+      for (uint32_t i = 0; i < plen; ++i, ++k) {
+        if (k == 16) {  // the prefetched block; the one after it is issued now
+          blk += 16;
+          v = nv;
+          if (blk + 16 < pend) nv = load16(blk + 16);
+          k = 0;
+        }
+        const uint32_t wd = k < 8 ? (k < 4 ? v.x : v.y) : (k < 12 ? v.z : v.w);
+        const uint8_t b = (uint8_t)(wd >> (8 * (k & 3)));
         hi |= b >= 0x80;
         const uint32_t nx = delta[st * G.pac_classes + cls[b]];
         st = nx & 0x7FFFu;
@@ -2551,6 +2739,15 @@ __global__ __launch_bounds__(256) void k_path_gate(GateParams G) {
       const uint32_t b = prog < G.n_progs ? pbit[prog] : 0xFFu;
       return b == 0xFFu || ((mask >> b) & 1);
     };
+    if (kPass == 1) {  // a program that may match: the file goes to kPass 2 whole
+      const bool any = !G.pac || G.gpath_nobit || (mask & G.gpath_bits) ||
+                       (G.any_rule_paths && (G.rpath_nobit || (mask & G.rpath_bits)));
+      if (any) {
+        G.defer[1 + atomicAdd(&G.defer[0], 1u)] = f;
+        continue;
+      }
+      if (!G.any_rule_paths) continue;  // no global allow path can match, and no rule has a path
+    }
     // MatchString: the program's (?s:.)*?(?:re) DFA walked once over the path
     // (ruleset.cpp path_dfa), the Pike VM when there is none or a rune the DFA
     // cannot decide
@@ -2908,6 +3105,7 @@ struct VerifyParams {
   CapJob* matches;   // k_verify_fast's matches, for k_allow
   uint64_t match_cap;
   uint32_t no_accel;  // 1 but in the exp build with TSG_ACCEL: DFA run acceleration (measured slower)
+  uint32_t jpw;       // k_verify: jobs per wave (64 = every lane; fewer = lanes [0, jpw) of each wave)
 };
 
 
@@ -3836,14 +4034,23 @@ __device__ inline uint32_t run_job(const VerifyParams& V, uint32_t job, Pos pos0
   return 0;
 }
 
+// Lanes of one wave run their jobs in lock-step: a wave whose 64 jobs walk
+// different windows, DFA paths and emits executes the union of them, so on a
+// short job list (a few waves per CU: configs[2]) the wave's time grows with
+// its job count.  V.jpw < 64 gives each wave only jpw jobs (lanes [0, jpw))
+// and the list more waves.
 template <uint32_t kBlock, class Pos>
 __global__ __launch_bounds__(kBlock) void k_verify(VerifyParams V) {
   __shared__ __align__(16) uint16_t dfa_lds[kVerifyDfaLds / 2];
   __shared__ __align__(16) uint8_t cls_lds[128];
-  const uint32_t nthreads = gridDim.x * blockDim.x;
-  gre::VmScratch sc = make_scratch(V.scratch + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * V.scratch_stride, V.rs);
+  const uint32_t jpw = V.jpw;
+  const uint32_t per_block = (kBlock / 64) * jpw;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t jslot = (threadIdx.x >> 6) * jpw + lane;  // this lane's job in the block's group
+  // (VM scratch per active lane: grid x per_block <= vm_threads, checked by the launch)
+  gre::VmScratch sc = make_scratch(V.scratch + ((uint64_t)blockIdx.x * per_block + jslot) * V.scratch_stride, V.rs);
   const uint32_t n_jobs = *V.n_jobs_dev;
-  for (uint32_t jb = blockIdx.x * blockDim.x; jb < n_jobs; jb += nthreads) {  // block-uniform
+  for (uint32_t jb = blockIdx.x * per_block; jb < n_jobs; jb += gridDim.x * per_block) {  // block-uniform
     const uint32_t r0 = (uint32_t)(V.keys[V.job_start[jb]] >> kPosBits);
     const RuleDev& rd0 = V.rs.rules[r0];
     const bool staged = rd0.dfa_off != kNoFollow && rd0.dfa_size * 2 <= kVerifyDfaLds;
@@ -3860,8 +4067,8 @@ __global__ __launch_bounds__(kBlock) void k_verify(VerifyParams V) {
       for (uint32_t i = threadIdx.x; i < rd0.nfa_bytes / 4; i += blockDim.x) ((uint32_t*)dfa_lds)[i] = src[i];
     }
     __syncthreads();
-    const uint32_t j = jb + threadIdx.x;
-    if (j >= n_jobs) continue;
+    const uint32_t j = jb + jslot;
+    if (lane >= jpw || j >= n_jobs) continue;
     const uint64_t t0 = V.prof ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz wall clock
     const uint64_t c0 = V.job_start[j];
     const uint64_t c1 = (j + 1 < n_jobs) ? V.job_start[j + 1] : V.n_cands;
@@ -4306,23 +4513,46 @@ __global__ __launch_bounds__(256) void k_nl_spans(const uint8_t* data, uint64_t 
       need = phase == 0 ? sp <= next : ((l & kNlFull) && (!lim || sp > next));
     }
   }
+  // the needed spans four at a time: their 16 KiB of loads are issued
+  // before any count, so a wave keeps four spans in flight instead of one
+  // (one span per round left the kernel latency-bound: a wave inside a big
+  // candidate file walked its 64 spans one load latency each)
   uint64_t m = __ballot(need);
   while (m) {
-    const uint32_t k = __builtin_ctzll(m);
-    m &= m - 1;
-    const uint64_t b = (sp0 + k) * kNlBlock + 64ull * lane;
-    uint32_t cnt = 0;
-    if (b + 64 <= nbytes) {
+    uint32_t ks[4];
+    uint32_t nk = 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint4 v = *(const uint4*)(data + b + 16 * q);
-        cnt += nl_count_dword(v.x) + nl_count_dword(v.y) + nl_count_dword(v.z) + nl_count_dword(v.w);
+    for (int t = 0; t < 4; ++t) {
+      ks[t] = m ? (uint32_t)__builtin_ctzll(m) : 64u;
+      if (m) {
+        m &= m - 1;
+        ++nk;
       }
-    } else {
-      for (uint64_t x = b; x < b + 64 && x < nbytes; ++x) cnt += data[x] == '\n';
     }
-    for (uint32_t d = 32; d; d >>= 1) cnt += __shfl_xor(cnt, d);
-    if (lane == 0) nl_blocks[sp0 + k] = cnt;
+    uint4 v[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint64_t b = (sp0 + ks[t]) * kNlBlock + 64ull * lane;
+      const bool full = (uint32_t)t < nk && b + 64 <= nbytes;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[t][q] = full ? *(const uint4*)(data + b + 16 * q) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if ((uint32_t)t >= nk) break;
+      const uint64_t b = (sp0 + ks[t]) * kNlBlock + 64ull * lane;
+      uint32_t cnt = 0;
+      if (b + 64 <= nbytes) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          cnt += nl_count_dword(v[t][q].x) + nl_count_dword(v[t][q].y) + nl_count_dword(v[t][q].z) +
+                 nl_count_dword(v[t][q].w);
+      } else {
+        for (uint64_t x = b; x < b + 64 && x < nbytes; ++x) cnt += data[x] == '\n';
+      }
+      for (uint32_t d = 32; d; d >>= 1) cnt += __shfl_xor(cnt, d);
+      if (lane == 0) nl_blocks[sp0 + ks[t]] = cnt;
+    }
   }
   }
 }
@@ -4412,6 +4642,7 @@ struct FindParams {
   uint32_t* gran_carry;
   uint64_t n_gran;
   uint8_t* arena;
+  uint64_t arena_cap;  // bytes of `arena` (sized before find_bytes is known; a larger need redoes the stage)
   uint64_t* sort_key;
   uint32_t* sort_idx;
   uint32_t rank_bits;  // bits of RuleDev::id_rank: sort key = file << rank_bits | rank
@@ -5241,7 +5472,7 @@ __device__ inline uint64_t arena_gran_seg(const FindParams& F, uint64_t g, uint6
 // between the covering segments of the chunk's granule and the next one,
 // source bytes from the batch, bytes inside the file's censor intervals as '*'.
 __global__ __launch_bounds__(256) void k_arena_fill(FindParams F) {
-  const uint64_t total = F.ctrl->find_bytes;
+  const uint64_t total = F.ctrl->find_bytes < F.arena_cap ? F.ctrl->find_bytes : F.arena_cap;  // (cap: redone larger)
   for (uint64_t a = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; a < total;
        a += (uint64_t)gridDim.x * blockDim.x * 16) {
     // last segment with seg_off <= a: in [covering(g), covering(g + 1)]
@@ -5856,6 +6087,7 @@ struct DevImage {
   DBuf<uint32_t> lower_map;  // kLowerMap: {rune, lowercase} pairs
   uint32_t n_uni = 0, uni_back = 0;
   uint32_t pac_states = 0, pac_classes = 0, pac_bytes = 0;
+  std::vector<uint8_t> pac_prog_bit;  // per regex: its bit in k_path_gate's literal mask (0xFF: none)
   uint32_t o_pac_cls = 0, o_pac_out_off = 0, o_pac_out = 0, o_pac_lits = 0, o_pac_req = 0, o_pac_bit = 0;
   uint64_t pac_always = 0;
   RuleSetDev view{};
@@ -5956,6 +6188,7 @@ struct tsg_engine {
   DBuf<FindRec> f_rec, f_rec2;
   DBuf<uint32_t> f_ties;   // k_tie_list
   DBuf<tsg_loc> out_locs;  // k_out_locs
+  DBuf<uint32_t> gate_defer;  // k_path_gate: files for its DFA / VM pass ([0] = count)
   DBuf<uint8_t> f_arena;
   DBuf<uint32_t> f_gran, f_gcarry;  // arena granule index (k_arena_gran_*)
   DBuf<uint64_t> f_lkeyb;            // Match bytes 8..15 (k_match_prefix)
@@ -5965,7 +6198,9 @@ struct tsg_engine {
   DBuf<uint32_t> f_gstart;
   DBuf<uint8_t> f_dense;
   uint64_t* h_dense = nullptr;  // page-locked: the region's bytes and file groups, read mid-pipeline
-  hipEvent_t ev_dense = nullptr, ev_dfill = nullptr, ev_frec = nullptr;
+  uint64_t* h_find = nullptr;   // page-locked: the arena's find_bytes / match_bytes, read under the arena fill
+  uint64_t arena_need = 0;      // arena capacity the next call starts with (the last need + 1/4)
+  hipEvent_t ev_dense = nullptr, ev_dfill = nullptr, ev_frec = nullptr, ev_fb = nullptr;
   bool dense_active = false;   // this call's locations have dense_at (dense_begin)
   DBuf<uint64_t> f_pmax;       // per location: (file << 40 | max end so far in its file), k_dense_fill's censoring
   DBuf<uint32_t> f_spidx;      // per location: exclusive prefix of the sparse ones (FindParams::slot_base)
@@ -6482,6 +6717,7 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
         im.pac_states = (uint32_t)S;
         im.pac_classes = (uint32_t)K;
         im.pac_always = always;
+        im.pac_prog_bit = bit;
       }
     }
   }
@@ -6508,7 +6744,7 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
   v.max_ncap = max_ncap;
   v.max_ninst_cap = max_ninst_cap;
   const uint8_t* fast = nullptr;
-  uint32_t o_out_off = 0, o_out_pat = 0, o_pats = 0, o_pbytes = 0, rep_bytes = 0, o_pair = 0;
+  uint32_t o_out_off = 0, o_out_pat = 0, o_pats = 0, o_pbytes = 0, rep_bytes = 0, o_pair = 0, o_fkw = 0;
   if (!ac.fast.empty()) {
     // k_report blob: the scan image followed by the small output tables
     std::vector<uint8_t> blob(ac.fast.begin(), ac.fast.end());
@@ -6525,13 +6761,19 @@ int upload_ruleset(tsg_engine* e, const tsg_ruleset* rs) {
     blob.resize((blob.size() + 15) & ~(size_t)15);
     rep_bytes = (uint32_t)blob.size();  // (k_report stages [0, rep_bytes); the pair table follows)
     if (!ac.fast_pair.empty()) o_pair = put(ac.fast_pair.data(), ac.fast_pair.size() * 2);
+    // the keyword states' records and the local bits' keyword ids (k_scan_fast stages them in LDS)
+    o_fkw = put(ac.fast_kw.data(), ac.fast_kw.size());
+    std::vector<uint16_t> kw_map(ac.fast_kw_map);
+    kw_map.resize(kFastKwBits, 0);  // (the scan stages all kFastKwBits entries)
+    put(kw_map.data(), kw_map.size() * 2);
     HIP_TRY(im.fast.ensure(blob.size() + 16));
     HIP_TRY(hipMemcpy(im.fast.p, blob.data(), blob.size(), hipMemcpyHostToDevice));
     fast = im.fast.p;
   }
   v.ac = AcDev{im.delta.p, im.cls.p, im.out_off.p, im.out_pat.p, im.pats.p, im.pat_bytes.p, im.pat_rules.p,
-               ac.nstates, ac.nclasses, fast, (uint32_t)ac.fast.size(), ac.fast_out_entry, ac.depth,
-               rep_bytes, o_out_off, o_out_pat, o_pats, o_pbytes, o_pair};
+               ac.nstates, ac.nclasses, fast, (uint32_t)ac.fast.size(), ac.fast_out_entry,
+               fast ? ac.fast_ev_entry : ac.fast_out_entry, fast ? ac.fast_ev_entry - ac.fast_out_entry : 0u,
+               fast ? fast + o_fkw : nullptr, ac.depth, rep_bytes, o_out_off, o_out_pat, o_pats, o_pbytes, o_pair};
   // keywords whose lowercase holds a non-ASCII rune (k_uni_keywords)
   {
     std::vector<uint8_t> ub;
@@ -6588,6 +6830,7 @@ hipError_t ensure_side(tsg_engine* e) {
   if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_dense, hipEventDisableTiming);
   if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_dfill, hipEventDisableTiming);
   if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_frec, hipEventDisableTiming);
+  if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_fb, hipEventDisableTiming);
   if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_nl[0], hipEventDisableTiming);
   if (r == hipSuccess) r = hipEventCreateWithFlags(&e->ev_nl[1], hipEventDisableTiming);
   if (r == hipSuccess) r = hipEventCreate(&e->ev_pg[0]);  // (timed: the path gate's stage time)
@@ -6662,17 +6905,9 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
   HIP_TRY(e->region_file.ensure(P.n_regions + 1));
   P.region_file = e->region_file.p;
   if (P.n_files) {
-    HIP_TRY(e->region_tmp.ensure(P.n_regions + 1));
-    HIP_TRY(hipMemsetAsync(e->region_tmp.p, 0, (P.n_regions + 1) * 4, s));
-    hipLaunchKernelGGL(k_region_mark, dim3((P.n_files + 255) / 256), dim3(256), 0, s, P.off, P.n_files,
-                       P.n_regions, e->region_tmp.p, P.ctrl);
+    hipLaunchKernelGGL(k_region_fill, dim3((P.n_files + 255) / 256), dim3(256), 0, s, P.off, P.n_files, P.n_regions,
+                       e->region_file.p, P.ctrl);
     HIP_TRY(hipGetLastError());
-    size_t tmp = 0;
-    HIP_TRY(hipcub::DeviceScan::InclusiveScan(nullptr, tmp, e->region_tmp.p, e->region_file.p, hipcub::Max(),
-                                              (int)P.n_regions, s));
-    HIP_TRY(e->cub_tmp.ensure(tmp + 1));
-    HIP_TRY(hipcub::DeviceScan::InclusiveScan(e->cub_tmp.p, tmp, e->region_tmp.p, e->region_file.p, hipcub::Max(),
-                                              (int)P.n_regions, s));
   }
   if (!e->num_cus) {
     hipDeviceProp_t prop;
@@ -7169,27 +7404,94 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   hipLaunchKernelGGL(k_seg_total, dim3(1), dim3(64), 0, s, F);
   hipLaunchKernelGGL(k_find_finalize, dim3(lane_blocks), dim3(256), 0, s, F);
   HIP_TRY(hipGetLastError());
-  Ctrl c;
-  if (int rc = read_ctrl(e, &c)) return rc;  // the arena size
-  if (res->impl.timings.size() > 25) {
-    res->impl.timings[24] = (double)c.find_bytes;
-    res->impl.timings[25] = (double)c.match_bytes;
+  // The arena's size (find_bytes) is known only on the device.  The arena
+  // stage is queued at a capacity that covers it almost always (the last
+  // call's need + 1/4, at least 16 MiB and 1 KiB per location) while the
+  // size comes back by an async copy; the host lays out the result block
+  // under that stage and redoes the stage, larger, in the rare case the
+  // capacity was short.  (A blocking read here left the GPU idle for the
+  // round trip and the next launches: ~0.1 ms on configs[2], profiles/r05zd.)
+  const bool use_dma = experiment_env("TSG_DMA_OFF") == nullptr;
+  HIP_TRY(e->out_locs.ensure(n_locs));
+  if (!e->h_find) HIP_TRY(hipHostMalloc((void**)&e->h_find, sizeof(Ctrl), hipHostMallocDefault));
+  HIP_TRY(hipMemcpyAsync(e->h_find, e->ctrl.p, sizeof(Ctrl), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipEventRecord(e->ev_fb, s));
+  uint64_t cap = std::max<uint64_t>({1ull << 24, n_locs * 1024, e->arena_need});
+  if (!use_dma) {  // (exp A/B: the copies below are queued now and need the layout: read the size first)
+    HIP_TRY(hipEventSynchronize(e->ev_fb));
+    cap = ((const Ctrl*)e->h_find)->find_bytes;
   }
-  HIP_TRY(e->f_arena.ensure(c.find_bytes + 16));
-  F.arena = e->f_arena.p;
-  F.n_gran = c.find_bytes / kArenaGran + 2;
-  const uint32_t gran_blocks = (uint32_t)((F.n_gran + 1023) / 1024);
-  HIP_TRY(e->f_gran.ensure(F.n_gran));
-  HIP_TRY(e->f_gcarry.ensure(gran_blocks + 1));
-  F.gran_seg = e->f_gran.p;
-  F.gran_carry = e->f_gcarry.p;
-  // the result's page-locked block, laid out now.  The Code records and the
-  // kept locations are final already: their D2H starts on a side stream under
-  // the arena fill; the string arena's (most of the bytes) follows it there,
-  // under the Match sorts
   const uint64_t tie_cap = std::max<uint64_t>(1024, n_locs / 8);
   const size_t rec_bytes = n_locs * sizeof(FindRec);
-  const size_t o_locs = (rec_bytes + c.find_bytes + 15) & ~(size_t)15;
+  HIP_TRY(e->f_lkeyb.ensure(n_locs));
+  HIP_TRY(e->f_ties.ensure(tie_cap));
+  // k_out_locs, then the arena and the (file, RuleID rank, Match) order
+  auto arena_stage = [&](uint64_t arena_cap) -> int {
+    HIP_TRY(e->f_arena.ensure(arena_cap + 16));
+    F.arena = e->f_arena.p;
+    F.arena_cap = arena_cap;
+    F.n_gran = arena_cap / kArenaGran + 2;
+    const uint32_t gran_blocks = (uint32_t)((F.n_gran + 1023) / 1024);
+    HIP_TRY(e->f_gran.ensure(F.n_gran));
+    HIP_TRY(e->f_gcarry.ensure(gran_blocks + 1));
+    F.gran_seg = e->f_gran.p;
+    F.gran_carry = e->f_gcarry.p;
+    HIP_TRY(hipMemsetAsync(F.gran_seg, 0, F.n_gran * 4, s));
+    hipLaunchKernelGGL(k_arena_gran_mark, dim3((uint32_t)((n_seg + 255) / 256)), dim3(256), 0, s, F);
+    hipLaunchKernelGGL(k_arena_gran_scan, dim3(gran_blocks), dim3(1024), 0, s, F);
+    hipLaunchKernelGGL(k_arena_gran_carry, dim3(1), dim3(1024), 0, s, F, gran_blocks);
+    hipLaunchKernelGGL(k_arena_fill, dim3((uint32_t)std::min<uint64_t>((arena_cap / 16 + 255) / 256 + 1, 8192)),
+                       dim3(256), 0, s, F);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(e->ev_fill, s));
+    // order: (file, RuleID rank) major, Match prefix minor -- two stable radix
+    // sorts, least significant key first (f_lkey / f_lkey2 / f_lslot* are free now)
+    if (R.dense) HIP_TRY(hipStreamWaitEvent(s, e->ev_dfill, 0));  // (the Match windows of dense files)
+    hipLaunchKernelGGL(k_match_prefix, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->f_arena.p, e->f_dense.p,
+                       n_locs, e->f_lkey.p, e->f_lkeyb.p, e->f_lslot.p);
+    size_t tmp2 = 0;
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p, e->f_lslot2.p,
+                                               (int)n_locs, 0, 64, s));
+    HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
+    // Match bytes 8..15, then (stable) bytes 0..7, then (file, RuleID rank)
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->f_lkeyb.p, e->f_lkey2.p, e->f_lslot.p,
+                                               e->f_lslot2.p, (int)n_locs, 0, 64, s));
+    hipLaunchKernelGGL(k_gather_u64, dim3(lane_blocks), dim3(256), 0, s, e->f_lkey.p, e->f_lslot2.p, n_locs, e->keys2.p);
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys2.p, e->f_lkey2.p, e->f_lslot2.p,
+                                               e->f_lslot.p, (int)n_locs, 0, 64, s));
+    hipLaunchKernelGGL(k_gather_u64, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lslot.p, n_locs, e->keys2.p);
+    tmp2 = 0;
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->keys2.p, e->keys.p, e->f_lslot.p, e->vals2.p,
+                                               (int)n_locs, 0, key_bits, s));
+    HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys2.p, e->keys.p, e->f_lslot.p, e->vals2.p,
+                                               (int)n_locs, 0, key_bits, s));
+    hipLaunchKernelGGL(k_find_gather, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->vals2.p, n_locs, e->f_rec2.p);
+    HIP_TRY(hipMemsetAsync(&e->ctrl.p->n_ties, 0, 8, s));
+    hipLaunchKernelGGL(k_tie_list, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lkey.p, e->f_lkeyb.p, e->vals2.p,
+                       n_locs, e->f_ties.p, tie_cap, e->ctrl.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(e->ev_frec, s));
+    return TSG_OK;
+  };
+  // the kept locations as tsg_loc records
+  hipLaunchKernelGGL(k_out_locs, dim3(lane_blocks), dim3(256), 0, s, e->locs2.p, n_locs, e->out_locs.p, e->ctrl.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(e->ev_code, s));
+  if (int rc = arena_stage(cap)) return rc;
+  HIP_TRY(hipEventSynchronize(e->ev_fb));  // (the GPU runs the arena stage meanwhile)
+  const uint64_t find_bytes = ((const Ctrl*)e->h_find)->find_bytes;
+  const uint64_t match_bytes = ((const Ctrl*)e->h_find)->match_bytes;
+  e->arena_need = find_bytes + find_bytes / 4;
+  if (find_bytes > cap) {  // short: the stage again at the size now known
+    if (int rc = arena_stage(find_bytes)) return rc;
+  }
+  if (res->impl.timings.size() > 25) {
+    res->impl.timings[24] = (double)find_bytes;
+    res->impl.timings[25] = (double)match_bytes;
+  }
+  // the result's page-locked block
+  const size_t o_locs = (rec_bytes + find_bytes + 15) & ~(size_t)15;
   const size_t o_flags = o_locs + n_locs * sizeof(tsg_loc);
   const size_t o_ties = (o_flags + n_files + 15) & ~(size_t)15;
   const size_t o_ctrl = (o_ties + tie_cap * 4 + 15) & ~(size_t)15;
@@ -7205,87 +7507,29 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   R.file_flags = {base + o_flags, n_files};
   R.ties = {(uint32_t*)(base + o_ties), 0};
   R.ctrl_off = o_ctrl;
-  // the kept locations as tsg_loc records
-  HIP_TRY(e->out_locs.ensure(n_locs));
-  hipLaunchKernelGGL(k_out_locs, dim3(lane_blocks), dim3(256), 0, s, e->locs2.p, n_locs, e->out_locs.p, e->ctrl.p);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(e->ev_code, s));
-  // The kept locations and the string arena go back on a DMA engine
-  // (dma_d2h) once their producers are done -- issued after the rest of the
-  // stage is enqueued, so the sorts below keep the CUs; without it as
-  // blit-kernel copies (hipMemcpyAsync) on the side stream.  (hipMemcpyAsync
-  // with hipMemcpyDeviceToDeviceNoCU into the page-locked block still ran as
-  // blit kernels, profiles/r05h_c4.)
-  const bool use_dma = experiment_env("TSG_DMA_OFF") == nullptr;
-  if (!use_dma) {
-    HIP_TRY(hipStreamWaitEvent(e->side, e->ev_code, 0));
-    HIP_TRY(hipMemcpyAsync(R.locs.p, e->out_locs.p, n_locs * sizeof(tsg_loc), hipMemcpyDeviceToHost, e->side));
-  }
-  if (c.find_bytes) {
-    HIP_TRY(hipMemsetAsync(F.gran_seg, 0, F.n_gran * 4, s));
-    hipLaunchKernelGGL(k_arena_gran_mark, dim3((uint32_t)((n_seg + 255) / 256)), dim3(256), 0, s, F);
-    hipLaunchKernelGGL(k_arena_gran_scan, dim3(gran_blocks), dim3(1024), 0, s, F);
-    hipLaunchKernelGGL(k_arena_gran_carry, dim3(1), dim3(1024), 0, s, F, gran_blocks);
-    hipLaunchKernelGGL(k_arena_fill, dim3((uint32_t)std::min<uint64_t>((c.find_bytes / 16 + 255) / 256 + 1, 8192)),
-                       dim3(256), 0, s, F);
-  }
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(e->ev_fill, s));
-  if (!use_dma) {
-    HIP_TRY(hipStreamWaitEvent(e->side, e->ev_fill, 0));
-    if (c.find_bytes)
-      HIP_TRY(hipMemcpyAsync(base + rec_bytes, e->f_arena.p, c.find_bytes, hipMemcpyDeviceToHost, e->side));
-  }
-  HIP_TRY(hipEventRecord(e->ev_side, e->side));
-  // order: (file, RuleID rank) major, Match prefix minor -- two stable radix
-  // sorts, least significant key first (f_lkey / f_lkey2 / f_lslot* are free now)
-  HIP_TRY(e->f_lkeyb.ensure(n_locs));
-  if (R.dense) HIP_TRY(hipStreamWaitEvent(s, e->ev_dfill, 0));  // (the Match windows of dense files)
-  hipLaunchKernelGGL(k_match_prefix, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->f_arena.p, e->f_dense.p,
-                     n_locs, e->f_lkey.p, e->f_lkeyb.p, e->f_lslot.p);
-  size_t tmp2 = 0;
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p, e->f_lslot2.p,
-                                             (int)n_locs, 0, 64, s));
-  HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
-  // Match bytes 8..15, then (stable) bytes 0..7, then (file, RuleID rank)
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->f_lkeyb.p, e->f_lkey2.p, e->f_lslot.p,
-                                             e->f_lslot2.p, (int)n_locs, 0, 64, s));
-  hipLaunchKernelGGL(k_gather_u64, dim3(lane_blocks), dim3(256), 0, s, e->f_lkey.p, e->f_lslot2.p, n_locs, e->keys2.p);
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys2.p, e->f_lkey2.p, e->f_lslot2.p,
-                                             e->f_lslot.p, (int)n_locs, 0, 64, s));
-  hipLaunchKernelGGL(k_gather_u64, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lslot.p, n_locs, e->keys2.p);
-  tmp2 = 0;
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->keys2.p, e->keys.p, e->f_lslot.p, e->vals2.p,
-                                             (int)n_locs, 0, key_bits, s));
-  HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys2.p, e->keys.p, e->f_lslot.p, e->vals2.p,
-                                             (int)n_locs, 0, key_bits, s));
-  hipLaunchKernelGGL(k_find_gather, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->vals2.p, n_locs, e->f_rec2.p);
-  HIP_TRY(e->f_ties.ensure(tie_cap));
-  hipLaunchKernelGGL(k_tie_list, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lkey.p, e->f_lkeyb.p, e->vals2.p,
-                     n_locs, e->f_ties.p, tie_cap, e->ctrl.p);
-  HIP_TRY(hipGetLastError());
-  if (!use_dma) {
-    HIP_TRY(hipMemcpyAsync(R.frec.p, e->f_rec2.p, rec_bytes, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(R.ties.p, e->f_ties.p, tie_cap * 4, hipMemcpyDeviceToHost, s));
-  }
-  HIP_TRY(hipEventRecord(e->ev_frec, s));
-  HIP_TRY(hipStreamWaitEvent(s, e->ev_side, 0));  // the caller's final synchronisation covers the side copies
-  if (use_dma) {  // (run_pipeline waits for the DMA copies with its final synchronisation)
-    HIP_TRY(hipEventSynchronize(e->ev_code));
-    if (!dma_d2h(e, R.locs.p, e->out_locs.p, n_locs * sizeof(tsg_loc)))
-      HIP_TRY(hipMemcpyAsync(R.locs.p, e->out_locs.p, n_locs * sizeof(tsg_loc), hipMemcpyDeviceToHost, s));
-    if (c.find_bytes) {
-      HIP_TRY(hipEventSynchronize(e->ev_fill));
-      if (!dma_d2h(e, base + rec_bytes, e->f_arena.p, c.find_bytes))
-        HIP_TRY(hipMemcpyAsync(base + rec_bytes, e->f_arena.p, c.find_bytes, hipMemcpyDeviceToHost, s));
+  // The kept locations, the string arena and the ordered records go back on
+  // a DMA engine (dma_d2h) once their producers are done -- the host waits
+  // for each producer's event (the GPU has the rest of the stage queued);
+  // without DMA as copies on the stream.  (hipMemcpyAsync into the
+  // page-locked block ran as blit kernels on the CUs, even with
+  // hipMemcpyDeviceToDeviceNoCU, profiles/r05h_c4.)
+  auto d2h = [&](void* dst, const void* src, size_t bytes, hipEvent_t ev) -> int {
+    if (!bytes) return TSG_OK;
+    if (use_dma) {
+      HIP_TRY(hipEventSynchronize(ev));
+      if (dma_d2h(e, dst, src, bytes)) return TSG_OK;
     }
-    HIP_TRY(hipEventSynchronize(e->ev_frec));  // the ordered records and the tie list
-    if (!dma_d2h(e, R.frec.p, e->f_rec2.p, rec_bytes))
-      HIP_TRY(hipMemcpyAsync(R.frec.p, e->f_rec2.p, rec_bytes, hipMemcpyDeviceToHost, s));
-    if (!dma_d2h(e, R.ties.p, e->f_ties.p, tie_cap * 4))
-      HIP_TRY(hipMemcpyAsync(R.ties.p, e->f_ties.p, tie_cap * 4, hipMemcpyDeviceToHost, s));
-  }
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+    return TSG_OK;
+  };
+  if (int rc = d2h(R.locs.p, e->out_locs.p, n_locs * sizeof(tsg_loc), e->ev_code)) return rc;
+  if (int rc = d2h(base + rec_bytes, e->f_arena.p, find_bytes, e->ev_fill)) return rc;
+  if (int rc = d2h(R.frec.p, e->f_rec2.p, rec_bytes, e->ev_frec)) return rc;
+  if (int rc = d2h(R.ties.p, e->f_ties.p, tie_cap * 4, e->ev_frec)) return rc;
+  // the caller's final synchronisation covers the side stream's copies (the
+  // dense region's, when it did not go to a DMA engine)
+  HIP_TRY(hipEventRecord(e->ev_side, e->side));
+  HIP_TRY(hipStreamWaitEvent(s, e->ev_side, 0));
   R.ties_cap = tie_cap;
   return TSG_OK;
 }
@@ -7924,7 +8168,32 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     G.pdfa = im.u32.p + im.o_pdfa;
     gate_blocks = std::max(1u, std::min<uint32_t>((nf + 255) / 256, e->vm_threads / 256));
     if (!gate_on_side) {
-      hipLaunchKernelGGL(k_path_gate<true>, dim3(gate_blocks), dim3(256), 0, s, G);
+      // the literal pass over every file at full occupancy, then the files a
+      // path program may match with the DFA / VM (grid: one scratch slot per lane)
+      HIP_TRY(e->gate_defer.ensure((size_t)nf + 1));
+      HIP_TRY(hipMemsetAsync(e->gate_defer.p, 0, 4, s));
+      G.defer = e->gate_defer.p;
+      if (!e->num_cus) {
+        hipDeviceProp_t prop;
+        HIP_TRY(hipGetDeviceProperties(&prop, e->device));
+        e->num_cus = (uint32_t)prop.multiProcessorCount;
+      }
+      G.pac_lds = G.pac && G.pac_bytes <= 64 * 1024 ? (G.pac_bytes + 15) & ~15u : 0;
+      auto prog_bit = [&](int prog, uint64_t* bits, uint32_t* nobit) {
+        const uint8_t b = prog >= 0 && (size_t)prog < im.pac_prog_bit.size() ? im.pac_prog_bit[prog] : 0xFF;
+        if (b == 0xFF) *nobit = 1;
+        else *bits |= 1ull << b;
+      };
+      G.gpath_bits = G.rpath_bits = 0;
+      G.gpath_nobit = G.rpath_nobit = 0;
+      for (int x : rs->global_allow_path) prog_bit(x, &G.gpath_bits, &G.gpath_nobit);
+      for (auto& r : rs->rules) {
+        if (r.path >= 0) prog_bit(r.path, &G.rpath_bits, &G.rpath_nobit);
+        for (int x : r.allow_path) prog_bit(x, &G.rpath_bits, &G.rpath_nobit);
+      }
+      const uint32_t ac_blocks = std::max(1u, std::min<uint32_t>((nf + 255) / 256, e->num_cus * 8));
+      hipLaunchKernelGGL((k_path_gate<true, 1>), dim3(ac_blocks), dim3(256), G.pac_lds, s, G);
+      hipLaunchKernelGGL((k_path_gate<true, 2>), dim3(gate_blocks), dim3(256), G.pac_lds, s, G);
       HIP_TRY(hipGetLastError());
     } else {
       HIP_TRY(ensure_side(e));
@@ -7996,6 +8265,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
       // global memory)
       HIP_TRY(hipStreamWaitEvent(e->side, e->fast_timed ? e->ev[11] : e->ev[9], 0));
       HIP_TRY(hipEventRecord(e->ev_pg[0], e->side));
+      G.pac_lds = 0;
       hipLaunchKernelGGL(k_path_gate<false>, dim3(gate_blocks), dim3(256), 0, e->side, G);
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(e->ev_pg[1], e->side));
@@ -8223,6 +8493,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     V.span_hi = (rs->ac.fast.size() || P.big.blob) && nbytes ? e->span_hi.p : nullptr;
     const bool prof = experiment_env("TSG_PROFILE_VERIFY") != nullptr;
     V.no_accel = experiment_env("TSG_ACCEL") == nullptr;
+    V.jpw = 64;
     if (prof) {  // diagnostics only: the job count on the host
       HIP_TRY(hipMemcpyAsync(&n_jobs, e->nsel.p, 4, hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
@@ -8259,7 +8530,9 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     // quicker (0.43 vs 0.62 ms, profiles/r04e); it also serves the per-job
     // profile (TSG_PROFILE_VERIFY) and A/B (TSG_VERIFY_SINGLE).
     const bool long_list = n_cands > (uint64_t)e->num_cus * kVerifyBlockWide * 4;
-    const bool single = (!long_list && !e->verify_split) || prof || experiment_env("TSG_VERIFY_SINGLE") != nullptr;
+    const bool force_split = experiment_env("TSG_VERIFY_SPLIT") != nullptr;  // (A/B: the split on a short list)
+    const bool single = (!long_list && !e->verify_split && !force_split) || prof ||
+                        experiment_env("TSG_VERIFY_SINGLE") != nullptr;
     if (!single) {
       {
         const uint32_t blocks = (uint32_t)((n_cands + kVerifyBlockWide - 1) / kVerifyBlockWide);
@@ -8283,11 +8556,29 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
         hipLaunchKernelGGL((k_verify<kVerifyBlockWide, uint64_t>), dim3(std::max(1u, blocks)), dim3(kVerifyBlockWide),
                            0, s, V);
     } else {
-      const uint32_t blocks = (uint32_t)std::min<uint64_t>((n_cands + kVerifyBlock - 1) / kVerifyBlock, e->vm_threads / kVerifyBlock);
-      hipLaunchKernelGGL((k_verify<kVerifyBlock, uint32_t>), dim3(std::max(1u, blocks)), dim3(kVerifyBlock), 0, s, V);
-      if (any_long)
-        hipLaunchKernelGGL((k_verify<kVerifyBlock, uint64_t>), dim3(std::max(1u, blocks)), dim3(kVerifyBlock), 0, s,
-                           V);
+      // a short list: 64-lane blocks, every lane a job.  Fewer jobs per wave
+      // (more waves, 256-lane blocks sharing one staged table) measured
+      // slower: 0.75 / 0.81 / 0.95 ms at 32 / 17 / 8 jobs per wave against
+      // 0.57 ms (configs[2], profiles/r06b_ab) -- the jobs' own dependent
+      // chains, not the wave's lock-step union of them, set the time
+      uint32_t blk = kVerifyBlock;
+#ifdef TSG_EXPERIMENTS
+      if (const char* v = getenv("TSG_VERIFY_JPW")) {  // (A/B: 256-lane blocks, jpw jobs per wave)
+        blk = kVerifyBlockWide;
+        V.jpw = (uint32_t)std::max(1, std::min(64, atoi(v)));
+      }
+#endif
+      const uint32_t per_block = blk / 64 * V.jpw;
+      const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_cands + per_block - 1) / per_block,
+                                                                                  e->vm_threads / per_block));
+      if (blk == kVerifyBlockWide) {
+        hipLaunchKernelGGL((k_verify<kVerifyBlockWide, uint32_t>), dim3(blocks), dim3(kVerifyBlockWide), 0, s, V);
+        if (any_long)
+          hipLaunchKernelGGL((k_verify<kVerifyBlockWide, uint64_t>), dim3(blocks), dim3(kVerifyBlockWide), 0, s, V);
+      } else {
+        hipLaunchKernelGGL((k_verify<kVerifyBlock, uint32_t>), dim3(blocks), dim3(kVerifyBlock), 0, s, V);
+        if (any_long) hipLaunchKernelGGL((k_verify<kVerifyBlock, uint64_t>), dim3(blocks), dim3(kVerifyBlock), 0, s, V);
+      }
     }
     // speculative chains: conflicts re-run in order (grid: one lane per job
     // start at most; the re-run grid keeps every lane's VM scratch slot below
@@ -8756,10 +9047,11 @@ void tsg_engine_free(tsg_engine* e) {
   e->f_luid.release(); e->f_sfile.release(); e->f_sgrp.release(); e->f_grp.release();
   e->f_rec.release(); e->f_rec2.release(); e->f_arena.release();
   e->f_gran.release(); e->f_gcarry.release(); e->big_outs.release(); e->f_lkeyb.release();
-  e->f_ties.release(); e->out_locs.release();
+  e->f_ties.release(); e->out_locs.release(); e->gate_defer.release();
   e->f_dsize.release(); e->f_doff.release(); e->f_dense_at.release(); e->f_gstart.release(); e->f_dense.release();
   e->f_pmax.release(); e->f_spidx.release(); e->f_long.release();
   if (e->h_dense) (void)hipHostFree(e->h_dense);
+  if (e->h_find) (void)hipHostFree(e->h_find);
   if (e->dma_sig.handle) {
     (void)dma_wait(e);
     (void)hsa_signal_destroy(e->dma_sig);
@@ -8774,6 +9066,7 @@ void tsg_engine_free(tsg_engine* e) {
     (void)hipEventDestroy(e->ev_dense);
     (void)hipEventDestroy(e->ev_dfill);
     (void)hipEventDestroy(e->ev_frec);
+    (void)hipEventDestroy(e->ev_fb);
     (void)hipEventDestroy(e->ev_nl[0]);
     (void)hipEventDestroy(e->ev_nl[1]);
     (void)hipEventDestroy(e->ev_pg[0]);

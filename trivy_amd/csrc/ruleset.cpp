@@ -225,6 +225,9 @@ static bool build_fast(tsg_ruleset* rs, int depth, const std::vector<uint8_t>& p
   ac.fast_out_pat.clear();
   ac.fast_states = 0;
   ac.fast_out_entry = 0;
+  ac.fast_ev_entry = 0;
+  ac.fast_kw.clear();
+  ac.fast_kw_map.clear();
   ac.fast_ext.assign(rs->patterns.size(), 0);
   ac.fast_pair.clear();
   for (auto& p : rs->patterns)
@@ -293,13 +296,54 @@ static bool build_fast(tsg_ruleset* rs, int depth, const std::vector<uint8_t>& p
   }
   const int S = (int)states.size();
   if ((size_t)S > max_rows) return false;
-  // renumber: start first, states without outputs, then output states
+  // keyword states: output states whose every output (at most kFastKwPer) is
+  // a keyword-only pattern -- a keyword some non-implied gate needs, no anchor
+  // role, not truncated, no class extension, printable ASCII -- so the scan
+  // confirms it on the real bytes and ORs the file's keyword bit itself (no
+  // k_report event: the 2-3 letter keywords jwt / lob / key of the builtin
+  // rules were most of configs[2]'s 6.3 M events).  At most kFastKwBits
+  // keywords and kFastKwStates states; the rest stay events.
+  auto kw_simple = [&](uint32_t pi) {
+    const PatternHost& p = rs->patterns[pi];
+    if (p.special || p.kw < 0 || !p.kw_needed || !p.rules.empty() || p.lower.size() > (size_t)depth ||
+        p.lower.size() > 8 || seq[pi].size() != p.lower.size())
+      return false;
+    for (unsigned char c : p.lower)
+      if (c < 0x20 || c >= 0x7F) return false;
+    return true;
+  };
+  std::vector<int> kw_bit_of(rs->keywords.size(), -1);
+  std::vector<uint16_t> kw_map;
+  std::vector<char> is_kw(S, 0);
+  int n_kw = 0;
+  for (int st = 0; st < S; ++st) {
+    const auto& o = states[st].outs;
+    if (o.empty() || o.size() > kFastKwPer || n_kw >= (int)kFastKwStates) continue;
+    bool ok = true;
+    for (auto pi : o) ok &= kw_simple(pi);
+    if (!ok) continue;
+    int need = 0;
+    for (auto pi : o) need += kw_bit_of[rs->patterns[pi].kw] < 0;
+    if ((int)kw_map.size() + need > (int)kFastKwBits) continue;
+    for (auto pi : o)
+      if (kw_bit_of[rs->patterns[pi].kw] < 0) {
+        kw_bit_of[rs->patterns[pi].kw] = (int)kw_map.size();
+        kw_map.push_back((uint16_t)rs->patterns[pi].kw);
+      }
+    is_kw[st] = 1;
+    ++n_kw;
+  }
+  // renumber: start first, states without outputs, keyword states, then the
+  // other output states (events)
   std::vector<int> perm(S), inv;
   for (int st = 0; st < S; ++st)
     if (states[st].outs.empty()) { perm[st] = (int)inv.size(); inv.push_back(st); }
   const int first_out = (int)inv.size();
   for (int st = 0; st < S; ++st)
-    if (!states[st].outs.empty()) { perm[st] = (int)inv.size(); inv.push_back(st); }
+    if (is_kw[st]) { perm[st] = (int)inv.size(); inv.push_back(st); }
+  const int first_ev = (int)inv.size();
+  for (int st = 0; st < S; ++st)
+    if (!states[st].outs.empty() && !is_kw[st]) { perm[st] = (int)inv.size(); inv.push_back(st); }
   const size_t img = ((size_t)S * kFastRowBytes + 3) & ~(size_t)3;
   ac.fast.assign(img, 0);
   ac.fast_out_off.assign(S + 1, 0);
@@ -311,7 +355,27 @@ static bool build_fast(tsg_ruleset* rs, int depth, const std::vector<uint8_t>& p
   }
   ac.fast_out_off[S] = (uint32_t)ac.fast_out_pat.size();
   ac.fast_out_entry = (uint32_t)first_out;
+  ac.fast_ev_entry = (uint32_t)first_ev;
   ac.fast_states = (uint32_t)S;
+  {  // the keyword states' records (pattern window as PatDev::lo64 / m64: ext 0, len <= depth)
+    std::vector<FastKwRec> recs((size_t)(first_ev - first_out) * kFastKwPer, FastKwRec{1, 0, 0, 0});
+    for (int n = first_out; n < first_ev; ++n) {
+      const auto& o = states[inv[n]].outs;
+      for (size_t q = 0; q < o.size(); ++q) {
+        const PatternHost& p = rs->patterns[o[q]];
+        FastKwRec r{0, 0, (uint32_t)kw_bit_of[p.kw], 0};
+        const size_t tl = p.lower.size();
+        for (size_t k = 0; k < tl; ++k) {
+          const int sh = 8 * (int)(8 - tl + k);
+          r.lo64 |= (uint64_t)(uint8_t)p.lower[k] << sh;
+          r.m64 |= 0xFFull << sh;
+        }
+        recs[(size_t)(n - first_out) * kFastKwPer + q] = r;
+      }
+    }
+    ac.fast_kw.assign((const uint8_t*)recs.data(), (const uint8_t*)(recs.data() + recs.size()));
+    ac.fast_kw_map = kw_map;
+  }
   ac.fast_pair.clear();
   bool one_step_out = false;  // (a pair step skips the middle state: it must never be an output)
   for (uint32_t v = 0; v < kFastCols; ++v) one_step_out |= perm[go[0][v]] >= first_out;
@@ -583,6 +647,7 @@ int tsg_ruleset_compile(const tsg_rule* rules, size_t n_rules, const tsg_allow_r
           for (size_t k = 0; k < rs->keywords.size(); ++k)
             if (!kw.empty() && rs->keywords[k] == kw) kw_needed[k] = 1;
     for (auto& ph : rs->patterns) {
+      ph.kw_needed = ph.kw >= 0 && kw_needed[ph.kw];
       if (ph.special || ph.rules.empty() || (ph.kw >= 0 && kw_needed[ph.kw])) continue;
       bool first = true;
       for (uint32_t ri : ph.rules) {
@@ -698,6 +763,24 @@ int tsg_ruleset_scan_image(const tsg_ruleset* rs, uint8_t* buf, size_t cap, size
   *len = rs->ac.fast.size();
   if (out_entry) *out_entry = rs->ac.fast_out_entry;
   if (buf) memcpy(buf, rs->ac.fast.data(), std::min(cap, rs->ac.fast.size()));
+  return TSG_OK;
+}
+
+// k_scan_fast's keyword states (diagnostics): their count and the keywords
+// (lowercased, NUL-separated into buf) whose bits the scan sets itself.
+int tsg_ruleset_kw_states(const tsg_ruleset* rs, uint32_t* n_states, uint32_t* n_keywords, char* buf, size_t cap) {
+  if (!rs || !n_states || !n_keywords) return TSG_ERR_INVALID_ARG;
+  *n_states = rs->ac.fast.empty() ? 0 : rs->ac.fast_ev_entry - rs->ac.fast_out_entry;
+  *n_keywords = (uint32_t)rs->ac.fast_kw_map.size();
+  size_t at = 0;
+  for (uint16_t k : rs->ac.fast_kw_map) {
+    const std::string& w = rs->keywords[k];
+    if (buf && at + w.size() + 1 <= cap) {
+      memcpy(buf + at, w.data(), w.size());
+      buf[at + w.size()] = 0;
+    }
+    at += w.size() + 1;
+  }
   return TSG_OK;
 }
 
