@@ -60,4 +60,24 @@ $(EXP_LIB): $(EXP_OBJS)
 clean:
 	rm -rf $(BUILD) build_exp $(LIB) $(BENCH_LIB) $(GEN_LIB) $(EXP_LIB)
 
-.PHONY: all clean exp
+.PHONY: all clean exp alt
+
+# product build of another revision's sources (tools/build_alt.sh exports them
+# to build_<ALT>/src): TSG_LIB_VARIANT=<ALT> (alt, alt2, ...) loads it, for
+# same-box A/B runs
+ALT      ?= alt
+ALT_SRC  = build_$(ALT)/src
+ALT_LIB  = trivy_amd/libtrivy_secret_gpu_$(ALT).so
+ALT_OBJS = $(patsubst $(SRC_DIR)/%.cpp,build_$(ALT)/%.o,$(HOST_SRCS)) $(patsubst $(SRC_DIR)/%.hip,build_$(ALT)/%.o,$(HIP_SRCS))
+ALT_FLAGS = -O3 -std=c++17 -fPIC -Wno-unused-function -I$(ALT_SRC)/include -I$(ALT_SRC)/$(SRC_DIR)
+
+alt: $(ALT_LIB)
+
+build_$(ALT)/%.o: $(ALT_SRC)/$(SRC_DIR)/%.cpp
+	$(HIPCC) $(ALT_FLAGS) -x hip --offload-arch=$(ARCH) -munsafe-fp-atomics -c $< -o $@
+
+build_$(ALT)/%.o: $(ALT_SRC)/$(SRC_DIR)/%.hip
+	$(HIPCC) $(ALT_FLAGS) -x hip --offload-arch=$(ARCH) -munsafe-fp-atomics -c $< -o $@
+
+$(ALT_LIB): $(ALT_OBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(ALT_OBJS) -lamdhip64 -lhsa-runtime64

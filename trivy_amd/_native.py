@@ -13,10 +13,11 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # TSG_LIB_VARIANT selects a diagnostic build of the same sources: "exp" = the
 # ablation build (`make exp`, tools/*.sh only), "asan" = host ASan/UBSan
-# (`make -f tools/asan.mk`, tests/test_asan.py on the CPU only)
+# (`make -f tools/asan.mk`, tests/test_asan.py on the CPU only), "alt" = the
+# product build of another revision (tools/build_alt.sh: same-box A/B runs)
 _VARIANT = os.environ.get("TSG_LIB_VARIANT", "")
 LIB_PATH = os.path.join(
-    _HERE, f"libtrivy_secret_gpu_{_VARIANT}.so" if _VARIANT in ("exp", "asan") else "libtrivy_secret_gpu.so")
+    _HERE, f"libtrivy_secret_gpu_{_VARIANT}.so" if _VARIANT in ("exp", "asan") or _VARIANT.startswith("alt") else "libtrivy_secret_gpu.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

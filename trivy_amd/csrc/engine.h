@@ -293,11 +293,11 @@ struct AcHost {
 // PatDev::lo64 / m64), and the keyword's local bit (< kFastKwBits).
 constexpr uint32_t kFastKwPer = 2;     // patterns per keyword state (an unused record: m64 = 0, lo64 = 1, never matches)
 constexpr uint32_t kFastKwBits = 32;   // local keyword bits a scan lane accumulates
-constexpr uint32_t kFastKwStates = 64; // keyword states at most (the LDS table's size)
+constexpr uint32_t kFastKwStates = 32; // keyword states at most (the LDS table's size; a lane's seen mask is 32 bits)
 struct FastKwRec {
   uint64_t lo64, m64;
   uint32_t bit;
-  uint32_t pad;
+  uint32_t used;  // 1: a pattern of the state (0: padding)
 };
 
 struct PatternHost {

@@ -182,6 +182,7 @@ struct ScanParams {
   uint64_t hit_cap;
   uint64_t nl_big;  // lazy newline counts: the scan counts the spans of files this big (0: none)
   uint64_t kw_plain;  // report_event: files below this many bytes set keyword bits with plain atomics (else read first)
+  uint32_t kw_drain_at;  // k_scan_fast: drain the wave's keyword queue after a step once it holds this many (0: span ends only)
   // k_report: each report wave's own hit region (hit_seg_cap records at
   // hit_seg + wave * hit_seg_cap; counts in hit_seg_n), packed into `hits` by
   // k_hits_pack -- null: flushes reserve on ctrl->hits
@@ -575,53 +576,85 @@ __device__ inline uint64_t lower64(uint64_t x) {
 // state -- in [fast_out_entry, fast_ev_entry) -- holds only keyword-only
 // outputs, which the scan resolves itself instead of handing k_report an event
 // (the 2-3 letter keywords jwt / lob / key of the builtin rules were most of
-// configs[2]'s 6.3 M events).  The lane appends the group (a FastEvent) to
-// its wave's queue in LDS; at the end of each span the wave drains the queue,
-// one record per lane: replay of the 8 bytes from the entry state (8 LDS
-// steps, as k_report), each keyword state's patterns confirmed on the real
-// bytes (lowered window: FastKwRec lo64 / m64), the file looked up by
-// position and the keyword's bit set (one atomic, read-first in files of
-// kw_plain bytes or more, whose words every lane hits).  A full queue turns
-// the group into an event.  The drain sits outside the scan's unrolled step
-// (inlined per group it doubled the loop's code, which the compiler then no
-// longer unrolled: the register ring went to scratch).
-constexpr uint32_t kFastKwQ = 48;  // queue records per wave (16 waves x 48 x 32 B of LDS)
+// configs[2]'s 6.3 M events; 'sk' once per KiB of configs[1]).  The lane
+// appends the group (a 16-byte KwRec) to its wave's queue in LDS; the wave
+// drains the queue after a step once it holds kw_drain_at records and at the
+// end of each span, one record per lane: replay of the 8 bytes from the entry
+// state (8 LDS steps, as k_report), each keyword state's patterns confirmed on
+// the real bytes (lowered window: FastKwRec lo64 / m64; the 8 bytes before the
+// group re-read from the batch), the file found from the span's region (a
+// span inside one file needs no search) and the keyword's bit set (one
+// atomic, read-first in files of kw_plain bytes or more, whose words every
+// lane hits).  Repeats: in a span inside one file, a state whose patterns all
+// confirmed is marked in the owning lane's seen mask (LDS); the lane then
+// skips a group whose max m has every keyword state <= m seen (the group's
+// states all lie in [fast_out_entry, m]; states are numbered shortest keyword
+// first, so 'sk' / jwt are the low ones).  A full queue turns the group into
+// an event.  Per-drain latency dominates the cost (threshold 8 / 16 / 32 of a
+// 48 x 32 B queue: k_scan_fast +2.9 / +1.9 / +0.9 ms on configs[1],
+// profiles/r06f): hence the small records and the dedupe.  The drain sits
+// outside the scan's unrolled step (inlined per group it doubled the loop's
+// code, which the compiler then no longer unrolled: the register ring went to
+// scratch).
+constexpr uint32_t kFastKwQ = 88;    // queue records per wave (16 waves x 88 x 16 B of LDS)
+constexpr uint32_t kKwDrainAt = 64;  // ScanParams::kw_drain_at
+constexpr int kScanKwMid = 64;       // k_scan_fast kMode bit: keyword queue drains after steps too (the gate scan)
+
+struct KwRec {
+  uint32_t span;  // the group's span (position / kNlBlock)
+  uint32_t meta;  // entry state (10 bits) | group in the span (9 bits) << 10 | queuing lane << 19
+  uint2 cur;      // the group's 8 bytes
+};
+static_assert(kFastMaxRows <= 1024 && kNlBlock / 8 <= 512, "KwRec::meta fields");
 
 struct KwScan {
   const FastKwRec* rec;
   const uint16_t* map;
-  FastEvent* q;   // this wave's queue (LDS)
-  uint32_t ev_e;  // first event state
+  KwRec* q;        // this wave's queue (LDS)
+  uint32_t* seen;  // this wave's lanes' seen masks (LDS)
+  uint32_t ev_e;   // first event state (== fast_out_entry: no keyword states)
 };
 
-__device__ inline uint32_t file_of_pos_off(const uint64_t* off, const uint32_t* region_file, uint64_t n_regions,
-                                           uint32_t n_files, uint64_t pos) {
-  const uint64_t r = pos / kNlBlock;
-  const uint32_t hi = r + 1 < n_regions ? min(region_file[r + 1] + 1, n_files) : n_files;
-  return find_file(off, region_file[r], hi, pos);
-}
+__device__ inline bool kw_scan_ok(const ScanParams& P) { return P.nbytes / kNlBlock < (1ull << 32); }
 
 __device__ inline void kw_resolve(const ScanParams& P, const uint8_t* T, const KwScan& kw, uint32_t out_e,
-                                  const FastEvent& ev) {
-  uint64_t hlow = lower64(((uint64_t)ev.prev.y << 32) | ev.prev.x);
-  uint32_t e = ev.entry;
-  const uint32_t f0 = fold6(ev.cur.x), f1 = fold6(ev.cur.y);
-  uint32_t fi = 0xFFFFFFFFu;
+                                  const KwRec& rq) {
+  const uint32_t meta = rq.meta;
+  const uint64_t gp = (uint64_t)rq.span * kNlBlock + 8 * ((meta >> 10) & 511u);
+  const uint2 pv = gp >= 8 ? *(const uint2*)(fast_src(P, gp - 8) + gp - 8) : make_uint2(0, 0);
+  const uint64_t rg = rq.span;
+  const uint32_t rf0 = P.region_file[rg];
+  const uint32_t rf1 = rg + 1 < P.n_regions ? P.region_file[rg + 1] : 0xFFFFFFFFu;
+  const bool single = rf0 == rf1;  // the span lies in one file
+  const uint2 cur = rq.cur;
+  uint64_t hlow = lower64(((uint64_t)pv.y << 32) | pv.x);
+  uint32_t e = meta & 1023u;
+  const uint32_t f0 = fold6(cur.x), f1 = fold6(cur.y);
+  uint32_t fi = 0xFFFFFFFFu, seen = 0;
+  bool read_first = false;
+#pragma unroll
   for (int j = 0; j < 8; ++j) {
     e = fstep(T, e, j < 4 ? f0 : f1, j & 3);
-    const uint32_t c = ((j < 4 ? ev.cur.x : ev.cur.y) >> (8 * (j & 3))) & 0xFFu;
+    const uint32_t c = ((j < 4 ? cur.x : cur.y) >> (8 * (j & 3))) & 0xFFu;
     hlow = (hlow >> 8) | ((uint64_t)lower_ascii((uint8_t)c) << 56);
     if (e < out_e) continue;
     const FastKwRec* r = kw.rec + (size_t)(e - out_e) * kFastKwPer;
     uint32_t bits = 0;
+    bool full = true;
 #pragma unroll
-    for (uint32_t q = 0; q < kFastKwPer; ++q)
-      if ((hlow & r[q].m64) == r[q].lo64) bits |= 1u << r[q].bit;
+    for (uint32_t q = 0; q < kFastKwPer; ++q) {
+      const bool hit = (hlow & r[q].m64) == r[q].lo64;
+      bits |= hit ? 1u << r[q].bit : 0u;
+      full &= hit || !r[q].used;
+    }
     if (!bits) continue;
+    if (full) seen |= 1u << (e - out_e);
     // (a file separator resets the automaton: every pattern lies in one file)
-    if (fi == 0xFFFFFFFFu || ev.pos + j >= P.off[fi + 1])
-      fi = file_of_pos_off(P.off, P.region_file, P.n_regions, P.n_files, ev.pos + j);
-    const bool read_first = P.off[fi + 1] - P.off[fi] >= P.kw_plain;
+    const uint64_t pos = gp + j;
+    if (fi == 0xFFFFFFFFu || (!single && pos >= P.off[fi + 1])) {
+      fi = single ? rf0 : find_file(P.off, rf0, rf1 == 0xFFFFFFFFu ? P.n_files : min(rf1 + 1, P.n_files), pos);
+      read_first = P.off[fi + 1] - P.off[fi] >= P.kw_plain;
+    }
     while (bits) {
       const uint32_t b = (uint32_t)__builtin_ctz(bits);
       bits &= bits - 1;
@@ -631,15 +664,18 @@ __device__ inline void kw_resolve(const ScanParams& P, const uint8_t* T, const K
       if (!read_first || !(__hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(wp, bit);
     }
   }
+  if (single && seen) atomicOr(&kw.seen[meta >> 19], seen);
 }
 
-// The wave's queued keyword groups, one per lane (wave-uniform count).
+// The wave's queued keyword groups, one per lane (wave-uniform count); then
+// each lane takes its seen mask back.
 __device__ inline void kw_drain(const ScanParams& P, const uint8_t* T, const KwScan& kw, uint32_t out_e,
-                                uint32_t& kwn, uint32_t lane) {
+                                uint32_t& kwn, uint32_t& kseen, uint32_t lane) {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the queue's stores before its loads
   for (uint32_t q0 = 0; q0 < kwn; q0 += 64)
     if (q0 + lane < kwn) kw_resolve(P, T, kw, out_e, kw.q[q0 + lane]);
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the loads before the queue is refilled
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the loads and seen bits before the queue is refilled
+  kseen = kw.seen[lane];
   kwn = 0;
 }
 
@@ -732,7 +768,7 @@ template <int V, int kMode, int G, bool kPair = false>
 __device__ inline void fast_window(const ScanParams& P, const uint8_t* T, uint32_t out_e, FastChain<V>& C,
                                    const uint32_t (&d)[2 * G], uint64_t gpos, bool live, uint64_t lanes_lt,
                                    FastEvent* ev_seg, uint32_t* ev_count, const KwScan* kw = nullptr,
-                                   uint32_t* kwn = nullptr) {
+                                   uint32_t* kwn = nullptr, uint32_t kseen = 0) {
   uint32_t gs[G], m[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -767,17 +803,18 @@ __device__ inline void fast_window(const ScanParams& P, const uint8_t* T, uint32
       for (int g = 0; g < G; ++g) {
         uint32_t mg = m[g];
         if (kw) {  // keyword groups into the queue; a full queue makes them events
-          const bool kl = live && mg >= out_e && mg < ev_e;
+          const bool kg = live && mg >= out_e && mg < ev_e;
+          // (every keyword state <= mg seen: nothing new in this group)
+          const bool kl = kg && (((2u << (mg - out_e)) - 1u) & ~kseen) != 0;
           const uint64_t kb = __ballot(kl);
           if (kb) {
             const uint32_t nq = (uint32_t)__popcll(kb);
             if (*kwn + nq <= kFastKwQ) {
               if (kl) {
-                FastEvent r;
-                r.pos = gpos + 8 * g;
-                r.entry = gs[g];
-                r.pad = 0;
-                r.prev = C.prev;
+                KwRec r;
+                const uint64_t q = gpos + 8 * g;
+                r.span = (uint32_t)(q / kNlBlock);
+                r.meta = gs[g] | (uint32_t)((q % kNlBlock) / 8) << 10 | __lane_id() << 19;
                 r.cur = make_uint2(d[2 * g], d[2 * g + 1]);
                 kw->q[*kwn + (uint32_t)__popcll(kb & lanes_lt)] = r;
               }
@@ -825,6 +862,16 @@ __device__ inline RepView rep_view(const AcDev& ac, const uint8_t* B) {
 
 constexpr uint64_t kKwReadFirst = 1ull << 20;  // (report_event's keyword bits)
 
+// The file of an output at pos, given the file of the event's previous output
+// (or ~0): one 8-byte group can hold the end of one file, its NUL separator(s)
+// and the start of the next, so a cached index is kept only while pos stays
+// inside that file.
+__device__ inline uint32_t event_file(const ScanParams& P, uint32_t fi, uint64_t pos) {
+  if (P.report_mode & 1) return (uint32_t)((pos >> 12) % P.n_files);
+  if (fi != 0xFFFFFFFFu && pos < P.off[fi + 1]) return fi;
+  return file_of_pos(P, pos);
+}
+
 // One event on one lane: replay its 8 bytes on the image, and per output
 // confirm the pattern on the real bytes, set the file's keyword gate bit and
 // stage the anchor hit in the wave's LDS slots (wbuf / *hcnt_w).
@@ -856,7 +903,7 @@ __device__ inline void report_event(const ScanParams& P, const AcDev& ac, const 
       const uint32_t tl = pd.len < ac.depth ? pd.len : ac.depth;
       const uint64_t start = pos + 1 - tl - pd.ext;
       if (pd.trunc) {  // the rest of a long pattern, on the batch (rare)
-        if (fi == 0xFFFFFFFFu) fi = (P.report_mode & 1) ? (uint32_t)((pos >> 12) % P.n_files) : file_of_pos(P, pos);
+        fi = event_file(P, fi, pos);
         const uint64_t fend = P.off[fi + 1] - 1;
         if (start + pd.len > fend) continue;
         // chunks of 8 batch bytes issued before any compare (one memory
@@ -881,7 +928,7 @@ __device__ inline void report_event(const ScanParams& P, const AcDev& ac, const 
       }
       ++my_out;
       if (want_kw) {
-        if (fi == 0xFFFFFFFFu) fi = (P.report_mode & 1) ? (uint32_t)((pos >> 12) % P.n_files) : file_of_pos(P, pos);
+        fi = event_file(P, fi, pos);
         const uint64_t key = ((uint64_t)fi << 32) | pd.kw;  // per-lane dedupe of repeated keywords
         if (last_kw != key) {
           last_kw = key;
@@ -991,10 +1038,12 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
   __shared__ uint64_t hbuf[kFuse ? kReportHitCap : 1];
   __shared__ uint32_t hcnt[kFuse ? kFastThreads / 64 : 1];
   // keyword states' records and local bits (kw_resolve; not in the exp shapes)
-  constexpr bool kKw = !kFuse && !kPair && CH == 1 && kWin != 1;
+  constexpr bool kKw = !kFuse && !kPair && CH == 1 && kWin != 1 && !(kMode & 4);
+  constexpr bool kKwMid = kKw && (kMode & kScanKwMid);
   __shared__ __align__(16) FastKwRec kwrec[kKw ? kFastKwStates * kFastKwPer : 1];
   __shared__ uint16_t kwmap[kKw ? kFastKwBits : 1];
-  __shared__ __align__(16) FastEvent kwq[kKw ? kFastThreads / 64 * kFastKwQ : 1];
+  __shared__ __align__(16) KwRec kwq[kKw ? kFastThreads / 64 * kFastKwQ : 1];
+  __shared__ uint32_t kwseen[kKw ? kFastThreads : 1];
   const AcDev& ac = P.rs.ac;
   {
     const uint32_t words = (kFuse ? ac.rep_bytes : ac.fast_bytes) / 4;
@@ -1012,6 +1061,7 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
         ((uint32_t*)(smem + kFastImgMax))[i] = ps[i];
     }
     if (kFuse && (threadIdx.x & 63) == 0) hcnt[threadIdx.x >> 6] = 0;
+    if (kKw) kwseen[threadIdx.x] = 0;
   }
   __syncthreads();
   const uint8_t* T = smem;
@@ -1036,8 +1086,10 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
   uint64_t u = (uint64_t)blockIdx.x * kFastThreads + threadIdx.x;
   FastChain<V> C[CH];
   uint4 nxt[CH][V];
-  const KwScan kws{kwrec, kwmap, kwq + (kKw ? (threadIdx.x >> 6) * kFastKwQ : 0), kKw ? ac.fast_ev_entry : out_e};
-  uint32_t kwn = 0;  // wave-uniform: records in this wave's keyword queue
+  const KwScan kws{kwrec, kwmap, kwq + (kKw ? (threadIdx.x >> 6) * kFastKwQ : 0), kwseen + (kKw ? threadIdx.x & ~63u : 0),
+                   kKw && kw_scan_ok(P) ? ac.fast_ev_entry : out_e};
+  uint32_t kwn = 0;    // wave-uniform: records in this wave's keyword queue
+  uint32_t kseen = 0;  // keyword states (bit: state - out_e) of this span's file already set
   if (u < units) {
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
@@ -1112,21 +1164,21 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
           const uint4 v = C[0].cur[k];
           const uint32_t d[4] = {v.x, v.y, v.z, v.w};
           fast_window<V, kMode, 2>(P, T, out_e, C[0], d, C[0].pos + 16 * k, live, lanes_lt, ev_seg, &ev_count,
-                                   kKw ? &kws : nullptr, &kwn);
+                                   kKw ? &kws : nullptr, &kwn, kseen);
         } else if (kWin == 8) {
           if (k % 4 == 0) {
             const uint4 a = C[0].cur[k], b = C[0].cur[k + 1 < V ? k + 1 : k];
             const uint4 c2 = C[0].cur[k + 2 < V ? k + 2 : k], d2 = C[0].cur[k + 3 < V ? k + 3 : k];
             const uint32_t d[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c2.x, c2.y, c2.z, c2.w, d2.x, d2.y, d2.z, d2.w};
             fast_window<V, kMode, 8>(P, T, out_e, C[0], d, C[0].pos + 16 * k, live, lanes_lt, ev_seg, &ev_count,
-                                     kKw ? &kws : nullptr, &kwn);
+                                     kKw ? &kws : nullptr, &kwn, kseen);
           }
         } else if (kWin == 4) {
           if (k % 2 == 0) {
             const uint4 v = C[0].cur[k], w = C[0].cur[k + 1 < V ? k + 1 : k];
             const uint32_t d[8] = {v.x, v.y, v.z, v.w, w.x, w.y, w.z, w.w};
             fast_window<V, kMode, 4, kPair>(P, T, out_e, C[0], d, C[0].pos + 16 * k, live, lanes_lt, ev_seg,
-                                            &ev_count, kKw ? &kws : nullptr, &kwn);
+                                            &ev_count, kKw ? &kws : nullptr, &kwn, kseen);
           }
         } else {
           const uint4 v = C[0].cur[k];
@@ -1136,6 +1188,12 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
       }
 #pragma unroll
       for (int c = 0; c < CH; ++c) C[c].pos = np[c];
+      // a step of a wave can queue ~8 groups on keyword-dense text (configs[1]:
+      // 'sk' once per KiB), a span ~256: drained after a step before it fills
+      // -- kKwMid only (the prefilter-only scan): the drain's code inside the
+      // step loop cost the full ruleset's scan 0.5 ms on configs[2] even where
+      // it never ran (same-box A/B, profiles/r06k), span-end drains none
+      if (kKwMid && P.kw_drain_at && kwn >= P.kw_drain_at) kw_drain(P, T, kws, out_e, kwn, kseen, lane);  // (wave-uniform)
     }
     if (live) {
 #pragma unroll
@@ -1147,7 +1205,11 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
         }
       }
     }
-    if (kKw && kwn) kw_drain(P, T, kws, out_e, kwn, lane);  // (wave-uniform)
+    if (kKw && kwn) kw_drain(P, T, kws, out_e, kwn, kseen, lane);  // (wave-uniform)
+    if (kKw) {  // the next span's file: nothing seen
+      kseen = 0;
+      kws.seen[lane] = 0;
+    }
     u = un;
     if (kFuse && !(P.report_mode & 4)) {  // whole rounds of 64 only: the wave goes back to streaming after them
       const uint32_t lim = ev_count < P.ev_cap_per_wave ? ev_count : (uint32_t)P.ev_cap_per_wave;
@@ -6898,7 +6960,7 @@ int read_ctrl(tsg_engine* e, Ctrl* h) {
 
 // Launch the AC pass: k_scan_fast when the automaton fits its LDS image,
 // else the generic kernel (transition table in LDS or, if too large, global).
-int launch_scan(tsg_engine* e, ScanParams& P) {
+int launch_scan(tsg_engine* e, ScanParams& P, bool kw_mid = false) {
   hipStream_t s = e->stream;
   bool nl_skipped = false;
   P.n_regions = P.nbytes / kNlBlock + 1;
@@ -7007,6 +7069,10 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
       nl_skipped = true;
       fused = true;
     }
+    else if (chains == 1 && vecs == 8 && win == 4 && e->nl_lazy && kw_mid) {
+      hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 2 | kScanKwMid, 4>), dim3(blocks), dim3(nt), 0, s, P);
+      nl_skipped = true;
+    }
     else if (chains == 1 && vecs == 8 && win == 4 && e->nl_lazy) {
       hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 2, 4>), dim3(blocks), dim3(nt), 0, s, P);
       nl_skipped = true;
@@ -7019,7 +7085,10 @@ int launch_scan(tsg_engine* e, ScanParams& P) {
     fuse = fused;
 #else
     // (kMode 2: no newline counts -- the engine counts them lazily, k_nl_spans)
-    if (e->nl_lazy) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 2, kFastEventWin>), dim3(blocks), dim3(nt), 0, s, P);
+    // (kw_mid: the prefilter-only scan, whose outputs are all keywords)
+    if (e->nl_lazy && kw_mid)
+      hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 2 | kScanKwMid, kFastEventWin>), dim3(blocks), dim3(nt), 0, s, P);
+    else if (e->nl_lazy) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 2, kFastEventWin>), dim3(blocks), dim3(nt), 0, s, P);
     else hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, kFastEventWin>), dim3(blocks), dim3(nt), 0, s, P);
     nl_skipped = e->nl_lazy;
 #endif
@@ -8232,6 +8301,8 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   P.nl_big = e->nl_big;
   P.kw_plain = kKwReadFirst;
   if (const char* v = experiment_env("TSG_KW_PLAIN")) P.kw_plain = strtoull(v, nullptr, 10);  // (A/B)
+  P.kw_drain_at = kKwDrainAt;
+  if (const char* v = experiment_env("TSG_KW_DRAIN")) P.kw_drain_at = (uint32_t)strtoul(v, nullptr, 10);  // (A/B)
   const bool merge = sp && sp->mode == 2;
   // newline counts: counted lazily after the locations (k_nl_spans), except
   // for a part scan, whose blob exports its range's counts, and a batch of
@@ -9675,6 +9746,8 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
   P.nl_blocks = e->nl_blocks.p;
   P.kw_plain = kKwReadFirst;
   if (const char* v = experiment_env("TSG_KW_PLAIN")) P.kw_plain = strtoull(v, nullptr, 10);  // (A/B)
+  P.kw_drain_at = kKwDrainAt;
+  if (const char* v = experiment_env("TSG_KW_DRAIN")) P.kw_drain_at = (uint32_t)strtoul(v, nullptr, 10);  // (A/B)
   const bool want_gates = h_gates_out && nf && gate_words_per_file;
   const uint32_t R = (uint32_t)rs->rules.size();
   std::vector<uint32_t> csr;
@@ -9705,7 +9778,7 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
   bool scanned = false;
   for (int attempt = 0; attempt < 3 && !scanned; ++attempt) {
     if (nbytes) {
-      if ((rc = launch_scan(e, P))) return rc;
+      if ((rc = launch_scan(e, P, true))) return rc;
       if ((rc = launch_fold_windows(e, P, false))) return rc;
       if ((rc = launch_uni_keywords(e, P))) return rc;
     }

@@ -316,12 +316,27 @@ static bool build_fast(tsg_ruleset* rs, int depth, const std::vector<uint8_t>& p
   std::vector<uint16_t> kw_map;
   std::vector<char> is_kw(S, 0);
   int n_kw = 0;
+  // shortest keywords first (the most frequent in text: 'sk', then jwt /
+  // key / lob ...): they get the low numbers, which a lane's seen-prefix test
+  // (kw_resolve) needs to skip repeats
+  std::vector<std::pair<size_t, int>> cand;
   for (int st = 0; st < S; ++st) {
     const auto& o = states[st].outs;
-    if (o.empty() || o.size() > kFastKwPer || n_kw >= (int)kFastKwStates) continue;
+    if (o.empty() || o.size() > kFastKwPer) continue;
     bool ok = true;
-    for (auto pi : o) ok &= kw_simple(pi);
-    if (!ok) continue;
+    size_t len = 8;
+    for (auto pi : o) {
+      ok &= kw_simple(pi);
+      len = std::min(len, rs->patterns[pi].lower.size());
+    }
+    if (ok) cand.emplace_back(len, st);
+  }
+  std::stable_sort(cand.begin(), cand.end());
+  std::vector<int> kw_order;
+  for (auto& [len, st] : cand) {
+    (void)len;
+    const auto& o = states[st].outs;
+    if (n_kw >= (int)kFastKwStates) break;
     int need = 0;
     for (auto pi : o) need += kw_bit_of[rs->patterns[pi].kw] < 0;
     if ((int)kw_map.size() + need > (int)kFastKwBits) continue;
@@ -331,6 +346,7 @@ static bool build_fast(tsg_ruleset* rs, int depth, const std::vector<uint8_t>& p
         kw_map.push_back((uint16_t)rs->patterns[pi].kw);
       }
     is_kw[st] = 1;
+    kw_order.push_back(st);
     ++n_kw;
   }
   // renumber: start first, states without outputs, keyword states, then the
@@ -339,8 +355,7 @@ static bool build_fast(tsg_ruleset* rs, int depth, const std::vector<uint8_t>& p
   for (int st = 0; st < S; ++st)
     if (states[st].outs.empty()) { perm[st] = (int)inv.size(); inv.push_back(st); }
   const int first_out = (int)inv.size();
-  for (int st = 0; st < S; ++st)
-    if (is_kw[st]) { perm[st] = (int)inv.size(); inv.push_back(st); }
+  for (int st : kw_order) { perm[st] = (int)inv.size(); inv.push_back(st); }
   const int first_ev = (int)inv.size();
   for (int st = 0; st < S; ++st)
     if (!states[st].outs.empty() && !is_kw[st]) { perm[st] = (int)inv.size(); inv.push_back(st); }
@@ -363,7 +378,7 @@ static bool build_fast(tsg_ruleset* rs, int depth, const std::vector<uint8_t>& p
       const auto& o = states[inv[n]].outs;
       for (size_t q = 0; q < o.size(); ++q) {
         const PatternHost& p = rs->patterns[o[q]];
-        FastKwRec r{0, 0, (uint32_t)kw_bit_of[p.kw], 0};
+        FastKwRec r{0, 0, (uint32_t)kw_bit_of[p.kw], 1};
         const size_t tl = p.lower.size();
         for (size_t k = 0; k < tl; ++k) {
           const int sh = 8 * (int)(8 - tl + k);
