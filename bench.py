@@ -612,6 +612,7 @@ def oracle_parity(N, c, res, rules, seed, density, random_gb, workers):
     bad = []
     n_find = 0
     done = 0
+    t_note = t0
     # spawned, not forked: the workers never hold this process's GPU handles
     ctx = mp.get_context("spawn")
     with ctx.Pool(workers, initializer=_oracle_worker_init, initargs=(N.GEN_PATH, seed, density)) as pool:
@@ -621,7 +622,8 @@ def oracle_parity(N, c, res, rules, seed, density, random_gb, workers):
             if got != want:
                 bad.append(f)
             done += 1
-            if done % 20000 == 0:
+            if done % 20000 == 0 or time.perf_counter() - t_note > 30:
+                t_note = time.perf_counter()
                 print(f"oracle parity: {done}/{len(items)} files, {len(bad)} mismatched, "
                       f"{time.perf_counter() - t0:.0f}s", file=sys.stderr, flush=True)
     return dict(checker="oracle/secret_oracle.py (Python regex engine, independent of the engine's parser and VM)",
@@ -791,6 +793,10 @@ def main():
                     help="configs[2]: the Python oracle over every plant / decoy / finding / non-ASCII file "
                          "and --oracle-random-gb of random files (independent checker)")
     ap.add_argument("--oracle-random-gb", type=float, default=1.0)
+    ap.add_argument("--staged", action="store_true",
+                    help="configs[0] through the caller-filled page-locked staging (tsg_staging_add + "
+                         "tsg_analyze_staged, as the tagged Go build's analyzer): the step copies every file into "
+                         "its slot (16 threads) and runs the staged call")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group for N > 1 (nccl = RCCL; gloo for several ranks on one GPU in tests)")
     ap.add_argument("--shared", action="store_true",
@@ -888,6 +894,30 @@ def main():
             host_files[i].len = int(c["sizes"][i])
             host_files[i].path = path_objs[i]
         c["host_keep"] = (host, path_objs)
+        if args.staged:
+            st = ctypes.c_void_p()
+            N.check(N.lib.tsg_staging_create(int(c["packed"]) + c["n_files"] + (1 << 20), ctypes.byref(st)))
+            blib = cpu_lib()
+            blib.tsgb_stage_files.restype = ctypes.c_size_t
+            blib.tsgb_stage_files.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+            s_off = np.ascontiguousarray(c["off"][: c["n_files"]], dtype=np.uint64)
+            s_len = np.ascontiguousarray(c["sizes"][: c["n_files"]], dtype=np.uint64)
+            s_paths = (ctypes.c_char_p * c["n_files"])(*path_objs)
+            add_fn = ctypes.cast(N.lib.tsg_staging_add, ctypes.c_void_p)
+            threads = min(16, cpu_quota())
+
+            def staged_step():
+                N.lib.tsg_staging_reset(st)
+                k = blib.tsgb_stage_files(st, add_fn, ctypes.c_void_p(base), s_off.ctypes.data, s_len.ctypes.data,
+                                          s_paths, c["n_files"], threads)
+                if k != c["n_files"]:
+                    raise RuntimeError(f"staging took {k} of {c['n_files']} files")
+                r = ctypes.c_void_p()
+                N.check(N.lib.tsg_analyze_staged(eng, rs, st, ctypes.byref(r)))
+                return r
+            c["staged_step"] = staged_step
+            c["staged_keep"] = (st, s_off, s_len, s_paths, blib)
 
     layers = None
     if args.config == 3:
@@ -958,6 +988,8 @@ def main():
             c["layer_results"] = rs_[:-1]
             c["layer_scan_ms"] = sum(result_timings(N, r)[17] for r in rs_)
             return rs_[-1]
+        if args.config == 0 and args.staged:
+            return c["staged_step"]()
         if args.config == 0:
             r = ctypes.c_void_p()
             N.check(N.lib.tsg_analyze(eng, rs, host_files, c["n_files"], ctypes.byref(r)))
@@ -1073,6 +1105,24 @@ def main():
                                     max(1, (args.cpu_cores or cpu_quota()) - 1))
     if last is not None and args.config != 3:
         N.lib.tsg_result_free(last)
+    h2d = None
+    if rank == 0 and args.config in (0, 3):
+        # the PCIe floor of a PCIe-inclusive step: the step's input bytes as
+        # one page-locked H2D at the rate measured here (1 GiB, 3 copies)
+        n = int(min(c["total"], 1 << 30))
+        hb = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        db = torch.empty(n, dtype=torch.uint8, device=device)
+        db.copy_(hb, non_blocking=True)
+        torch.cuda.synchronize()
+        t_h = time.perf_counter()
+        for _ in range(3):
+            db.copy_(hb, non_blocking=True)
+        torch.cuda.synchronize()
+        rate = 3 * n / (time.perf_counter() - t_h)
+        step_bytes = c["layer_bytes"] if args.config == 3 else c["total"]
+        h2d = {"gbps": round(rate / 1e9, 2), "floor_ms": round(step_bytes / rate * 1e3, 3),
+               "step_bytes": int(step_bytes)}
+        del hb, db
     if rank == 0:
         out = {
             "metric": "secret-scan GB/s (whole node), builtin rules, 1/2/4/8 MI355X; % HBM peak",
@@ -1089,12 +1139,15 @@ def main():
             "data": "synthetic (seeded SURVEY.md §8(d) text model, builtin-rule secrets planted at "
                     f"{args.density:g}/byte, generated in HBM)",
             "config": {"workload": WORKLOADS[args.config] + (f" ({args.stress_rules} generated rules)"
-                                                              if args.config == 4 else ""),
+                                                              if args.config == 4 else "")
+                       + (" -- through the caller-filled staging (tsg_staging_add, 16-thread slot fill, "
+                          "tsg_analyze_staged)" if args.config == 0 and args.staged else ""),
                        "gb_per_gpu": round(c["total"] / 1e9, 3), "files_per_gpu": c["n_files"],
                        "density": args.density, "parallelism": f"file shards x{world}, no collective",
                        **({"layer_tar_bytes": c["layer_bytes"], "layer_build_s": round(c["layer_build_s"], 1)}
                           if args.config == 3 else {})},
             "pct_hbm_peak": round(100.0 * value / (HBM_PEAK_GBPS * world), 2),
+            **({"h2d_floor": h2d} if h2d else {}),
             "roofline": {"bound": "hbm", "kernel": scan_kernel, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic[0], "traffic_source": traffic[1],

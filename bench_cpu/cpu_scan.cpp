@@ -549,4 +549,40 @@ uint64_t tsgb_finding_hash_c(uint32_t rule, uint64_t start, uint64_t end, uint32
   return tsgb_finding_hash(rule, start, end, start_line, end_line, match_hash, lines.data(), n_lines);
 }
 
+// configs[0] through the caller-filled staging (bench --staged): every file
+// reserved in order through `add` (the product library's tsg_staging_add,
+// passed in as a pointer: this library does not link it), then the contents
+// copied into their slots by `threads` threads over equal byte shares -- as
+// the tagged build's analyzer workers io.ReadFull into theirs.  Returns the
+// files staged (n unless the staging filled up).
+typedef int (*tsgb_stage_add_fn)(void* st, const char* path, uint64_t len, uint8_t** dst);
+size_t tsgb_stage_files(void* st, tsgb_stage_add_fn add, const uint8_t* data, const uint64_t* off,
+                        const uint64_t* len, const char* const* paths, size_t n, int threads) {
+  std::vector<uint8_t*> dst(n);
+  size_t k = 0;
+  for (; k < n; ++k)
+    if (add(st, paths[k], len[k], &dst[k]) != TSG_OK) break;
+  uint64_t total = 0;
+  for (size_t i = 0; i < k; ++i) total += len[i];
+  threads = std::max(1, threads);
+  std::vector<std::thread> pool;
+  std::atomic<size_t> next{0};
+  const uint64_t share = total / threads + 1;
+  // file ranges of about `share` bytes each, claimed in order
+  std::vector<size_t> cut{0};
+  uint64_t acc = 0;
+  for (size_t i = 0; i < k; ++i) {
+    acc += len[i];
+    if (acc >= share * cut.size()) cut.push_back(i + 1);
+  }
+  if (cut.back() != k) cut.push_back(k);
+  for (int t = 0; t < threads; ++t)
+    pool.emplace_back([&] {
+      for (size_t c; (c = next.fetch_add(1)) + 1 < cut.size();)
+        for (size_t i = cut[c]; i < cut[c + 1]; ++i) memcpy(dst[i], data + off[i], len[i]);
+    });
+  for (auto& t : pool) t.join();
+  return k;
+}
+
 }  // extern "C"

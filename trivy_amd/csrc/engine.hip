@@ -797,6 +797,13 @@ __device__ inline void fast_window(const ScanParams& P, const uint8_t* T, uint32
     uint32_t mx = m[0];
 #pragma unroll
     for (int g = 1; g < G; ++g) mx = mx > m[g] ? mx : m[g];
+    if ((kMode & kScanKwMid) && kw) {
+      // the prefilter-only scan ('sk' once per KiB of configs[1] sent almost
+      // every window down this path): a lane whose window max is a keyword
+      // state with every keyword state <= it seen has nothing new (the
+      // window's states are all <= its max)
+      if (mx >= out_e && mx < kw->ev_e && (((2u << (mx - out_e)) - 1u) & ~kseen) == 0) mx = 0;
+    }
     if (__builtin_amdgcn_uicmp(mx, out_e, 35) & __ballot(live)) {
       const uint32_t ev_e = kw ? kw->ev_e : out_e;
 #pragma unroll
