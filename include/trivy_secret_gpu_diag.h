@@ -141,6 +141,14 @@ int tsg_regex_find_all(const char* pattern, const uint8_t* text, size_t len, int
  * batches); 0 restores the default. */
 int tsg_engine_force_verify_split(tsg_engine* e, int on);
 
+/* The engine's post-scan key-value sort (sort_pairs) on host arrays: n
+ * (key, value) pairs ordered by key bits [0, end_bit), stable --
+ * hipcub::DeviceRadixSort::SortPairs' contract; small != 0 takes the
+ * two-launch LDS sort up to 64 K pairs (measured slower, not the product's
+ * path; tests/test_gpu_small_sort.py checks both). */
+int tsg_diag_sort_pairs(tsg_engine* e, const uint64_t* keys, const uint32_t* vals, size_t n, int end_bit,
+                        uint64_t* out_keys, uint32_t* out_vals, int small);
+
 #ifdef __cplusplus
 }
 #endif

@@ -123,6 +123,8 @@ _SIGS = {
                                              ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t,
                                              ctypes.POINTER(ctypes.c_uint32)]),
     "tsg_engine_force_verify_split": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "tsg_diag_sort_pairs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "tsg_big_cold_lds_floor": (ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
     "tsg_ruleset_big_forge_check": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "tsg_ruleset_group_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int),
@@ -206,6 +208,8 @@ _SIGS = {
 }
 
 for _name, (_res, _args) in _SIGS.items():
+    if _VARIANT.startswith("alt") and not hasattr(lib, _name):
+        continue  # (an older revision's build for A/B: diagnostics it predates stay unbound)
     _fn = getattr(lib, _name)  # AttributeError here = symbol missing from the .so
     _fn.restype = _res
     _fn.argtypes = _args

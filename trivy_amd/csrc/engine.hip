@@ -797,13 +797,6 @@ __device__ inline void fast_window(const ScanParams& P, const uint8_t* T, uint32
     uint32_t mx = m[0];
 #pragma unroll
     for (int g = 1; g < G; ++g) mx = mx > m[g] ? mx : m[g];
-    if ((kMode & kScanKwMid) && kw) {
-      // the prefilter-only scan ('sk' once per KiB of configs[1] sent almost
-      // every window down this path): a lane whose window max is a keyword
-      // state with every keyword state <= it seen has nothing new (the
-      // window's states are all <= its max)
-      if (mx >= out_e && mx < kw->ev_e && (((2u << (mx - out_e)) - 1u) & ~kseen) == 0) mx = 0;
-    }
     if (__builtin_amdgcn_uicmp(mx, out_e, 35) & __ballot(live)) {
       const uint32_t ev_e = kw ? kw->ev_e : out_e;
 #pragma unroll
@@ -5692,6 +5685,114 @@ __global__ void k_gather_u64(const uint64_t* in, const uint32_t* idx, uint64_t n
   if (i < n) out[i] = in[idx[i]];
 }
 
+// Small key-value sorts (u64 keys on bits [0, end_bit), u32 values), tried
+// for the post-scan lists of configs[2] (candidates, locations, Match keys:
+// 29-35 K each), which hipcub's radix sort runs as a cascade of a block sort,
+// five to seven merge passes and two trampolines -- ~9 launches per sort, 50
+// of the tail's 150 kernels -- and measured slower (sort_pairs): not the
+// product's path.  Two launches: k_tile_sort orders each tile of
+// kSortTile (masked key, index) pairs in LDS (bitonic; the index breaks ties,
+// so the order equals the stable radix sort's), and k_tile_merge places every
+// element at its rank: its index in its own tile plus, per other tile, how
+// many of that tile's pairs precede it (the tiles' binary searches advance
+// level by level together, so a thread waits ~13 L2 latencies, not 13 per
+// tile).  Larger lists go to hipcub (sort_pairs).
+constexpr uint32_t kSortTile = 4096;
+constexpr uint32_t kSortTiles = 16;  // up to 64 K pairs
+constexpr uint32_t kSortSmall = kSortTile * kSortTiles;
+
+__global__ __launch_bounds__(1024) void k_tile_sort(const uint64_t* kin, uint64_t n, uint64_t mask, uint64_t* skey,
+                                                    uint32_t* sidx) {
+  __shared__ uint64_t k[kSortTile];
+  __shared__ uint32_t x[kSortTile];
+  const uint32_t base = blockIdx.x * kSortTile;
+  for (uint32_t i = threadIdx.x; i < kSortTile; i += blockDim.x) {
+    const bool in = base + i < n;
+    k[i] = in ? kin[base + i] & mask : ~0ull;
+    x[i] = in ? base + i : 0xFFFFFFFFu;  // (padding sorts last: its index beats every real one)
+  }
+  __syncthreads();
+  // a stage of distance j <= 64 keeps each wave inside its own two 128-pair
+  // segments (pairs q = tid and tid + 1024): 63 of the 78 stages then need
+  // only the wave's own ordering, the rest a block barrier (one barrier per
+  // stage cost the sort ~2x hipcub's time on configs[2]'s 34 K candidates)
+  for (uint32_t len = 2; len <= kSortTile; len <<= 1) {
+    for (uint32_t j = len >> 1; j > 0; j >>= 1) {
+#pragma unroll
+      for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t q = threadIdx.x + h * (kSortTile / 4);
+        const uint32_t a = 2 * j * (q / j) + (q % j), b = a + j;
+        const bool up = (a & len) == 0;
+        const uint64_t ka = k[a], kb = k[b];
+        const uint32_t xa = x[a], xb = x[b];
+        const bool gt = ka > kb || (ka == kb && xa > xb);
+        if (gt == up) {
+          k[a] = kb;
+          k[b] = ka;
+          x[a] = xb;
+          x[b] = xa;
+        }
+      }
+      const uint32_t jn = j > 1 ? j >> 1 : len;  // the next stage's distance
+      if (j > 64 || jn > 64) {
+        __syncthreads();
+      } else {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < kSortTile; i += blockDim.x) {
+    skey[base + i] = k[i];
+    sidx[base + i] = x[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_tile_merge(const uint64_t* kin, const uint32_t* vin, uint64_t n,
+                                                    const uint64_t* skey, const uint32_t* sidx, uint32_t n_tiles,
+                                                    uint64_t* kout, uint32_t* vout) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t t = g / kSortTile, r = g % kSortTile;
+  if (t >= n_tiles) return;
+  const uint32_t len_t = (uint32_t)min<uint64_t>(kSortTile, n - (uint64_t)t * kSortTile);
+  if (r >= len_t) return;
+  const uint64_t mk = skey[g];
+  const uint32_t ix = sidx[g];
+  uint32_t lo[kSortTiles], hi[kSortTiles];
+#pragma unroll
+  for (uint32_t u = 0; u < kSortTiles; ++u) {
+    lo[u] = 0;
+    hi[u] = u < n_tiles && u != t ? (uint32_t)min<uint64_t>(kSortTile, n - (uint64_t)u * kSortTile) : 0u;
+  }
+  for (int level = 0; level < 13; ++level) {  // (4096 = 2^12: 13 halvings empty any range)
+    // all 16 probes loaded before any compare, unconditionally (an empty
+    // range reads a stale slot of the scratch and ignores it): one L2
+    // latency per level, not one per tile
+    uint64_t pk[kSortTiles];
+    uint32_t px[kSortTiles];
+#pragma unroll
+    for (uint32_t u = 0; u < kSortTiles; ++u) {
+      const uint32_t m = (lo[u] + hi[u]) >> 1;
+      pk[u] = skey[u * kSortTile + min(m, kSortTile - 1)];
+      px[u] = sidx[u * kSortTile + min(m, kSortTile - 1)];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kSortTiles; ++u) {
+      const uint32_t m = (lo[u] + hi[u]) >> 1;
+      const bool less = pk[u] < mk || (pk[u] == mk && px[u] < ix);
+      const bool open = lo[u] < hi[u];
+      lo[u] = open && less ? m + 1 : lo[u];
+      hi[u] = open && !less ? m : hi[u];
+    }
+  }
+  uint32_t rank = r;
+#pragma unroll
+  for (uint32_t u = 0; u < kSortTiles; ++u) rank += lo[u];
+  kout[rank] = kin[ix];
+  vout[rank] = vin[ix];
+}
+
 // Positions i (> 0) of the ordered findings whose (file, rank) key AND Match
 // prefix equal those of i - 1: the only places the host has to compare whole
 // Match strings (appended unordered; the host sorts the short list).
@@ -6205,6 +6306,8 @@ struct tsg_engine {
   DBuf<uint32_t> job_start;
   DBuf<uint32_t> nsel;
   DBuf<uint8_t> cub_tmp;
+  DBuf<uint64_t> ss_key;  // sort_pairs: the tile-sorted (masked key, index) pairs
+  DBuf<uint32_t> ss_idx;
   DBuf<uint64_t> hit_seg, hit_pre, ev_pre;  // k_report's per-wave hit regions, their exclusive offsets (+ the base)
   DBuf<uint32_t> hit_seg_n;
   DBuf<DevLoc> locs, locs2;
@@ -6887,6 +6990,36 @@ inline const char* experiment_env(const char* name) {
 #endif
 }
 
+// Sort n (key, value) pairs by key bits [0, end_bit), stable, kin/vin ->
+// kout/vout (distinct buffers): hipcub::DeviceRadixSort::SortPairs, or with
+// `small` (TSG_SORT_SMALL in the exp build; tsg_diag_sort_pairs) the two
+// launches k_tile_sort + k_tile_merge up to kSortSmall pairs.  Measured on
+// configs[2] (profiles/r06r): 45 + 23 us per 34 K-pair sort against ~25 us
+// for hipcub's cascade unprofiled (sort_jobs 0.102 vs 0.078 ms, lines 0.98 vs
+// 0.89 ms, step +0.06 ms over two alternating runs): the LDS bitonic's 78
+// stages and the merge's 13 dependent L2 levels cost more than the ~8 launches
+// they replace, so the product keeps hipcub.
+hipError_t sort_pairs(tsg_engine* e, const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout,
+                      uint64_t n, int end_bit, hipStream_t s, bool small = false) {
+  if (!n) return hipSuccess;
+  if (n <= kSortSmall && (small || experiment_env("TSG_SORT_SMALL"))) {
+    hipError_t r = e->ss_key.ensure(kSortSmall);
+    if (r == hipSuccess) r = e->ss_idx.ensure(kSortSmall);
+    if (r != hipSuccess) return r;
+    const uint64_t mask = end_bit >= 64 ? ~0ull : (1ull << end_bit) - 1;
+    const uint32_t nt = (uint32_t)((n + kSortTile - 1) / kSortTile);
+    hipLaunchKernelGGL(k_tile_sort, dim3(nt), dim3(1024), 0, s, kin, n, mask, e->ss_key.p, e->ss_idx.p);
+    hipLaunchKernelGGL(k_tile_merge, dim3(nt * kSortTile / 256), dim3(256), 0, s, kin, vin, n, e->ss_key.p,
+                       e->ss_idx.p, nt, kout, vout);
+    return hipGetLastError();
+  }
+  size_t tmp = 0;
+  hipError_t r = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, kin, kout, vin, vout, (int)n, 0, end_bit, s);
+  if (r == hipSuccess) r = e->cub_tmp.ensure(tmp + 1);
+  if (r == hipSuccess) r = hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp, kin, kout, vin, vout, (int)n, 0, end_bit, s);
+  return r;
+}
+
 // The side stream (D2H of the findings, the phase-0 newline count) and its events.
 hipError_t ensure_side(tsg_engine* e) {
   if (e->side) return hipSuccess;
@@ -7459,11 +7592,7 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
   // distinct Code lines: sort the slots by (file, line start), number the runs
   size_t tmp = 0;
   if (n_lslots) {
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p, e->f_lslot2.p,
-                                               (int)n_lslots, 0, 64, s));
-    HIP_TRY(e->cub_tmp.ensure(tmp + 1));
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p,
-                                               e->f_lslot2.p, (int)n_lslots, 0, 64, s));
+    HIP_TRY(sort_pairs(e, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p, e->f_lslot2.p, n_lslots, 64, s));
     hipLaunchKernelGGL(k_line_heads, dim3(lslot_blocks), dim3(256), 0, s, e->f_lkey2.p, n_lslots, e->f_lhead.p);
     tmp = 0;
     HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, e->f_lhead.p, e->f_lscan.p, (int)n_lslots, s));
@@ -7525,23 +7654,12 @@ int build_findings_dev(tsg_engine* e, const uint8_t* d_data, const uint64_t* d_o
     if (R.dense) HIP_TRY(hipStreamWaitEvent(s, e->ev_dfill, 0));  // (the Match windows of dense files)
     hipLaunchKernelGGL(k_match_prefix, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->f_arena.p, e->f_dense.p,
                        n_locs, e->f_lkey.p, e->f_lkeyb.p, e->f_lslot.p);
-    size_t tmp2 = 0;
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->f_lkey.p, e->f_lkey2.p, e->f_lslot.p, e->f_lslot2.p,
-                                               (int)n_locs, 0, 64, s));
-    HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
     // Match bytes 8..15, then (stable) bytes 0..7, then (file, RuleID rank)
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->f_lkeyb.p, e->f_lkey2.p, e->f_lslot.p,
-                                               e->f_lslot2.p, (int)n_locs, 0, 64, s));
+    HIP_TRY(sort_pairs(e, e->f_lkeyb.p, e->f_lkey2.p, e->f_lslot.p, e->f_lslot2.p, n_locs, 64, s));
     hipLaunchKernelGGL(k_gather_u64, dim3(lane_blocks), dim3(256), 0, s, e->f_lkey.p, e->f_lslot2.p, n_locs, e->keys2.p);
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys2.p, e->f_lkey2.p, e->f_lslot2.p,
-                                               e->f_lslot.p, (int)n_locs, 0, 64, s));
+    HIP_TRY(sort_pairs(e, e->keys2.p, e->f_lkey2.p, e->f_lslot2.p, e->f_lslot.p, n_locs, 64, s));
     hipLaunchKernelGGL(k_gather_u64, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lslot.p, n_locs, e->keys2.p);
-    tmp2 = 0;
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->keys2.p, e->keys.p, e->f_lslot.p, e->vals2.p,
-                                               (int)n_locs, 0, key_bits, s));
-    HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys2.p, e->keys.p, e->f_lslot.p, e->vals2.p,
-                                               (int)n_locs, 0, key_bits, s));
+    HIP_TRY(sort_pairs(e, e->keys2.p, e->keys.p, e->f_lslot.p, e->vals2.p, n_locs, key_bits, s));
     hipLaunchKernelGGL(k_find_gather, dim3(lane_blocks), dim3(256), 0, s, e->f_rec.p, e->vals2.p, n_locs, e->f_rec2.p);
     HIP_TRY(hipMemsetAsync(&e->ctrl.p->n_ties, 0, 8, s));
     hipLaunchKernelGGL(k_tie_list, dim3(lane_blocks), dim3(256), 0, s, e->keys.p, e->f_lkey.p, e->f_lkeyb.p, e->vals2.p,
@@ -8459,12 +8577,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(e->vals2.ensure(n_cands));
     int end_bit = kPosBits;
     while ((1ull << (end_bit - kPosBits)) < RS.n_rules + 1ull) ++end_bit;
-    size_t tmp = 0;
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
-                                               (int)n_cands, 0, end_bit, s));
-    HIP_TRY(e->cub_tmp.ensure(tmp + 1));
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp, e->keys.p, e->keys2.p, e->vals.p,
-                                               e->vals2.p, (int)n_cands, 0, end_bit, s));
+    HIP_TRY(sort_pairs(e, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p, n_cands, end_bit, s));
     HIP_TRY(e->flags8.ensure(n_cands));
     HIP_TRY(e->job_start.ensure(n_cands));
     HIP_TRY(e->nsel.ensure(1));
@@ -8835,11 +8948,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     hipLaunchKernelGGL(k_excl_keys, dim3((uint32_t)((n_locs + 255) / 256)), dim3(256), 0, s, e->locs.p, n_locs, X,
                        e->keys.p, e->vals.p);
     size_t tmp = 0;
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p, (int)nk,
-                                               0, 64, s));
-    HIP_TRY(e->cub_tmp.ensure(tmp + 1));
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
-                                               (int)nk, 0, 64, s));
+    HIP_TRY(sort_pairs(e, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p, nk, 64, s));
     hipLaunchKernelGGL(k_excl_uniq, dim3((uint32_t)((nk + 255) / 256)), dim3(256), 0, s, e->keys2.p, nk,
                        e->flags8.p);
     HIP_TRY(hipGetLastError());
@@ -8879,11 +8988,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     if (n_r) {
       hipLaunchKernelGGL(k_excl_rkeys, dim3((uint32_t)((n_r + 255) / 256)), dim3(256), 0, s, e->excl_out.p, n_r,
                          e->f_iv.p, e->f_lslot.p);
-      HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, e->f_iv.p, e->f_lkey2.p, e->f_lslot.p, e->f_lslot2.p,
-                                                 (int)n_r, 0, 64, s));
-      HIP_TRY(e->cub_tmp.ensure(tmp + 1));
-      HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp, e->f_iv.p, e->f_lkey2.p, e->f_lslot.p,
-                                                 e->f_lslot2.p, (int)n_r, 0, 64, s));
+      HIP_TRY(sort_pairs(e, e->f_iv.p, e->f_lkey2.p, e->f_lslot.p, e->f_lslot2.p, n_r, 64, s));
       hipLaunchKernelGGL(k_excl_pmax, dim3((uint32_t)((n_r + 255) / 256)), dim3(256), 0, s, e->f_lkey2.p,
                          e->f_lslot2.p, e->excl_out.p, e->f_ssrc.p, n_r);
     }
@@ -8944,12 +9049,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(e->locs2.ensure(n_locs));
     hipLaunchKernelGGL(k_loc_keys, dim3((uint32_t)((n_locs + 255) / 256)), dim3(256), 0, s, e->locs.p, n_locs,
                        e->keys.p, e->vals.p);
-    size_t tmp2 = 0;
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
-                                               (int)n_locs, 0, 64, s));
-    HIP_TRY(e->cub_tmp.ensure(tmp2 + 1));
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(e->cub_tmp.p, tmp2, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p,
-                                               (int)n_locs, 0, 64, s));
+    HIP_TRY(sort_pairs(e, e->keys.p, e->keys2.p, e->vals.p, e->vals2.p, n_locs, 64, s));
     hipLaunchKernelGGL(k_loc_gather, dim3((uint32_t)((n_locs + 255) / 256)), dim3(256), 0, s, e->locs.p,
                        e->vals2.p, n_locs, e->locs2.p);
     if ((rc = dense_begin(e, d_data, d_off, nbytes, n_locs))) return rc;
@@ -9837,6 +9937,37 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
   }
   e->gate_tm[15] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - wall0).count();
   return TSG_OK;
+}
+
+int tsg_diag_sort_pairs(tsg_engine* e, const uint64_t* keys, const uint32_t* vals, size_t n, int end_bit,
+                        uint64_t* out_keys, uint32_t* out_vals, int small) {
+  if (!e || (n && (!keys || !vals || !out_keys || !out_vals)) || end_bit < 1 || end_bit > 64)
+    return TSG_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lk(e->mu);
+  HIP_TRY(hipSetDevice(e->device));
+  if (!n) return TSG_OK;
+  DBuf<uint64_t> k[2];
+  DBuf<uint32_t> v[2];
+  int rc = TSG_OK;
+  auto run = [&]() -> int {
+    for (int i = 0; i < 2; ++i) {
+      HIP_TRY(k[i].ensure(n));
+      HIP_TRY(v[i].ensure(n));
+    }
+    HIP_TRY(hipMemcpyAsync(k[0].p, keys, n * 8, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(v[0].p, vals, n * 4, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(sort_pairs(e, k[0].p, k[1].p, v[0].p, v[1].p, n, end_bit, e->stream, small != 0));
+    HIP_TRY(hipMemcpyAsync(out_keys, k[1].p, n * 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(out_vals, v[1].p, n * 4, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return TSG_OK;
+  };
+  rc = run();
+  for (int i = 0; i < 2; ++i) {
+    k[i].release();
+    v[i].release();
+  }
+  return rc;
 }
 
 int tsg_engine_force_verify_split(tsg_engine* e, int on) {
