@@ -2878,6 +2878,8 @@ struct ExpandParams {
   uint32_t rule_words;
   const uint64_t* hits;
   uint64_t n_hits;
+  const unsigned long long* n_hits_dev;  // or the count on the device (clamped to hit_cap): the speculative launch
+  uint64_t hit_cap;
   uint64_t* keys;
   uint32_t* vals;
   uint64_t cand_cap;
@@ -2970,73 +2972,79 @@ __device__ inline void emit_cand(const ExpandParams& E, uint32_t rule, uint64_t 
 // atomic on the candidate counter (a returning atomic on one word serialises
 // chip-wide at ~90 per us: per wave it was ~14 K of them on configs[2]).
 // Rules 32+ of a pattern (large custom rule sets) take a per-candidate atomic.
+// Launched before the host knows the hit count (n_hits_dev: beside the scan's
+// counter read), the grid strides over it.
 __global__ __launch_bounds__(256) void k_expand(ExpandParams E) {
   __shared__ uint32_t wsum[4];
   __shared__ unsigned long long bbase;
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t acc = 0;  // accepted rules k < 32 of the hit's pattern
-  uint64_t gpos = 0;
-  uint32_t fi = 0, rule_off = 0;
-  if (i < E.n_hits) {
-    const uint64_t h = E.hits[i];
-    const bool fold = (h & kFoldHit) != 0;  // literal spelled with K / ſ (k_fold_windows)
-    gpos = (h & ~kFoldHit) >> 16;
-    const uint32_t pid = (uint32_t)(h & 0xFFFF);
-    const uint64_t rg = gpos / kNlBlock;
-    const uint32_t fhi = rg + 1 < E.n_regions ? min(E.region_file[rg + 1] + 1, E.n_files) : E.n_files;
-    fi = find_file(E.off, E.region_file[rg], fhi, gpos);
-    const uint32_t fl = E.file_flags[fi];
-    if (!(fl & kFileAllowed)) {
-      const PatDev pd = E.rs.ac.pats[pid];
-      rule_off = pd.rule_off;
-      const uint32_t* kw = E.file_kw + (size_t)fi * E.rs.kw_words;
-      const uint64_t fend = E.off[fi + 1] - 1;
-      for (uint32_t k = 0; k < pd.rule_n; ++k) {
-        const uint32_t r = E.rs.ac.pat_rules[pd.rule_off + k];
-        if (E.path_mask && ((E.path_mask[(size_t)fi * E.rule_words + (r >> 5)] >> (r & 31)) & 1)) continue;
-        const RuleDev& rd = E.rs.rules[r];
-        // an ASCII literal hit that holds a keyword proves the gate (gate_implied);
-        // a K/ſ spelling does not (ToLower(ſ) == ſ)
-        if ((fold || !rd.gate_implied) && !rule_gate(E.rs, rd, kw)) continue;
-        if (!follow_accepts_dev(E.rs, rd, E.data, gpos, fend)) continue;
-        if (!precede_accepts_dev(rd, E.data, gpos, E.off[fi])) continue;
-        if (k < 32) {
-          acc |= 1u << k;
-        } else {
-          emit_cand(E, r, gpos, fi);
-          if (E.nl_last) atomicMax(&E.nl_last[fi], (unsigned long long)(gpos + kNlCandReach + 1));
+  const uint64_t n_hits = E.n_hits_dev ? min((uint64_t)*E.n_hits_dev, E.hit_cap) : E.n_hits;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n_hits; i0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = i0 + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t acc = 0;  // accepted rules k < 32 of the hit's pattern
+    uint64_t gpos = 0;
+    uint32_t fi = 0, rule_off = 0;
+    if (i < n_hits) {
+      const uint64_t h = E.hits[i];
+      const bool fold = (h & kFoldHit) != 0;  // literal spelled with K / ſ (k_fold_windows)
+      gpos = (h & ~kFoldHit) >> 16;
+      const uint32_t pid = (uint32_t)(h & 0xFFFF);
+      const uint64_t rg = gpos / kNlBlock;
+      const uint32_t fhi = rg + 1 < E.n_regions ? min(E.region_file[rg + 1] + 1, E.n_files) : E.n_files;
+      fi = find_file(E.off, E.region_file[rg], fhi, gpos);
+      const uint32_t fl = E.file_flags[fi];
+      if (!(fl & kFileAllowed)) {
+        const PatDev pd = E.rs.ac.pats[pid];
+        rule_off = pd.rule_off;
+        const uint32_t* kw = E.file_kw + (size_t)fi * E.rs.kw_words;
+        const uint64_t fend = E.off[fi + 1] - 1;
+        for (uint32_t k = 0; k < pd.rule_n; ++k) {
+          const uint32_t r = E.rs.ac.pat_rules[pd.rule_off + k];
+          if (E.path_mask && ((E.path_mask[(size_t)fi * E.rule_words + (r >> 5)] >> (r & 31)) & 1)) continue;
+          const RuleDev& rd = E.rs.rules[r];
+          // an ASCII literal hit that holds a keyword proves the gate (gate_implied);
+          // a K/ſ spelling does not (ToLower(ſ) == ſ)
+          if ((fold || !rd.gate_implied) && !rule_gate(E.rs, rd, kw)) continue;
+          if (!follow_accepts_dev(E.rs, rd, E.data, gpos, fend)) continue;
+          if (!precede_accepts_dev(rd, E.data, gpos, E.off[fi])) continue;
+          if (k < 32) {
+            acc |= 1u << k;
+          } else {
+            emit_cand(E, r, gpos, fi);
+            if (E.nl_last) atomicMax(&E.nl_last[fi], (unsigned long long)(gpos + kNlCandReach + 1));
+          }
         }
       }
     }
-  }
-  // block-wide exclusive prefix of the accepted counts, one reservation
-  const uint32_t cnt = (uint32_t)__popc(acc);
-  uint32_t incl = cnt;
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t v = __shfl_up(incl, d);
-    if (lane >= d) incl += v;
-  }
-  if (lane == 63) wsum[wv] = incl;
-  __syncthreads();
-  uint32_t before = 0, total = 0;
-  for (uint32_t w = 0; w < blockDim.x / 64; ++w) {
-    before += w < wv ? wsum[w] : 0;
-    total += wsum[w];
-  }
-  if (threadIdx.x == 0) bbase = total ? atomicAdd(&E.ctrl->cands, (unsigned long long)total) : 0ull;
-  __syncthreads();
-  uint64_t idx = bbase + before + incl - cnt;
-  if (acc && E.nl_last) atomicMax(&E.nl_last[fi], (unsigned long long)(gpos + kNlCandReach + 1));
-  while (acc) {
-    const uint32_t k = (uint32_t)__ffs(acc) - 1;
-    acc &= acc - 1;
-    if (idx < E.cand_cap) {
-      E.keys[idx] = ((uint64_t)E.rs.ac.pat_rules[rule_off + k] << kPosBits) | gpos;
-      E.vals[idx] = fi;
+    // block-wide exclusive prefix of the accepted counts, one reservation
+    const uint32_t cnt = (uint32_t)__popc(acc);
+    uint32_t incl = cnt;
+  #pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t v = __shfl_up(incl, d);
+      if (lane >= d) incl += v;
     }
-    ++idx;
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+    for (uint32_t w = 0; w < blockDim.x / 64; ++w) {
+      before += w < wv ? wsum[w] : 0;
+      total += wsum[w];
+    }
+    if (threadIdx.x == 0) bbase = total ? atomicAdd(&E.ctrl->cands, (unsigned long long)total) : 0ull;
+    __syncthreads();
+    uint64_t idx = bbase + before + incl - cnt;
+    if (acc && E.nl_last) atomicMax(&E.nl_last[fi], (unsigned long long)(gpos + kNlCandReach + 1));
+    while (acc) {
+      const uint32_t k = (uint32_t)__ffs(acc) - 1;
+      acc &= acc - 1;
+      if (idx < E.cand_cap) {
+        E.keys[idx] = ((uint64_t)E.rs.ac.pat_rules[rule_off + k] << kPosBits) | gpos;
+        E.vals[idx] = fi;
+      }
+      ++idx;
+    }
+    __syncthreads();  // (wsum / bbase are rewritten by the next round)
   }
 }
 
@@ -6372,6 +6380,8 @@ struct tsg_engine {
   uint64_t* h_dense = nullptr;  // page-locked: the region's bytes and file groups, read mid-pipeline
   uint64_t* h_find = nullptr;   // page-locked: the arena's find_bytes / match_bytes, read under the arena fill
   uint64_t arena_need = 0;      // arena capacity the next call starts with (the last need + 1/4)
+  uint64_t cand_need = 0;       // candidate capacity of the next call's speculative k_expand (the last count + 1/4)
+  uint64_t hit_need = 0;        // hits the next call's speculative k_expand grid covers (the last count + 1/4)
   hipEvent_t ev_dense = nullptr, ev_dfill = nullptr, ev_frec = nullptr, ev_fb = nullptr;
   bool dense_active = false;   // this call's locations have dense_at (dense_begin)
   DBuf<uint64_t> f_pmax;       // per location: (file << 40 | max end so far in its file), k_dense_fill's censoring
@@ -8450,6 +8460,60 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   }
   Ctrl c_scan{};
   bool have_c = false;  // c_scan holds the counters after the scan (k_uni_keywords changes none)
+  // ---- 3. candidates (set up here: k_expand is queued speculatively behind
+  // the scan, before the host has read the hit count -- one counter read for
+  // both passes instead of one after each; a scan whose buffers overflowed is
+  // redone with its candidates, and a candidate list over the speculative
+  // capacity is expanded again once the count is known)
+  ExpandParams E{};
+  auto launch_expand = [&](uint64_t n_hits_host, bool on_device, uint64_t cap) -> int {
+    // (every engine buffer read at launch time: launch_scan may have grown
+    // region_file / file_kw since this lambda was made)
+    E.data = d_data;
+    E.off = d_off;
+    E.region_file = e->region_file.p;
+    E.n_regions = nbytes / kNlBlock + 1;
+    E.n_files = nf;
+    E.rs = RS;
+    E.file_kw = e->file_kw.p;
+    E.file_flags = e->file_flags.p;
+    E.path_mask = rs->any_path_rules ? e->path_mask.p : nullptr;
+    E.rule_words = rule_words;
+    E.ctrl = e->ctrl.p;
+    E.full_rules = im.u32.p + im.o_full;
+    E.n_full_rules = im.n_full;
+    HIP_TRY(e->keys.ensure(cap));
+    HIP_TRY(e->vals.ensure(cap));
+    E.keys = e->keys.p;
+    E.vals = e->vals.p;
+    E.cand_cap = e->keys.n;
+    E.hits = e->hits.p;
+    E.hit_cap = hit_cap;
+    E.n_hits = n_hits_host;
+    E.n_hits_dev = on_device ? &e->ctrl.p->hits : nullptr;
+    E.nl_last = nullptr;
+    if (e->nl_deferred) {  // the lazy newline counts' reach per file, marked by the candidates' kernels
+      HIP_TRY(ensure_side(e));
+      HIP_TRY(e->nl_last.ensure(nf));
+      E.nl_last = e->nl_last.p;
+    }
+    HIP_TRY(hipMemsetAsync(&e->ctrl.p->cands, 0, 8, s));
+    if (E.nl_last) HIP_TRY(hipMemsetAsync(e->nl_last.p, 0, (size_t)nf * 8, s));
+    if (on_device)  // (grid: the last call's hit count + 1/4, the stride covers more; configs[4]'s 2.3 M
+                    // hits on a 16-blocks-per-CU grid: k_expand 0.76 -> 0.89 ms, profiles/r06s_ab)
+      hipLaunchKernelGGL(k_expand,
+                         dim3((uint32_t)std::min<uint64_t>((hit_cap + 255) / 256,
+                                                           std::max<uint64_t>(e->num_cus * 16ull, (e->hit_need + 255) / 256))),
+                         dim3(256), 0, s, E);
+    else if (n_hits_host)
+      hipLaunchKernelGGL(k_expand, dim3((uint32_t)((n_hits_host + 255) / 256)), dim3(256), 0, s, E);
+    if (nf) hipLaunchKernelGGL(k_full_jobs, dim3((nf + 255) / 256), dim3(256), 0, s, E);
+    HIP_TRY(hipGetLastError());
+    return TSG_OK;
+  };
+  const bool spec = !(sp && sp->mode == 1) && !experiment_env("TSG_SPEC_OFF");
+  const uint64_t spec_cap = std::max<uint64_t>(1 << 20, e->cand_need);
+  bool spec_done = false;  // the successful scan attempt's candidates were expanded with it
   for (int attempt = 0; attempt < 3 && !scanned; ++attempt) {
     HIP_TRY(hipMemsetAsync(e->nl_blocks.p, 0, n_nlb * 4, s));
     HIP_TRY(hipEventRecord(e->ev[8], s));
@@ -8470,9 +8534,17 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     // the fold-window pass reads the scan's rune count on the device; one
     // read of the counters afterwards checks every buffer of both passes
     if ((rc = launch_fold_windows(e, P, true))) return rc;
+    if (spec) {
+      if ((rc = launch_uni_keywords(e, P))) return rc;
+      if (gate_pending) HIP_TRY(hipStreamWaitEvent(s, e->ev_pg[1], 0));  // file flags and path masks complete
+      HIP_TRY(hipEventRecord(e->ev[2], s));
+      if ((rc = launch_expand(0, true, spec_cap))) return rc;
+      HIP_TRY(hipEventRecord(e->ev[3], s));
+    }
     Ctrl& c = c_scan;
     if ((rc = read_ctrl(e, &c))) return rc;
     have_c = true;
+    spec_done = spec;
     const bool ev_lost = (rs->ac.fast.size() || P.big.blob) && c.ev_overflow > e->ev_overflow.n;
     const bool fold_lost = c.n_fold > P.fold_cap;
     const bool outs_lost = P.big.blob && c.outputs > P.big_out_cap;  // (k_big_walk's records)
@@ -8500,9 +8572,11 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     set_last_error("internal: scan buffers still overflowed after regrowing them twice");
     return TSG_ERR_INTERNAL;
   }
-  if ((rc = launch_uni_keywords(e, P))) return rc;
-  if (gate_pending) HIP_TRY(hipStreamWaitEvent(s, e->ev_pg[1], 0));  // file flags and path masks complete
-  HIP_TRY(hipEventRecord(e->ev[2], s));
+  if (!spec_done) {
+    if ((rc = launch_uni_keywords(e, P))) return rc;
+    if (gate_pending) HIP_TRY(hipStreamWaitEvent(s, e->ev_pg[1], 0));  // file flags and path masks complete
+    HIP_TRY(hipEventRecord(e->ev[2], s));
+  }
   Ctrl c = c_scan;
   if (!have_c && (rc = read_ctrl(e, &c))) return rc;  // (one host round trip fewer after a scan)
   const uint64_t n_hits = c.hits;
@@ -8513,52 +8587,27 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   // files past kMaxVerifyFile: their jobs run the 64-bit instantiations of the
   // search kernels (launched only then)
   const bool any_long = c.long_files != 0 || (merge && sp->file_len > kMaxVerifyFile);
-  // ---- 3. candidates
   uint64_t cand_cap = std::max<uint64_t>(1 << 16, n_hits * 2 + nf / 4);
-  ExpandParams E{};
-  E.data = d_data;
-  E.off = d_off;
-  E.region_file = e->region_file.p;
-  E.n_regions = nbytes / kNlBlock + 1;
-  E.n_files = nf;
-  E.rs = RS;
-  E.file_kw = e->file_kw.p;
-  E.file_flags = e->file_flags.p;
-  E.path_mask = rs->any_path_rules ? e->path_mask.p : nullptr;
-  E.rule_words = rule_words;
-  E.hits = e->hits.p;
-  E.n_hits = n_hits;
-  E.ctrl = e->ctrl.p;
-  E.full_rules = im.u32.p + im.o_full;
-  E.n_full_rules = im.n_full;
   uint64_t n_cands = 0;
-  if (e->nl_deferred) {  // the lazy newline counts' reach per file, marked by the candidates' kernels
-    HIP_TRY(ensure_side(e));
-    HIP_TRY(e->nl_last.ensure(nf));
-    E.nl_last = e->nl_last.p;
-  }
-  for (int attempt = 0; attempt < 3; ++attempt) {
-    HIP_TRY(e->keys.ensure(cand_cap));
-    HIP_TRY(e->vals.ensure(cand_cap));
-    E.keys = e->keys.p;
-    E.vals = e->vals.p;
-    E.cand_cap = e->keys.n;
-    HIP_TRY(hipMemsetAsync(&e->ctrl.p->cands, 0, 8, s));
-    if (E.nl_last) HIP_TRY(hipMemsetAsync(e->nl_last.p, 0, (size_t)nf * 8, s));
-    if (n_hits)
-      hipLaunchKernelGGL(k_expand, dim3((uint32_t)((n_hits + 255) / 256)), dim3(256), 0, s, E);
-    if (nf) hipLaunchKernelGGL(k_full_jobs, dim3((nf + 255) / 256), dim3(256), 0, s, E);
-    HIP_TRY(hipGetLastError());
-    if ((rc = read_ctrl(e, &c))) return rc;
+  if (spec_done && c.cands <= E.cand_cap) {
     n_cands = c.cands;
-    if (n_cands <= E.cand_cap) break;
-    if (attempt == 2) {
-      set_last_error("internal: candidate buffers still overflowed after regrowing them");
-      return TSG_ERR_INTERNAL;
+  } else {
+    if (spec_done) cand_cap = std::max<uint64_t>(cand_cap, c.cands);
+    for (int attempt = 0; attempt < 3; ++attempt) {
+      if ((rc = launch_expand(n_hits, false, cand_cap))) return rc;
+      if ((rc = read_ctrl(e, &c))) return rc;
+      n_cands = c.cands;
+      if (n_cands <= E.cand_cap) break;
+      if (attempt == 2) {
+        set_last_error("internal: candidate buffers still overflowed after regrowing them");
+        return TSG_ERR_INTERNAL;
+      }
+      cand_cap = n_cands;
     }
-    cand_cap = n_cands;
+    HIP_TRY(hipEventRecord(e->ev[3], s));
   }
-  HIP_TRY(hipEventRecord(e->ev[3], s));
+  e->cand_need = n_cands + n_cands / 4;
+  e->hit_need = n_hits + n_hits / 4;
   const bool nl_early = experiment_env("TSG_NL_EARLY") != nullptr;  // (A/B: the count under the candidate sort too)
   if (e->nl_deferred && n_cands && nl_early) {
     HIP_TRY(hipEventRecord(e->ev_nl[0], s));
