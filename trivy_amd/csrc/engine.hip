@@ -5434,15 +5434,23 @@ struct LaneSrch {
 // is listed for the wave search.
 __global__ __launch_bounds__(256) void k_find_spans_lane(FindParams F) {
   const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= F.n_locs) return;
-  // a location inside a 4 KiB block without newlines (a minified line) goes
-  // straight to the wave search (a stale count only sends it there early)
-  const DevLoc& L = F.locs[w];
-  const uint64_t blk = (F.off[L.file] + L.start) / kNlBlock;
-  LaneSrch srch(F);
-  if ((blk < F.n_nlb && F.nl_blocks[blk] == 0) || !find_spans_one(F, w, true, srch)) {
-    const unsigned long long k = atomicAdd(&F.ctrl->n_long_spans, 1ull);
-    F.long_list[k] = (uint32_t)w;
+  bool go_long = false;
+  if (w < F.n_locs) {
+    // a location inside a 4 KiB block without newlines (a minified line) goes
+    // straight to the wave search (a stale count only sends it there early)
+    const DevLoc& L = F.locs[w];
+    const uint64_t blk = (F.off[L.file] + L.start) / kNlBlock;
+    LaneSrch srch(F);
+    go_long = (blk < F.n_nlb && F.nl_blocks[blk] == 0) || !find_spans_one(F, w, true, srch);
+  }
+  // one list reservation per wave
+  const uint64_t b = __ballot(go_long);
+  if (b) {
+    const uint32_t lead = (uint32_t)__builtin_ctzll(b);
+    unsigned long long base = 0;
+    if (__lane_id() == lead) base = atomicAdd(&F.ctrl->n_long_spans, (unsigned long long)__popcll(b));
+    base = __shfl(base, lead);
+    if (go_long) F.long_list[base + __popcll(b & ((1ull << __lane_id()) - 1))] = (uint32_t)w;
   }
 }
 
