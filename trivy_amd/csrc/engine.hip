@@ -183,6 +183,7 @@ struct ScanParams {
   uint64_t nl_big;  // lazy newline counts: the scan counts the spans of files this big (0: none)
   uint64_t kw_plain;  // report_event: files below this many bytes set keyword bits with plain atomics (else read first)
   uint32_t kw_drain_at;  // k_scan_fast: drain the wave's keyword queue after a step once it holds this many (0: span ends only)
+  uint32_t kw_off;       // exp A/B (TSG_KW_OFF): keyword states resolved as k_report events
   // k_report: each report wave's own hit region (hit_seg_cap records at
   // hit_seg + wave * hit_seg_cap; counts in hit_seg_n), packed into `hits` by
   // k_hits_pack -- null: flushes reserve on ctrl->hits
@@ -1087,7 +1088,7 @@ __global__ __launch_bounds__(kFastThreads) void k_scan_fast(ScanParams P) {
   FastChain<V> C[CH];
   uint4 nxt[CH][V];
   const KwScan kws{kwrec, kwmap, kwq + (kKw ? (threadIdx.x >> 6) * kFastKwQ : 0), kwseen + (kKw ? threadIdx.x & ~63u : 0),
-                   kKw && kw_scan_ok(P) ? ac.fast_ev_entry : out_e};
+                   kKw && kw_scan_ok(P) && !P.kw_off ? ac.fast_ev_entry : out_e};
   uint32_t kwn = 0;    // wave-uniform: records in this wave's keyword queue
   uint32_t kseen = 0;  // keyword states (bit: state - out_e) of this span's file already set
   if (u < units) {
@@ -3611,6 +3612,24 @@ __device__ __noinline__ void emit_match(const VerifyParams& V, uint32_t rule, ui
   for (uint32_t k = 0; k < allow_n; ++k)
     if (match_string_pf(V.rs, V.rs.allow_progs[allow_off + k], text + ms, (uint32_t)(me - ms), sc)) return;
   emit_kept<Pos>(V, rd, rule, fi, job, text, ms, me);
+}
+
+// Zeroes what a verify attempt counts into: the Ctrl counters (locs, n_caps /
+// n_caps_big, n_redo / n_dropped / n_caps_run, n_defer / n_match), the
+// location shard counters and the per-job flag bytes.
+__global__ __launch_bounds__(256) void k_verify_reset(Ctrl* ctrl, unsigned long long* loc_cnt, uint8_t* job_bad,
+                                                      uint64_t n_jobs) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0) {
+    ctrl->locs = 0;
+    ctrl->n_caps = ctrl->n_caps_big = 0;
+    ctrl->n_redo = ctrl->n_dropped = ctrl->n_caps_run = 0;
+    ctrl->n_defer = ctrl->n_match = 0;
+  }
+  if (loc_cnt && t <= kLocShards) loc_cnt[t] = 0;
+  const uint64_t n16 = n_jobs / 16;
+  for (uint64_t i = t; i < n16; i += (uint64_t)gridDim.x * blockDim.x) ((uint4*)job_bad)[i] = make_uint4(0, 0, 0, 0);
+  for (uint64_t i = n16 * 16 + t; i < n_jobs; i += (uint64_t)gridDim.x * blockDim.x) job_bad[i] = 0;
 }
 
 // emit_match for k_verify_fast: the match goes to the raw match list; the
@@ -8446,6 +8465,7 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   if (const char* v = experiment_env("TSG_KW_PLAIN")) P.kw_plain = strtoull(v, nullptr, 10);  // (A/B)
   P.kw_drain_at = kKwDrainAt;
   if (const char* v = experiment_env("TSG_KW_DRAIN")) P.kw_drain_at = (uint32_t)strtoul(v, nullptr, 10);  // (A/B)
+  P.kw_off = experiment_env("TSG_KW_OFF") != nullptr;  // (A/B)
   const bool merge = sp && sp->mode == 2;
   // newline counts: counted lazily after the locations (k_nl_spans), except
   // for a part scan, whose blob exports its range's counts, and a batch of
@@ -8691,7 +8711,6 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     if (shard_locs) {
       HIP_TRY(e->locs2.ensure(loc_total));
       HIP_TRY(e->loc_cnt.ensure(kLocShards + 1));
-      HIP_TRY(hipMemsetAsync(e->loc_cnt.p, 0, (kLocShards + 1) * 8, s));
     }
     HIP_TRY(e->caps.ensure(caps_cap));
     HIP_TRY(e->caps_big.ensure(caps_big_cap));
@@ -8702,11 +8721,10 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
     HIP_TRY(e->redo.ensure(redo_cap));
     HIP_TRY(e->defer.ensure(n_cands));
     HIP_TRY(e->matches.ensure(loc_cap));
-    HIP_TRY(hipMemsetAsync(&e->ctrl.p->n_defer, 0, 16, s));  // n_defer, n_match
-    HIP_TRY(hipMemsetAsync(e->job_bad.p, 0, n_cands, s));
-    HIP_TRY(hipMemsetAsync(&e->ctrl.p->locs, 0, 8, s));
-    HIP_TRY(hipMemsetAsync(&e->ctrl.p->n_caps, 0, 16, s));  // n_caps, n_caps_big
-    HIP_TRY(hipMemsetAsync(&e->ctrl.p->n_redo, 0, 24, s));  // n_redo, n_dropped, n_caps_run
+    // the verify counters, the location shards and the job flags: one launch
+    // (was six fills)
+    hipLaunchKernelGGL(k_verify_reset, dim3((uint32_t)std::min<uint64_t>((n_cands + 4095) / 4096 + 1, 4096)), dim3(256),
+                       0, s, e->ctrl.p, shard_locs ? e->loc_cnt.p : nullptr, e->job_bad.p, n_cands);
     VerifyParams V{};
     V.data = d_data;
     V.off = d_off;
@@ -9912,6 +9930,7 @@ int tsg_gate_device(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data,
   if (const char* v = experiment_env("TSG_KW_PLAIN")) P.kw_plain = strtoull(v, nullptr, 10);  // (A/B)
   P.kw_drain_at = kKwDrainAt;
   if (const char* v = experiment_env("TSG_KW_DRAIN")) P.kw_drain_at = (uint32_t)strtoul(v, nullptr, 10);  // (A/B)
+  P.kw_off = experiment_env("TSG_KW_OFF") != nullptr;  // (A/B)
   const bool want_gates = h_gates_out && nf && gate_words_per_file;
   const uint32_t R = (uint32_t)rs->rules.size();
   std::vector<uint32_t> csr;
