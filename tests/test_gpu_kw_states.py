@@ -104,3 +104,53 @@ def test_gpu_keyword_states_findings_vs_oracle():
         n += len(want["Findings"])
         assert _canon(_plain(g)) == _canon(want), p
     assert n > 100
+
+
+def _many_keywords_config(tmp_path, n_rules=70, seed=17):
+    """Custom rules whose keywords are short strings over a small alphabet
+    (suffixes of one another: states with two outputs) and whose regex never
+    holds them (so every keyword is needed by a non-implied gate): more
+    keyword-only states than the scan keeps (kFastKwStates / kFastKwBits), the
+    rest resolved as events."""
+    from . import stress_rules
+    rng = random.Random(seed)
+    words = set()
+    while len(words) < n_rules:
+        words.add("".join(rng.choice("abcdefgh") for _ in range(rng.randint(2, 4))))
+    words = sorted(words, key=lambda w: (len(w), w))
+    rules = [({"id": f"kwmany-{i}", "category": "test", "title": "t", "severity": "LOW",
+               "regex": r"zq[0-9]{6}", "keywords": [w]}, None) for i, w in enumerate(words)]
+    path = str(tmp_path / "trivy-secret.yaml")
+    stress_rules.write_config(path, rules)
+    return path, words
+
+
+def test_many_keywords_states_capped(tmp_path):
+    path, _ = _many_keywords_config(tmp_path)
+    sc = S.new_scanner(S.parse_config(path))
+    ns, words = _kw_states(sc)
+    assert 0 < ns <= 32 and len(words) <= 32
+
+
+@pytest.mark.gpu
+def test_gpu_many_keywords_gates_and_findings_vs_oracle(tmp_path):
+    from .test_gpu_parity import _canon, _oracle_plain, _plain
+    from .test_gpu_stress import _check_gates
+    path, words = _many_keywords_config(tmp_path)
+    files = _tiny_files(21, 2000, words)
+    rng = random.Random(22)
+    for i in range(400):
+        body = " ".join(rng.choice(words) for _ in range(rng.randint(0, 6)))
+        body += f" zq{rng.randrange(10**6):06d} " + " ".join(rng.choice(words) for _ in range(rng.randint(0, 3)))
+        files.append((f"f/{i}.txt", body.encode()))
+    files.append(("dense.txt", (" ".join(words) + " zq123456\n").encode() * 300))
+    assert _check_gates(path, files) > 0
+    sc = S.new_scanner(S.parse_config(path))
+    oc = o.Scanner(o.parse_config(path))
+    got = sc.scan_batch_device([S.ScanArgs(p, d) for p, d in files])
+    n = 0
+    for (p, d), g in zip(files, got):
+        want = _oracle_plain(oc.scan(p, d))
+        n += len(want["Findings"])
+        assert _canon(_plain(g)) == _canon(want), p
+    assert n > 200
