@@ -66,3 +66,22 @@ def test_bench_shared_two_ranks_gloo_equals_one_rank(tmp_path):
         if k.startswith("locs"):
             n += len(a[k])
     assert n > 0 and one["counts"]["locs"] == two["counts"]["locs"] == n
+
+
+@pytest.mark.gpu
+def test_bench_config2_two_ranks_gloo(tmp_path):
+    """The headline path's N > 1 shape (the driver's SCALE run: one rank per
+    GPU, a barrier and the max over ranks around the timed steps, the whole
+    job's bytes / that time), here as two ranks sharing one GPU over gloo:
+    one JSON line from rank 0, n_gpus 2, the aggregate over both ranks'
+    corpora, rank 0's parity properties intact."""
+    common = ["--config", "2", "--gb", "1", "--steps", "2", "--warmup", "1", "--no-cpu"]
+    two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+                *common, "--dist-backend", "gloo"], str(tmp_path / "two.log"))
+    assert two["n_gpus"] == 2 and two["scaling"] == "weak"
+    assert abs(two["config"]["gb_per_gpu"] - 1.0) < 0.01
+    # value = both ranks' bytes / the slowest rank's time
+    assert abs(two["value"] - 2 * two["config"]["gb_per_gpu"] * 1e3 / two["ms_per_step"]) / two["value"] < 0.02
+    p = two["parity"]
+    assert p["planted_found"] == p["planted"] and p["decoys_found"] == 0 and p["spot_mismatched_files"] == 0
