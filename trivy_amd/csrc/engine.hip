@@ -502,6 +502,18 @@ __device__ inline uint32_t nl_count_dword(uint32_t w) {
 // ASCII: k_report re-checks every pattern on the real bytes.
 __device__ inline uint32_t fold6(uint32_t w) { return ((w << 1) & 0x3E3E3E3Eu) | (w & 0x40404040u); }
 
+// fold6 in three VALU (shift, and, and_or) for k_scan_fast's step: written
+// as C the compiler emitted four plus a fused byte-0 op.  Full-ruleset scan
+// 11.39 -> 11.28 ms on configs[2]; in the prefilter-only kernel (kScanKwMid)
+// its register allocation went the other way, 5.74 -> 6.36 ms on configs[1]
+// (same-box A/B, profiles/r06zo_ab), so that kernel keeps the C form.
+__device__ inline uint32_t fold6_ao(uint32_t w) {
+  const uint32_t t = w << 1, m = w & 0x40404040u;
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(t), "s"(0x3E3E3E3Eu), "v"(m));
+  return r;
+}
+
 // One automaton step on byte j of a folded dword w: e = T[e * row + 2 col].
 // Entries are row indices and rows are kFastRowBytes apart (a stride an LDS
 // bank-conflict simulation of the scan picked: 134 B conflicts ~13 % less
@@ -776,7 +788,8 @@ __device__ inline void fast_window(const ScanParams& P, const uint8_t* T, uint32
     const uint32_t d0 = d[2 * g], d1 = d[2 * g + 1];
     if (!(kMode & 2) || C.cnt) C.nl += nl_count_dword(d0) + nl_count_dword(d1);
     C.hi |= d0 | d1;
-    const uint32_t f0 = fold6(d0), f1 = fold6(d1);
+    const uint32_t f0 = (kMode & kScanKwMid) ? fold6(d0) : fold6_ao(d0);
+    const uint32_t f1 = (kMode & kScanKwMid) ? fold6(d1) : fold6_ao(d1);
     gs[g] = C.e;
     uint32_t mm = 0;
     if (kPair) {
