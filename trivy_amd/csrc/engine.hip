@@ -612,6 +612,7 @@ __device__ inline uint64_t lower64(uint64_t x) {
 constexpr uint32_t kFastKwQ = 88;    // queue records per wave (16 waves x 88 x 16 B of LDS)
 constexpr uint32_t kKwDrainAt = 64;  // ScanParams::kw_drain_at
 constexpr int kScanKwMid = 64;       // k_scan_fast kMode bit: keyword queue drains after steps too (the gate scan)
+constexpr int kScanNoCount = 128;    // k_scan_fast kMode bit: the scan never counts newlines (no per-group test)
 
 struct KwRec {
   uint32_t span;  // the group's span (position / kNlBlock)
@@ -730,7 +731,7 @@ template <int V, int kMode = 0>
 __device__ inline void fast_group(const ScanParams& P, const uint8_t* T, uint32_t out_e, FastChain<V>& C, uint32_t d0,
                                   uint32_t d1, uint64_t gpos, bool live, uint64_t lanes_lt, FastEvent* ev_seg,
                                   uint32_t* ev_count) {
-  if (!(kMode & 2) || C.cnt) C.nl += nl_count_dword(d0) + nl_count_dword(d1);
+  if (!(kMode & 2) || (!(kMode & kScanNoCount) && C.cnt)) C.nl += nl_count_dword(d0) + nl_count_dword(d1);
   C.hi |= d0 | d1;
   const uint32_t f0 = fold6(d0), f1 = fold6(d1);
   const uint32_t gs = C.e;
@@ -786,7 +787,7 @@ __device__ inline void fast_window(const ScanParams& P, const uint8_t* T, uint32
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const uint32_t d0 = d[2 * g], d1 = d[2 * g + 1];
-    if (!(kMode & 2) || C.cnt) C.nl += nl_count_dword(d0) + nl_count_dword(d1);
+    if (!(kMode & 2) || (!(kMode & kScanNoCount) && C.cnt)) C.nl += nl_count_dword(d0) + nl_count_dword(d1);
     C.hi |= d0 | d1;
     const uint32_t f0 = (kMode & kScanKwMid) ? fold6(d0) : fold6_ao(d0);
     const uint32_t f1 = (kMode & kScanKwMid) ? fold6(d1) : fold6_ao(d1);
@@ -7308,9 +7309,18 @@ int launch_scan(tsg_engine* e, ScanParams& P, bool kw_mid = false) {
     fuse = fused;
 #else
     // (kMode 2: no newline counts -- the engine counts them lazily, k_nl_spans)
-    // (kw_mid: the prefilter-only scan, whose outputs are all keywords)
-    if (e->nl_lazy && kw_mid)
+    // (kw_mid: the prefilter-only scan, whose outputs are all keywords;
+    // kScanNoCount: no span of this batch is counted in the scan, so the
+    // kernel carries no count code -- its per-group test cost ~1.6 % of the
+    // scan, configs[2] 11.97 -> 11.78 ms over three alternating runs,
+    // profiles/r06zq_c2)
+    if (e->nl_lazy && kw_mid && !P.nl_big)
+      hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 2 | kScanKwMid | kScanNoCount, kFastEventWin>), dim3(blocks), dim3(nt), 0,
+                         s, P);
+    else if (e->nl_lazy && kw_mid)
       hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 2 | kScanKwMid, kFastEventWin>), dim3(blocks), dim3(nt), 0, s, P);
+    else if (e->nl_lazy && !P.nl_big)
+      hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 2 | kScanNoCount, kFastEventWin>), dim3(blocks), dim3(nt), 0, s, P);
     else if (e->nl_lazy) hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 2, kFastEventWin>), dim3(blocks), dim3(nt), 0, s, P);
     else hipLaunchKernelGGL((k_scan_fast<1, 8, 1024, 0, kFastEventWin>), dim3(blocks), dim3(nt), 0, s, P);
     nl_skipped = e->nl_lazy;
@@ -8517,6 +8527,11 @@ int run_pipeline(tsg_engine* e, const tsg_ruleset* rs, const uint8_t* d_data, co
   // for a part scan, whose blob exports its range's counts, and a batch of
   // one file the scan would count anyway (span_scan_counted: every span)
   e->nl_lazy = !(sp && sp->mode == 1) && !(nf == 1 && e->nl_big && nbytes > e->nl_big);
+  // a lazy scan counts nothing itself (the count-free kernel): the files of
+  // nl_big bytes or more inside a multi-file batch are counted by k_nl_spans
+  // like the rest (one file that large is its own, counted batch above;
+  // TSG_NL_INSCAN keeps the round-5 in-scan counting for A/B)
+  if (e->nl_lazy && !experiment_env("TSG_NL_INSCAN")) e->nl_big = P.nl_big = 0;
   e->nl_deferred = false;
   if (e->nl_pending) {  // (an earlier call ended before its lines stage: its side count must not overlap this one)
     HIP_TRY(hipStreamWaitEvent(s, e->ev_nl[1], 0));
